@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Benchmark: pods/sec in Scheduler.Solve at 50k pods x 400 instance types (BASELINE.json configs[1]).
+
+One step = one complete Solve (scheduler.go:140-189) of the C2 problem with fresh scheduler state,
+inputs already resident in HBM (the snapshot is encoded and uploaded once, like NewScheduler).
+Solve does not shard (every placement depends on all earlier ones), so N GPUs run N independent
+replicas, one per rank ("replicas only"); value = pods solved by all ranks / max-rank time.
+
+Prints ONE JSON line on rank 0 (the driver's contract), including:
+  roofline     : dominant kernel k_solve, algorithmic bytes (counted by the kernel) /
+                 its HIP-event duration vs the 8 TB/s HBM peak; traffic from profiles/ PMC data if any
+  cpu_baseline : the oracle (C++ restatement of the reference Solve, single thread) timed on this
+                 host on the same workload
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "karpenter-sigs_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pods", type=int, default=50000)
+    ap.add_argument("--its", type=int, default=400)
+    ap.add_argument("--cpu-pods", type=int, default=50000, help="oracle sample size (same workload shape)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist  # noqa: F811
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from karpenter_amd import Scheduler, synth
+
+    snap = synth.config2(args.pods) if args.its == 400 else synth.benchmark_snapshot(args.pods, args.its, 42, False)
+    snap_json = json.dumps(snap)
+    sch = Scheduler(snap_json)
+
+    # one full solve to verify the result shape (every pod placed once) outside the timed region
+    check = sch.solve(device=local)
+    placed = sum(len(c["pods"]) for c in check.new_nodeclaims)
+    assert placed + len(check.pod_errors) == args.pods, "solve lost pods"
+    nclaims = len(check.new_nodeclaims)
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        sch.solve(device=local, timing_only=True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    solve_ms, total_ms, algb = [], [], []
+    for _ in range(args.steps):
+        r = sch.solve(device=local, timing_only=True)
+        solve_ms.append(r.solve_kernel_ms)
+        total_ms.append(r.kernel_ms)
+        algb.append(r.algorithmic_bytes)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = args.pods * world * args.steps / elapsed
+    k_ms = sum(solve_ms) / len(solve_ms)
+    bytes_per_launch = sum(algb) / len(algb)
+    achieved = bytes_per_launch / (k_ms / 1000.0) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_c2.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        from oracle import bridge
+
+        csnap = synth.config2(args.cpu_pods) if args.cpu_pods != args.pods else snap
+        secs = bridge.time_solve(json.dumps(csnap), 1)
+        cpu = {"value": round(args.cpu_pods / secs, 1), "unit": "pods/s", "cores": 1, "kind": "port",
+               "sample": "1 Solve of C2 with %d pods x %d instance types (oracle/cpu_ref.cpp, single thread, "
+                         "%.1f s)" % (args.cpu_pods, args.its, secs)}
+    out = {
+        "metric": "pods/sec in Scheduler.Solve @50k pods x 400 types",
+        "value": round(value, 1),
+        "unit": "pods/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic",
+        "config": {"workload": "C2: %d resource-only pods x %d fake.InstanceTypes, 1 NodeClaimTemplate, no limits, "
+                               "empty topology (BenchmarkScheduling shape)" % (args.pods, args.its),
+                   "pods": args.pods, "instance_types": args.its, "parallelism": "replicas%d" % world,
+                   "new_nodeclaims": nclaims},
+        "roofline": {"bound": "hbm", "kernel": "k_solve", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": bytes_per_launch, "kernel_ms": round(k_ms, 3),
+                     "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

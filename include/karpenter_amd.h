@@ -1,0 +1,91 @@
+/* karpenter_amd.h — C-ABI of the MI355X Karpenter scheduler hot path (libkarpenter_amd.so).
+ *
+ * Drop-in boundary for pkg/controllers/provisioning/scheduling in the reference
+ * (/root/reference, paths relative to it).  A Go cgo shim marshals the arguments of
+ *   NewScheduler(ctx, kubeClient, nodeClaimTemplates, nodePools, cluster, stateNodes, topology,
+ *                instanceTypes, daemonSetPods, recorder, opts)        scheduler.go:49-83
+ * plus the `pods` argument of
+ *   (*Scheduler).Solve(ctx, pods) *Results                             scheduler.go:140-189
+ * into one JSON snapshot (see INTEGRATION.md for the schema and the shim), and rebuilds
+ *   Results{NewNodeClaims, ExistingNodes, PodErrors}                  scheduler.go:102-106
+ * from the result, mapping pod indices back to the caller's *v1.Pod pointers.
+ *
+ * Plain C types only; no torch or HIP types cross this boundary.  Every call returns 0 on success
+ * or a negative KS_ERR_* code; ks_last_error() then holds thread-local text.  A ks_problem is not
+ * re-entrant (mirrors the single-goroutine Scheduler); use one per thread.
+ */
+#ifndef KARPENTER_AMD_H_
+#define KARPENTER_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KS_OK 0
+#define KS_ERR_PARSE -1       /* malformed snapshot JSON / quantity */
+#define KS_ERR_UNSUPPORTED -2 /* input uses a feature this build does not encode (message says which) */
+#define KS_ERR_CAPACITY -3    /* encoding limits exceeded (keys > 64, taints > 128, claims > cap) */
+#define KS_ERR_HIP -4         /* HIP runtime error (no device, launch failure, fault) */
+#define KS_ERR_INTERNAL -5    /* kernel reported an inconsistent state (iteration cap, overflow) */
+#define KS_ERR_ARG -6
+
+typedef struct ks_problem ks_problem;
+typedef struct ks_results ks_results;
+
+typedef struct ks_solve_opts {
+  int device;          /* HIP device ordinal; -1 = current device */
+  int simulation_mode; /* SchedulerOptions.SimulationMode (scheduler.go:44-47); decisions identical */
+  int replicas;        /* >1: solve `replicas` independent copies in one launch (one wavefront each) */
+  int timing_only;     /* 1: do not copy results back (counters and timings only); benchmarks */
+  int reserved[4];
+} ks_solve_opts;
+
+/* NewScheduler equivalent: parse + encode the snapshot and upload it to HBM.  Replaces the Go
+ * allocation-heavy construction at scheduler.go:49-83 + nodeclaimtemplate.go:43-53 +
+ * existingnode.go:40-62; the caller keeps ownership of `snapshot_json`. */
+int ks_problem_create(const char* snapshot_json, size_t len, ks_problem** out);
+void ks_problem_free(ks_problem* p);
+
+/* Host-only encode of a snapshot (no device needed): returns JSON with the universe sizes (keys,
+ * value words, resources, instance types, relaxation states).  Diagnostics / CPU tests. */
+int ks_problem_inspect(const char* snapshot_json, size_t len, char** dims_json);
+
+/* Solve (scheduler.go:140-189) on the GPU.  Fresh scheduler state every call (a Scheduler is
+ * single-use in production, scheduler.go:49 is called per Schedule / per simulation). */
+int ks_solve(ks_problem* p, const ks_solve_opts* opts, ks_results** out);
+void ks_results_free(ks_results* r);
+
+/* Results as canonical JSON: {"newNodeClaims":[{nodePoolName, hostname, pods[], instanceTypeOptions[],
+ * requests{}, requirements[], requirementsString}], "existingNodes":[{name, pods[]}],
+ * "podErrors":{"<pod index>": "<error text>"}}.  Free with ks_free. */
+int ks_results_json(const ks_results* r, char** json_out);
+
+/* Structured accessors for a cgo shim (no JSON on the hot return path). */
+int ks_results_num_new_nodeclaims(const ks_results* r);
+int ks_results_nodeclaim(const ks_results* r, int i, int* template_index, const int32_t** pods, int* n_pods,
+                         const int32_t** instance_types, int* n_instance_types);
+int ks_results_num_existing_nodes(const ks_results* r);
+int ks_results_existing_node(const ks_results* r, int i, int* state_node_index, const int32_t** pods, int* n_pods);
+int ks_results_num_pod_errors(const ks_results* r);
+int ks_results_pod_error(const ks_results* r, int i, int* pod_index, const char** message);
+
+/* Device time of the solve kernel(s) of the last ks_solve, measured with HIP events on the
+ * stream the kernel ran on (milliseconds). */
+double ks_results_kernel_ms(const ks_results* r);
+/* The k_solve launch alone (the dominant kernel; excludes workspace init and the queue sort). */
+double ks_results_solve_kernel_ms(const ks_results* r);
+/* Algorithmic bytes the solve scanned (SURVEY.md §8d formula, counted by the kernel). */
+double ks_results_algorithmic_bytes(const ks_results* r);
+
+void ks_free(void* p);
+const char* ks_last_error(void);
+int ks_device_count(void);
+const char* ks_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KARPENTER_AMD_H_ */

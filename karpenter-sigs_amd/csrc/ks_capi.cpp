@@ -1,0 +1,584 @@
+// ks_capi.cpp — the C-ABI (include/karpenter_amd.h): HBM upload of the encoded problem, per-solve
+// workspace, kernel launch and reconstruction of scheduling.Results (scheduler.go:102-106).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/karpenter_amd.h"
+#include "ks_host.h"
+
+namespace ks {
+hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, int32_t* qorder, hipStream_t st,
+                        hipEvent_t mid);
+size_t solve_lds_bytes(const KsDims& d);
+}  // namespace ks
+
+using namespace ks;
+
+static thread_local std::string g_err;
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) throw KsError(KS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+// One hipMalloc carved into 256-byte aligned arrays.
+struct Arena {
+  std::vector<std::pair<size_t, size_t>> parts;  // offset, bytes
+  size_t total = 0;
+  size_t add(size_t bytes) {
+    size_t off = total;
+    total += (bytes + 255) & ~(size_t)255;
+    return off;
+  }
+};
+
+struct WorkLayout {
+  size_t c_tpl, c_cnt, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
+      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, total;
+};
+
+WorkLayout work_layout(const KsDims& d) {
+  Arena a;
+  WorkLayout w{};
+  size_t K = d.Kcap, P = std::max(d.P, 1), N = std::max(d.N, 1);
+  w.c_tpl = a.add(4 * K);
+  w.c_cnt = a.add(4 * K);
+  w.c_host = a.add(4 * K);
+  w.c_req = a.add(8 * K * d.R);
+  w.c_max = a.add(8 * K * d.R);
+  w.c_rs = a.add(4 * K * d.RSW);
+  w.c_rem = a.add(4 * K * d.TW);
+  w.order = a.add(4 * K);
+  w.n_req = a.add(8 * N * d.R);
+  w.n_rs = a.add(4 * N * d.RSW);
+  w.queue = a.add(4 * P);
+  w.qorder = a.add(4 * P);
+  w.pod_state = a.add(4 * P);
+  w.last_len = a.add(8 * (size_t)d.NU);
+  w.log_pod = a.add(4 * P);
+  w.log_tgt = a.add(4 * P);
+  w.pod_status = a.add(4 * P);
+  w.pod_fstate = a.add(4 * P);
+  w.fail_code = a.add(4 * P * std::max(d.NTPL, 1));
+  w.fail_host = a.add(4 * P * std::max(d.NTPL, 1));
+  w.pool_rem = a.add(8 * (size_t)std::max(d.NPOOL, 1) * d.R);
+  w.counters = a.add(8 * CT_NCOUNTERS);
+  w.total = a.total;
+  return w;
+}
+
+KsWork work_ptrs(char* base, const WorkLayout& w) {
+  KsWork k;
+  k.c_tpl = (int32_t*)(base + w.c_tpl);
+  k.c_cnt = (int32_t*)(base + w.c_cnt);
+  k.c_host = (int32_t*)(base + w.c_host);
+  k.c_req = (int64_t*)(base + w.c_req);
+  k.c_max = (int64_t*)(base + w.c_max);
+  k.c_rs = (uint32_t*)(base + w.c_rs);
+  k.c_rem = (uint32_t*)(base + w.c_rem);
+  k.order = (int32_t*)(base + w.order);
+  k.n_req = (int64_t*)(base + w.n_req);
+  k.n_rs = (uint32_t*)(base + w.n_rs);
+  k.queue = (int32_t*)(base + w.queue);
+  k.qorder = (int32_t*)(base + w.qorder);
+  k.pod_state = (int32_t*)(base + w.pod_state);
+  k.last_len = (uint64_t*)(base + w.last_len);
+  k.log_pod = (int32_t*)(base + w.log_pod);
+  k.log_tgt = (int32_t*)(base + w.log_tgt);
+  k.pod_status = (int32_t*)(base + w.pod_status);
+  k.pod_fstate = (int32_t*)(base + w.pod_fstate);
+  k.fail_code = (uint32_t*)(base + w.fail_code);
+  k.fail_host = (int32_t*)(base + w.fail_host);
+  k.pool_rem = (int64_t*)(base + w.pool_rem);
+  k.counters = (int64_t*)(base + w.counters);
+  return k;
+}
+
+template <class T>
+void dl(std::vector<T>& v, const void* src, size_t n, hipStream_t st) {
+  v.resize(n);
+  if (n) HIPCHK(hipMemcpyAsync(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, st));
+}
+
+}  // namespace
+
+struct ks_results {
+  struct Claim {
+    int tpl;
+    int64_t host;
+    std::vector<int32_t> pods, its;
+    std::string json;
+  };
+  struct ENode {
+    int index;
+    std::string name;
+    std::vector<int32_t> pods;
+  };
+  std::vector<Claim> claims;
+  std::vector<ENode> nodes;
+  std::vector<std::pair<int32_t, std::string>> errors;
+  double kernel_ms = 0, solve_ms = 0, algbytes = 0;
+  std::vector<int64_t> counters;
+};
+
+struct ks_problem {
+  Host host;
+  KsDev dev{};
+  void* dbuf = nullptr;
+  void* wbuf = nullptr;
+  size_t wbytes = 0;
+  KsWork* works_dev = nullptr;
+  int wreps = 0;
+  hipStream_t stream = nullptr;
+  int device = -1;
+  ~ks_problem() {
+    if (dbuf) (void)hipFree(dbuf);
+    if (wbuf) (void)hipFree(wbuf);
+    if (works_dev) (void)hipFree(works_dev);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+static void upload(ks_problem* pb) {
+  Host& h = pb->host;
+  auto& t = h.tab;
+  Arena a;
+  struct Item { size_t off; const void* src; size_t bytes; };
+  std::vector<Item> items;
+  auto put = [&](const void* src, size_t bytes) {
+    size_t off = a.add(std::max<size_t>(bytes, 16));
+    items.push_back({off, src, bytes});
+    return off;
+  };
+  size_t o_keys = put(h.keys.data(), h.keys.size() * sizeof(KeyMeta));
+  size_t o_wv = put(h.wordValid.data(), h.wordValid.size() * 4);
+  size_t o_vi = put(h.vIsInt.data(), h.vIsInt.size() * 4);
+  size_t o_vint = put(h.vInt.data(), h.vInt.size() * 8);
+  size_t o_ita = put(t.it_alloc.data(), t.it_alloc.size() * 8);
+  size_t o_itc = put(t.it_cap.data(), t.it_cap.size() * 8);
+  size_t o_itr = put(t.it_rs.data(), t.it_rs.size() * 4);
+  size_t o_ofb = put(t.it_off_beg.data(), t.it_off_beg.size() * 4);
+  size_t o_ofz = put(t.off_zone.data(), t.off_zone.size() * 4);
+  size_t o_ofc = put(t.off_ct.data(), t.off_ct.size() * 4);
+  size_t o_tr = put(t.tpl_rs.data(), t.tpl_rs.size() * 4);
+  size_t o_tt = put(t.tpl_taint.data(), t.tpl_taint.size() * 8);
+  size_t o_td = put(t.tpl_daemon.data(), t.tpl_daemon.size() * 8);
+  size_t o_tb = put(t.tpl_it_beg.data(), t.tpl_it_beg.size() * 4);
+  size_t o_ti = put(t.tpl_its.data(), t.tpl_its.size() * 4);
+  size_t o_tp = put(t.tpl_pool.data(), t.tpl_pool.size() * 4);
+  size_t o_pr = put(t.pool_rem0.data(), t.pool_rem0.size() * 8);
+  size_t o_pm = put(t.pool_mask.data(), t.pool_mask.size() * 4);
+  size_t o_preq = put(t.pod_req.data(), t.pod_req.size() * 8);
+  size_t o_ps0 = put(t.pod_state0.data(), t.pod_state0.size() * 4);
+  size_t o_pns = put(t.pod_nstate.data(), t.pod_nstate.size() * 4);
+  size_t o_pu = put(t.pod_uid.data(), t.pod_uid.size() * 4);
+  size_t o_psk = put(t.pod_sortkey.data(), t.pod_sortkey.size() * 8);
+  size_t o_sr = put(t.st_rs.data(), t.st_rs.size() * 4);
+  size_t o_st = put(t.st_tol.data(), t.st_tol.size() * 8);
+  size_t o_sf = put(t.st_flags.data(), t.st_flags.size() * 4);
+  size_t o_na = put(t.n_avail.data(), t.n_avail.size() * 8);
+  size_t o_nr = put(t.n_req0.data(), t.n_req0.size() * 8);
+  size_t o_nrs = put(t.n_rs0.data(), t.n_rs0.size() * 4);
+  size_t o_nt = put(t.n_taint.data(), t.n_taint.size() * 8);
+  HIPCHK(hipMalloc(&pb->dbuf, a.total));
+  std::vector<char> staging(a.total, 0);
+  for (auto& it : items)
+    if (it.bytes) memcpy(staging.data() + it.off, it.src, it.bytes);
+  HIPCHK(hipMemcpy(pb->dbuf, staging.data(), a.total, hipMemcpyHostToDevice));
+  char* b = (char*)pb->dbuf;
+  KsDev& D = pb->dev;
+  D.d = h.dims;
+  D.keys = (const KeyMeta*)(b + o_keys);
+  D.wordValid = (const uint32_t*)(b + o_wv);
+  D.vIsInt = (const uint32_t*)(b + o_vi);
+  D.vInt = (const int64_t*)(b + o_vint);
+  D.it_alloc = (const int64_t*)(b + o_ita);
+  D.it_cap = (const int64_t*)(b + o_itc);
+  D.it_rs = (const uint32_t*)(b + o_itr);
+  D.it_off_beg = (const int32_t*)(b + o_ofb);
+  D.off_zone = (const int32_t*)(b + o_ofz);
+  D.off_ct = (const int32_t*)(b + o_ofc);
+  D.tpl_rs = (const uint32_t*)(b + o_tr);
+  D.tpl_taint = (const uint64_t*)(b + o_tt);
+  D.tpl_daemon = (const int64_t*)(b + o_td);
+  D.tpl_it_beg = (const int32_t*)(b + o_tb);
+  D.tpl_its = (const int32_t*)(b + o_ti);
+  D.tpl_pool = (const int32_t*)(b + o_tp);
+  D.pool_rem0 = (const int64_t*)(b + o_pr);
+  D.pool_mask = (const uint32_t*)(b + o_pm);
+  D.pod_req = (const int64_t*)(b + o_preq);
+  D.pod_state0 = (const int32_t*)(b + o_ps0);
+  D.pod_nstate = (const int32_t*)(b + o_pns);
+  D.pod_uid = (const int32_t*)(b + o_pu);
+  D.pod_sortkey = (const int64_t*)(b + o_psk);
+  D.st_rs = (const uint32_t*)(b + o_sr);
+  D.st_tol = (const uint64_t*)(b + o_st);
+  D.st_flags = (const int32_t*)(b + o_sf);
+  D.n_avail = (const int64_t*)(b + o_na);
+  D.n_req0 = (const int64_t*)(b + o_nr);
+  D.n_rs0 = (const uint32_t*)(b + o_nrs);
+  D.n_taint = (const uint64_t*)(b + o_nt);
+}
+
+// Rebuild Results from the replica-0 workspace.
+static ks_results* collect(ks_problem* pb, const KsWork& W) {
+  Host& h = pb->host;
+  const KsDims& d = h.dims;
+  hipStream_t st = pb->stream;
+  std::vector<int64_t> ctr;
+  dl(ctr, W.counters, CT_NCOUNTERS, st);
+  HIPCHK(hipStreamSynchronize(st));
+  if (ctr[CT_ERROR] != KE_OK)
+    throw KsError(ctr[CT_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
+                  ctr[CT_ERROR] == KE_CLAIM_CAP ? "NodeClaim capacity exceeded" : "solve kernel iteration cap hit");
+  int nc = (int)ctr[CT_NCLAIMS], nl = (int)ctr[CT_NLOG];
+  std::vector<int32_t> order, ctpl, chost, logp, logt, status, fstate;
+  std::vector<int64_t> creq;
+  std::vector<uint32_t> crs, crem, fcode;
+  std::vector<int32_t> fhost;
+  dl(order, W.order, nc, st);
+  dl(ctpl, W.c_tpl, nc, st);
+  dl(chost, W.c_host, nc, st);
+  dl(creq, W.c_req, (size_t)nc * d.R, st);
+  dl(crs, W.c_rs, (size_t)nc * d.RSW, st);
+  dl(crem, W.c_rem, (size_t)nc * d.TW, st);
+  dl(logp, W.log_pod, nl, st);
+  dl(logt, W.log_tgt, nl, st);
+  dl(status, W.pod_status, d.P, st);
+  dl(fstate, W.pod_fstate, d.P, st);
+  dl(fcode, W.fail_code, (size_t)d.P * std::max(d.NTPL, 1), st);
+  dl(fhost, W.fail_host, (size_t)d.P * std::max(d.NTPL, 1), st);
+  HIPCHK(hipStreamSynchronize(st));
+
+  auto* res = new ks_results();
+  res->counters = ctr;
+  res->algbytes = (double)ctr[CT_ALGBYTES];
+  std::vector<std::vector<int32_t>> claimPods(nc), nodePods(d.N);
+  for (int i = 0; i < nl; i++) {
+    if (logt[i] >= 0) claimPods[logt[i]].push_back(logp[i]);
+    else nodePods[-logt[i] - 1].push_back(logp[i]);
+  }
+  for (int k = 0; k < nc; k++) {
+    int c = order[k];
+    ks_results::Claim cl;
+    cl.tpl = ctpl[c];
+    cl.host = chost[c];
+    cl.pods = claimPods[c];
+    const Host::Tpl& tp = h.tpls[cl.tpl];
+    for (int pos = 0; pos < (int)tp.its.size(); pos++)
+      if ((crem[(size_t)c * d.TW + (pos >> 5)] >> (pos & 31)) & 1u) cl.its.push_back(tp.its[pos]);
+    // requests = Merge(daemon, RequestsForPods(pod_1), ...) replayed in commit order
+    QList req = tp.daemon;
+    for (int p : cl.pods)
+      for (auto& kv : h.pods[p].requests) req[kv.first].add(kv.second);
+    for (auto& kv : req) {
+      int r = h.resId.at(kv.first);
+      if (h.toDev(r, kv.second) != creq[(size_t)c * d.R + r])
+        throw KsError(KS_ERR_INTERNAL, "device requests diverge from the replayed Merge for " + kv.first);
+    }
+    const uint32_t* rec = &crs[(size_t)c * d.RSW];
+    std::string j = "{\"nodePoolName\":";
+    ksjson::quote(j, tp.pool);
+    j += ",\"hostname\":";
+    ksjson::quote(j, h.placeholder(cl.host));
+    j += ",\"pods\":[";
+    for (size_t i = 0; i < cl.pods.size(); i++) j += (i ? "," : "") + std::to_string(cl.pods[i]);
+    j += "],\"instanceTypeOptions\":[";
+    for (size_t i = 0; i < cl.its.size(); i++) {
+      if (i) j += ",";
+      ksjson::quote(j, h.its[cl.its[i]].name);
+    }
+    j += "],\"requests\":{";
+    bool first = true;
+    for (auto& kv : req) {
+      if (!first) j += ",";
+      first = false;
+      ksjson::quote(j, kv.first);
+      j += ":";
+      ksjson::quote(j, qty_str(kv.second));
+    }
+    j += "},\"requirements\":[";
+    first = true;
+    uint64_t pr = rs_present(rec);
+    for (int kk = 0; kk < d.NK; kk++) {  // FinalizeScheduling drops the hostname requirement
+      if (!bit(pr, kk) || kk == h.hostKey) continue;
+      if (!first) j += ",";
+      first = false;
+      ksjson::quote(j, h.reqString(rec, kk, true, cl.host));
+    }
+    j += "],\"requirementsString\":";
+    ksjson::quote(j, h.reqsString(rec, cl.host));
+    j += "}";
+    cl.json = j;
+    res->claims.push_back(std::move(cl));
+  }
+  for (int n = 0; n < d.N; n++) res->nodes.push_back(ks_results::ENode{h.nodes[n].origIndex, h.nodes[n].name, nodePods[n]});
+  // PodErrors (scheduler.go:179-183 keeps non-nil errors only)
+  for (int p = 0; p < d.P; p++) {
+    if (status[p] != ST_FAILED) continue;
+    int s = fstate[p];
+    int s0 = h.tab.pod_state0[p];
+    const PodState& ps = h.states[p][s - s0];
+    std::vector<std::string> segs;
+    for (int t = 0; t < d.NTPL; t++) {
+      uint32_t code = fcode[(size_t)p * d.NTPL + t];
+      int64_t host = fhost[(size_t)p * d.NTPL + t];
+      const Host::Tpl& tp = h.tpls[t];
+      std::string pre = "incompatible with nodepool " + go_quote(tp.pool) + ", daemonset overhead=" + qlist_json(tp.daemon) + ", ";
+      switch (code & 0xff) {
+        case FC_LIMITS:
+          segs.push_back("all available instance types exceed limits for nodepool: " + go_quote(tp.pool));
+          break;
+        case FC_TAINTS: {
+          std::string m;
+          for (auto& x : tp.taints) {
+            bool ok = false;
+            for (auto& tol : ps.tols) {
+              bool e = tol.effect.empty() || tol.effect == x.effect;
+              bool k = tol.key.empty() || tol.key == x.key;
+              bool v = (tol.op.empty() || tol.op == "Equal") ? tol.value == x.value : tol.op == "Exists";
+              ok = ok || (e && k && v);
+            }
+            if (!ok) m += (m.empty() ? "" : "; ") + std::string("did not tolerate ") + x.key + "=" + x.value + ":" + x.effect;
+          }
+          segs.push_back(pre + m);
+          break;
+        }
+        case FC_COMPAT: {
+          std::vector<uint32_t> r(h.tab.tpl_rs.begin() + (size_t)t * d.RSW, h.tab.tpl_rs.begin() + (size_t)(t + 1) * d.RSW);
+          auto errs = h.compatErrors(r.data(), ps.rsAll.data(), true, host);
+          std::string m;
+          for (size_t i = 0; i < errs.size(); i++) m += (i ? "; " : "") + errs[i];
+          segs.push_back(pre + "incompatible requirements, " + m);
+          break;
+        }
+        case FC_NO_IT: {
+          uint32_t f = code >> 8;
+          std::vector<uint32_t> r(h.tab.tpl_rs.begin() + (size_t)t * d.RSW, h.tab.tpl_rs.begin() + (size_t)(t + 1) * d.RSW);
+          rs_add(h.L, r.data(), ps.rsAll.data());
+          QList cum = tp.daemon;
+          for (auto& kv : h.pods[p].requests) cum[kv.first].add(kv.second);
+          bool rq = f & FF_REQ, fi = f & FF_FITS, of = f & FF_OFF;
+          std::string why;  // filterResults.FailureReason (nodeclaim.go:165-221)
+          if (!rq && !fi && !of) why = "no instance type met the scheduling requirements or had enough resources or had a required offering";
+          else if (!rq && !fi) why = "no instance type met the scheduling requirements or had enough resources";
+          else if (!rq && !of) why = "no instance type met the scheduling requirements or had a required offering";
+          else if (!fi && !of) why = "no instance type had enough resources or had a required offering";
+          else if (!rq) why = "no instance type met all requirements";
+          else if (!fi) {
+            why = "no instance type has enough resources";
+            auto c = cum.find("cpu");
+            if (c != cum.end() && c->second.n >= (__int128)1000000 * 1000000000) why += " (CPU request >= 1 Million, m vs M typo?)";
+          } else if (!of) why = "no instance type has the required offering";
+          else if (f & FF_REQ_FITS) why = "no instance type which met the scheduling requirements and had enough resources, had a required offering";
+          else if (f & FF_FITS_OFF) why = "no instance type which had enough resources and the required offering met the scheduling requirements";
+          else if (f & FF_REQ_OFF) why = "no instance type which met the scheduling requirements and the required offering had the required resources";
+          else why = "no instance type met the requirements/resources/offering tuple";
+          segs.push_back(pre + "no instance type satisfied resources " + qlist_json(cum) + " and requirements " +
+                         h.reqsString(r.data(), host) + " (" + why + ")");
+          break;
+        }
+        default:
+          throw KsError(KS_ERR_INTERNAL, "failed pod without a failure code");
+      }
+    }
+    std::string msg;
+    for (size_t i = 0; i < segs.size(); i++) msg += (i ? "; " : "") + segs[i];
+    res->errors.push_back({p, msg});
+  }
+  return res;
+}
+
+#define API_TRY try {
+#define API_CATCH                                  \
+  }                                                \
+  catch (const KsError& e) {                       \
+    g_err = e.what();                              \
+    return e.code;                                 \
+  }                                                \
+  catch (const std::exception& e) {                \
+    g_err = e.what();                              \
+    return KS_ERR_PARSE;                           \
+  }
+
+extern "C" {
+
+const char* ks_last_error(void) { return g_err.c_str(); }
+void ks_free(void* p) { free(p); }
+const char* ks_build_info(void) { return "karpenter_amd gfx950 one-wavefront-per-Solve v1"; }
+
+int ks_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ks_problem_create(const char* json, size_t len, ks_problem** out) {
+  API_TRY
+  if (!json || !out) throw KsError(KS_ERR_ARG, "null argument");
+  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  std::unique_ptr<ks_problem> pb(new ks_problem());
+  pb->host.build(root);
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw KsError(KS_ERR_HIP, "no HIP device visible");
+  HIPCHK(hipGetDevice(&pb->device));
+  HIPCHK(hipStreamCreateWithFlags(&pb->stream, hipStreamNonBlocking));
+  upload(pb.get());
+  *out = pb.release();
+  return KS_OK;
+  API_CATCH
+}
+
+// Host-only encode (no device): layout sizes for diagnostics and CPU tests.
+int ks_problem_inspect(const char* json, size_t len, char** out) {
+  API_TRY
+  if (!json || !out) throw KsError(KS_ERR_ARG, "null argument");
+  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  Host h;
+  h.build(root);
+  const KsDims& d = h.dims;
+  std::string o = "{";
+  auto kv = [&](const char* k, long long v) { o += std::string(o.size() > 1 ? "," : "") + "\"" + k + "\":" + std::to_string(v); };
+  kv("R", d.R); kv("keys", d.NK); kv("W", d.W); kv("NB", d.NB); kv("RSW", d.RSW); kv("T", d.T); kv("templates", d.NTPL);
+  kv("pools", d.NPOOL); kv("nodes", d.N); kv("pods", d.P); kv("states", d.S); kv("uids", d.NU); kv("TW", d.TW);
+  kv("Kcap", d.Kcap); kv("taints", (long long)h.taints.size());
+  o += ",\"keyNames\":[";
+  for (size_t i = 0; i < h.keyNames.size(); i++) { if (i) o += ","; ksjson::quote(o, h.keyNames[i]); }
+  o += "],\"resources\":[";
+  for (size_t i = 0; i < h.resNames.size(); i++) { if (i) o += ","; ksjson::quote(o, h.resNames[i]); }
+  o += "]}";
+  *out = strdup(o.c_str());
+  return KS_OK;
+  API_CATCH
+}
+
+void ks_problem_free(ks_problem* p) { delete p; }
+void ks_results_free(ks_results* r) { delete r; }
+
+int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
+  API_TRY
+  if (!pb || !out) throw KsError(KS_ERR_ARG, "null argument");
+  int reps = opts && opts->replicas > 1 ? opts->replicas : 1;
+  if (opts && opts->device >= 0) HIPCHK(hipSetDevice(opts->device));
+  const KsDims& d = pb->host.dims;
+  if (solve_lds_bytes(d) > 160 * 1024) throw KsError(KS_ERR_CAPACITY, "solve state exceeds 160 KiB of LDS");
+  WorkLayout wl = work_layout(d);
+  size_t need = wl.total * reps;
+  if (need > pb->wbytes || reps != pb->wreps) {
+    if (pb->wbuf) HIPCHK(hipFree(pb->wbuf));
+    if (pb->works_dev) HIPCHK(hipFree(pb->works_dev));
+    pb->wbuf = nullptr;
+    pb->works_dev = nullptr;
+    HIPCHK(hipMalloc(&pb->wbuf, need));
+    HIPCHK(hipMalloc(&pb->works_dev, sizeof(KsWork) * reps));
+    std::vector<KsWork> ws;
+    for (int r = 0; r < reps; r++) ws.push_back(work_ptrs((char*)pb->wbuf + wl.total * r, wl));
+    HIPCHK(hipMemcpy(pb->works_dev, ws.data(), sizeof(KsWork) * reps, hipMemcpyHostToDevice));
+    pb->wbytes = need;
+    pb->wreps = reps;
+  }
+  KsWork w0 = work_ptrs((char*)pb->wbuf, wl);
+  hipEvent_t e0, em, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&em));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, pb->stream));
+  HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, w0.qorder, pb->stream, em));
+  HIPCHK(hipEventRecord(e1, pb->stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0, setup = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  HIPCHK(hipEventElapsedTime(&setup, e0, em));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(em);
+  (void)hipEventDestroy(e1);
+  ks_results* r;
+  if (opts && opts->timing_only) {
+    r = new ks_results();
+    dl(r->counters, w0.counters, CT_NCOUNTERS, pb->stream);
+    HIPCHK(hipStreamSynchronize(pb->stream));
+    if (r->counters[CT_ERROR] != KE_OK) {
+      std::string msg = "solve kernel reported error " + std::to_string(r->counters[CT_ERROR]);
+      delete r;
+      throw KsError(KS_ERR_INTERNAL, msg);
+    }
+    r->algbytes = (double)r->counters[CT_ALGBYTES];
+  } else {
+    r = collect(pb, w0);
+  }
+  r->kernel_ms = ms;
+  r->solve_ms = ms - setup;
+  *out = r;
+  return KS_OK;
+  API_CATCH
+}
+
+int ks_results_json(const ks_results* r, char** json_out) {
+  API_TRY
+  std::string o = "{\"newNodeClaims\":[";
+  for (size_t i = 0; i < r->claims.size(); i++) o += (i ? "," : "") + r->claims[i].json;
+  o += "],\"existingNodes\":[";
+  // existing nodes are reported by name in calculateExistingNodeClaims order
+  for (size_t i = 0; i < r->nodes.size(); i++) {
+    o += i ? ",{\"name\":" : "{\"name\":";
+    ksjson::quote(o, r->nodes[i].name);
+    o += ",\"pods\":[";
+    for (size_t k = 0; k < r->nodes[i].pods.size(); k++) o += (k ? "," : "") + std::to_string(r->nodes[i].pods[k]);
+    o += "]}";
+  }
+  o += "],\"podErrors\":{";
+  for (size_t i = 0; i < r->errors.size(); i++) {
+    if (i) o += ",";
+    ksjson::quote(o, std::to_string(r->errors[i].first));
+    o += ":";
+    ksjson::quote(o, r->errors[i].second);
+  }
+  o += "},\"stats\":{";
+  static const char* names[] = {"nclaims", "ncommits", "hostnameCounter", "error", "pops", "algBytes",
+                                "sorts", "sortsWithDescent"};
+  for (int i = 0; i < 8; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
+  o += "}}";
+  *json_out = strdup(o.c_str());
+  return KS_OK;
+  API_CATCH
+}
+
+int ks_results_num_new_nodeclaims(const ks_results* r) { return (int)r->claims.size(); }
+int ks_results_nodeclaim(const ks_results* r, int i, int* tpl, const int32_t** pods, int* np, const int32_t** its, int* nit) {
+  if (i < 0 || i >= (int)r->claims.size()) return KS_ERR_ARG;
+  const auto& c = r->claims[i];
+  if (tpl) *tpl = c.tpl;
+  if (pods) *pods = c.pods.data();
+  if (np) *np = (int)c.pods.size();
+  if (its) *its = c.its.data();
+  if (nit) *nit = (int)c.its.size();
+  return KS_OK;
+}
+int ks_results_num_existing_nodes(const ks_results* r) { return (int)r->nodes.size(); }
+int ks_results_existing_node(const ks_results* r, int i, int* idx, const int32_t** pods, int* np) {
+  if (i < 0 || i >= (int)r->nodes.size()) return KS_ERR_ARG;
+  if (idx) *idx = r->nodes[i].index;
+  if (pods) *pods = r->nodes[i].pods.data();
+  if (np) *np = (int)r->nodes[i].pods.size();
+  return KS_OK;
+}
+int ks_results_num_pod_errors(const ks_results* r) { return (int)r->errors.size(); }
+int ks_results_pod_error(const ks_results* r, int i, int* pod, const char** msg) {
+  if (i < 0 || i >= (int)r->errors.size()) return KS_ERR_ARG;
+  if (pod) *pod = r->errors[i].first;
+  if (msg) *msg = r->errors[i].second.c_str();
+  return KS_OK;
+}
+double ks_results_kernel_ms(const ks_results* r) { return r->kernel_ms; }
+double ks_results_solve_kernel_ms(const ks_results* r) { return r->solve_ms; }
+double ks_results_algorithmic_bytes(const ks_results* r) { return r->algbytes; }
+
+}  // extern "C"

@@ -1,0 +1,941 @@
+// ks_host.cpp — snapshot parsing, universe interning and encoding (the NewScheduler half of the
+// boundary), plus the text renderers used to rebuild Results (Requirements.String, PodErrors).
+//
+// Reference behaviour encoded here (paths under /root/reference):
+//   NewNodeClaimTemplate            pkg/controllers/provisioning/scheduling/nodeclaimtemplate.go:43-53
+//   NewScheduler / getDaemonOverhead / calculateExistingNodeClaims     scheduler.go:49-83,287-341
+//   NewExistingNode                 existingnode.go:40-62
+//   NewPodRequirements / NewStrictPodRequirements / HasPreferredNodeAffinity  requirements.go:56-109
+//   Preferences.Relax               preferences.go:38-147 (precomputed as a chain of pod states)
+//   RequestsForPods / Ceiling       pkg/utils/resources/resources.go:27-35,99-115
+//   InstanceType.Allocatable        pkg/cloudprovider/types.go:100-110
+//   Taints.Tolerates / ToleratesTaint pkg/scheduling/taints.go:38-50 (k8s.io/api v0.28.4)
+#include "ks_host.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "ks_gosort.h"
+
+namespace ks {
+
+static const char* kHostname = "kubernetes.io/hostname";
+static const char* kZone = "topology.kubernetes.io/zone";
+static const char* kCT = "karpenter.sh/capacity-type";
+static const char* kNodePoolKey = "karpenter.sh/nodepool";
+
+std::string normalize_key(const std::string& k) {  // v1beta1.NormalizedLabels (labels.go:94-100)
+  if (k == "failure-domain.beta.kubernetes.io/zone") return kZone;
+  if (k == "beta.kubernetes.io/arch") return "kubernetes.io/arch";
+  if (k == "beta.kubernetes.io/os") return "kubernetes.io/os";
+  if (k == "beta.kubernetes.io/instance-type") return "node.kubernetes.io/instance-type";
+  if (k == "failure-domain.beta.kubernetes.io/region") return "topology.kubernetes.io/region";
+  return k;
+}
+
+std::string go_quote(const std::string& s) {
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
+    else if (c == '\n') o += "\\n";
+    else if (c == '\t') o += "\\t";
+    else if (c < 0x20 || c == 0x7f) { char b[8]; snprintf(b, sizeof b, "\\x%02x", c); o += b; }
+    else o += (char)c;
+  }
+  return o + "\"";
+}
+
+std::string qlist_json(const QList& l) {
+  if (l.empty()) return "{}";
+  std::string s = "{";
+  bool first = true;
+  for (auto& kv : l) {
+    if (!first) s += ",";
+    first = false;
+    ksjson::quote(s, kv.first);
+    s += ":";
+    ksjson::quote(s, qty_str(kv.second));
+  }
+  return s + "}";
+}
+
+static bool go_atoi(const std::string& s, int64_t& out) {  // strconv.Atoi
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; }
+  if (i == s.size()) return false;
+  unsigned __int128 v = 0;
+  for (; i < s.size(); i++) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (unsigned)(s[i] - '0');
+    if (v > ((unsigned __int128)1 << 63)) return false;
+  }
+  if (!neg && v == ((unsigned __int128)1 << 63)) return false;
+  out = neg ? (int64_t)(0 - (uint64_t)v) : (int64_t)v;
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// JSON helpers
+// ---------------------------------------------------------------------------------------------
+using ksjson::Value;
+static std::string jstr(const Value* v, const char* k, const std::string& d = "") {
+  if (!v) return d;
+  const Value* x = v->get(k);
+  return x && x->is_str() ? x->s : d;
+}
+static std::map<std::string, std::string> jmap(const Value* v) {
+  std::map<std::string, std::string> m;
+  if (v) for (auto& kv : v->obj()) m[kv.first] = kv.second.str();
+  return m;
+}
+static QList jqlist(const Value* v) {
+  QList q;
+  if (v)
+    for (auto& kv : v->obj()) {
+      try {
+        q[kv.first] = qty_parse(kv.second.is_str() ? kv.second.s : kv.second.s);
+      } catch (const std::exception& e) {
+        throw KsError(-1, std::string("quantity ") + kv.first + ": " + e.what());
+      }
+    }
+  return q;
+}
+static std::vector<NSR> jnsr(const Value* v) {
+  std::vector<NSR> out;
+  if (!v) return out;
+  for (auto& e : v->arr()) {
+    NSR n;
+    n.key = jstr(&e, "key");
+    n.op = jstr(&e, "operator");
+    if (auto* vs = e.get("values")) for (auto& x : vs->arr()) n.values.push_back(x.str());
+    out.push_back(n);
+  }
+  return out;
+}
+static std::vector<TaintH> jtaints(const Value* v) {
+  std::vector<TaintH> out;
+  if (!v) return out;
+  for (auto& e : v->arr()) out.push_back(TaintH{jstr(&e, "key"), jstr(&e, "value"), jstr(&e, "effect")});
+  return out;
+}
+static int64_t jtime(const std::string& s) {
+  if (s.size() < 19) return 0;
+  int Y = atoi(s.substr(0, 4).c_str()), M = atoi(s.substr(5, 2).c_str()), D = atoi(s.substr(8, 2).c_str());
+  int h = atoi(s.substr(11, 2).c_str()), mi = atoi(s.substr(14, 2).c_str()), se = atoi(s.substr(17, 2).c_str());
+  int y = Y - (M <= 2);
+  int era = (y >= 0 ? y : y - 399) / 400;
+  int yoe = y - era * 400;
+  int doy = (153 * (M + (M > 2 ? -3 : 9)) + 2) / 5 + D - 1;
+  int doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return ((int64_t)era * 146097 + doe - 719468) * 86400 + h * 3600 + mi * 60 + se;
+}
+
+static void mergeInto(QList& dst, const QList& src) {
+  for (auto& kv : src) dst[kv.first].add(kv.second);
+}
+
+// Ceiling(pod).Requests + pods (resources.go:27-35,99-115,124-147)
+static QList podRequests(const Value& pod, bool& hostPorts, bool& volumes) {
+  QList req;
+  const Value* sp = pod.get("spec");
+  auto limitsIntoRequests = [](const Value& c) {
+    QList r, l;
+    if (auto* res = c.get("resources")) {
+      r = jqlist(res->get("requests"));
+      l = jqlist(res->get("limits"));
+    }
+    for (auto& kv : l) if (!r.count(kv.first)) r[kv.first] = kv.second;
+    return r;
+  };
+  if (sp) {
+    if (auto* cs = sp->get("containers"))
+      for (auto& c : cs->arr()) {
+        mergeInto(req, limitsIntoRequests(c));
+        if (auto* ps = c.get("ports"))
+          for (auto& p : ps->arr())
+            if (p.get("hostPort") && p.get("hostPort")->i64() != 0) hostPorts = true;
+      }
+    if (auto* cs = sp->get("initContainers"))
+      for (auto& c : cs->arr()) {
+        QList m = limitsIntoRequests(c);
+        QList out = req;  // MaxResources(req, m): keep the earlier quantity unless strictly greater
+        for (auto& kv : m) {
+          auto it = out.find(kv.first);
+          if (it == out.end() || kv.second.n > it->second.n) out[kv.first] = kv.second;
+        }
+        req = out;
+      }
+    if (auto* oh = sp->get("overhead"); oh && !oh->is_null()) mergeInto(req, jqlist(oh));
+    if (auto* vs = sp->get("volumes"))
+      for (auto& v : vs->arr())
+        if (v.get("persistentVolumeClaim") || v.get("ephemeral")) volumes = true;
+  }
+  Qty one;
+  one.n = 1000000000;
+  one.f = QFmt::DecExp;
+  req["pods"] = one;  // NewQuantity(1, DecimalExponent)
+  return req;
+}
+
+static PodH parsePod(const Value& v) {
+  PodH p;
+  const Value* md = v.get("metadata");
+  p.name = jstr(md, "name");
+  p.ns = jstr(md, "namespace");
+  p.uid = jstr(md, "uid");
+  p.created = jtime(jstr(md, "creationTimestamp"));
+  if (md) p.labels = jmap(md->get("labels"));
+  const Value* sp = v.get("spec");
+  if (sp) {
+    p.nodeSelector = jmap(sp->get("nodeSelector"));
+    if (auto* af = sp->get("affinity"); af && !af->is_null()) {
+      p.hasAffinity = true;
+      if (auto* na = af->get("nodeAffinity"); na && !na->is_null()) {
+        p.hasNodeAffinity = true;
+        if (auto* rq = na->get("requiredDuringSchedulingIgnoredDuringExecution"); rq && !rq->is_null()) {
+          p.hasRequired = true;
+          if (auto* ts = rq->get("nodeSelectorTerms"))
+            for (auto& t : ts->arr()) p.requiredTerms.push_back(jnsr(t.get("matchExpressions")));
+        }
+        if (auto* pr = na->get("preferredDuringSchedulingIgnoredDuringExecution"))
+          for (auto& t : pr->arr())
+            p.preferred.push_back(PrefTerm{(int32_t)(t.get("weight") ? t.get("weight")->i64() : 0),
+                                           t.get("preference") ? jnsr(t.get("preference")->get("matchExpressions"))
+                                                               : std::vector<NSR>{}});
+      }
+      for (int anti = 0; anti < 2; anti++) {
+        auto* pa = af->get(anti ? "podAntiAffinity" : "podAffinity");
+        if (!pa || pa->is_null()) continue;
+        (anti ? p.hasPodAnti : p.hasPodAffinity) = true;
+        if (auto* r = pa->get("preferredDuringSchedulingIgnoredDuringExecution"))
+          for (auto& t : r->arr())
+            (anti ? p.podAntiPrefW : p.podAffPrefW).push_back((int32_t)(t.get("weight") ? t.get("weight")->i64() : 0));
+      }
+    }
+    if (auto* ts = sp->get("tolerations"))
+      for (auto& t : ts->arr()) p.tols.push_back(TolH{jstr(&t, "key"), jstr(&t, "operator"), jstr(&t, "value"), jstr(&t, "effect")});
+    if (auto* ts = sp->get("topologySpreadConstraints"))
+      for (auto& t : ts->arr()) p.tscWhen.push_back(jstr(&t, "whenUnsatisfiable"));
+  }
+  p.requests = podRequests(v, p.hostPorts, p.volumes);
+  return p;
+}
+
+static bool toleratesTaint(const TolH& t, const TaintH& x) {  // v1.Toleration.ToleratesTaint
+  if (!t.effect.empty() && t.effect != x.effect) return false;
+  if (!t.key.empty() && t.key != x.key) return false;
+  if (t.op.empty() || t.op == "Equal") return t.value == x.value;
+  return t.op == "Exists";
+}
+static bool tolerates(const std::vector<TaintH>& taints, const std::vector<TolH>& tols) {
+  for (auto& x : taints) {
+    bool ok = false;
+    for (auto& t : tols) ok = ok || toleratesTaint(t, x);
+    if (!ok) return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Universe
+// ---------------------------------------------------------------------------------------------
+void Host::internKey(const std::string& key) {
+  if (!keyId.count(key)) { keyId[key] = -1; }
+}
+void Host::intern(const std::string& key, const std::string& val) {
+  internKey(key);
+  valueSet_[key].insert(val);
+}
+
+void Host::addNSR(std::vector<uint32_t>& rec, const std::string& key0, const std::string& op,
+                  const std::vector<std::string>& vals) const {
+  std::string key = normalize_key(key0);
+  int k = keyId.at(key);
+  std::vector<uint32_t> one = emptyRec();
+  const KeyMeta& km = keys[k];
+  uint64_t bitk = 1ull << k;
+  wr64(one.data(), 0, bitk);
+  auto setv = [&](const std::string& v) {
+    int b = valueId[k].at(v);
+    one[L.HDR + km.off + (b >> 5)] |= 1u << (b & 31);
+  };
+  if (op == "In") {
+    for (auto& v : vals) setv(v);
+  } else if (op == "NotIn") {
+    wr64(one.data(), 2, bitk);
+    for (auto& v : vals) setv(v);
+  } else if (op == "Exists") {
+    wr64(one.data(), 2, bitk);
+  } else if (op == "DoesNotExist") {
+  } else if (op == "Gt" || op == "Lt") {
+    int64_t x = 0;
+    go_atoi(vals.empty() ? "" : vals[0], x);  // prevalidated in Go; errors -> 0
+    wr64(one.data(), 2, bitk);
+    if (op == "Gt") { wr64(one.data(), 4, bitk); rs_set_gt(one.data(), km.bslot, x); }
+    else { wr64(one.data(), 6, bitk); rs_set_lt(one.data(), km.bslot, x); }
+  } else {
+    throw KsError(-2, "unsupported node selector operator: " + op);
+  }
+  rs_add(L, rec.data(), one.data());
+}
+
+void Host::addLabels(std::vector<uint32_t>& rec, const std::map<std::string, std::string>& labels) const {
+  for (auto& kv : labels) addNSR(rec, kv.first, "In", {kv.second});
+}
+
+// newPodRequirements (requirements.go:64-100).  Sorting the preferred terms mutates the pod, as
+// the reference's sort.Slice does.
+std::vector<uint32_t> Host::podRequirements(PodH& p, bool all) const {
+  std::vector<uint32_t> r = emptyRec();
+  addLabels(r, p.nodeSelector);
+  if (!p.hasAffinity || !p.hasNodeAffinity) return r;
+  if (all && !p.preferred.empty()) {
+    int n = (int)p.preferred.size();
+    std::vector<int32_t> key(n), idx(n);
+    for (int i = 0; i < n; i++) { key[i] = -p.preferred[i].weight; idx[i] = i; }
+    GoSortExact s{GoSort{key.data(), idx.data()}};
+    s.run(n);
+    std::vector<PrefTerm> sorted(n);
+    for (int i = 0; i < n; i++) sorted[i] = p.preferred[idx[i]];
+    p.preferred = sorted;
+    for (auto& e : p.preferred[0].exprs) addNSR(r, e.key, e.op, e.values);
+  }
+  if (p.hasRequired && !p.requiredTerms.empty())
+    for (auto& e : p.requiredTerms[0]) addNSR(r, e.key, e.op, e.values);
+  return r;
+}
+
+uint64_t Host::tolMask(const std::vector<TolH>& tols, uint64_t out[2]) const {
+  out[0] = out[1] = 0;
+  for (size_t i = 0; i < taints.size(); i++) {
+    bool ok = false;
+    for (auto& t : tols) ok = ok || toleratesTaint(t, taints[i]);
+    if (ok) out[i >> 6] |= 1ull << (i & 63);
+  }
+  return out[0];
+}
+
+int64_t Host::toDev(int r, const Qty& q) const {
+  __int128 d = 1;
+  for (int i = 0; i < resShift[r]; i++) d *= 10;
+  return (int64_t)(q.n / d);
+}
+Qty Host::fromDev(int r, int64_t v) const {
+  __int128 d = 1;
+  for (int i = 0; i < resShift[r]; i++) d *= 10;
+  Qty q;
+  q.n = (__int128)v * d;
+  return q;
+}
+
+std::string Host::placeholder(int64_t id) const {
+  char b[64];
+  snprintf(b, sizeof b, "hostname-placeholder-%04lld", (long long)id);
+  return b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// build: the NewScheduler half of the boundary
+// ---------------------------------------------------------------------------------------------
+void Host::build(const Value& root) {
+  if (auto* t = root.get("topology"); t && !t->is_null())
+    throw KsError(-2, "topology groups (spread / pod affinity) are not encoded by this build; "
+                      "pass an empty topology like BenchmarkScheduling does");
+  if (auto* wk = root.get("wellKnownLabels")) for (auto& x : wk->arr()) wellKnown.insert(x.str());
+  else
+    wellKnown = {kNodePoolKey, kZone, "topology.kubernetes.io/region", "node.kubernetes.io/instance-type",
+                 "kubernetes.io/arch", "kubernetes.io/os", kCT, "node.kubernetes.io/windows-build"};
+  if (auto* hs = root.get("hostnameSeed")) hostnameSeed = hs->i64();
+
+  // --- instance types
+  if (auto* v = root.get("instanceTypes"))
+    for (auto& e : v->arr()) {
+      IT it;
+      it.name = jstr(&e, "name");
+      it.reqs = jnsr(e.get("requirements"));
+      it.capacity = jqlist(e.get("capacity"));
+      QList total;
+      if (auto* oh = e.get("overhead")) {
+        mergeInto(total, jqlist(oh->get("kubeReserved")));
+        mergeInto(total, jqlist(oh->get("systemReserved")));
+        mergeInto(total, jqlist(oh->get("evictionThreshold")));
+      }
+      it.alloc = it.capacity;  // Subtract keeps the lhs keys only
+      for (auto& kv : it.alloc) {
+        auto o = total.find(kv.first);
+        if (o != total.end()) {
+          if (kv.second.n == 0) kv.second.f = o->second.f;
+          kv.second.n -= o->second.n;
+        }
+      }
+      if (auto* os = e.get("offerings"))
+        for (auto& o : os->arr()) {
+          bool avail = o.get("available") ? o.get("available")->boolean(true) : true;
+          if (avail) it.offers.push_back({jstr(&o, "zone"), jstr(&o, "capacityType")});
+        }
+      its.push_back(std::move(it));
+    }
+  const Value* byPool = root.get("instanceTypesByNodePool");
+  // --- templates
+  if (auto* v = root.get("nodeClaimTemplates"))
+    for (auto& np : v->arr()) {
+      Tpl t;
+      t.pool = jstr(np.get("metadata"), "name");
+      const Value* tpl = np.get("spec") ? np.get("spec")->get("template") : nullptr;
+      if (tpl) {
+        if (auto* tm = tpl->get("metadata")) t.labels = jmap(tm->get("labels"));
+        if (auto* ts = tpl->get("spec")) {
+          t.reqs = jnsr(ts->get("requirements"));
+          t.taints = jtaints(ts->get("taints"));
+        }
+      }
+      t.labels[kNodePoolKey] = t.pool;
+      if (byPool && byPool->get(t.pool))
+        for (auto& x : byPool->get(t.pool)->arr()) {
+          int64_t i = x.i64();
+          if (i < 0 || i >= (int64_t)its.size()) throw KsError(-1, "instanceTypesByNodePool index out of range");
+          t.its.push_back((int)i);
+        }
+      tpls.push_back(std::move(t));
+    }
+  if ((int)tpls.size() > kMaxTpl) throw KsError(-3, "too many NodeClaimTemplates");
+  // --- node pools (limits, PreferNoSchedule taints)
+  if (auto* v = root.get("nodePools"))
+    for (auto& np : v->arr()) {
+      Pool p;
+      p.name = jstr(np.get("metadata"), "name");
+      const Value* spec = np.get("spec");
+      if (spec && spec->get("limits") && !spec->get("limits")->is_null()) p.remaining = jqlist(spec->get("limits"));
+      if (spec && spec->get("template") && spec->get("template")->get("spec"))
+        for (auto& t : jtaints(spec->get("template")->get("spec")->get("taints")))
+          if (t.effect == "PreferNoSchedule") toleratePreferNoSchedule = true;
+      pools.push_back(p);
+    }
+  // --- existing nodes
+  if (auto* v = root.get("stateNodes"))
+    for (auto& e : v->arr()) {
+      Node n;
+      n.name = jstr(&e, "name");
+      n.hostName = jstr(&e, "hostName", n.name);
+      n.labels = jmap(e.get("labels"));
+      n.taints = jtaints(e.get("taints"));
+      n.available = jqlist(e.get("available"));
+      n.capacity = jqlist(e.get("capacity"));
+      n.dsRequests = jqlist(e.get("daemonSetRequests"));
+      n.initialized = e.get("initialized") ? e.get("initialized")->boolean(true) : true;
+      n.origIndex = (int)nodes.size();
+      nodes.push_back(std::move(n));
+    }
+  std::stable_sort(nodes.begin(), nodes.end(), [](const Node& a, const Node& b) {  // scheduler.go:313-321
+    if (a.initialized != b.initialized) return a.initialized;
+    return a.name < b.name;
+  });
+  if (auto* v = root.get("daemonSetPods")) for (auto& e : v->arr()) daemons.push_back(parsePod(e));
+  if (auto* v = root.get("pods")) for (auto& e : v->arr()) pods.push_back(parsePod(e));
+  for (auto& p : pods) {
+    if (p.hostPorts) throw KsError(-2, "pod " + p.ns + "/" + p.name + " uses hostPorts (not encoded by this build)");
+    if (p.volumes) throw KsError(-2, "pod " + p.ns + "/" + p.name + " mounts PVC volumes (not encoded by this build)");
+  }
+
+  // --- universe of keys and values
+  internKey(kHostname);
+  internKey(kZone);
+  internKey(kCT);
+  std::set<std::string> bounded;
+  auto visitNSR = [&](const std::vector<NSR>& v) {
+    for (auto& n : v) {
+      std::string k = normalize_key(n.key);
+      internKey(k);
+      if (n.op == "In" || n.op == "NotIn") for (auto& x : n.values) intern(k, x);
+      if (n.op == "Gt" || n.op == "Lt") bounded.insert(k);
+    }
+  };
+  auto visitLabels = [&](const std::map<std::string, std::string>& m) {
+    for (auto& kv : m) intern(normalize_key(kv.first), kv.second);
+  };
+  auto visitPod = [&](const PodH& p) {
+    visitLabels(p.nodeSelector);
+    for (auto& t : p.requiredTerms) visitNSR(t);
+    for (auto& t : p.preferred) visitNSR(t.exprs);
+  };
+  for (auto& it : its) {
+    visitNSR(it.reqs);
+    for (auto& o : it.offers) { intern(kZone, o.first); intern(kCT, o.second); }
+  }
+  for (auto& t : tpls) { visitNSR(t.reqs); visitLabels(t.labels); }
+  for (auto& n : nodes) { visitLabels(n.labels); intern(kHostname, n.hostName); }
+  for (auto& p : pods) visitPod(p);
+  for (auto& p : daemons) visitPod(p);
+  for (auto& kv : valueSet_[kHostname])
+    if (kv.rfind("hostname-placeholder-", 0) == 0)
+      throw KsError(-2, "input names a hostname-placeholder value (reserved for new NodeClaims)");
+
+  if (keyId.size() > 64) throw KsError(-3, "more than 64 distinct label keys");
+  int k = 0, off = 0, nb = 0, vint = 0;
+  for (auto& kv : keyId) {  // std::map: keys sorted by name -> id order == Go's sorted error order
+    kv.second = k++;
+    keyNames.push_back(kv.first);
+    auto& vs = valueSet_[kv.first];
+    values.emplace_back(vs.begin(), vs.end());
+    std::map<std::string, int> ids;
+    for (size_t i = 0; i < values.back().size(); i++) ids[values.back()[i]] = (int)i;
+    valueId.push_back(ids);
+    KeyMeta m{};
+    m.nv = (int)values.back().size() + (kv.first == kHostname ? 1 : 0);
+    m.nw = std::max(1, (m.nv + 31) / 32);
+    m.off = off;
+    off += m.nw;
+    m.bslot = bounded.count(kv.first) ? nb++ : -1;
+    m.vint = m.bslot >= 0 ? vint : -1;
+    if (m.bslot >= 0) vint += m.nv;
+    keys.push_back(m);
+  }
+  hostKey = keyId[kHostname];
+  zoneKey = keyId[kZone];
+  ctKey = keyId[kCT];
+  hostPrivBit = keys[hostKey].nv - 1;
+  int W = off;
+  wordValid.assign(W, 0);
+  vIsInt.assign(W, 0);
+  vInt.assign(std::max(vint, 1), 0);
+  for (size_t kk = 0; kk < keys.size(); kk++) {
+    const KeyMeta& m = keys[kk];
+    for (int b = 0; b < m.nv; b++) wordValid[m.off + b / 32] |= 1u << (b % 32);
+    if (m.bslot >= 0)
+      for (int b = 0; b < (int)values[kk].size(); b++) {
+        int64_t x;
+        if (go_atoi(values[kk][b], x)) {
+          vIsInt[m.off + b / 32] |= 1u << (b % 32);
+          vInt[m.vint + b] = x;
+        }
+      }
+  }
+  for (auto& w : wellKnown) {
+    auto it = keyId.find(w);
+    if (it != keyId.end()) allowWK |= 1ull << it->second;
+  }
+  dims.NK = (int)keys.size();
+  dims.W = W;
+  dims.NB = nb;
+  dims.HDR = 8 + 4 * nb;
+  dims.RSW = (dims.HDR + W + 1) & ~1;
+  L.nkeys = dims.NK;
+  L.W = W;
+  L.NB = nb;
+  L.HDR = dims.HDR;
+  L.RSW = dims.RSW;
+  L.keys = keys.data();
+  L.wordValid = wordValid.data();
+  L.vIsInt = vIsInt.data();
+  L.vInt = vInt.data();
+
+  // --- resources
+  std::map<std::string, std::vector<__int128>> seen;
+  auto visitQ = [&](const QList& q) { for (auto& kv : q) seen[kv.first].push_back(kv.second.n); };
+  for (auto& it : its) { visitQ(it.capacity); visitQ(it.alloc); }
+  for (auto& p : pods) visitQ(p.requests);
+  for (auto& p : daemons) visitQ(p.requests);
+  for (auto& n : nodes) { visitQ(n.available); visitQ(n.capacity); visitQ(n.dsRequests); }
+  for (auto& p : pools) visitQ(p.remaining);
+  if (seen.size() > (size_t)kMaxR) throw KsError(-3, "more than 16 resource names");
+  for (auto& kv : seen) {
+    int shift = 9;
+    for (__int128 x : kv.second) {
+      while (shift > 0) {
+        __int128 d = 1;
+        for (int i = 0; i < shift; i++) d *= 10;
+        if (x % d == 0) break;
+        shift--;
+      }
+    }
+    __int128 d = 1;
+    for (int i = 0; i < shift; i++) d *= 10;
+    for (__int128 x : kv.second) {
+      __int128 v = x / d;
+      if (v > ((__int128)1 << 52) || v < -((__int128)1 << 52))
+        throw KsError(-3, "quantity of " + kv.first + " exceeds the int64 fixed-point range");
+    }
+    resId[kv.first] = (int)resNames.size();
+    resNames.push_back(kv.first);
+    resShift.push_back(shift);
+  }
+  int R = (int)resNames.size();
+  dims.R = R;
+  auto vec = [&](const QList& q, int64_t* out) {
+    for (int r = 0; r < R; r++) out[r] = 0;
+    for (auto& kv : q) out[resId.at(kv.first)] = toDev(resId.at(kv.first), kv.second);
+  };
+
+  // --- taints universe
+  auto internTaint = [&](const TaintH& t) {
+    for (auto& x : taints) if (x.key == t.key && x.value == t.value && x.effect == t.effect) return;
+    taints.push_back(t);
+  };
+  for (auto& t : tpls) for (auto& x : t.taints) internTaint(x);
+  for (auto& n : nodes) for (auto& x : n.taints) internTaint(x);
+  if (taints.size() > 128) throw KsError(-3, "more than 128 distinct taints");
+  auto taintMask = [&](const std::vector<TaintH>& ts, uint64_t* out) {
+    out[0] = out[1] = 0;
+    for (auto& t : ts)
+      for (size_t i = 0; i < taints.size(); i++)
+        if (taints[i].key == t.key && taints[i].value == t.value && taints[i].effect == t.effect)
+          out[i >> 6] |= 1ull << (i & 63);
+  };
+
+  // --- instance types
+  int T = (int)its.size();
+  dims.T = T;
+  tab.it_alloc.assign((size_t)T * R, 0);
+  tab.it_cap.assign((size_t)T * R, 0);
+  tab.it_rs.assign((size_t)T * dims.RSW, 0);
+  tab.it_off_beg.assign(T + 1, 0);
+  for (int i = 0; i < T; i++) {
+    vec(its[i].alloc, &tab.it_alloc[(size_t)i * R]);
+    vec(its[i].capacity, &tab.it_cap[(size_t)i * R]);
+    std::vector<uint32_t> rs = emptyRec();
+    for (auto& n : its[i].reqs) addNSR(rs, n.key, n.op, n.values);
+    std::copy(rs.begin(), rs.end(), tab.it_rs.begin() + (size_t)i * dims.RSW);
+    itKeys |= rs_present(rs.data());
+    for (auto& o : its[i].offers) {
+      tab.off_zone.push_back(valueId[zoneKey].at(o.first));
+      tab.off_ct.push_back(valueId[ctKey].at(o.second));
+    }
+    tab.it_off_beg[i + 1] = (int)tab.off_zone.size();
+  }
+  itKeys |= (1ull << zoneKey) | (1ull << ctKey);
+  if (tab.off_zone.empty()) { tab.off_zone.push_back(0); tab.off_ct.push_back(0); }
+
+  // --- templates: requirements, daemon overhead (getDaemonOverhead scheduler.go:324-341)
+  int NT = (int)tpls.size();
+  dims.NTPL = NT;
+  tab.tpl_rs.assign((size_t)std::max(NT, 1) * dims.RSW, 0);
+  tab.tpl_taint.assign((size_t)std::max(NT, 1) * 2, 0);
+  tab.tpl_daemon.assign((size_t)std::max(NT, 1) * R, 0);
+  tab.tpl_it_beg.assign(NT + 1, 0);
+  tab.tpl_pool.assign(std::max(NT, 1), -1);
+  int maxIts = 0;
+  std::vector<std::vector<uint32_t>> daemonAll;
+  for (auto& d : daemons) {
+    PodH c = d;
+    daemonAll.push_back(podRequirements(c, true));
+  }
+  for (int t = 0; t < NT; t++) {
+    Tpl& tp = tpls[t];
+    tp.rs = emptyRec();
+    for (auto& n : tp.reqs) addNSR(tp.rs, n.key, n.op, n.values);
+    addLabels(tp.rs, tp.labels);
+    std::vector<uint32_t> withHost = tp.rs;
+    {
+      std::vector<uint32_t> h = emptyRec();
+      const KeyMeta& hm = keys[hostKey];
+      wr64(h.data(), 0, 1ull << hostKey);
+      h[L.HDR + hm.off + (hostPrivBit >> 5)] |= 1u << (hostPrivBit & 31);
+      rs_add(L, withHost.data(), h.data());
+    }
+    std::copy(withHost.begin(), withHost.end(), tab.tpl_rs.begin() + (size_t)t * dims.RSW);
+    taintMask(tp.taints, &tab.tpl_taint[(size_t)t * 2]);
+    QList overhead;
+    int nd = 0;
+    for (size_t i = 0; i < daemons.size(); i++) {
+      if (!tolerates(tp.taints, daemons[i].tols)) continue;
+      if (!rs_compatible(L, tp.rs.data(), daemonAll[i].data(), allowWK)) continue;
+      QList r = daemons[i].requests;
+      r.erase("pods");
+      mergeInto(overhead, r);
+      nd++;
+    }
+    Qty pods;
+    pods.n = (__int128)nd * 1000000000;
+    pods.f = QFmt::DecExp;
+    overhead["pods"] = pods;
+    tp.daemon = overhead;
+    if (!resId.count("pods")) throw KsError(-5, "pods resource missing");
+    vec(overhead, &tab.tpl_daemon[(size_t)t * R]);
+    for (int i : tp.its) tab.tpl_its.push_back(i);
+    tab.tpl_it_beg[t + 1] = (int)tab.tpl_its.size();
+    maxIts = std::max(maxIts, (int)tp.its.size());
+    for (size_t p = 0; p < pools.size(); p++)
+      if (pools[p].name == tp.pool) tab.tpl_pool[t] = (int)p;
+  }
+  if (tab.tpl_its.empty()) tab.tpl_its.push_back(0);
+  dims.maxTplIts = maxIts;
+  dims.TW = std::max(1, (maxIts + 31) / 32);
+
+  // --- existing nodes (NewExistingNode, calculateExistingNodeClaims)
+  int N = (int)nodes.size();
+  dims.N = N;
+  tab.n_avail.assign((size_t)std::max(N, 1) * R, 0);
+  tab.n_req0.assign((size_t)std::max(N, 1) * R, 0);
+  tab.n_rs0.assign((size_t)std::max(N, 1) * dims.RSW, 0);
+  tab.n_taint.assign((size_t)std::max(N, 1) * 2, 0);
+  for (int i = 0; i < N; i++) {
+    Node& n = nodes[i];
+    std::vector<uint32_t> lab = emptyRec();
+    addLabels(lab, n.labels);
+    QList dreq;
+    int nd = 0;
+    for (size_t d = 0; d < daemons.size(); d++) {
+      if (!tolerates(n.taints, daemons[d].tols)) continue;
+      if (!rs_compatible(L, lab.data(), daemonAll[d].data(), 0)) continue;
+      QList r = daemons[d].requests;
+      r.erase("pods");
+      mergeInto(dreq, r);
+      nd++;
+    }
+    Qty pq;
+    pq.n = (__int128)nd * 1000000000;
+    pq.f = QFmt::DecExp;
+    dreq["pods"] = pq;
+    n.req0 = dreq;  // Subtract(daemon, DaemonSetRequests) keeps lhs keys; negatives clamp to 0
+    for (auto& kv : n.req0) {
+      auto s = n.dsRequests.find(kv.first);
+      if (s != n.dsRequests.end()) {
+        if (kv.second.n == 0) kv.second.f = s->second.f;
+        kv.second.n -= s->second.n;
+      }
+      if (kv.second.n < 0) kv.second.n = 0;
+    }
+    vec(n.available, &tab.n_avail[(size_t)i * R]);
+    vec(n.req0, &tab.n_req0[(size_t)i * R]);
+    addNSR(lab, kHostname, "In", {n.hostName});
+    std::copy(lab.begin(), lab.end(), tab.n_rs0.begin() + (size_t)i * dims.RSW);
+    taintMask(n.taints, &tab.n_taint[(size_t)i * 2]);
+  }
+  // --- limits: remaining = Limits - capacity of existing nodes in the pool
+  int NP = (int)pools.size();
+  dims.NPOOL = NP;
+  tab.pool_rem0.assign((size_t)std::max(NP, 1) * R, 0);
+  tab.pool_mask.assign(std::max(NP, 1), 0);
+  for (int p = 0; p < NP; p++) {
+    QList rem = pools[p].remaining;
+    for (auto& n : nodes) {
+      auto l = n.labels.find(kNodePoolKey);
+      if (l == n.labels.end() || l->second != pools[p].name) continue;
+      for (auto& kv : rem) {
+        auto c = n.capacity.find(kv.first);
+        if (c != n.capacity.end()) {
+          if (kv.second.n == 0) kv.second.f = c->second.f;
+          kv.second.n -= c->second.n;
+        }
+      }
+    }
+    pools[p].remaining = rem;
+    for (auto& kv : rem) {
+      auto it = resId.find(kv.first);
+      if (it == resId.end()) continue;
+      tab.pool_mask[p] |= 1u << it->second;
+      tab.pool_rem0[(size_t)p * R + it->second] = toDev(it->second, kv.second);
+    }
+  }
+
+  // --- pods: requests, queue sort keys, relaxation chains
+  int P = (int)pods.size();
+  dims.P = P;
+  tab.pod_req.assign((size_t)std::max(P, 1) * R, 0);
+  tab.pod_sortkey.assign((size_t)std::max(P, 1) * 4, 0);
+  tab.pod_state0.assign(std::max(P, 1), 0);
+  tab.pod_nstate.assign(std::max(P, 1), 0);
+  tab.pod_uid.assign(std::max(P, 1), 0);
+  std::map<std::string, int> uids;
+  for (auto& p : pods) uids[p.uid] = 0;
+  int u = 0;
+  for (auto& kv : uids) kv.second = u++;  // id == rank in Go string order
+  dims.NU = std::max(u, 1);
+  int cpuR = resId.count("cpu") ? resId["cpu"] : -1, memR = resId.count("memory") ? resId["memory"] : -1;
+  std::vector<std::array<int64_t, 4>> sk(P);
+  int S = 0;
+  for (int i = 0; i < P; i++) {
+    PodH& p = pods[i];
+    vec(p.requests, &tab.pod_req[(size_t)i * R]);
+    int64_t cpu = cpuR >= 0 ? tab.pod_req[(size_t)i * R + cpuR] : 0;
+    int64_t mem = memR >= 0 ? tab.pod_req[(size_t)i * R + memR] : 0;
+    int64_t* k4 = &tab.pod_sortkey[(size_t)i * 4];
+    k4[0] = -cpu;  // descending
+    k4[1] = -mem;
+    k4[2] = p.created;
+    k4[3] = uids[p.uid];
+    sk[i] = {k4[0], k4[1], k4[2], k4[3]};
+    tab.pod_uid[i] = uids[p.uid];
+    // relaxation chain
+    PodH cur = p;
+    std::vector<PodState> chain;
+    for (int guard = 0; guard < 256; guard++) {
+      PodState st;
+      st.rsAll = podRequirements(cur, true);
+      st.rsStrict = podRequirements(cur, false);
+      st.hasPreferred = cur.hasAffinity && cur.hasNodeAffinity && !cur.preferred.empty();
+      st.tols = cur.tols;
+      chain.push_back(std::move(st));
+      // Preferences.Relax (preferences.go:38-58)
+      bool relaxed = false;
+      if (cur.hasAffinity && cur.hasNodeAffinity && cur.hasRequired && cur.requiredTerms.size() > 1) {
+        cur.requiredTerms.erase(cur.requiredTerms.begin());
+        relaxed = true;
+      } else if (cur.hasAffinity && cur.hasPodAffinity && !cur.podAffPrefW.empty()) {
+        std::stable_sort(cur.podAffPrefW.begin(), cur.podAffPrefW.end(), std::greater<int32_t>());
+        cur.podAffPrefW.erase(cur.podAffPrefW.begin());
+        relaxed = true;
+      } else if (cur.hasAffinity && cur.hasPodAnti && !cur.podAntiPrefW.empty()) {
+        std::stable_sort(cur.podAntiPrefW.begin(), cur.podAntiPrefW.end(), std::greater<int32_t>());
+        cur.podAntiPrefW.erase(cur.podAntiPrefW.begin());
+        relaxed = true;
+      } else if (cur.hasAffinity && cur.hasNodeAffinity && !cur.preferred.empty()) {
+        std::stable_sort(cur.preferred.begin(), cur.preferred.end(),
+                         [](const PrefTerm& a, const PrefTerm& b) { return a.weight > b.weight; });
+        cur.preferred.erase(cur.preferred.begin());
+        relaxed = true;
+      } else {
+        for (size_t j = 0; j < cur.tscWhen.size(); j++)
+          if (cur.tscWhen[j] == "ScheduleAnyway") {
+            cur.tscWhen[j] = cur.tscWhen.back();
+            cur.tscWhen.pop_back();
+            relaxed = true;
+            break;
+          }
+        if (!relaxed && toleratePreferNoSchedule) {
+          bool have = false;
+          for (auto& t : cur.tols)
+            if (t.key.empty() && t.op == "Exists" && t.value.empty() && t.effect == "PreferNoSchedule") have = true;
+          if (!have) {
+            cur.tols.push_back(TolH{"", "Exists", "", "PreferNoSchedule"});
+            relaxed = true;
+          }
+        }
+      }
+      if (!relaxed) break;
+    }
+    tab.pod_state0[i] = S;
+    tab.pod_nstate[i] = (int)chain.size();
+    S += (int)chain.size();
+    states.push_back(std::move(chain));
+  }
+  {
+    std::vector<int> idx(P);
+    for (int i = 0; i < P; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](int a, int b) { return sk[a] < sk[b]; });
+    for (int i = 1; i < P; i++)
+      if (sk[idx[i]] == sk[idx[i - 1]])
+        throw KsError(-2, "pods " + pods[idx[i - 1]].name + " and " + pods[idx[i]].name +
+                              " tie on (cpu, memory, creationTimestamp, uid); queue order would depend on sort.Slice tie order");
+  }
+  dims.S = std::max(S, 1);
+  tab.st_rs.assign((size_t)dims.S * dims.RSW, 0);
+  tab.st_tol.assign((size_t)dims.S * 2, 0);
+  tab.st_flags.assign(dims.S, 0);
+  int s = 0;
+  for (auto& chain : states)
+    for (auto& st : chain) {
+      std::copy(st.rsAll.begin(), st.rsAll.end(), tab.st_rs.begin() + (size_t)s * dims.RSW);
+      uint64_t m[2];
+      tolMask(st.tols, m);
+      tab.st_tol[(size_t)s * 2] = m[0];
+      tab.st_tol[(size_t)s * 2 + 1] = m[1];
+      uint64_t pres = rs_present(st.rsAll.data());
+      tab.st_flags[s] = (st.hasPreferred ? SF_HAS_PREFERRED : 0) | ((pres & itKeys) ? SF_TOUCHES_IT_KEYS : 0) |
+                        (pres ? SF_HAS_KEYS : 0);
+      s++;
+    }
+  dims.zoneKey = zoneKey;
+  dims.ctKey = ctKey;
+  dims.hostKey = hostKey;
+  dims.allowWK = allowWK;
+  dims.itKeys = itKeys;
+  dims.hostnameSeed = (int32_t)hostnameSeed;
+  dims.Kcap = std::max(1, std::min(P, 16384));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Renderers
+// ---------------------------------------------------------------------------------------------
+std::string Host::reqString(const uint32_t* rec, int k, bool full, int64_t privateHost) const {
+  int op = rs_op(L, rec, k);
+  static const char* opn[] = {"In", "NotIn", "Exists", "DoesNotExist"};
+  std::string s = keyNames[k] + " " + opn[op];
+  if (op == OP_IN || op == OP_NOTIN) {
+    std::vector<std::string> vs;
+    const KeyMeta& km = keys[k];
+    for (int b = 0; b < km.nv; b++)
+      if ((rec[L.HDR + km.off + (b >> 5)] >> (b & 31)) & 1u)
+        vs.push_back(k == hostKey && b == hostPrivBit ? placeholder(privateHost) : values[k][b]);
+    std::sort(vs.begin(), vs.end());
+    if (!full && vs.size() > 5) {
+      size_t n = vs.size();
+      vs.resize(5);
+      vs.push_back("and " + std::to_string(n - 5) + " others");
+    }
+    s += " [";
+    for (size_t i = 0; i < vs.size(); i++) { if (i) s += " "; s += vs[i]; }
+    s += "]";
+  }
+  const KeyMeta& km = keys[k];
+  if (km.bslot >= 0) {
+    if (bit(rs_hasgt(rec), k)) s += " >" + std::to_string(rs_gt(rec, km.bslot));
+    if (bit(rs_haslt(rec), k)) s += " <" + std::to_string(rs_lt(rec, km.bslot));
+  }
+  return s;
+}
+
+std::string Host::reqsString(const uint32_t* rec, int64_t privateHost) const {
+  std::vector<std::string> parts;
+  uint64_t pr = rs_present(rec);
+  for (int k = 0; k < dims.NK; k++)
+    if (bit(pr, k) && k != hostKey) parts.push_back(reqString(rec, k, false, privateHost));
+  std::sort(parts.begin(), parts.end());
+  std::string s;
+  for (size_t i = 0; i < parts.size(); i++) { if (i) s += ", "; s += parts[i]; }
+  return s;
+}
+
+static int editDistance(const std::string& s, const std::string& t) {  // requirements.go:177-210
+  int m = (int)s.size(), n = (int)t.size();
+  if (m == 0) return n;
+  if (n == 0) return m;
+  std::vector<int> prev(n, 0), cur(n, 0);
+  for (int j = 1; j < n; j++) prev[j] = j;
+  for (int i = 1; i < m; i++) {
+    for (int j = 1; j < n; j++)
+      cur[j] = std::min(std::min(prev[j] + 1, cur[j - 1] + 1), prev[j - 1] + (s[i] != t[j] ? 1 : 0));
+    std::swap(prev, cur);
+  }
+  return prev[n - 1];
+}
+
+std::vector<std::string> Host::compatErrors(const uint32_t* r, const uint32_t* in, bool loose,
+                                            int64_t privateHost) const {
+  std::vector<std::string> out;
+  uint64_t uf = 0, xf = 0;
+  rs_compatible(L, r, in, loose ? allowWK : 0, &uf, &xf);
+  auto hint = [&](const std::string& key) -> std::string {  // labelHint requirements.go:220-238
+    auto suffix = [](const std::string& k) {
+      auto p = k.find('/');
+      return p == std::string::npos ? k : k.substr(p + 1);
+    };
+    auto endsWith = [](const std::string& a, const std::string& b) {
+      return a.size() >= b.size() && a.compare(a.size() - b.size(), b.size(), b) == 0;
+    };
+    std::vector<std::string> cands;
+    if (loose) cands.assign(wellKnown.begin(), wellKnown.end());
+    for (const auto& c : cands)
+      if (c.find(key) != std::string::npos || editDistance(key, c) < (int)c.size() / 5 || endsWith(c, suffix(key)))
+        return " (typo of " + go_quote(c) + "?)";
+    uint64_t pr = rs_present(r);
+    for (int k = 0; k < dims.NK; k++) {
+      if (!bit(pr, k)) continue;
+      const std::string& c = keyNames[k];
+      if (c.find(key) != std::string::npos || editDistance(key, c) < (int)c.size() / 5 || endsWith(c, suffix(key)))
+        return " (typo of " + go_quote(c) + "?)";
+    }
+    return "";
+  };
+  for (int k = 0; k < dims.NK; k++)
+    if (bit(uf, k)) out.push_back("label " + go_quote(keyNames[k]) + " does not have known values" + hint(keyNames[k]));
+  for (int k = 0; k < dims.NK; k++)
+    if (bit(xf, k))
+      out.push_back("key " + keyNames[k] + ", " + reqString(in, k, false, privateHost) + " not in " +
+                    reqString(r, k, false, privateHost));
+  return out;
+}
+
+}  // namespace ks

@@ -1,0 +1,137 @@
+// ks_host.h — host-side problem model, encoder and renderer (declarations).
+#pragma once
+#include <array>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "ks_json.h"
+#include "ks_problem.h"
+#include "ks_quantity.h"
+#include "ks_reqset.h"
+
+namespace ks {
+
+struct KsError : std::runtime_error {
+  int code;
+  KsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+using QList = std::map<std::string, Qty>;  // v1.ResourceList
+struct NSR { std::string key, op; std::vector<std::string> values; };
+struct TaintH { std::string key, value, effect; };
+struct TolH { std::string key, op, value, effect; };
+struct PrefTerm { int32_t weight; std::vector<NSR> exprs; };
+
+// The pod fields the Solve path reads (pod spec subset; pkg/utils/pod, requirements.go:64-100,
+// preferences.go, resources.go Ceiling).
+struct PodH {
+  std::string name, ns, uid;
+  int64_t created = 0;
+  std::map<std::string, std::string> labels, nodeSelector;
+  bool hasAffinity = false, hasNodeAffinity = false, hasRequired = false;
+  std::vector<std::vector<NSR>> requiredTerms;
+  std::vector<PrefTerm> preferred;
+  bool hasPodAffinity = false, hasPodAnti = false;
+  std::vector<int32_t> podAffPrefW, podAntiPrefW;
+  std::vector<std::string> tscWhen;
+  std::vector<TolH> tols;
+  QList requests;  // RequestsForPods(pod) incl. pods=1
+  bool hostPorts = false, volumes = false;
+  bool provisionable = true;
+};
+
+struct PodState {  // one point of the relaxation chain
+  std::vector<uint32_t> rsAll, rsStrict;
+  bool hasPreferred = false;
+  std::vector<TolH> tols;
+};
+
+struct Host {
+  // universe
+  std::vector<std::string> keyNames;             // sorted; id = index
+  std::map<std::string, int> keyId;
+  std::vector<std::vector<std::string>> values;  // per key, sorted
+  std::vector<std::map<std::string, int>> valueId;
+  std::vector<KeyMeta> keys;
+  std::vector<uint32_t> wordValid, vIsInt;
+  std::vector<int64_t> vInt;
+  ReqLayout L{};
+  int hostKey = -1, zoneKey = -1, ctKey = -1, hostPrivBit = -1;
+  uint64_t allowWK = 0, itKeys = 0;
+  std::set<std::string> wellKnown;
+  // resources
+  std::vector<std::string> resNames;
+  std::map<std::string, int> resId;
+  std::vector<int> resShift;  // device value = nano / 10^shift
+  // taints
+  std::vector<TaintH> taints;
+  // instance types
+  struct IT { std::string name; std::vector<NSR> reqs; QList capacity, alloc; std::vector<std::pair<std::string, std::string>> offers; };
+  std::vector<IT> its;
+  // templates
+  struct Tpl {
+    std::string pool;
+    std::vector<NSR> reqs;
+    std::map<std::string, std::string> labels;
+    std::vector<TaintH> taints;
+    std::vector<int> its;
+    QList daemon;
+    int limitPool = -1;
+    std::vector<uint32_t> rs;  // without hostname
+  };
+  std::vector<Tpl> tpls;
+  struct Pool { std::string name; QList remaining; };
+  std::vector<Pool> pools;
+  bool toleratePreferNoSchedule = false;
+  // existing nodes (sorted)
+  struct Node { std::string name, hostName; std::map<std::string, std::string> labels; std::vector<TaintH> taints;
+                QList available, capacity, dsRequests, req0; bool initialized = true; int origIndex = 0; };
+  std::vector<Node> nodes;
+  std::vector<PodH> daemons;
+  std::vector<PodH> pods;
+  std::vector<std::vector<PodState>> states;  // per pod relaxation chain
+  int64_t hostnameSeed = 0;
+  KsDims dims{};
+
+  // host images of the device tables
+  struct Tables {
+    std::vector<int64_t> it_alloc, it_cap, tpl_daemon, pool_rem0, pod_req, pod_sortkey, n_avail, n_req0;
+    std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask;
+    std::vector<uint64_t> tpl_taint, st_tol, n_taint;
+    std::vector<int32_t> it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,
+        st_flags;
+  } tab;
+
+  void build(const ksjson::Value& root);
+
+  // encoded algebra helpers
+  std::vector<uint32_t> emptyRec() const { return std::vector<uint32_t>(dims.RSW, 0); }
+  void addNSR(std::vector<uint32_t>& rec, const std::string& key, const std::string& op,
+              const std::vector<std::string>& vals) const;
+  void addLabels(std::vector<uint32_t>& rec, const std::map<std::string, std::string>& labels) const;
+  std::vector<uint32_t> podRequirements(PodH& p, bool all) const;
+  uint64_t tolMask(const std::vector<TolH>& tols, uint64_t out[2]) const;
+  int64_t toDev(int r, const Qty& q) const;
+  Qty fromDev(int r, int64_t v) const;
+
+  // rendering
+  std::string reqString(const uint32_t* rec, int k, bool full, int64_t privateHost) const;
+  std::string reqsString(const uint32_t* rec, int64_t privateHost) const;  // Requirements.String()
+  std::vector<std::string> compatErrors(const uint32_t* r, const uint32_t* in, bool loose, int64_t privateHost) const;
+  std::string placeholder(int64_t id) const;
+
+ private:
+  void intern(const std::string& key, const std::string& val);
+  void internKey(const std::string& key);
+  std::map<std::string, std::set<std::string>> valueSet_;
+};
+
+std::string qlist_json(const QList& l);  // resources.String (pretty.Concise)
+std::string go_quote(const std::string& s);
+std::string normalize_key(const std::string& k);
+
+}  // namespace ks

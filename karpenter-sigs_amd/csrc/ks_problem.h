@@ -1,0 +1,118 @@
+// ks_problem.h — HBM layout of an encoded scheduling problem and of the per-solve workspace.
+//
+// Everything the reference's Scheduler reads during Solve (scheduler.go:140-285) is flattened into
+// structure-of-arrays tables: int64 fixed-point resource vectors (one decimal scale per resource
+// name, chosen so every quantity in the problem is an exact integer), ReqSet records
+// (ks_reqset.h), taint bitmasks and CSR instance-type lists.  The tables are written once by
+// ks_problem_create and stay resident; each ks_solve gets a fresh workspace.
+#pragma once
+#include <stdint.h>
+
+#include "ks_reqset.h"
+
+namespace ks {
+
+constexpr int kMaxR = 16;         // resource names per problem
+constexpr int kMaxTpl = 32;       // NodeClaimTemplates (NodePools) per problem
+constexpr int kWave = 64;
+
+enum PodStatus : int32_t { ST_PENDING = 0, ST_SCHEDULED = 1, ST_FAILED = 2 };
+enum FailCode : uint32_t {
+  FC_NONE = 0,
+  FC_LIMITS = 1,    // all available instance types exceed limits for nodepool
+  FC_TAINTS = 2,    // Taints.Tolerates failed
+  FC_HOSTPORT = 3,  // checking host port usage
+  FC_COMPAT = 4,    // incompatible requirements
+  FC_NO_IT = 5,     // no instance type satisfied resources ... (flags in bits 8..13)
+};
+enum FilterFlag : uint32_t {  // filterResults booleans (nodeclaim.go:144-160)
+  FF_REQ = 1, FF_FITS = 2, FF_OFF = 4, FF_REQ_FITS = 8, FF_REQ_OFF = 16, FF_FITS_OFF = 32,
+};
+enum StateFlag : int32_t { SF_HAS_PREFERRED = 1, SF_TOUCHES_IT_KEYS = 2, SF_HAS_KEYS = 4 };
+
+struct KsDims {
+  int32_t R, NK, W, NB, HDR, RSW;
+  int32_t T, NTPL, NPOOL, N, P, S, NU;
+  int32_t TW;          // words of the largest template instance-type bitset
+  int32_t maxTplIts;   // longest template instance-type list
+  int32_t zoneKey, ctKey, hostKey;
+  int32_t Kcap;        // claim capacity per solve
+  int32_t hostnameSeed;
+  uint64_t allowWK;    // WellKnownLabels key mask (AllowUndefinedWellKnownLabels)
+  uint64_t itKeys;     // keys any instance type constrains, plus zone and capacity-type
+};
+
+// Device view (all pointers into one HBM allocation).
+struct KsDev {
+  KsDims d;
+  const KeyMeta* keys;
+  const uint32_t* wordValid;
+  const uint32_t* vIsInt;
+  const int64_t* vInt;
+  // instance types
+  const int64_t* it_alloc;    // [T][R]  Allocatable() = Capacity - Overhead (types.go:100-110)
+  const int64_t* it_cap;      // [T][R]
+  const uint32_t* it_rs;      // [T][RSW]
+  const int32_t* it_off_beg;  // [T+1] available offerings
+  const int32_t* off_zone;    // zone value bit
+  const int32_t* off_ct;      // capacity-type value bit
+  // templates (NodeClaimTemplates in caller order)
+  const uint32_t* tpl_rs;     // [NTPL][RSW] template requirements + hostname (private bit)
+  const uint64_t* tpl_taint;  // [NTPL][2]
+  const int64_t* tpl_daemon;  // [NTPL][R] getDaemonOverhead (scheduler.go:324-341)
+  const int32_t* tpl_it_beg;  // [NTPL+1]
+  const int32_t* tpl_its;     // IT index per template position
+  const int32_t* tpl_pool;    // [NTPL] limit pool or -1
+  // NodePool limits (remainingResources, scheduler.go:76-78,306-308)
+  const int64_t* pool_rem0;   // [NPOOL][R]
+  const uint32_t* pool_mask;  // [NPOOL] resource names present in the remaining ResourceList
+  // pods
+  const int64_t* pod_req;     // [P][R] RequestsForPods(pod) (resources.go:27-35)
+  const int32_t* pod_state0;  // [P] first relaxation state
+  const int32_t* pod_nstate;  // [P]
+  const int32_t* pod_uid;     // [P] interned UID (queue staleness key, queue.go:54-69)
+  const int64_t* pod_sortkey; // [P][4] cpu, memory, creation second, uid rank (queue.go:83-112)
+  // relaxation states (preferences.go:38-147 applied 0..n times)
+  const uint32_t* st_rs;      // [S][RSW] NewPodRequirements
+  const uint64_t* st_tol;     // [S][2] tolerated-taint masks
+  const int32_t* st_flags;    // [S]
+  // existing nodes, in calculateExistingNodeClaims order (scheduler.go:313-321)
+  const int64_t* n_avail;     // [N][R] StateNode.Available()
+  const int64_t* n_req0;      // [N][R] remaining daemon requests (existingnode.go:43-52)
+  const uint32_t* n_rs0;      // [N][RSW] node labels + hostname
+  const uint64_t* n_taint;    // [N][2]
+};
+
+// Per-solve workspace (one slice per replica / simulation).
+struct KsWork {
+  int32_t* c_tpl;      // [Kcap]
+  int32_t* c_cnt;      // [Kcap]
+  int32_t* c_host;     // [Kcap] hostname-placeholder ordinal
+  int64_t* c_req;      // [Kcap][R]
+  int64_t* c_max;      // [Kcap][R] per-resource max Allocatable over the remaining options
+  uint32_t* c_rs;      // [Kcap][RSW]
+  uint32_t* c_rem;     // [Kcap][TW] InstanceTypeOptions as a bitset over the template list
+  int32_t* order;      // [Kcap] final s.newNodeClaims order
+  int64_t* n_req;      // [N][R]
+  uint32_t* n_rs;      // [N][RSW]
+  int32_t* queue;      // [P] ring
+  int32_t* qorder;     // [P] NewQueue order
+  int32_t* pod_state;  // [P] current relaxation state
+  uint64_t* last_len;  // [NU] (epoch << 32) | len
+  int32_t* log_pod;    // [P] commit log
+  int32_t* log_tgt;    // [P] >=0 claim id, <0 -(node+1)
+  int32_t* pod_status; // [P]
+  int32_t* pod_fstate; // [P] relaxation state of the final failed attempt
+  uint32_t* fail_code; // [P][NTPL]
+  int32_t* fail_host;  // [P][NTPL]
+  int64_t* pool_rem;   // [NPOOL][R]
+  int64_t* counters;   // [16]
+};
+
+enum Counter {
+  CT_NCLAIMS = 0, CT_NLOG, CT_HOSTCTR, CT_ERROR, CT_POPS, CT_ALGBYTES, CT_SORTS, CT_SORT_SLOW,
+  CT_CLAIM_FULL, CT_CLAIM_QUICK_FAIL, CT_NCOUNTERS = 16
+};
+enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3 };
+
+}  // namespace ks

@@ -1,0 +1,537 @@
+// ks_solve.hip — MI355X (gfx950) kernels for Scheduler.Solve.
+//
+// One Solve = one 64-lane wavefront (one workgroup).  The reference's Solve is a sequential commit
+// chain (scheduler.go:140-189: every placement depends on all earlier ones), so the chain stays in
+// one wave with wave-uniform control flow and no inter-wave synchronisation; the data-parallel
+// parts of each step map onto the 64 lanes:
+//   - existing-node first-fit (scheduler.go:240-244)   lane per node, ballot + ffs picks the first
+//   - in-flight NodeClaim scan (scheduler.go:250-254)  lane per sorted position: a quick reject
+//     (template taints, requests + pod <= max Allocatable of the remaining options, Compatible)
+//     then a wave-cooperative NodeClaim.Add on candidates in order (nodeclaim.go:65-119)
+//   - instance-type filter (nodeclaim.go:225-260)      lane per template IT position, ballots build
+//     the remaining-options bitset and the six filterResults flags in one pass
+//   - new NodeClaim per template (scheduler.go:258-283) incl. limits (filterByRemainingResources,
+//     subtractMax)
+// Independent Solves (replicas, consolidation simulations) are independent workgroups, so a launch
+// of thousands of them fills the 256 CUs.  Nothing here is a dense contraction: no MFMA.
+#include <hip/hip_runtime.h>
+
+#include "ks_gosort.h"
+#include "ks_problem.h"
+#include "ks_reqset.h"
+
+namespace ks {
+
+__device__ __forceinline__ int lane() { return (int)threadIdx.x; }
+__device__ __forceinline__ uint64_t wballot(bool p) { return __ballot(p ? 1 : 0); }
+__device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
+__device__ __forceinline__ void wsync() { __syncthreads(); }  // one-wave workgroup: LDS ordering point
+
+// ------------------------------------------------------------------------------------------------
+// Init: per-replica workspace state (copies of the resident initial state), one grid-stride pass.
+// ------------------------------------------------------------------------------------------------
+__global__ void k_init(KsDev D, const KsWork* works, int nrep) {
+  const KsDims d = D.d;
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gsz = (int64_t)gridDim.x * blockDim.x;
+  for (int r = 0; r < nrep; r++) {
+    const KsWork W = works[r];
+    for (int64_t i = gtid; i < (int64_t)d.N * d.R; i += gsz) W.n_req[i] = D.n_req0[i];
+    for (int64_t i = gtid; i < (int64_t)d.N * d.RSW; i += gsz) W.n_rs[i] = D.n_rs0[i];
+    for (int64_t i = gtid; i < d.P; i += gsz) {
+      W.pod_state[i] = D.pod_state0[i];
+      W.pod_status[i] = ST_PENDING;
+      W.pod_fstate[i] = -1;
+    }
+    for (int64_t i = gtid; i < d.NU; i += gsz) W.last_len[i] = 0;
+    for (int64_t i = gtid; i < (int64_t)d.NPOOL * d.R; i += gsz) W.pool_rem[i] = D.pool_rem0[i];
+    for (int64_t i = gtid; i < CT_NCOUNTERS; i += gsz) W.counters[i] = 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// NewQueue (queue.go:37-43): rank of each pod under byCPUAndMemoryDescending (cpu desc, memory desc,
+// creationTimestamp asc, uid asc; queue.go:83-112).  The host rejects exact ties, so the order is a
+// strict total order and any correct sort reproduces sort.Slice.  256-thread blocks stream the key
+// table through LDS.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool key_less(const int64_t* a, const int64_t* b) {
+  if (a[0] != b[0]) return a[0] < b[0];
+  if (a[1] != b[1]) return a[1] < b[1];
+  if (a[2] != b[2]) return a[2] < b[2];
+  return a[3] < b[3];
+}
+
+__global__ __launch_bounds__(256) void k_queue_rank(KsDev D, int32_t* qorder) {
+  __shared__ int64_t tile[256][4];
+  const int P = D.d.P;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  int64_t mine[4] = {0, 0, 0, 0};
+  if (i < P)
+    for (int k = 0; k < 4; k++) mine[k] = D.pod_sortkey[(int64_t)i * 4 + k];
+  int rank = 0;
+  for (int base = 0; base < P; base += 256) {
+    const int j = base + threadIdx.x;
+    for (int k = 0; k < 4; k++) tile[threadIdx.x][k] = j < P ? D.pod_sortkey[(int64_t)j * 4 + k] : INT64_MAX;
+    __syncthreads();
+    const int lim = min(256, P - base);
+    for (int t = 0; t < lim; t++) rank += key_less(tile[t], mine) ? 1 : 0;
+    __syncthreads();
+  }
+  if (i < P) qorder[rank] = i;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Solve
+// ------------------------------------------------------------------------------------------------
+struct Solver {
+  const KsDev& D;
+  const KsDims& d;
+  const KsWork& W;
+  ReqLayout L;
+  int32_t* s_order;
+  int32_t* s_okey;
+  uint32_t* s_rs;
+  uint32_t* s_rem;
+  uint32_t* s_cand;
+  int64_t* s_req;
+  int64_t* s_pod;
+  int64_t algbytes = 0;
+
+  __device__ Solver(const KsDev& D_, const KsWork& W_) : D(D_), d(D_.d), W(W_) {}
+
+  __device__ bool fits(const int64_t* req, const int64_t* alloc) const {  // resources.go:162-175
+    for (int r = 0; r < d.R; r++) {
+      int64_t a = alloc[r];
+      if (a < 0 || req[r] > a) return false;
+    }
+    return true;
+  }
+  __device__ bool has_offering(int it, const uint32_t* rs) const {  // nodeclaim.go:270-278
+    const int b = D.it_off_beg[it], e = D.it_off_beg[it + 1];
+    for (int o = b; o < e; o++)
+      if (rs_member(L, rs, d.zoneKey, D.off_zone[o]) && rs_member(L, rs, d.ctKey, D.off_ct[o])) return true;
+    return false;
+  }
+  __device__ bool tolerates(const uint64_t* taint, const uint64_t* tol) const {
+    return ((taint[0] & ~tol[0]) | (taint[1] & ~tol[1])) == 0;
+  }
+  __device__ void copy_words(uint32_t* dst, const uint32_t* src, int n) const {
+    for (int i = lane(); i < n; i += kWave) dst[i] = src[i];
+  }
+
+  // --- existing nodes (ExistingNode.Add, existingnode.go:64-124) -------------------------------
+  __device__ bool node_ok(int n, int s, int sflags) const {
+    if (!tolerates(D.n_taint + 2 * n, D.st_tol + 2 * s)) return false;
+    const int64_t* av = D.n_avail + (int64_t)n * d.R;
+    const int64_t* rq = W.n_req + (int64_t)n * d.R;
+    for (int r = 0; r < d.R; r++) {
+      int64_t a = av[r];
+      if (a < 0 || rq[r] + s_pod[r] > a) return false;
+    }
+    if (sflags & SF_HAS_KEYS)  // strict Compatible: no AllowUndefinedWellKnownLabels
+      return rs_compatible(L, W.n_rs + (int64_t)n * d.RSW, D.st_rs + (int64_t)s * d.RSW, 0);
+    return true;
+  }
+
+  // --- NodeClaim quick reject: necessary conditions of NodeClaim.Add ----------------------------
+  __device__ bool claim_quick(int c, int s, int sflags) const {
+    const int t = W.c_tpl[c];
+    if (!tolerates(D.tpl_taint + 2 * t, D.st_tol + 2 * s)) return false;
+    const int64_t* rq = W.c_req + (int64_t)c * d.R;
+    const int64_t* mx = W.c_max + (int64_t)c * d.R;
+    for (int r = 0; r < d.R; r++)
+      if (rq[r] + s_pod[r] > mx[r]) return false;
+    if (sflags & SF_HAS_KEYS)
+      return rs_compatible(L, W.c_rs + (int64_t)c * d.RSW, D.st_rs + (int64_t)s * d.RSW, d.allowWK);
+    return true;
+  }
+
+  // --- wave-cooperative NodeClaim.Add on claim c: builds s_rs / s_req / s_rem; true if any IT remains
+  __device__ bool claim_full(int c, int s, int sflags) {
+    const uint32_t* crs = W.c_rs + (int64_t)c * d.RSW;
+    copy_words(s_rs, crs, d.RSW);
+    wsync();
+    if (sflags & SF_HAS_KEYS) {
+      if (lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
+      wsync();
+    }
+    const bool changed = (sflags & SF_TOUCHES_IT_KEYS) && !rs_equal_keys(L, s_rs, crs, d.itKeys);
+    const int t = W.c_tpl[c];
+    const int64_t* crq = W.c_req + (int64_t)c * d.R;
+    if (lane() < d.R) s_req[lane()] = crq[lane()] + s_pod[lane()];
+    wsync();
+    const int tb = D.tpl_it_beg[t], nIT = D.tpl_it_beg[t + 1] - tb;
+    const uint32_t* rem = W.c_rem + (int64_t)c * d.TW;
+    uint64_t any = 0;
+    for (int base = 0; base < nIT; base += kWave) {
+      const int pos = base + lane();
+      bool ok = pos < nIT && ((rem[pos >> 5] >> (pos & 31)) & 1u);
+      if (ok) {
+        const int it = D.tpl_its[tb + pos];
+        ok = fits(s_req, D.it_alloc + (int64_t)it * d.R);
+        if (ok && changed)
+          ok = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs) && has_offering(it, s_rs);
+      }
+      const uint64_t m = wballot(ok);
+      if (lane() == 0) {
+        s_rem[base >> 5] = (uint32_t)m;
+        if ((base >> 5) + 1 < d.TW) s_rem[(base >> 5) + 1] = (uint32_t)(m >> 32);
+      }
+      any |= m;
+    }
+    algbytes += 4 * d.RSW + 4 * d.TW + 16 * d.R + (int64_t)nIT * 8 * d.R / 2;
+    wsync();
+    return any != 0;
+  }
+
+  // max Allocatable per resource over the options in `bits` (quick-reject bound)
+  __device__ void update_max(int c, const uint32_t* bits, int t) {
+    const int tb = D.tpl_it_beg[t], nIT = D.tpl_it_beg[t + 1] - tb;
+    for (int r = 0; r < d.R; r++) {
+      int64_t m = INT64_MIN;
+      for (int pos = lane(); pos < nIT; pos += kWave)
+        if ((bits[pos >> 5] >> (pos & 31)) & 1u) {
+          int64_t a = D.it_alloc[(int64_t)D.tpl_its[tb + pos] * d.R + r];
+          m = a > m ? a : m;
+        }
+      for (int off = 32; off >= 1; off >>= 1) {
+        int64_t o = __shfl_xor(m, off);
+        m = o > m ? o : m;
+      }
+      if (lane() == 0) W.c_max[(int64_t)c * d.R + r] = m;
+    }
+  }
+
+  __device__ void commit_claim(int c, int pos, int p, int s, int sflags, int& nlog) {
+    int64_t* crq = W.c_req + (int64_t)c * d.R;
+    if (lane() < d.R) crq[lane()] = s_req[lane()];
+    if (sflags & SF_HAS_KEYS) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
+    uint32_t* rem = W.c_rem + (int64_t)c * d.TW;
+    bool diff = false;
+    for (int i = lane(); i < d.TW; i += kWave) {
+      diff |= rem[i] != s_rem[i];
+      rem[i] = s_rem[i];
+    }
+    if (lane() == 0) {
+      W.c_cnt[c] += 1;
+      s_okey[pos] += 1;
+      W.log_pod[nlog] = p;
+      W.log_tgt[nlog] = c;
+      W.pod_status[p] = ST_SCHEDULED;
+    }
+    nlog++;
+    if (wballot(diff)) update_max(c, s_rem, W.c_tpl[c]);
+    algbytes += 16 * d.R + 4 * d.RSW + 4 * d.TW;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wsync();
+  }
+
+  // --- new NodeClaim from each template in order (scheduler.go:258-283) -----------------------
+  // Returns 1 placed, 0 failed (fail codes recorded), 2 no templates (add() returns nil).
+  __device__ int try_templates(int p, int s, int sflags, int& nclaims, int& nlog, int& hostCtr) {
+    if (d.NTPL == 0) return 2;
+    const uint64_t* tol = D.st_tol + 2 * s;
+    for (int t = 0; t < d.NTPL; t++) {
+      uint32_t code = FC_NONE;
+      int hostid = -1;
+      const int tb = D.tpl_it_beg[t], nIT = D.tpl_it_beg[t + 1] - tb;
+      const int pool = D.tpl_pool[t];
+      // filterByRemainingResources (scheduler.go:364-383)
+      uint64_t anyCand = 0;
+      for (int base = 0; base < nIT; base += kWave) {
+        const int pos = base + lane();
+        bool ok = pos < nIT;
+        if (ok && pool >= 0) {
+          const uint32_t mask = D.pool_mask[pool];
+          const int64_t* cap = D.it_cap + (int64_t)D.tpl_its[tb + pos] * d.R;
+          const int64_t* rem = W.pool_rem + (int64_t)pool * d.R;
+          for (int r = 0; r < d.R; r++)
+            if (((mask >> r) & 1u) && cap[r] > rem[r]) ok = false;
+        }
+        const uint64_t m = wballot(ok);
+        if (lane() == 0) {
+          s_cand[base >> 5] = (uint32_t)m;
+          if ((base >> 5) + 1 < d.TW) s_cand[(base >> 5) + 1] = (uint32_t)(m >> 32);
+        }
+        anyCand |= m;
+      }
+      wsync();
+      if (pool >= 0 && anyCand == 0) {
+        code = FC_LIMITS;
+      } else {
+        hostid = ++hostCtr;  // NewNodeClaim: atomic.AddInt64(&nodeID, 1) (nodeclaim.go:48)
+        if (!tolerates(D.tpl_taint + 2 * t, tol)) {
+          code = FC_TAINTS;
+        } else {
+          copy_words(s_rs, D.tpl_rs + (int64_t)t * d.RSW, d.RSW);
+          wsync();
+          bool ok = true;
+          if (sflags & SF_HAS_KEYS) {
+            ok = rs_compatible(L, s_rs, D.st_rs + (int64_t)s * d.RSW, d.allowWK);
+            if (ok && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
+            wsync();
+          }
+          if (!ok) {
+            code = FC_COMPAT;
+          } else {
+            if (lane() < d.R) s_req[lane()] = D.tpl_daemon[(int64_t)t * d.R + lane()] + s_pod[lane()];
+            wsync();
+            uint32_t flags = 0;
+            uint64_t any = 0;
+            for (int base = 0; base < nIT; base += kWave) {
+              const int pos = base + lane();
+              const bool in = pos < nIT && ((s_cand[pos >> 5] >> (pos & 31)) & 1u);
+              bool ic = false, fi = false, of = false;
+              if (in) {
+                const int it = D.tpl_its[tb + pos];
+                ic = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs);
+                fi = fits(s_req, D.it_alloc + (int64_t)it * d.R);
+                of = has_offering(it, s_rs);
+              }
+              if (wballot(ic)) flags |= FF_REQ;
+              if (wballot(fi)) flags |= FF_FITS;
+              if (wballot(of)) flags |= FF_OFF;
+              if (wballot(ic && fi && !of)) flags |= FF_REQ_FITS;
+              if (wballot(ic && of && !fi)) flags |= FF_REQ_OFF;
+              if (wballot(fi && of && !ic)) flags |= FF_FITS_OFF;
+              const uint64_t m = wballot(ic && fi && of);
+              if (lane() == 0) {
+                s_rem[base >> 5] = (uint32_t)m;
+                if ((base >> 5) + 1 < d.TW) s_rem[(base >> 5) + 1] = (uint32_t)(m >> 32);
+              }
+              any |= m;
+            }
+            algbytes += 4 * d.RSW + (int64_t)nIT * (8 * d.R + 4 * d.RSW + 16);
+            wsync();
+            if (any == 0) {
+              code = FC_NO_IT | (flags << 8);
+            } else {
+              // commit a new NodeClaim
+              if (nclaims >= d.Kcap) {
+                if (lane() == 0) W.counters[CT_ERROR] = KE_CLAIM_CAP;
+                return -1;
+              }
+              const int c = nclaims++;
+              copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
+              copy_words(W.c_rem + (int64_t)c * d.TW, s_rem, d.TW);
+              if (lane() < d.R) W.c_req[(int64_t)c * d.R + lane()] = s_req[lane()];
+              if (lane() == 0) {
+                W.c_tpl[c] = t;
+                W.c_cnt[c] = 1;
+                W.c_host[c] = hostid;
+                s_order[c] = c;
+                s_okey[c] = 1;
+                W.log_pod[nlog] = p;
+                W.log_tgt[nlog] = c;
+                W.pod_status[p] = ST_SCHEDULED;
+              }
+              nlog++;
+              update_max(c, s_rem, t);
+              if (pool >= 0) {  // subtractMax (scheduler.go:347-362)
+                const uint32_t mask = D.pool_mask[pool];
+                for (int r = 0; r < d.R; r++) {
+                  if (!((mask >> r) & 1u)) continue;
+                  int64_t m = INT64_MIN;
+                  for (int pos = lane(); pos < nIT; pos += kWave)
+                    if ((s_rem[pos >> 5] >> (pos & 31)) & 1u) {
+                      int64_t v = D.it_cap[(int64_t)D.tpl_its[tb + pos] * d.R + r];
+                      m = v > m ? v : m;
+                    }
+                  for (int off = 32; off >= 1; off >>= 1) {
+                    int64_t o = __shfl_xor(m, off);
+                    m = o > m ? o : m;
+                  }
+                  if (lane() == 0) W.pool_rem[(int64_t)pool * d.R + r] -= m;
+                }
+              }
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+              wsync();
+              return 1;
+            }
+          }
+        }
+      }
+      if (lane() == 0) {
+        W.fail_code[(int64_t)p * d.NTPL + t] = code;
+        W.fail_host[(int64_t)p * d.NTPL + t] = hostid;
+      }
+    }
+    return 0;
+  }
+
+  // --- s.newNodeClaims re-sort (scheduler.go:247) --------------------------------------------------
+  __device__ void sort_claims(int n, int64_t& sorts, int64_t& slow) {
+    bool desc = false;
+    for (int base = 0; base < n; base += kWave) {
+      const int j = base + lane();
+      const bool dd = j > 0 && j < n && s_okey[j] < s_okey[j - 1];
+      desc |= wballot(dd) != 0;
+    }
+    sorts++;
+    if (!desc) return;  // non-decreasing: pdqsort performs no swap
+    slow++;
+    if (lane() == 0) {
+      GoSortExact g{GoSort{s_okey, s_order}};
+      g.run(n);
+    }
+    wsync();
+  }
+};
+
+__global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, const int32_t* qorder) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const KsWork W = works[blockIdx.x];
+  const KsDims& d = D.d;
+  Solver S(D, W);
+  // LDS carve-up (16-byte aligned pieces)
+  char* sp = smem;
+  auto take = [&](size_t bytes) { char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
+  KeyMeta* s_keys = (KeyMeta*)take(sizeof(KeyMeta) * d.NK);
+  S.s_order = (int32_t*)take(4 * (size_t)d.Kcap);
+  S.s_okey = (int32_t*)take(4 * (size_t)d.Kcap);
+  S.s_rs = (uint32_t*)take(4 * (size_t)d.RSW);
+  S.s_rem = (uint32_t*)take(4 * (size_t)d.TW + 8);
+  S.s_cand = (uint32_t*)take(4 * (size_t)d.TW + 8);
+  S.s_req = (int64_t*)take(8 * kMaxR);
+  S.s_pod = (int64_t*)take(8 * kMaxR);
+  for (int i = lane(); i < d.NK * (int)(sizeof(KeyMeta) / 4); i += kWave)
+    ((uint32_t*)s_keys)[i] = ((const uint32_t*)D.keys)[i];
+  S.L.nkeys = d.NK;
+  S.L.W = d.W;
+  S.L.NB = d.NB;
+  S.L.HDR = d.HDR;
+  S.L.RSW = d.RSW;
+  S.L.keys = s_keys;
+  S.L.wordValid = D.wordValid;
+  S.L.vIsInt = D.vIsInt;
+  S.L.vInt = D.vInt;
+  const int P = d.P;
+  for (int i = lane(); i < P; i += kWave) W.queue[i] = qorder[i];
+  wsync();
+
+  int nclaims = 0, nlog = 0, hostCtr = d.hostnameSeed;
+  uint32_t epoch = 1;
+  int qhead = 0, qlen = P;
+  int64_t pops = 0, sorts = 0, slow = 0;
+  const int64_t popCap = (int64_t)(P + 1) * (P + 1) * 8 + 1024;
+  int err = KE_OK;
+
+  while (qlen > 0) {
+    // Queue.Pop (queue.go:46-61)
+    const int p = __builtin_amdgcn_readfirstlane(W.queue[qhead]);
+    const int uid = D.pod_uid[p];
+    const uint64_t ll = W.last_len[uid];
+    if ((uint32_t)(ll >> 32) == epoch && (uint32_t)ll == (uint32_t)qlen) break;
+    qhead = qhead + 1 == P ? 0 : qhead + 1;
+    qlen--;
+    if (++pops > popCap) { err = KE_ITER_CAP; break; }
+    const int s = __builtin_amdgcn_readfirstlane(W.pod_state[p]);
+    const int sflags = D.st_flags[s];
+    if (lane() < d.R) S.s_pod[lane()] = D.pod_req[(int64_t)p * d.R + lane()];
+    wsync();
+    bool placed = false;
+    // 1) existing nodes in order
+    for (int base = 0; base < d.N && !placed; base += kWave) {
+      const int n = base + lane();
+      const bool ok = n < d.N && S.node_ok(n, s, sflags);
+      const uint64_t m = wballot(ok);
+      S.algbytes += (int64_t)min(kWave, d.N - base) * (16 * d.R + 16);
+      if (m) {
+        const int j = base + ctz64(m);
+        if (lane() < d.R) W.n_req[(int64_t)j * d.R + lane()] += S.s_pod[lane()];
+        if ((sflags & SF_HAS_KEYS) && lane() == 0)
+          rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+        if (lane() == 0) {
+          W.log_pod[nlog] = p;
+          W.log_tgt[nlog] = -(j + 1);
+          W.pod_status[p] = ST_SCHEDULED;
+        }
+        nlog++;
+        placed = true;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        wsync();
+      }
+    }
+    // 2) in-flight NodeClaims, sorted by pod count
+    if (!placed && nclaims > 0) {
+      S.sort_claims(nclaims, sorts, slow);
+      for (int base = 0; base < nclaims && !placed; base += kWave) {
+        const int j = base + lane();
+        const bool q = j < nclaims && S.claim_quick(S.s_order[j], s, sflags);
+        uint64_t m = wballot(q);
+        S.algbytes += (int64_t)min(kWave, nclaims - base) * (16 * d.R + 24);
+        while (m && !placed) {
+          const int jj = base + ctz64(m);
+          m &= m - 1;
+          const int c = S.s_order[jj];
+          if (S.claim_full(c, s, sflags)) {
+            S.commit_claim(c, jj, p, s, sflags, nlog);
+            placed = true;
+          }
+        }
+      }
+    }
+    // 3) new NodeClaim per template
+    if (!placed) {
+      const int r = S.try_templates(p, s, sflags, nclaims, nlog, hostCtr);
+      if (r < 0) { err = KE_CLAIM_CAP; break; }
+      if (r == 1) placed = true;
+      if (r == 2) {  // no templates: add() returns a nil error
+        if (lane() == 0) W.pod_status[p] = ST_SCHEDULED;
+        placed = true;
+      }
+    }
+    if (placed) continue;
+    // failure: Preferences.Relax (preferences.go:38) + Queue.Push (queue.go:64-71)
+    const int s0 = D.pod_state0[p], ns = D.pod_nstate[p];
+    const bool relaxed = s - s0 + 1 < ns;
+    if (lane() == 0) {
+      W.pod_status[p] = ST_FAILED;
+      W.pod_fstate[p] = s;
+      if (relaxed) W.pod_state[p] = s + 1;
+    }
+    if (relaxed) epoch++;
+    int tail = qhead + qlen;
+    if (tail >= P) tail -= P;
+    if (lane() == 0) W.queue[tail] = p;
+    qlen++;
+    if (!relaxed && lane() == 0) W.last_len[uid] = ((uint64_t)epoch << 32) | (uint32_t)qlen;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wsync();
+  }
+  for (int i = lane(); i < nclaims; i += kWave) W.order[i] = S.s_order[i];
+  if (lane() == 0) {
+    W.counters[CT_NCLAIMS] = nclaims;
+    W.counters[CT_NLOG] = nlog;
+    W.counters[CT_HOSTCTR] = hostCtr;
+    W.counters[CT_ERROR] = err ? err : W.counters[CT_ERROR];
+    W.counters[CT_POPS] = pops;
+    W.counters[CT_ALGBYTES] = S.algbytes;
+    W.counters[CT_SORTS] = sorts;
+    W.counters[CT_SORT_SLOW] = slow;
+  }
+}
+
+size_t solve_lds_bytes(const KsDims& d) {
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  return r16(sizeof(KeyMeta) * d.NK) + 2 * r16(4 * (size_t)d.Kcap) + r16(4 * (size_t)d.RSW) +
+         2 * r16(4 * (size_t)d.TW + 8) + 2 * r16(8 * kMaxR);
+}
+
+// Host-side launch sequence for one ks_solve: init -> queue rank -> solve (one stream).
+// `mid` (optional) is recorded between the setup kernels and k_solve so the solve kernel's own
+// duration can be read with HIP events on this stream.
+hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, int32_t* qorder, hipStream_t st,
+                        hipEvent_t mid) {
+  const KsDims& d = D.d;
+  const size_t lds = solve_lds_bytes(d);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep);
+  if (d.P > 0) hipLaunchKernelGGL(k_queue_rank, dim3((d.P + 255) / 256), dim3(256), 0, st, D, qorder);
+  if (mid) (void)hipEventRecord(mid, st);
+  hipLaunchKernelGGL(k_solve, dim3(nrep), dim3(kWave), lds, st, D, works_dev, (const int32_t*)qorder);
+  return hipGetLastError();
+}
+
+}  // namespace ks

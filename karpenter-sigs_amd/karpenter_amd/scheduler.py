@@ -1,0 +1,144 @@
+"""ctypes binding of include/karpenter_amd.h, shaped like the reference's scheduling package.
+
+Reference surface (pkg/controllers/provisioning/scheduling/scheduler.go):
+    NewScheduler(ctx, kubeClient, nodeClaimTemplates, nodePools, cluster, stateNodes, topology,
+                 instanceTypes, daemonSetPods, recorder, opts) *Scheduler        :49-83
+    (*Scheduler).Solve(ctx, pods) *Results                                     :140-189
+    Results{NewNodeClaims, ExistingNodes, PodErrors}                           :102-106
+Here the NewScheduler arguments and the pods travel as one JSON snapshot.
+"""
+import ctypes
+import json
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libkarpenter_amd.so")
+_lib = None
+
+KS_ERRORS = {-1: "KS_ERR_PARSE", -2: "KS_ERR_UNSUPPORTED", -3: "KS_ERR_CAPACITY", -4: "KS_ERR_HIP",
+             -5: "KS_ERR_INTERNAL", -6: "KS_ERR_ARG"}
+
+
+class KsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (KS_ERRORS.get(code, code), msg))
+        self.code = code
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("simulation_mode", ctypes.c_int), ("replicas", ctypes.c_int),
+                ("timing_only", ctypes.c_int), ("reserved", ctypes.c_int * 4)]
+
+
+def library_path():
+    return _LIB_PATH
+
+
+def lib():
+    """Load libkarpenter_amd.so (built in-tree by `make -C karpenter-sigs_amd`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise KsError(-4, "libkarpenter_amd.so not built (%s); run __graft_entry__.build()" % _LIB_PATH)
+    l = ctypes.CDLL(_LIB_PATH)
+    vp = ctypes.c_void_p
+    l.ks_problem_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
+    l.ks_problem_inspect.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
+    l.ks_problem_free.argtypes = [vp]
+    l.ks_solve.argtypes = [vp, ctypes.POINTER(_Opts), ctypes.POINTER(vp)]
+    l.ks_results_free.argtypes = [vp]
+    l.ks_results_json.argtypes = [vp, ctypes.POINTER(vp)]
+    l.ks_results_kernel_ms.argtypes = [vp]
+    l.ks_results_kernel_ms.restype = ctypes.c_double
+    l.ks_results_solve_kernel_ms.argtypes = [vp]
+    l.ks_results_solve_kernel_ms.restype = ctypes.c_double
+    l.ks_results_algorithmic_bytes.argtypes = [vp]
+    l.ks_results_algorithmic_bytes.restype = ctypes.c_double
+    l.ks_free.argtypes = [vp]
+    l.ks_last_error.restype = ctypes.c_char_p
+    l.ks_build_info.restype = ctypes.c_char_p
+    _lib = l
+    return l
+
+
+def _check(rc):
+    if rc != 0:
+        raise KsError(rc, lib().ks_last_error().decode())
+
+
+def _take_str(ptr):
+    s = ctypes.cast(ptr, ctypes.c_char_p).value.decode()
+    lib().ks_free(ptr)
+    return s
+
+
+def _encode(snapshot):
+    return (snapshot if isinstance(snapshot, str) else json.dumps(snapshot)).encode()
+
+
+def inspect(snapshot):
+    """Encode a snapshot on the host only (no device): universe sizes and layout, for diagnostics."""
+    b = _encode(snapshot)
+    out = ctypes.c_void_p()
+    _check(lib().ks_problem_inspect(b, len(b), ctypes.byref(out)))
+    return json.loads(_take_str(out))
+
+
+class Results:
+    """scheduling.Results: new_nodeclaims, existing_nodes, pod_errors (keys = input pod index)."""
+
+    def __init__(self, doc, kernel_ms, alg_bytes, solve_kernel_ms=0.0):
+        self.doc = doc
+        self.new_nodeclaims = doc["newNodeClaims"]
+        self.existing_nodes = doc["existingNodes"]
+        self.pod_errors = {int(k): v for k, v in doc["podErrors"].items()}
+        self.stats = doc.get("stats", {})
+        self.kernel_ms = kernel_ms
+        self.solve_kernel_ms = solve_kernel_ms
+        self.algorithmic_bytes = alg_bytes
+
+    def canonical(self):
+        d = dict(self.doc)
+        d.pop("stats", None)
+        return d
+
+
+class Scheduler:
+    """NewScheduler(...) on the GPU: the snapshot is encoded once and stays resident in HBM."""
+
+    def __init__(self, snapshot):
+        b = _encode(snapshot)
+        h = ctypes.c_void_p()
+        _check(lib().ks_problem_create(b, len(b), ctypes.byref(h)))
+        self._h = h
+
+    def solve(self, replicas=1, device=-1, simulation_mode=True, timing_only=False):
+        """Solve(ctx, pods) with fresh scheduler state; replicas>1 runs that many independent copies
+        of the same Solve in one launch (one wavefront each) and returns replica 0's results."""
+        o = _Opts(device, 1 if simulation_mode else 0, replicas, 1 if timing_only else 0)
+        r = ctypes.c_void_p()
+        _check(lib().ks_solve(self._h, ctypes.byref(o), ctypes.byref(r)))
+        try:
+            if timing_only:
+                return Results({"newNodeClaims": [], "existingNodes": [], "podErrors": {}},
+                               lib().ks_results_kernel_ms(r), lib().ks_results_algorithmic_bytes(r),
+                               lib().ks_results_solve_kernel_ms(r))
+            js = ctypes.c_void_p()
+            _check(lib().ks_results_json(r, ctypes.byref(js)))
+            doc = json.loads(_take_str(js))
+            return Results(doc, lib().ks_results_kernel_ms(r), lib().ks_results_algorithmic_bytes(r),
+                           lib().ks_results_solve_kernel_ms(r))
+        finally:
+            lib().ks_results_free(r)
+
+    def close(self):
+        if self._h:
+            lib().ks_problem_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,187 @@
+"""Synthetic snapshots shaped like the reference's own test fixtures (BASELINE.json configs).
+
+Mirrors pkg/cloudprovider/fake/instancetype.go (InstanceTypes(n), NewInstanceType,
+priceFromResources), pkg/test (NodePool(), Pod()) and
+pkg/controllers/provisioning/scheduling/scheduling_benchmark_test.go (makeDiversePods).  Go's
+math/rand stream is not reproducible here, so distributions match the reference while the sequence
+comes from numpy's PCG64 with the stated seed.
+"""
+import numpy as np
+
+ZONE = "topology.kubernetes.io/zone"
+CT = "karpenter.sh/capacity-type"
+ARCH = "kubernetes.io/arch"
+OS = "kubernetes.io/os"
+IT_LABEL = "node.kubernetes.io/instance-type"
+NODEPOOL = "karpenter.sh/nodepool"
+HOSTNAME = "kubernetes.io/hostname"
+WELL_KNOWN = [NODEPOOL, ZONE, "topology.kubernetes.io/region", IT_LABEL, ARCH, OS, CT,
+              "node.kubernetes.io/windows-build"]
+# fake/instancetype.go:42-48 — linking the fake provider inserts these into WellKnownLabels
+FAKE_WELL_KNOWN = WELL_KNOWN + ["size", "special", "integer"]
+GI = 1 << 30
+
+
+def price_from_resources(cpu, mem_bytes, gpus=0):  # fake/instancetype.go:177-189
+    return 0.1 * cpu + 0.1 * mem_bytes / 1e9 + 1.0 * gpus
+
+
+def fake_instance_type(name, cpu, mem_gi, pods=None, arch="amd64", oses=("darwin", "linux", "windows"),
+                       offerings=None, extra_capacity=None):
+    """fake.NewInstanceType (instancetype.go:50-110) with integer cpu and Gi memory."""
+    mem_bytes = mem_gi * GI
+    price = price_from_resources(cpu, mem_bytes, len(extra_capacity or {}))
+    if offerings is None:
+        offerings = [
+            {"capacityType": "spot", "zone": "test-zone-1", "price": price, "available": True},
+            {"capacityType": "spot", "zone": "test-zone-2", "price": price, "available": True},
+            {"capacityType": "on-demand", "zone": "test-zone-1", "price": price, "available": True},
+            {"capacityType": "on-demand", "zone": "test-zone-2", "price": price, "available": True},
+            {"capacityType": "on-demand", "zone": "test-zone-3", "price": price, "available": True},
+        ]
+    avail = [o for o in offerings if o.get("available", True)]
+    large = cpu > 4 and mem_gi > 8
+    reqs = [
+        {"key": IT_LABEL, "operator": "In", "values": [name]},
+        {"key": ARCH, "operator": "In", "values": [arch]},
+        {"key": OS, "operator": "In", "values": sorted(oses)},
+        {"key": ZONE, "operator": "In", "values": sorted({o["zone"] for o in avail})},
+        {"key": CT, "operator": "In", "values": sorted({o["capacityType"] for o in avail})},
+        {"key": "size", "operator": "In", "values": ["large" if large else "small"]},
+        ({"key": "special", "operator": "In", "values": ["optional"]} if large
+         else {"key": "special", "operator": "DoesNotExist"}),
+        {"key": "integer", "operator": "In", "values": [str(cpu)]},
+    ]
+    cap = {"cpu": str(cpu), "memory": "%dGi" % mem_gi, "pods": str(pods if pods is not None else 5)}
+    if extra_capacity:
+        cap.update(extra_capacity)
+    return {"name": name, "requirements": reqs, "offerings": offerings, "capacity": cap,
+            "overhead": {"kubeReserved": {"cpu": "100m", "memory": "10Mi"}}}
+
+
+def fake_instance_types(n):
+    """fake.InstanceTypes(n) (instancetype.go:153-167): i+1 cpu, 2(i+1)Gi, 10(i+1) pods."""
+    return [fake_instance_type("fake-it-%d" % i, i + 1, 2 * (i + 1), pods=10 * (i + 1)) for i in range(n)]
+
+
+def node_pool(name, weight=None, limits=None, requirements=None, taints=None, labels=None):
+    """test.NodePool() (pkg/test/nodepool.go:33-61) as a NodePool JSON object."""
+    lab = {"testing/cluster": "unspecified"}
+    lab.update(labels or {})
+    spec = {"template": {"metadata": {"labels": lab},
+                         "spec": {"requirements": requirements or [], "taints": taints or []}}}
+    if weight is not None:
+        spec["weight"] = weight
+    if limits is not None:
+        spec["limits"] = limits
+    return {"metadata": {"name": name}, "spec": spec}
+
+
+def pod(i, cpu=None, mem=None, labels=None, node_selector=None, affinity=None, tolerations=None,
+        namespace="default", uid=None, extra=None):
+    """test.Pod() (pkg/test/pods.go:72-150) with a unique UID (queue.go keys staleness by UID)."""
+    lab = {"testing/cluster": "unspecified"}
+    lab.update(labels or {})
+    req = {}
+    if cpu is not None:
+        req["cpu"] = cpu
+    if mem is not None:
+        req["memory"] = mem
+    spec = {"containers": [{"name": "c", "resources": {"requests": req}}]}
+    if node_selector:
+        spec["nodeSelector"] = node_selector
+    if affinity:
+        spec["affinity"] = affinity
+    if tolerations:
+        spec["tolerations"] = tolerations
+    if extra:
+        spec.update(extra)
+    return {"metadata": {"name": "pod-%06d" % i, "namespace": namespace, "uid": uid or "pod-uid-%06d" % i,
+                         "labels": lab},
+            "spec": spec,
+            "status": {"conditions": [{"type": "PodScheduled", "reason": "Unschedulable", "status": "False"}]}}
+
+
+CPU_CHOICES = ["100m", "250m", "500m", "1000m", "1500m"]           # scheduling_benchmark_test.go:283-286
+MEM_CHOICES = ["100Mi", "256Mi", "512Mi", "1024Mi", "2048Mi", "4096Mi"]  # :278-281
+LABEL_VALUES = ["a", "b", "c", "d", "e", "f", "g"]                  # :273-276
+
+
+def make_diverse_pods(count, rng):
+    """makeDiversePods (scheduling_benchmark_test.go:184-196)."""
+    pods = []
+
+    def res():
+        return CPU_CHOICES[rng.integers(len(CPU_CHOICES))], MEM_CHOICES[rng.integers(len(MEM_CHOICES))]
+
+    def generic(n):
+        for _ in range(n):
+            lab = {"my-label": LABEL_VALUES[rng.integers(7)]}
+            c, m = res()
+            pods.append((lab, c, m, None))
+
+    def spread(n, key):
+        for _ in range(n):
+            lab = {"my-label": LABEL_VALUES[rng.integers(7)]}
+            sel = {"my-label": LABEL_VALUES[rng.integers(7)]}
+            c, m = res()
+            pods.append((lab, c, m, {"topologySpreadConstraints": [
+                {"maxSkew": 1, "topologyKey": key, "whenUnsatisfiable": "DoNotSchedule",
+                 "labelSelector": {"matchLabels": sel}}]}))
+
+    def affinity(n, key):
+        for _ in range(n):
+            lab = {"my-affininity": LABEL_VALUES[rng.integers(7)]}
+            sel = {"my-affininity": LABEL_VALUES[rng.integers(7)]}
+            c, m = res()
+            pods.append((lab, c, m, {"affinity": {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": {"matchLabels": sel}, "topologyKey": key}]}}}))
+
+    generic(count // 7)
+    spread(count // 7, ZONE)
+    spread(count // 7, HOSTNAME)
+    affinity(count // 7, HOSTNAME)
+    affinity(count // 7, ZONE)
+    generic(count - len(pods))
+    out = []
+    for i, (lab, c, m, extra) in enumerate(pods):
+        p = pod(i, cpu=c, mem=m, labels=lab)
+        if extra:
+            p["spec"].update(extra)
+        out.append(p)
+    return out
+
+
+def benchmark_snapshot(n_pods, n_its=400, seed=42, diverse=True):
+    """BenchmarkScheduling (scheduling_benchmark_test.go:116-182): one template from test.NodePool(),
+    no NodePools (so no limits), empty Topology, fake.InstanceTypes(n_its)."""
+    rng = np.random.default_rng(seed)
+    its = fake_instance_types(n_its)
+    np_obj = node_pool("default-pool")
+    if diverse:
+        pods = make_diverse_pods(n_pods, rng)
+    else:
+        pods = []
+        for i in range(n_pods):
+            pods.append(pod(i, cpu=CPU_CHOICES[rng.integers(5)], mem=MEM_CHOICES[rng.integers(6)],
+                            labels={"my-label": LABEL_VALUES[rng.integers(7)]}))
+    return {
+        "wellKnownLabels": FAKE_WELL_KNOWN,
+        "instanceTypes": its,
+        "instanceTypesByNodePool": {"default-pool": list(range(n_its))},
+        "nodeClaimTemplates": [np_obj],
+        "nodePools": [],
+        "stateNodes": [],
+        "daemonSetPods": [],
+        "pods": pods,
+    }
+
+
+def config1(seed=42):
+    """C1: BenchmarkScheduling2000 — makeDiversePods(2000) x fake.InstanceTypes(400)."""
+    return benchmark_snapshot(2000, 400, seed, diverse=True)
+
+
+def config2(n_pods=50000, seed=42):
+    """C2: 50k resource-only pods x 400 fake instance types, 1 template, no limits."""
+    return benchmark_snapshot(n_pods, 400, seed, diverse=False)

@@ -1,0 +1,69 @@
+"""ctypes bridge to oracle/_build/liboracle.so (test infrastructure only)."""
+import ctypes
+import json
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        l = ctypes.CDLL(_LIB)
+        l.oref_solve_json.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_double)]
+        l.oref_solve_json.restype = ctypes.c_int
+        l.oref_time_solve.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        l.oref_time_solve.restype = ctypes.c_int
+        l.oref_eval_ops.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+        l.oref_eval_ops.restype = ctypes.c_int
+        l.oref_last_error.restype = ctypes.c_char_p
+        l.oref_free.argtypes = [ctypes.c_void_p]
+        _lib = l
+    return _lib
+
+
+def _take(ptr):
+    l = lib()
+    s = ctypes.cast(ptr, ctypes.c_char_p).value.decode()
+    l.oref_free(ptr)
+    return s
+
+
+def solve(snapshot):
+    """Run the oracle Solve on a snapshot dict (or JSON string); returns (results dict, seconds)."""
+    l = lib()
+    s = snapshot if isinstance(snapshot, str) else json.dumps(snapshot)
+    out = ctypes.c_void_p()
+    secs = ctypes.c_double()
+    if l.oref_solve_json(s.encode(), ctypes.byref(out), ctypes.byref(secs)) != 0:
+        raise RuntimeError("oracle: " + l.oref_last_error().decode())
+    return json.loads(_take(out)), secs.value
+
+
+def time_solve(snapshot, reps):
+    l = lib()
+    s = snapshot if isinstance(snapshot, str) else json.dumps(snapshot)
+    secs = ctypes.c_double()
+    if l.oref_time_solve(s.encode(), reps, ctypes.byref(secs)) != 0:
+        raise RuntimeError("oracle: " + l.oref_last_error().decode())
+    return secs.value
+
+
+def eval_ops(ops, well_known=None):
+    l = lib()
+    doc = {"ops": ops}
+    if well_known is not None:
+        doc["wellKnownLabels"] = list(well_known)
+    out = ctypes.c_void_p()
+    if l.oref_eval_ops(json.dumps(doc).encode(), ctypes.byref(out)) != 0:
+        raise RuntimeError("oracle: " + l.oref_last_error().decode())
+    return json.loads(_take(out))["results"]

@@ -1,0 +1,176 @@
+"""Seeded random scheduling problems for oracle-vs-GPU parity tests.
+
+Covers the Solve features the reference's suite_test.go / provisioning suite exercise: node
+selectors, required node-affinity terms (In/NotIn/Exists/DoesNotExist/Gt/Lt, OR'd terms relaxed one
+at a time), preferred node affinity (relaxed), tolerations vs NoSchedule / PreferNoSchedule taints,
+NodePool limits, daemonset overhead, existing nodes (initialized / not), multiple weighted templates,
+instance types with partial offerings.
+"""
+import numpy as np
+
+from karpenter_amd import synth
+
+ZONES = ["test-zone-1", "test-zone-2", "test-zone-3", "test-zone-4"]
+CTS = ["spot", "on-demand"]
+ARCHS = ["amd64", "arm64"]
+TEAMS = ["red", "blue", "green"]
+
+
+def _pick(rng, seq, k=None):
+    if k is None:
+        return seq[int(rng.integers(len(seq)))]
+    idx = rng.choice(len(seq), size=min(k, len(seq)), replace=False)
+    return [seq[int(i)] for i in sorted(idx)]
+
+
+def random_its(rng, n):
+    its = []
+    for i in range(n):
+        cpu = int(rng.choice([1, 2, 4, 8, 16, 32, 48, 64]))
+        mem = int(cpu * rng.choice([1, 2, 4, 8]))
+        offers = []
+        for z in ZONES:
+            for ct in CTS:
+                if rng.random() < 0.45:
+                    price = synth.price_from_resources(cpu, mem * synth.GI) * (0.3 if ct == "spot" else 1.0)
+                    offers.append({"capacityType": ct, "zone": z, "price": price, "available": bool(rng.random() < 0.9)})
+        if not offers:
+            offers.append({"capacityType": "on-demand", "zone": ZONES[0], "price": 1.0, "available": True})
+        it = synth.fake_instance_type("it-%03d-%dc%dg" % (i, cpu, mem), cpu, mem, pods=int(rng.choice([8, 16, 32, 110])),
+                                      arch=_pick(rng, ARCHS), offerings=offers)
+        if rng.random() < 0.1:
+            it["capacity"]["example.com/gpu"] = str(int(rng.integers(1, 5)))
+        its.append(it)
+    return its
+
+
+def random_nsr(rng, allow_custom=True):
+    kind = rng.integers(7)
+    if kind == 0:
+        return {"key": synth.ZONE, "operator": "In", "values": _pick(rng, ZONES, int(rng.integers(1, 3)))}
+    if kind == 1:
+        return {"key": synth.ZONE, "operator": "NotIn", "values": _pick(rng, ZONES, 1)}
+    if kind == 2:
+        return {"key": synth.ARCH, "operator": "In", "values": [_pick(rng, ARCHS)]}
+    if kind == 3:
+        return {"key": synth.CT, "operator": "In", "values": [_pick(rng, CTS)]}
+    if kind == 4:
+        return {"key": "integer", "operator": _pick(rng, ["Gt", "Lt"]), "values": [str(int(rng.choice([2, 4, 8, 16, 32])))]}
+    if kind == 5 and allow_custom:
+        return {"key": "team", "operator": _pick(rng, ["In", "NotIn", "Exists", "DoesNotExist"]),
+                "values": _pick(rng, TEAMS, 1)}
+    return {"key": "size", "operator": _pick(rng, ["Exists", "DoesNotExist", "In"]), "values": ["large"]}
+
+
+def random_pod(rng, i):
+    cpu = _pick(rng, ["100m", "250m", "500m", "1", "1500m", "2", "3500m", "6"])
+    mem = _pick(rng, ["128Mi", "512Mi", "1Gi", "1.8G", "3Gi", "6Gi", "12Gi"])
+    p = synth.pod(i, cpu=cpu, mem=mem, labels={"app": "a%d" % (i % 5)})
+    spec = p["spec"]
+    if rng.random() < 0.25:
+        sel = {}
+        if rng.random() < 0.5:
+            sel[synth.ZONE] = _pick(rng, ZONES)
+        if rng.random() < 0.4:
+            sel[synth.ARCH] = _pick(rng, ARCHS)
+        if rng.random() < 0.2:
+            sel["team"] = _pick(rng, TEAMS)
+        if sel:
+            spec["nodeSelector"] = sel
+    aff = {}
+    if rng.random() < 0.3:
+        terms = [{"matchExpressions": [random_nsr(rng) for _ in range(int(rng.integers(1, 3)))]}
+                 for _ in range(int(rng.integers(1, 4)))]
+        aff.setdefault("nodeAffinity", {})["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": terms}
+    if rng.random() < 0.2:
+        prefs = [{"weight": int(rng.integers(1, 100)), "preference": {"matchExpressions": [random_nsr(rng)]}}
+                 for _ in range(int(rng.integers(1, 3)))]
+        aff.setdefault("nodeAffinity", {})["preferredDuringSchedulingIgnoredDuringExecution"] = prefs
+    if aff:
+        spec["affinity"] = aff
+    if rng.random() < 0.3:
+        tols = []
+        if rng.random() < 0.6:
+            tols.append({"key": "dedicated", "operator": "Equal", "value": _pick(rng, TEAMS), "effect": "NoSchedule"})
+        if rng.random() < 0.3:
+            tols.append({"operator": "Exists"})
+        if rng.random() < 0.3:
+            tols.append({"key": "spotty", "operator": "Exists"})
+        if tols:
+            spec["tolerations"] = tols
+    if rng.random() < 0.05:
+        spec["initContainers"] = [{"name": "init", "resources": {"requests": {"cpu": _pick(rng, ["2", "8", "100"])}}}]
+    if rng.random() < 0.05:
+        spec["containers"][0]["resources"]["requests"]["example.com/gpu"] = "1"
+    return p
+
+
+def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None):
+    rng = np.random.default_rng(seed)
+    its = random_its(rng, n_its)
+    n_templates = int(rng.integers(1, 4)) if n_templates is None else n_templates
+    templates, pools, by_pool = [], [], {}
+    for t in range(n_templates):
+        name = "pool-%d" % t
+        reqs = [random_nsr(rng, allow_custom=False) for _ in range(int(rng.integers(0, 2)))]
+        taints = []
+        if rng.random() < 0.35:
+            taints.append({"key": "dedicated", "value": _pick(rng, TEAMS), "effect": "NoSchedule"})
+        if rng.random() < 0.2:
+            taints.append({"key": "spotty", "value": "", "effect": "PreferNoSchedule"})
+        labels = {"team": _pick(rng, TEAMS)} if rng.random() < 0.5 else {}
+        limits = {"cpu": str(int(rng.choice([16, 64, 256, 1000])))} if rng.random() < 0.4 else None
+        np_obj = synth.node_pool(name, weight=int(rng.integers(0, 100)), limits=limits, requirements=reqs,
+                                 taints=taints, labels=labels)
+        templates.append(np_obj)
+        pools.append(np_obj)
+        k = max(1, int(n_its * rng.uniform(0.3, 1.0)))
+        by_pool[name] = sorted(int(i) for i in rng.choice(n_its, size=k, replace=False))
+    # Provisioner.NewScheduler orders templates by weight (nodepool.go:209-213); keep that order.
+    order = sorted(range(n_templates), key=lambda i: -templates[i]["spec"].get("weight", 0))
+    templates = [templates[i] for i in order]
+    n_nodes = int(rng.integers(0, 12)) if n_nodes is None else n_nodes
+    nodes = []
+    for i in range(n_nodes):
+        pool = templates[int(rng.integers(len(templates)))]["metadata"]["name"]
+        cpu = int(rng.choice([2, 4, 8, 16]))
+        name = "node-%03d" % i
+        labels = {synth.ZONE: _pick(rng, ZONES), synth.ARCH: _pick(rng, ARCHS), synth.NODEPOOL: pool,
+                  synth.HOSTNAME: name, synth.CT: _pick(rng, CTS)}
+        if rng.random() < 0.5:
+            labels["team"] = _pick(rng, TEAMS)
+        taints = [{"key": "dedicated", "value": _pick(rng, TEAMS), "effect": "NoSchedule"}] if rng.random() < 0.2 else []
+        used = float(rng.uniform(0, 0.8))
+        nodes.append({
+            "name": name, "hostName": name, "labels": labels, "taints": taints,
+            "available": {"cpu": "%dm" % int(cpu * 1000 * (1 - used)), "memory": "%dMi" % int(cpu * 2048 * (1 - used)),
+                          "pods": str(int(rng.integers(0, 30)))},
+            "capacity": {"cpu": str(cpu), "memory": "%dGi" % (cpu * 2), "pods": "110"},
+            "daemonSetRequests": {"cpu": "100m"} if rng.random() < 0.5 else {},
+            "initialized": bool(rng.random() < 0.8),
+        })
+    daemons = []
+    for i in range(int(rng.integers(0, 3))):
+        d = synth.pod(100000 + i, cpu=_pick(rng, ["50m", "100m", "200m"]), mem=_pick(rng, ["64Mi", "128Mi"]))
+        if rng.random() < 0.5:
+            d["spec"]["tolerations"] = [{"operator": "Exists"}]
+        if rng.random() < 0.3:
+            d["spec"]["nodeSelector"] = {synth.ARCH: _pick(rng, ARCHS)}
+        daemons.append(d)
+    pods = [random_pod(rng, i) for i in range(n_pods)]
+    return {
+        "wellKnownLabels": synth.FAKE_WELL_KNOWN,
+        "instanceTypes": its,
+        "instanceTypesByNodePool": by_pool,
+        "nodeClaimTemplates": templates,
+        "nodePools": pools,
+        "stateNodes": nodes,
+        "daemonSetPods": daemons,
+        "pods": pods,
+    }
+
+
+def canonical(results):
+    d = dict(results)
+    d.pop("stats", None)
+    return d

@@ -1,0 +1,78 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads and exports every declared symbol,
+the host encoder accepts the reference-shaped snapshots and rejects unsupported inputs loudly."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import problems
+from karpenter_amd import KsError, inspect, lib, synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "karpenter_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ks_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    l = lib()
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    missing = [s for s in syms if not hasattr(l, s)]
+    assert not missing, missing
+
+
+def test_build_info_and_device_count_without_gpu():
+    l = lib()
+    l.ks_build_info.restype = ctypes.c_char_p
+    assert b"gfx950" in l.ks_build_info()
+    assert l.ks_device_count() >= 0
+
+
+def test_inspect_config2_layout():
+    d = inspect(synth.config2(1000))
+    assert d["T"] == 400 and d["R"] == 3 and d["templates"] == 1 and d["pods"] == 1000
+    assert "kubernetes.io/hostname" in d["keyNames"]
+    assert d["TW"] == 13  # 400 instance types -> 13 bitset words
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_inspect_random_problems(seed):
+    d = inspect(problems.random_problem(seed))
+    assert d["keys"] <= 64 and d["states"] >= d["pods"]
+
+
+def test_unsupported_topology_is_loud():
+    snap = synth.config2(10)
+    snap["topology"] = {"groups": []}
+    with pytest.raises(KsError) as e:
+        inspect(snap)
+    assert e.value.code == -2
+
+
+def test_unsupported_host_ports_is_loud():
+    snap = synth.config2(10)
+    snap["pods"][0]["spec"]["containers"][0]["ports"] = [{"hostPort": 80, "containerPort": 80}]
+    with pytest.raises(KsError) as e:
+        inspect(snap)
+    assert e.value.code == -2
+
+
+def test_duplicate_queue_key_is_loud():
+    snap = synth.config2(10)
+    snap["pods"][1] = dict(snap["pods"][0])
+    with pytest.raises(KsError) as e:
+        inspect(snap)
+    assert e.value.code == -2
+
+
+def test_bad_quantity_is_parse_error():
+    snap = synth.config2(10)
+    snap["pods"][0]["spec"]["containers"][0]["resources"]["requests"]["cpu"] = "12q"
+    with pytest.raises(KsError) as e:
+        inspect(snap)
+    assert e.value.code == -1

@@ -1,0 +1,91 @@
+"""GPU parity: the HIP Solve path through the C-ABI vs the oracle, bit-exact on the canonical
+Results (NewNodeClaims in final order with pods / instance-type options / requests / requirements,
+ExistingNodes with pods, PodErrors text).  Go map-order choices are canonicalised identically on
+both sides."""
+import json
+
+import pytest
+
+import problems
+from karpenter_amd import Scheduler, synth
+from oracle import bridge
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve_both(snap):
+    s = json.dumps(snap)
+    want, _ = bridge.solve(s)
+    got = Scheduler(s).solve()
+    return problems.canonical(want), got
+
+
+def _diff(want, got):
+    g = got.canonical()
+    if want == g:
+        return None
+    for key in ("newNodeClaims", "existingNodes", "podErrors"):
+        if want[key] != g[key]:
+            if isinstance(want[key], list):
+                for i, (a, b) in enumerate(zip(want[key], g[key])):
+                    if a != b:
+                        return "%s[%d]: want %s\n got %s" % (key, i, json.dumps(a)[:1500], json.dumps(b)[:1500])
+                return "%s: length %d vs %d" % (key, len(want[key]), len(g[key]))
+            ks = sorted(set(want[key]) | set(g[key]), key=lambda x: int(x))
+            for k in ks:
+                if want[key].get(k) != g[key].get(k):
+                    return "%s[%s]: want %r\n got %r" % (key, k, want[key].get(k), g[key].get(k))
+    return "differs"
+
+
+@pytest.mark.parametrize("seed", list(range(48)))
+def test_random_problem_parity(seed):
+    want, got = _solve_both(problems.random_problem(seed))
+    d = _diff(want, got)
+    assert d is None, d
+
+
+@pytest.mark.parametrize("seed", [100, 101, 102, 103])
+def test_random_problem_parity_larger(seed):
+    want, got = _solve_both(problems.random_problem(seed, n_pods=800, n_its=120, n_nodes=30))
+    d = _diff(want, got)
+    assert d is None, d
+
+
+def test_config1_benchmark_scheduling_2000():
+    """BenchmarkScheduling2000 (scheduling_benchmark_test.go:72-74,116-182)."""
+    want, got = _solve_both(synth.config1())
+    assert _diff(want, got) is None
+    assert len(got.pod_errors) == 0
+
+
+def test_config2_10k_parity():
+    want, got = _solve_both(synth.config2(10000))
+    assert _diff(want, got) is None
+
+
+def test_config2_full_size_properties():
+    """50k pods x 400 ITs: size-independent properties (oracle parity is checked at 10k)."""
+    snap = synth.config2(50000)
+    got = Scheduler(snap).solve()
+    placed = [p for c in got.new_nodeclaims for p in c["pods"]]
+    assert sorted(placed) == list(range(50000))  # every pod placed exactly once
+    assert not got.pod_errors
+    its = {it["name"]: it for it in snap["instanceTypes"]}
+    for c in got.new_nodeclaims:
+        # the claim's options all fit its accumulated requests (Fits, resources.go:162-175)
+        cpu_m = int(c["requests"]["cpu"].rstrip("m")) if c["requests"]["cpu"].endswith("m") else int(c["requests"]["cpu"]) * 1000
+        for name in c["instanceTypeOptions"]:
+            cap_m = int(its[name]["capacity"]["cpu"]) * 1000 - 100
+            assert cpu_m <= cap_m
+    # determinism: a second solve is identical
+    again = Scheduler(snap).solve()
+    assert again.canonical() == got.canonical()
+
+
+def test_replicas_identical():
+    snap = problems.random_problem(7)
+    sch = Scheduler(snap)
+    one = sch.solve(replicas=1).canonical()
+    many = sch.solve(replicas=64).canonical()
+    assert one == many
