@@ -159,6 +159,7 @@ struct GoSortExact {
         wasPartitioned = already;
         int leftLen = mid - a, rightLen = b - mid;
         int thr = length / 8;
+        if (sp + 2 > 64) return;  // unreachable: depth <= 2*log2(n) + 2
         if (leftLen < rightLen) {
           wasBalanced = leftLen >= thr;
           stack[sp++] = Frame{mid + 1, b, limit, wasBalanced, wasPartitioned};  // continuation

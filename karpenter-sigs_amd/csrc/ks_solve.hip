@@ -414,7 +414,10 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, cons
   uint32_t epoch = 1;
   int qhead = 0, qlen = P;
   int64_t pops = 0, sorts = 0, slow = 0;
-  const int64_t popCap = (int64_t)(P + 1) * (P + 1) * 8 + 1024;
+  // Every pop either places a pod, relaxes it, or marks it stale; the reference's queue can cycle
+  // O(P^2) in adversarial inputs, far beyond any realistic batch.  Bound it so a logic error ends the
+  // kernel with KE_ITER_CAP instead of hanging the device.
+  const int64_t popCap = (int64_t)64 * (d.S + P) + 100000;
   int err = KE_OK;
 
   while (qlen > 0) {
