@@ -12,9 +12,11 @@
 #include "ks_host.h"
 
 namespace ks {
-hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, int32_t* qorder, hipStream_t st,
+hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
+                        uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
                         hipEvent_t mid);
-size_t solve_lds_bytes(const KsDims& d);
+Plan make_plan(const KsDims& d, size_t budget);
+size_t queue_sort_temp_bytes(int n);
 }  // namespace ks
 
 using namespace ks;
@@ -139,7 +141,15 @@ struct ks_problem {
   int wreps = 0;
   hipStream_t stream = nullptr;
   int device = -1;
+  // NewQueue radix-sort workspace
+  uint64_t* skeys = nullptr;
+  int32_t* svals = nullptr;
+  void* stemp = nullptr;
+  size_t stempBytes = 0;
   ~ks_problem() {
+    if (skeys) (void)hipFree(skeys);
+    if (svals) (void)hipFree(svals);
+    if (stemp) (void)hipFree(stemp);
     if (dbuf) (void)hipFree(dbuf);
     if (wbuf) (void)hipFree(wbuf);
     if (works_dev) (void)hipFree(works_dev);
@@ -238,7 +248,8 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
   HIPCHK(hipStreamSynchronize(st));
   if (ctr[CT_ERROR] != KE_OK)
     throw KsError(ctr[CT_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
-                  ctr[CT_ERROR] == KE_CLAIM_CAP ? "NodeClaim capacity exceeded" : "solve kernel iteration cap hit");
+                  ctr[CT_ERROR] == KE_CLAIM_CAP ? "NodeClaim capacity (8192 per Solve) exceeded"
+                                                : "solve kernel iteration cap hit");
   int nc = (int)ctr[CT_NCLAIMS], nl = (int)ctr[CT_NLOG];
   std::vector<int32_t> order, ctpl, chost, logp, logt, status, fstate;
   std::vector<int64_t> creq;
@@ -432,6 +443,13 @@ int ks_problem_create(const char* json, size_t len, ks_problem** out) {
   HIPCHK(hipGetDevice(&pb->device));
   HIPCHK(hipStreamCreateWithFlags(&pb->stream, hipStreamNonBlocking));
   upload(pb.get());
+  {
+    size_t n = std::max(pb->host.dims.P, 1);
+    HIPCHK(hipMalloc(&pb->skeys, 2 * n * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&pb->svals, 2 * n * sizeof(int32_t)));
+    pb->stempBytes = std::max<size_t>(queue_sort_temp_bytes((int)n), 256);
+    HIPCHK(hipMalloc(&pb->stemp, pb->stempBytes));
+  }
   *out = pb.release();
   return KS_OK;
   API_CATCH
@@ -469,7 +487,11 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   int reps = opts && opts->replicas > 1 ? opts->replicas : 1;
   if (opts && opts->device >= 0) HIPCHK(hipSetDevice(opts->device));
   const KsDims& d = pb->host.dims;
-  if (solve_lds_bytes(d) > 160 * 1024) throw KsError(KS_ERR_CAPACITY, "solve state exceeds 160 KiB of LDS");
+  // one Solve per CU gets the whole 160 KiB; larger batches trade LDS for waves per CU
+  size_t budget = 160 * 1024 - 256;
+  if (reps > 256) budget = std::max<size_t>(24 * 1024, budget * 256 / reps);
+  Plan pl = make_plan(d, budget);
+  if (pl.lds > 160 * 1024) throw KsError(KS_ERR_CAPACITY, "solve state exceeds 160 KiB of LDS");
   WorkLayout wl = work_layout(d);
   size_t need = wl.total * reps;
   if (need > pb->wbytes || reps != pb->wreps) {
@@ -491,7 +513,8 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   HIPCHK(hipEventCreate(&em));
   HIPCHK(hipEventCreate(&e1));
   HIPCHK(hipEventRecord(e0, pb->stream));
-  HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, w0.qorder, pb->stream, em));
+  HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp, pb->stempBytes,
+                      pb->stream, em));
   HIPCHK(hipEventRecord(e1, pb->stream));
   HIPCHK(hipEventSynchronize(e1));
   float ms = 0, setup = 0;
@@ -543,8 +566,10 @@ int ks_results_json(const ks_results* r, char** json_out) {
   }
   o += "},\"stats\":{";
   static const char* names[] = {"nclaims", "ncommits", "hostnameCounter", "error", "pops", "algBytes",
-                                "sorts", "sortsWithDescent"};
-  for (int i = 0; i < 8; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
+                                "sorts", "sortsWithDescent", "claimFull", "claimQuickFail", "windows",
+                                "cycPop", "cycNodes", "cycSort", "cycQuick", "cycFull", "cycCommit", "cycTemplates",
+                                "cycTotal"};
+  for (int i = 0; i < 19; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
   o += "}}";
   *json_out = strdup(o.c_str());
   return KS_OK;

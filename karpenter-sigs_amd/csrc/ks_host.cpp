@@ -661,6 +661,7 @@ void Host::build(const Value& root) {
   }
   if (tab.tpl_its.empty()) tab.tpl_its.push_back(0);
   dims.maxTplIts = maxIts;
+  dims.totalTplIts = (int)tab.tpl_it_beg[NT];
   dims.TW = std::max(1, (maxIts + 31) / 32);
 
   // --- existing nodes (NewExistingNode, calculateExistingNodeClaims)
@@ -811,6 +812,19 @@ void Host::build(const Value& root) {
     S += (int)chain.size();
     states.push_back(std::move(chain));
   }
+  for (int c = 0; c < 4; c++) {
+    int64_t mn = 0, mx = 0;
+    for (int i = 0; i < P; i++) {
+      mn = i ? std::min(mn, sk[i][c]) : sk[i][c];
+      mx = i ? std::max(mx, sk[i][c]) : sk[i][c];
+    }
+    uint64_t span = (uint64_t)(mx - mn);
+    int bits = 0;
+    while (span) { bits++; span >>= 1; }
+    dims.skMin[c] = mn;
+    dims.skBits[c] = bits;
+  }
+  dims.dupUids = (int)uids.size() < P ? 1 : 0;
   {
     std::vector<int> idx(P);
     for (int i = 0; i < P; i++) idx[i] = i;

@@ -40,6 +40,19 @@ struct KsDims {
   int32_t hostnameSeed;
   uint64_t allowWK;    // WellKnownLabels key mask (AllowUndefinedWellKnownLabels)
   uint64_t itKeys;     // keys any instance type constrains, plus zone and capacity-type
+  int64_t skMin[4];    // queue sort key components: minimum and bit width of (value - min)
+  int32_t skBits[4];
+  int32_t dupUids;     // 1 if two pods share a UID (queue staleness then re-reads last_len)
+  int32_t totalTplIts; // sum of template instance-type list lengths
+};
+
+// Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
+struct Plan {
+  int32_t KO;      // order/okey capacity = max NodeClaims per solve
+  int32_t KL;      // claims [0, KL) keep template/requests/max/options in LDS, the rest in HBM
+  int32_t talloc;  // 1: template instance-type Allocatable tables are LDS-resident
+  int32_t pad;
+  uint64_t lds;    // dynamic LDS bytes
 };
 
 // Device view (all pointers into one HBM allocation).
@@ -111,7 +124,10 @@ struct KsWork {
 
 enum Counter {
   CT_NCLAIMS = 0, CT_NLOG, CT_HOSTCTR, CT_ERROR, CT_POPS, CT_ALGBYTES, CT_SORTS, CT_SORT_SLOW,
-  CT_CLAIM_FULL, CT_CLAIM_QUICK_FAIL, CT_NCOUNTERS = 16
+  CT_CLAIM_FULL, CT_CLAIM_QUICK_FAIL, CT_WINDOWS,
+  // diagnostic build (-DKS_PHASE_STATS): s_memtime cycles per phase
+  CT_CYC_POP, CT_CYC_NODES, CT_CYC_SORT, CT_CYC_QUICK, CT_CYC_FULL, CT_CYC_COMMIT, CT_CYC_TPL, CT_CYC_TOTAL,
+  CT_NCOUNTERS = 24
 };
 enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3 };
 

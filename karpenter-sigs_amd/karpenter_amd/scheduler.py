@@ -12,7 +12,9 @@ import json
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libkarpenter_amd.so")
+# KS_LIB_VARIANT=stats loads the diagnostic build with per-phase cycle counters.
+_LIB_PATH = os.path.join(_HERE, "libkarpenter_amd_stats.so" if os.environ.get("KS_LIB_VARIANT") == "stats"
+                         else "libkarpenter_amd.so")
 _lib = None
 
 KS_ERRORS = {-1: "KS_ERR_PARSE", -2: "KS_ERR_UNSUPPORTED", -3: "KS_ERR_CAPACITY", -4: "KS_ERR_HIP",
