@@ -89,3 +89,17 @@ def test_replicas_identical():
     one = sch.solve(replicas=1).canonical()
     many = sch.solve(replicas=64).canonical()
     assert one == many
+
+
+with open(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "scenarios.json")) as _f:
+    SCENARIOS = json.load(_f)
+
+
+@pytest.mark.parametrize("scn", SCENARIOS, ids=[s["name"] for s in SCENARIOS])
+def test_reference_scenarios_gpu(scn):
+    """suite_test.go known answers through the HIP path, plus bit-exact vs the oracle."""
+    import scenario_check
+
+    want, got = _solve_both(scn["snapshot"])
+    assert scenario_check.check(scn, got.canonical()) == []
+    assert _diff(want, got) is None
