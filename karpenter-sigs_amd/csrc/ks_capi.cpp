@@ -1,6 +1,6 @@
 // ks_capi.cpp — the C-ABI (include/karpenter_amd.h): HBM upload of the encoded problem, per-solve
 // workspace, kernel launch and reconstruction of scheduling.Results (scheduler.go:102-106).
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 
 #include <chrono>
 #include <cstring>

@@ -14,9 +14,10 @@
 
 namespace ks {
 
-struct GoSort {
-  int32_t* key;
-  int32_t* val;
+template <class P>
+struct GoSortT {
+  P key;
+  P val;
 
   KS_HD bool less(int i, int j) const { return key[i] < key[j]; }
   KS_HD void swap(int i, int j) {
@@ -125,13 +126,14 @@ struct GoSort {
 
 // State-carrying iterative pdqsort (exact Go semantics): each frame is either a fresh call
 // (wasBalanced = wasPartitioned = true) or the continuation of a loop with carried flags.
-struct GoSortExact {
-  GoSort s;
+template <class P>
+struct GoSortExactT {
+  GoSortT<P> s;
   KS_HD void run(int n) {
     struct Frame { int a, b, limit; bool wb, wp; };
     Frame stack[64];
     int sp = 0;
-    stack[sp++] = Frame{0, n, GoSort::bitsLen((uint32_t)n), true, true};
+    stack[sp++] = Frame{0, n, GoSortT<P>::bitsLen((uint32_t)n), true, true};
     while (sp > 0) {
       Frame f = stack[--sp];
       int a = f.a, b = f.b, limit = f.limit;
@@ -174,5 +176,8 @@ struct GoSortExact {
     }
   }
 };
+
+using GoSort = GoSortT<int32_t*>;
+using GoSortExact = GoSortExactT<int32_t*>;
 
 }  // namespace ks

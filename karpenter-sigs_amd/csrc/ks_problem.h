@@ -10,6 +10,17 @@
 
 #include "ks_reqset.h"
 
+// Explicit address spaces for device code: HBM tables are global (1), solver state is LDS (3).
+// Generic (flat) accesses would wait on both the vector-memory and LDS counters, i.e. on every
+// outstanding commit-log store.  Host compilation sees plain pointers (identical layout).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define KS_G __attribute__((address_space(1)))
+#define KS_L __attribute__((address_space(3)))
+#else
+#define KS_G
+#define KS_L
+#endif
+
 namespace ks {
 
 constexpr int kMaxR = 16;         // resource names per problem
@@ -58,68 +69,68 @@ struct Plan {
 // Device view (all pointers into one HBM allocation).
 struct KsDev {
   KsDims d;
-  const KeyMeta* keys;
-  const uint32_t* wordValid;
-  const uint32_t* vIsInt;
-  const int64_t* vInt;
+  const KeyMeta KS_G* keys;
+  const uint32_t KS_G* wordValid;
+  const uint32_t KS_G* vIsInt;
+  const int64_t KS_G* vInt;
   // instance types
-  const int64_t* it_alloc;    // [T][R]  Allocatable() = Capacity - Overhead (types.go:100-110)
-  const int64_t* it_cap;      // [T][R]
-  const uint32_t* it_rs;      // [T][RSW]
-  const int32_t* it_off_beg;  // [T+1] available offerings
-  const int32_t* off_zone;    // zone value bit
-  const int32_t* off_ct;      // capacity-type value bit
+  const int64_t KS_G* it_alloc;    // [T][R]  Allocatable() = Capacity - Overhead (types.go:100-110)
+  const int64_t KS_G* it_cap;      // [T][R]
+  const uint32_t KS_G* it_rs;      // [T][RSW]
+  const int32_t KS_G* it_off_beg;  // [T+1] available offerings
+  const int32_t KS_G* off_zone;    // zone value bit
+  const int32_t KS_G* off_ct;      // capacity-type value bit
   // templates (NodeClaimTemplates in caller order)
-  const uint32_t* tpl_rs;     // [NTPL][RSW] template requirements + hostname (private bit)
-  const uint64_t* tpl_taint;  // [NTPL][2]
-  const int64_t* tpl_daemon;  // [NTPL][R] getDaemonOverhead (scheduler.go:324-341)
-  const int32_t* tpl_it_beg;  // [NTPL+1]
-  const int32_t* tpl_its;     // IT index per template position
-  const int32_t* tpl_pool;    // [NTPL] limit pool or -1
+  const uint32_t KS_G* tpl_rs;     // [NTPL][RSW] template requirements + hostname (private bit)
+  const uint64_t KS_G* tpl_taint;  // [NTPL][2]
+  const int64_t KS_G* tpl_daemon;  // [NTPL][R] getDaemonOverhead (scheduler.go:324-341)
+  const int32_t KS_G* tpl_it_beg;  // [NTPL+1]
+  const int32_t KS_G* tpl_its;     // IT index per template position
+  const int32_t KS_G* tpl_pool;    // [NTPL] limit pool or -1
   // NodePool limits (remainingResources, scheduler.go:76-78,306-308)
-  const int64_t* pool_rem0;   // [NPOOL][R]
-  const uint32_t* pool_mask;  // [NPOOL] resource names present in the remaining ResourceList
+  const int64_t KS_G* pool_rem0;   // [NPOOL][R]
+  const uint32_t KS_G* pool_mask;  // [NPOOL] resource names present in the remaining ResourceList
   // pods
-  const int64_t* pod_req;     // [P][R] RequestsForPods(pod) (resources.go:27-35)
-  const int32_t* pod_state0;  // [P] first relaxation state
-  const int32_t* pod_nstate;  // [P]
-  const int32_t* pod_uid;     // [P] interned UID (queue staleness key, queue.go:54-69)
-  const int64_t* pod_sortkey; // [P][4] cpu, memory, creation second, uid rank (queue.go:83-112)
+  const int64_t KS_G* pod_req;     // [P][R] RequestsForPods(pod) (resources.go:27-35)
+  const int32_t KS_G* pod_state0;  // [P] first relaxation state
+  const int32_t KS_G* pod_nstate;  // [P]
+  const int32_t KS_G* pod_uid;     // [P] interned UID (queue staleness key, queue.go:54-69)
+  const int64_t KS_G* pod_sortkey; // [P][4] cpu, memory, creation second, uid rank (queue.go:83-112)
   // relaxation states (preferences.go:38-147 applied 0..n times)
-  const uint32_t* st_rs;      // [S][RSW] NewPodRequirements
-  const uint64_t* st_tol;     // [S][2] tolerated-taint masks
-  const int32_t* st_flags;    // [S]
+  const uint32_t KS_G* st_rs;      // [S][RSW] NewPodRequirements
+  const uint64_t KS_G* st_tol;     // [S][2] tolerated-taint masks
+  const int32_t KS_G* st_flags;    // [S]
   // existing nodes, in calculateExistingNodeClaims order (scheduler.go:313-321)
-  const int64_t* n_avail;     // [N][R] StateNode.Available()
-  const int64_t* n_req0;      // [N][R] remaining daemon requests (existingnode.go:43-52)
-  const uint32_t* n_rs0;      // [N][RSW] node labels + hostname
-  const uint64_t* n_taint;    // [N][2]
+  const int64_t KS_G* n_avail;     // [N][R] StateNode.Available()
+  const int64_t KS_G* n_req0;      // [N][R] remaining daemon requests (existingnode.go:43-52)
+  const uint32_t KS_G* n_rs0;      // [N][RSW] node labels + hostname
+  const uint64_t KS_G* n_taint;    // [N][2]
 };
 
 // Per-solve workspace (one slice per replica / simulation).
 struct KsWork {
-  int32_t* c_tpl;      // [Kcap]
-  int32_t* c_cnt;      // [Kcap]
-  int32_t* c_host;     // [Kcap] hostname-placeholder ordinal
-  int64_t* c_req;      // [Kcap][R]
-  int64_t* c_max;      // [Kcap][R] per-resource max Allocatable over the remaining options
-  uint32_t* c_rs;      // [Kcap][RSW]
-  uint32_t* c_rem;     // [Kcap][TW] InstanceTypeOptions as a bitset over the template list
-  int32_t* order;      // [Kcap] final s.newNodeClaims order
-  int64_t* n_req;      // [N][R]
-  uint32_t* n_rs;      // [N][RSW]
-  int32_t* queue;      // [P] ring
-  int32_t* qorder;     // [P] NewQueue order
-  int32_t* pod_state;  // [P] current relaxation state
-  uint64_t* last_len;  // [NU] (epoch << 32) | len
-  int32_t* log_pod;    // [P] commit log
-  int32_t* log_tgt;    // [P] >=0 claim id, <0 -(node+1)
-  int32_t* pod_status; // [P]
-  int32_t* pod_fstate; // [P] relaxation state of the final failed attempt
-  uint32_t* fail_code; // [P][NTPL]
-  int32_t* fail_host;  // [P][NTPL]
-  int64_t* pool_rem;   // [NPOOL][R]
-  int64_t* counters;   // [16]
+  int32_t KS_G* c_tpl;      // [Kcap]
+  int32_t KS_G* c_cnt;      // [Kcap]
+  int32_t KS_G* c_host;     // [Kcap] hostname-placeholder ordinal
+  int64_t KS_G* c_req;      // [Kcap][R]
+  int64_t KS_G* c_max;      // [Kcap][R] per-resource max Allocatable over the remaining options
+  uint32_t KS_G* c_rs;      // [Kcap][RSW]
+  uint32_t KS_G* c_rem;     // [Kcap][TW] InstanceTypeOptions as a bitset over the template list
+  int32_t KS_G* order;      // [Kcap] final s.newNodeClaims order
+  int64_t KS_G* n_req;      // [N][R]
+  uint32_t KS_G* n_rs;      // [N][RSW]
+  int32_t KS_G* queue;      // [P] ring
+  int32_t KS_G* qorder;     // [P] NewQueue order
+  int32_t KS_G* pod_state;  // [P] current relaxation state
+  uint64_t KS_G* last_len;  // [NU] (epoch << 32) | len
+  int32_t KS_G* log_pod;    // [P] commit log
+  int32_t KS_G* log_tgt;    // [P] >=0 claim id, <0 -(node+1)
+  int32_t KS_G* pod_status; // [P]
+  int32_t KS_G* pod_fstate; // [P] relaxation state of the final failed attempt
+  uint32_t KS_G* fail_code; // [P][NTPL]
+  int32_t KS_G* fail_host;  // [P][NTPL]
+  int64_t KS_G* pool_rem;   // [NPOOL][R]
+  int64_t KS_G* counters;   // [16]
 };
 
 enum Counter {

@@ -43,32 +43,38 @@ struct KeyMeta {
   int32_t pad[3];
 };
 
-struct ReqLayout {
+// The layout's table pointers are template parameters so device code keeps their address spaces
+// (LDS key table, HBM value tables); the host uses plain pointers (ReqLayout).
+template <class KP, class P32, class P64>
+struct ReqLayoutT {
   int32_t nkeys, W, NB, HDR, RSW;
-  const KeyMeta* keys;
-  const uint32_t* wordValid;  // [W] valid-bit mask per word (padding bits zero)
-  const uint32_t* vIsInt;     // [W] bit set when the value parses with strconv.Atoi
-  const int64_t* vInt;        // per-value int (indexed by keys[k].vint + bit)
+  KP keys;
+  P32 wordValid;  // [W] valid-bit mask per word (padding bits zero)
+  P32 vIsInt;     // [W] bit set when the value parses with strconv.Atoi
+  P64 vInt;       // per-value int (indexed by keys[k].vint + bit)
 };
+using ReqLayout = ReqLayoutT<const KeyMeta*, const uint32_t*, const int64_t*>;
 
-KS_HD uint64_t rd64(const uint32_t* r, int i) { return (uint64_t)r[i] | ((uint64_t)r[i + 1] << 32); }
-KS_HD void wr64(uint32_t* r, int i, uint64_t v) { r[i] = (uint32_t)v; r[i + 1] = (uint32_t)(v >> 32); }
+// Record accessors are templates over the record pointer type (LDS / HBM / host).
+template <class P> KS_HD uint64_t rd64(P r, int i) { return (uint64_t)r[i] | ((uint64_t)r[i + 1] << 32); }
+template <class P> KS_HD void wr64(P r, int i, uint64_t v) { r[i] = (uint32_t)v; r[i + 1] = (uint32_t)(v >> 32); }
 
-KS_HD uint64_t rs_present(const uint32_t* r) { return rd64(r, 0); }
-KS_HD uint64_t rs_compl(const uint32_t* r) { return rd64(r, 2); }
-KS_HD uint64_t rs_hasgt(const uint32_t* r) { return rd64(r, 4); }
-KS_HD uint64_t rs_haslt(const uint32_t* r) { return rd64(r, 6); }
-KS_HD int64_t rs_gt(const uint32_t* r, int slot) { return (int64_t)rd64(r, 8 + 4 * slot); }
-KS_HD int64_t rs_lt(const uint32_t* r, int slot) { return (int64_t)rd64(r, 8 + 4 * slot + 2); }
-KS_HD void rs_set_gt(uint32_t* r, int slot, int64_t v) { wr64(r, 8 + 4 * slot, (uint64_t)v); }
-KS_HD void rs_set_lt(uint32_t* r, int slot, int64_t v) { wr64(r, 8 + 4 * slot + 2, (uint64_t)v); }
+template <class P> KS_HD uint64_t rs_present(P r) { return rd64(r, 0); }
+template <class P> KS_HD uint64_t rs_compl(P r) { return rd64(r, 2); }
+template <class P> KS_HD uint64_t rs_hasgt(P r) { return rd64(r, 4); }
+template <class P> KS_HD uint64_t rs_haslt(P r) { return rd64(r, 6); }
+template <class P> KS_HD int64_t rs_gt(P r, int slot) { return (int64_t)rd64(r, 8 + 4 * slot); }
+template <class P> KS_HD int64_t rs_lt(P r, int slot) { return (int64_t)rd64(r, 8 + 4 * slot + 2); }
+template <class P> KS_HD void rs_set_gt(P r, int slot, int64_t v) { wr64(r, 8 + 4 * slot, (uint64_t)v); }
+template <class P> KS_HD void rs_set_lt(P r, int slot, int64_t v) { wr64(r, 8 + 4 * slot + 2, (uint64_t)v); }
 
 KS_HD bool bit(uint64_t m, int k) { return (m >> k) & 1ull; }
 
 // Values of word `w` (absolute word index) that lie within (gt, lt) — withinIntPtrs, requirement.go:238-254.
-KS_HD uint32_t within_word(const ReqLayout& L, int k, int wrel, bool hg, int64_t gt, bool hl, int64_t lt) {
+template <class LT>
+KS_HD uint32_t within_word(const LT& L, int k, int wrel, bool hg, int64_t gt, bool hl, int64_t lt) {
   if (!hg && !hl) return 0xffffffffu;
-  const KeyMeta& km = L.keys[k];
+  const KeyMeta km = L.keys[k];
   uint32_t isint = L.vIsInt[km.off + wrel];
   uint32_t m = 0;
   for (int b = 0; b < 32; b++) {
@@ -83,16 +89,17 @@ KS_HD uint32_t within_word(const ReqLayout& L, int k, int wrel, bool hg, int64_t
   return m;
 }
 
-KS_HD bool rs_any(const ReqLayout& L, const uint32_t* r, int k) {
-  const KeyMeta& km = L.keys[k];
-  const uint32_t* w = r + L.HDR + km.off;
+template <class LT, class PR>
+KS_HD bool rs_any(const LT& L, PR r, int k) {
+  const KeyMeta km = L.keys[k];
   for (int i = 0; i < km.nw; i++)
-    if (w[i]) return true;
+    if (r[L.HDR + km.off + i]) return true;
   return false;
 }
 
 // Requirement.Operator (requirement.go:197-208); a missing key reads as Exists (requirements.go:145-151).
-KS_HD int rs_op(const ReqLayout& L, const uint32_t* r, int k) {
+template <class LT, class PR>
+KS_HD int rs_op(const LT& L, PR r, int k) {
   if (!bit(rs_present(r), k)) return OP_EXISTS;
   bool any = rs_any(L, r, k);
   if (bit(rs_compl(r), k)) return any ? OP_NOTIN : OP_EXISTS;
@@ -102,9 +109,10 @@ KS_HD int rs_op(const ReqLayout& L, const uint32_t* r, int k) {
 KS_HD bool op_neg(int op) { return op == OP_NOTIN || op == OP_DNE; }
 
 // Has(value) for one universe bit (requirement.go:182-187).
-KS_HD bool rs_member(const ReqLayout& L, const uint32_t* r, int k, int v) {
+template <class LT, class PR>
+KS_HD bool rs_member(const LT& L, PR r, int k, int v) {
   if (!bit(rs_present(r), k)) return true;  // Get() of a missing key is Exists
-  const KeyMeta& km = L.keys[k];
+  const KeyMeta km = L.keys[k];
   uint32_t w = r[L.HDR + km.off + (v >> 5)];
   bool in = (w >> (v & 31)) & 1u;
   if (!bit(rs_compl(r), k)) return in;
@@ -123,9 +131,10 @@ struct KeyIx {  // the header part of a per-key Intersection result
   int64_t gt, lt;
 };
 
-KS_HD KeyIx key_ix_header(const ReqLayout& L, const uint32_t* a, const uint32_t* b, int k) {
+template <class LT, class PA, class PB>
+KS_HD KeyIx key_ix_header(const LT& L, PA a, PB b, int k) {
   KeyIx x;
-  const KeyMeta& km = L.keys[k];
+  const KeyMeta km = L.keys[k];
   bool ca = bit(rs_compl(a), k), cb = bit(rs_compl(b), k);
   bool ga = bit(rs_hasgt(a), k), gb = bit(rs_hasgt(b), k);
   bool la = bit(rs_haslt(a), k), lb = bit(rs_haslt(b), k);
@@ -145,8 +154,9 @@ KS_HD KeyIx key_ix_header(const ReqLayout& L, const uint32_t* a, const uint32_t*
 }
 
 // One word of Intersection(a_k, b_k) (requirement.go:128-161) before dropping bounds.
-KS_HD uint32_t key_ix_word(const ReqLayout& L, const uint32_t* a, const uint32_t* b, int k, int wrel, const KeyIx& x) {
-  const KeyMeta& km = L.keys[k];
+template <class LT, class PA, class PB>
+KS_HD uint32_t key_ix_word(const LT& L, PA a, PB b, int k, int wrel, const KeyIx& x) {
+  const KeyMeta km = L.keys[k];
   if (x.dne) return 0;
   bool ca = bit(rs_compl(a), k), cb = bit(rs_compl(b), k);
   uint32_t wa = a[L.HDR + km.off + wrel], wb = b[L.HDR + km.off + wrel];
@@ -160,18 +170,20 @@ KS_HD uint32_t key_ix_word(const ReqLayout& L, const uint32_t* a, const uint32_t
 }
 
 // Intersection(a_k, b_k).Len() == 0 (only non-complement results can be empty).
-KS_HD bool key_ix_empty(const ReqLayout& L, const uint32_t* a, const uint32_t* b, int k) {
+template <class LT, class PA, class PB>
+KS_HD bool key_ix_empty(const LT& L, PA a, PB b, int k) {
   KeyIx x = key_ix_header(L, a, b, k);
   if (x.dne) return true;
   if (x.compl_) return false;
-  const KeyMeta& km = L.keys[k];
+  const KeyMeta km = L.keys[k];
   for (int i = 0; i < km.nw; i++)
     if (key_ix_word(L, a, b, k, i, x)) return false;
   return true;
 }
 
 // Requirements.Compatible (requirements.go:163-174): failing keys of each kind go to the masks.
-KS_HD bool rs_compatible(const ReqLayout& L, const uint32_t* r, const uint32_t* in, uint64_t allowUndefined,
+template <class LT, class PR, class PI>
+KS_HD bool rs_compatible(const LT& L, PR r, PI in, uint64_t allowUndefined,
                          uint64_t* undefinedFail = nullptr, uint64_t* intersectFail = nullptr) {
   uint64_t pr = rs_present(r), pi = rs_present(in);
   uint64_t uf = 0, xf = 0;
@@ -196,7 +208,8 @@ KS_HD bool rs_compatible(const ReqLayout& L, const uint32_t* r, const uint32_t* 
 }
 
 // Requirements.Intersects (requirements.go:241-258).
-KS_HD bool rs_intersects(const ReqLayout& L, const uint32_t* r, const uint32_t* in) {
+template <class LT, class PR, class PI>
+KS_HD bool rs_intersects(const LT& L, PR r, PI in) {
   uint64_t both = rs_present(r) & rs_present(in);
   while (both) {
     int k = __builtin_ctzll(both);
@@ -210,8 +223,9 @@ KS_HD bool rs_intersects(const ReqLayout& L, const uint32_t* r, const uint32_t* 
 }
 
 // out_k = Intersection(a_k, b_k) written into `out` (out may alias a).
-KS_HD void rs_intersect_key(const ReqLayout& L, uint32_t* out, const uint32_t* a, const uint32_t* b, int k) {
-  const KeyMeta& km = L.keys[k];
+template <class LT, class PO, class PA, class PB>
+KS_HD void rs_intersect_key(const LT& L, PO out, PA a, PB b, int k) {
+  const KeyMeta km = L.keys[k];
   KeyIx x = key_ix_header(L, a, b, k);
   for (int i = 0; i < km.nw; i++) out[L.HDR + km.off + i] = key_ix_word(L, a, b, k, i, x);
   uint64_t one = 1ull << k;
@@ -231,8 +245,9 @@ KS_HD void rs_intersect_key(const ReqLayout& L, uint32_t* out, const uint32_t* a
 }
 
 // Copy key k of src into out.
-KS_HD void rs_copy_key(const ReqLayout& L, uint32_t* out, const uint32_t* src, int k) {
-  const KeyMeta& km = L.keys[k];
+template <class LT, class PO, class PS>
+KS_HD void rs_copy_key(const LT& L, PO out, PS src, int k) {
+  const KeyMeta km = L.keys[k];
   for (int i = 0; i < km.nw; i++) out[L.HDR + km.off + i] = src[L.HDR + km.off + i];
   uint64_t one = 1ull << k;
   for (int h = 0; h < 4; h++) {
@@ -246,7 +261,8 @@ KS_HD void rs_copy_key(const ReqLayout& L, uint32_t* out, const uint32_t* src, i
 }
 
 // Requirements.Add for every key of `in` (requirements.go:118-125): out &= in.
-KS_HD void rs_add(const ReqLayout& L, uint32_t* out, const uint32_t* in) {
+template <class LT, class PO, class PI>
+KS_HD void rs_add(const LT& L, PO out, PI in) {
   uint64_t pi = rs_present(in), po = rs_present(out);
   while (pi) {
     int k = __builtin_ctzll(pi);
@@ -257,14 +273,15 @@ KS_HD void rs_add(const ReqLayout& L, uint32_t* out, const uint32_t* in) {
 }
 
 // Do a and b agree on every key in `mask` (presence, header, words)?
-KS_HD bool rs_equal_keys(const ReqLayout& L, const uint32_t* a, const uint32_t* b, uint64_t mask) {
+template <class LT, class PA, class PB>
+KS_HD bool rs_equal_keys(const LT& L, PA a, PB b, uint64_t mask) {
   for (int h = 0; h < 4; h++)
     if ((rd64(a, 2 * h) ^ rd64(b, 2 * h)) & mask) return false;
   uint64_t m = mask & rs_present(a);
   while (m) {
     int k = __builtin_ctzll(m);
     m &= m - 1;
-    const KeyMeta& km = L.keys[k];
+    const KeyMeta km = L.keys[k];
     for (int i = 0; i < km.nw; i++)
       if (a[L.HDR + km.off + i] != b[L.HDR + km.off + i]) return false;
     if (km.bslot >= 0 && (rs_gt(a, km.bslot) != rs_gt(b, km.bslot) || rs_lt(a, km.bslot) != rs_lt(b, km.bslot)))

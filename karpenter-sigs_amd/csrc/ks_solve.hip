@@ -12,11 +12,14 @@
 //     the remaining-options bitset and the six filterResults flags in one pass
 //   - new NodeClaim per template (scheduler.go:258-283) incl. limits (filterByRemainingResources,
 //     subtractMax)
-// Latency is the bound (the chain is sequential), so the state every step touches lives in LDS:
-// the claim order and pod counts, each claim's template / requests / max-Allocatable / options
-// bitset (for the first Plan::KL claims), the templates' instance-type Allocatable tables, and a
-// 64-pod window of queue entries fetched with one coalesced gather per 64 pops.  HBM holds the
-// cold state (requirement records, existing nodes, overflow claims) and the commit log.
+// Latency is the bound (the chain is sequential), so everything a step touches lives in LDS: the
+// claim order and pod counts, each claim's template / requests / max-Allocatable / options bitset
+// (for the first Plan::KL claims), the templates' instance-type Allocatable tables, the remaining
+// NodePool limits and a 64-pod window of queue entries gathered once per 64 pops.  Pointers carry
+// explicit address spaces (ks_problem.h) so no access is a flat access, and lanes never hand data
+// to each other through HBM except at the window refill (behind one release fence, read with sc1
+// loads that bypass the L1).  HBM holds the cold state (requirement records, existing nodes,
+// overflow claims) and the write-only commit log.
 // Independent Solves (replicas, consolidation simulations) are independent workgroups, so a launch
 // of thousands of them fills the 256 CUs.  Nothing here is a dense contraction: no MFMA.
 #include <hip/hip_runtime.h>
@@ -27,12 +30,35 @@
 
 namespace ks {
 
+using LI32 = int32_t KS_L*;
+using LI64 = int64_t KS_L*;
+using LU32 = uint32_t KS_L*;
+using LU64 = uint64_t KS_L*;
+using GI32 = int32_t KS_G*;
+using GI64 = int64_t KS_G*;
+using GU32 = uint32_t KS_G*;
+using DevLayout = ReqLayoutT<const KeyMeta KS_L*, const uint32_t KS_G*, const int64_t KS_G*>;
+
 __device__ __forceinline__ int lane() { return (int)threadIdx.x; }
 __device__ __forceinline__ uint64_t wballot(bool p) { return __ballot(p ? 1 : 0); }
 __device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-// One-wave workgroup: s_barrier is cheap and orders LDS traffic between lanes.
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)x));
+}
+// Ordering point for LDS traffic between the lanes of the (single) wave: the wave's LDS operations
+// execute in order, so only the compiler must be kept from reordering; no s_waitcnt, no s_barrier.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+// HBM hand-off point (rare paths): every outstanding store of this wave completes first.
+__device__ __forceinline__ void hbm_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+template <class T>
+__device__ __forceinline__ T ld_sc1(const T KS_G* p) {  // L1-bypassing load of HBM state other lanes wrote
+  return __hip_atomic_load((T*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 #ifdef KS_PHASE_STATS
 #define PH_BEGIN(v) uint64_t v = __builtin_amdgcn_s_memtime()
@@ -60,7 +86,6 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
       W.pod_fstate[i] = -1;
     }
     for (int64_t i = gtid; i < d.NU; i += gsz) W.last_len[i] = 0;
-    for (int64_t i = gtid; i < (int64_t)d.NPOOL * d.R; i += gsz) W.pool_rem[i] = D.pool_rem0[i];
     for (int64_t i = gtid; i < CT_NCOUNTERS; i += gsz) W.counters[i] = 0;
   }
 }
@@ -68,62 +93,76 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
 // ------------------------------------------------------------------------------------------------
 // Solve
 // ------------------------------------------------------------------------------------------------
+template <bool INL> struct ClaimView;
+template <> struct ClaimView<true> { LI32 tpl; LI64 req; LI64 max; LU32 rem; };
+template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; };
+
+template <int RT>  // RT > 0: resource count known at compile time (loops unrolled, requests in VGPRs)
 struct Solver {
   const KsDev& D;
   const KsDims& d;
   const KsWork& W;
   const Plan& pl;
-  ReqLayout L;
-  // LDS-resident state
-  int32_t* s_order;   // [KO] s.newNodeClaims as claim ids
-  int32_t* s_okey;    // [KO] len(Pods) of the claim at each position
-  int32_t* s_ctpl;    // [KL]
-  int64_t* s_creq;    // [KL][R]
-  int64_t* s_cmax;    // [KL][R]
-  uint32_t* s_crem;   // [KL][TW]
-  int64_t* s_talloc;  // [totalTplIts][R] (pl.talloc)
-  int32_t* s_tbeg;    // [NTPL+1]
-  uint32_t* s_rs;     // [RSW] candidate requirements
-  uint32_t* s_rem;    // [TW+2] candidate options
-  uint32_t* s_cand;   // [TW+2] limit-filtered template options
-  int64_t* s_req;     // [kMaxR] candidate requests
-  // 64-pod window
-  int32_t *w_p, *w_uid, *w_s, *w_flags;
-  uint64_t *w_ll, *w_tol;
-  int64_t* w_req;
+  DevLayout L;
+  ClaimView<true> lc;   // claims [0, KL)
+  ClaimView<false> gc;  // claims [KL, KO)
+  LI32 s_order;         // [KO] s.newNodeClaims as claim ids
+  LI32 s_okey;          // [KO] len(Pods) of the claim at each position
+  LI64 s_talloc;        // [totalTplIts][R] Allocatable per template position (pl.talloc)
+  LI32 s_tbeg;          // [NTPL+1]
+  LI64 s_pool;          // [NPOOL][R] remaining limits
+  LU32 s_rs;            // [RSW] candidate requirements
+  LU32 s_rem;           // [TW+2] candidate options
+  LU32 s_cand;          // [TW+2] limit-filtered template options
+  LI32 w_p, w_uid, w_s, w_flags;
+  LU64 w_ll, w_tol;
+  LI64 w_req;
   int64_t algbytes = 0;
 
   __device__ Solver(const KsDev& D_, const KsWork& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
+  __device__ __forceinline__ int R() const { return RT > 0 ? RT : d.R; }
 
-  // claim-state accessors: LDS for c < KL, HBM otherwise
-  __device__ int ctpl(int c) const { return c < pl.KL ? s_ctpl[c] : W.c_tpl[c]; }
-  __device__ int64_t* creq(int c) const { return c < pl.KL ? s_creq + (int64_t)c * d.R : W.c_req + (int64_t)c * d.R; }
-  __device__ int64_t* cmax(int c) const { return c < pl.KL ? s_cmax + (int64_t)c * d.R : W.c_max + (int64_t)c * d.R; }
-  __device__ uint32_t* crem(int c) const { return c < pl.KL ? s_crem + (int64_t)c * d.TW : W.c_rem + (int64_t)c * d.TW; }
-  __device__ const int64_t* talloc(int gpos) const {  // Allocatable of template position gpos
-    return pl.talloc ? s_talloc + (int64_t)gpos * d.R : D.it_alloc + (int64_t)D.tpl_its[gpos] * d.R;
+  template <bool INL>
+  __device__ __forceinline__ const ClaimView<INL>& cv() const {
+    if constexpr (INL) return lc;
+    else return gc;
   }
 
-  __device__ bool fits(const int64_t* req, const int64_t* alloc) const {  // resources.go:162-175
-    for (int r = 0; r < d.R; r++) {
+  template <class P>
+  __device__ __forceinline__ bool fits(const int64_t* req, P alloc) const {  // resources.go:162-175
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+      if (RT == 0 && r >= d.R) break;
       const int64_t a = alloc[r];
-      if (a < 0 || req[r] > a) return false;
+      ok &= (a >= 0) & (req[r] <= a);
     }
-    return true;
+    return ok;
   }
-  __device__ bool has_offering(int it, const uint32_t* rs) const {  // nodeclaim.go:270-278
+  __device__ __forceinline__ bool fits_pos(const int64_t* req, int gpos) const {
+    if (pl.talloc) return fits(req, s_talloc + (int64_t)gpos * R());
+    return fits(req, D.it_alloc + (int64_t)D.tpl_its[gpos] * R());
+  }
+  __device__ __forceinline__ int64_t alloc_pos(int gpos, int r) const {
+    if (pl.talloc) return s_talloc[(int64_t)gpos * R() + r];
+    return D.it_alloc[(int64_t)D.tpl_its[gpos] * R() + r];
+  }
+  template <class PR>
+  __device__ __forceinline__ bool has_offering(int it, PR rs) const {  // nodeclaim.go:270-278
     const int b = D.it_off_beg[it], e = D.it_off_beg[it + 1];
     for (int o = b; o < e; o++)
       if (rs_member(L, rs, d.zoneKey, D.off_zone[o]) && rs_member(L, rs, d.ctKey, D.off_ct[o])) return true;
     return false;
   }
-  __device__ static bool tolerates(const uint64_t* taint, const uint64_t* tol) {
+  template <class PT, class PL>
+  __device__ static bool tolerates(PT taint, PL tol) {
     return ((taint[0] & ~tol[0]) | (taint[1] & ~tol[1])) == 0;
   }
-  __device__ void copy_words(uint32_t* dst, const uint32_t* src, int n) const {
+  template <class PD, class PS>
+  __device__ void copy_words(PD dst, PS src, int n) const {
     for (int i = lane(); i < n; i += kWave) dst[i] = src[i];
   }
-  __device__ void store_bits(uint32_t* dst, int base, uint64_t m) const {
+  __device__ void store_bits(LU32 dst, int base, uint64_t m) const {
     if (lane() == 0) {
       dst[base >> 5] = (uint32_t)m;
       if ((base >> 5) + 1 < d.TW) dst[(base >> 5) + 1] = (uint32_t)(m >> 32);
@@ -131,37 +170,47 @@ struct Solver {
   }
 
   // --- existing nodes (ExistingNode.Add, existingnode.go:64-124) -------------------------------
-  __device__ bool node_ok(int n, int s, int sflags, const int64_t* pod, const uint64_t* tol) const {
+  // Lane (n & 63) is the only lane that ever reads or writes node n's mutable state.
+  __device__ __forceinline__ bool node_ok(int n, int s, int sflags, const int64_t* pod, LU64 tol) const {
     if (!tolerates(D.n_taint + 2 * n, tol)) return false;
-    const int64_t* av = D.n_avail + (int64_t)n * d.R;
-    const int64_t* rq = W.n_req + (int64_t)n * d.R;
-    for (int r = 0; r < d.R; r++) {
+    const int64_t KS_G* av = D.n_avail + (int64_t)n * R();
+    const int64_t KS_G* rq = W.n_req + (int64_t)n * R();
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+      if (RT == 0 && r >= d.R) break;
       const int64_t a = av[r];
-      if (a < 0 || rq[r] + pod[r] > a) return false;
+      ok &= (a >= 0) & (rq[r] + pod[r] <= a);
     }
-    if (sflags & SF_HAS_KEYS)  // strict Compatible: no AllowUndefinedWellKnownLabels
-      return rs_compatible(L, W.n_rs + (int64_t)n * d.RSW, D.st_rs + (int64_t)s * d.RSW, 0);
-    return true;
+    if (ok && (sflags & SF_HAS_KEYS))  // strict Compatible: no AllowUndefinedWellKnownLabels
+      ok = rs_compatible(L, W.n_rs + (int64_t)n * d.RSW, D.st_rs + (int64_t)s * d.RSW, 0);
+    return ok;
   }
 
   // --- NodeClaim quick reject: necessary conditions of NodeClaim.Add ----------------------------
-  __device__ bool claim_quick(int c, int s, int sflags, const int64_t* pod, const uint64_t* tol) const {
-    const int t = ctpl(c);
+  template <bool INL>
+  __device__ __forceinline__ bool claim_quick(int c, int s, int sflags, const int64_t* pod, LU64 tol) const {
+    const ClaimView<INL>& v = cv<INL>();
+    const int t = v.tpl[c];
     if (!tolerates(D.tpl_taint + 2 * t, tol)) return false;
-    const int64_t* rq = creq(c);
-    const int64_t* mx = cmax(c);
-    for (int r = 0; r < d.R; r++)
-      if (rq[r] + pod[r] > mx[r]) return false;
-    if (sflags & SF_HAS_KEYS)
-      return rs_compatible(L, W.c_rs + (int64_t)c * d.RSW, D.st_rs + (int64_t)s * d.RSW, d.allowWK);
-    return true;
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+      if (RT == 0 && r >= d.R) break;
+      ok &= v.req[(int64_t)c * R() + r] + pod[r] <= v.max[(int64_t)c * R() + r];
+    }
+    if (ok && (sflags & SF_HAS_KEYS))
+      ok = rs_compatible(L, W.c_rs + (int64_t)c * d.RSW, D.st_rs + (int64_t)s * d.RSW, d.allowWK);
+    return ok;
   }
 
-  // --- wave-cooperative NodeClaim.Add on claim c: builds s_rs / s_req / s_rem; true if any IT remains
-  __device__ bool claim_full(int c, int s, int sflags, const int64_t* pod) {
+  // --- wave-cooperative NodeClaim.Add on claim c: builds s_rs / s_rem and the new requests --------
+  template <bool INL>
+  __device__ __forceinline__ bool claim_full(int c, int s, int sflags, const int64_t* pod, int64_t* req) {
+    const ClaimView<INL>& v = cv<INL>();
     bool changed = false;
     if (sflags & SF_HAS_KEYS) {
-      const uint32_t* crs = W.c_rs + (int64_t)c * d.RSW;
+      const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
       copy_words(s_rs, crs, d.RSW);
       wsync();
       if (lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
@@ -169,27 +218,27 @@ struct Solver {
       changed = (sflags & SF_TOUCHES_IT_KEYS) && !rs_equal_keys(L, s_rs, crs, d.itKeys);
       algbytes += 8 * d.RSW;
     }
-    const int t = ctpl(c);
-    const int64_t* crq = creq(c);
-    if (lane() < d.R) s_req[lane()] = crq[lane()] + pod[lane()];
-    wsync();
+    const int t = uni(v.tpl[c]);
+#pragma unroll
+    for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+      if (RT == 0 && r >= d.R) break;
+      req[r] = v.req[(int64_t)c * R() + r] + pod[r];
+    }
     const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
-    const uint32_t* rem = crem(c);
     uint64_t any = 0;
     int scanned = 0;
     for (int base = 0; base < nIT; base += kWave) {
       const int wi = base >> 5;
-      const uint64_t bits = (uint64_t)rem[wi] | (wi + 1 < d.TW ? (uint64_t)rem[wi + 1] << 32 : 0ull);
+      const uint64_t bits = (uint64_t)v.rem[(int64_t)c * d.TW + wi] |
+                            (wi + 1 < d.TW ? (uint64_t)v.rem[(int64_t)c * d.TW + wi + 1] << 32 : 0ull);
       uint64_t m = 0;
       if (bits) {
-        const int pos = base + lane();
+        const int gpos = tb + base + lane();
         bool ok = (bits >> lane()) & 1ull;
-        if (ok) {
-          ok = fits(s_req, talloc(tb + pos));
-          if (ok && changed) {
-            const int it = D.tpl_its[tb + pos];
-            ok = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs) && has_offering(it, s_rs);
-          }
+        if (ok) ok = fits_pos(req, gpos);
+        if (ok && changed) {
+          const int it = D.tpl_its[gpos];
+          ok = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs) && has_offering(it, s_rs);
         }
         m = wballot(ok);
         scanned += __popcll(bits);
@@ -197,41 +246,44 @@ struct Solver {
       store_bits(s_rem, base, m);
       any |= m;
     }
-    algbytes += 4 * d.TW + 16 * d.R + (int64_t)scanned * 8 * d.R;
+    algbytes += 4 * d.TW + 16 * R() + (int64_t)scanned * 8 * R();
     wsync();
     return any != 0;
   }
 
-  // max Allocatable per resource over the options in `bits` (quick-reject bound)
-  __device__ void update_max(int c, const uint32_t* bits, int t) {
+  // exact max Allocatable per resource over the options (quick-reject bound)
+  template <bool INL, class PB>
+  __device__ __forceinline__ void recompute_max(int c, PB bits, int t) {
+    const ClaimView<INL>& v = cv<INL>();
     const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
-    int64_t* mx = cmax(c);
-    for (int r = 0; r < d.R; r++) {
+    for (int r = 0; r < R(); r++) {
       int64_t m = INT64_MIN;
       for (int pos = lane(); pos < nIT; pos += kWave)
         if ((bits[pos >> 5] >> (pos & 31)) & 1u) {
-          const int64_t a = talloc(tb + pos)[r];
+          const int64_t a = alloc_pos(tb + pos, r);
           m = a > m ? a : m;
         }
       for (int off = 32; off >= 1; off >>= 1) {
         const int64_t o = __shfl_xor(m, off);
         m = o > m ? o : m;
       }
-      if (lane() == 0) mx[r] = m;
+      if (lane() == 0) v.max[(int64_t)c * R() + r] = m;
     }
     wsync();
   }
 
-  __device__ void commit_claim(int c, int pos, int p, int sflags, int& nlog) {
-    int64_t* crq = creq(c);
-    if (lane() < d.R) crq[lane()] = s_req[lane()];
-    if (sflags & SF_HAS_KEYS) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
-    uint32_t* rem = crem(c);
-    bool diff = false;
-    for (int i = lane(); i < d.TW; i += kWave) {
-      diff |= rem[i] != s_rem[i];
-      rem[i] = s_rem[i];
+  template <bool INL>
+  __device__ __forceinline__ void commit_claim(int c, int pos, int p, int sflags, const int64_t* req, int& nlog) {
+    const ClaimView<INL>& v = cv<INL>();
+    if (lane() == 0) {
+#pragma unroll
+      for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+        if (RT == 0 && r >= d.R) break;
+        v.req[(int64_t)c * R() + r] = req[r];
+      }
     }
+    if (sflags & SF_HAS_KEYS) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
+    copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     if (lane() == 0) {
       s_okey[pos] += 1;
       W.log_pod[nlog] = p;
@@ -239,17 +291,17 @@ struct Solver {
       W.pod_status[p] = ST_SCHEDULED;
     }
     nlog++;
-    // HBM-resident claim state (requirements, overflow claims) is re-read by other lanes
-    if ((sflags & SF_HAS_KEYS) || c >= pl.KL) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    // The max bound stays valid as the options only shrink; it is tightened lazily when a full check
+    // fails.  HBM-resident claim state is re-read by other lanes: drain the stores first.
+    if ((sflags & SF_HAS_KEYS) || !INL) hbm_release();
     wsync();
-    if (wballot(diff)) update_max(c, s_rem, ctpl(c));
-    algbytes += 16 * d.R + 4 * d.TW;
+    algbytes += 16 * R() + 4 * d.TW;
   }
 
   // --- new NodeClaim from each template in order (scheduler.go:258-283) -----------------------
   // Returns 1 placed, 0 failed (fail codes recorded), 2 no templates (add() returns nil), -1 cap.
-  __device__ int try_templates(int p, int s, int sflags, const int64_t* pod, const uint64_t* tol, int& nclaims,
-                               int& nlog, int& hostCtr) {
+  __device__ __forceinline__ int try_templates(int p, int s, int sflags, const int64_t* pod, LU64 tol, int& nclaims, int& nlog,
+                               int& hostCtr) {
     if (d.NTPL == 0) return 2;
     for (int t = 0; t < d.NTPL; t++) {
       uint32_t code = FC_NONE;
@@ -263,10 +315,9 @@ struct Solver {
         bool ok = pos < nIT;
         if (ok && pool >= 0) {
           const uint32_t mask = D.pool_mask[pool];
-          const int64_t* cap = D.it_cap + (int64_t)D.tpl_its[tb + pos] * d.R;
-          const int64_t* rem = W.pool_rem + (int64_t)pool * d.R;
-          for (int r = 0; r < d.R; r++)
-            if (((mask >> r) & 1u) && cap[r] > rem[r]) ok = false;
+          const int64_t KS_G* cap = D.it_cap + (int64_t)D.tpl_its[tb + pos] * R();
+          for (int r = 0; r < R(); r++)
+            if (((mask >> r) & 1u) && cap[r] > s_pool[(int64_t)pool * R() + r]) ok = false;
         }
         const uint64_t m = wballot(ok);
         store_bits(s_cand, base, m);
@@ -291,8 +342,8 @@ struct Solver {
           if (!ok) {
             code = FC_COMPAT;
           } else {
-            if (lane() < d.R) s_req[lane()] = D.tpl_daemon[(int64_t)t * d.R + lane()] + pod[lane()];
-            wsync();
+            int64_t req[RT > 0 ? RT : kMaxR];
+            for (int r = 0; r < R(); r++) req[r] = D.tpl_daemon[(int64_t)t * R() + r] + pod[r];
             uint32_t flags = 0;
             uint64_t any = 0;
             for (int base = 0; base < nIT; base += kWave) {
@@ -302,7 +353,7 @@ struct Solver {
               if (in) {
                 const int it = D.tpl_its[tb + pos];
                 ic = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs);
-                fi = fits(s_req, talloc(tb + pos));
+                fi = fits_pos(req, tb + pos);
                 of = has_offering(it, s_rs);
               }
               if (wballot(ic)) flags |= FF_REQ;
@@ -315,7 +366,7 @@ struct Solver {
               store_bits(s_rem, base, m);
               any |= m;
             }
-            algbytes += 4 * d.RSW + (int64_t)nIT * (8 * d.R + 4 * d.RSW + 16);
+            algbytes += 4 * d.RSW + (int64_t)nIT * (8 * R() + 4 * d.RSW + 16);
             wsync();
             if (any == 0) {
               code = FC_NO_IT | (flags << 8);
@@ -323,10 +374,17 @@ struct Solver {
               if (nclaims >= pl.KO) return -1;
               const int c = nclaims++;
               copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
-              copy_words(crem(c), s_rem, d.TW);
-              if (lane() < d.R) creq(c)[lane()] = s_req[lane()];
+              if (c < pl.KL) {
+                copy_words(lc.rem + (int64_t)c * d.TW, s_rem, d.TW);
+              } else {
+                copy_words(gc.rem + (int64_t)c * d.TW, s_rem, d.TW);
+              }
               if (lane() == 0) {
-                if (c < pl.KL) s_ctpl[c] = t;
+                for (int r = 0; r < R(); r++) {
+                  if (c < pl.KL) lc.req[(int64_t)c * R() + r] = req[r];
+                  else gc.req[(int64_t)c * R() + r] = req[r];
+                }
+                if (c < pl.KL) lc.tpl[c] = t;
                 W.c_tpl[c] = t;
                 W.c_host[c] = hostid;
                 s_order[c] = c;
@@ -336,28 +394,28 @@ struct Solver {
                 W.pod_status[p] = ST_SCHEDULED;
               }
               nlog++;
-              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+              hbm_release();  // c_rs / c_tpl / overflow state are read by other lanes later
               wsync();
-              update_max(c, s_rem, t);
+              if (c < pl.KL) recompute_max<true>(c, s_rem, t);
+              else recompute_max<false>(c, s_rem, t);
               if (pool >= 0) {  // subtractMax (scheduler.go:347-362)
                 const uint32_t mask = D.pool_mask[pool];
-                for (int r = 0; r < d.R; r++) {
+                for (int r = 0; r < R(); r++) {
                   if (!((mask >> r) & 1u)) continue;
                   int64_t m = INT64_MIN;
                   for (int pos = lane(); pos < nIT; pos += kWave)
                     if ((s_rem[pos >> 5] >> (pos & 31)) & 1u) {
-                      const int64_t v = D.it_cap[(int64_t)D.tpl_its[tb + pos] * d.R + r];
+                      const int64_t v = D.it_cap[(int64_t)D.tpl_its[tb + pos] * R() + r];
                       m = v > m ? v : m;
                     }
                   for (int off = 32; off >= 1; off >>= 1) {
                     const int64_t o = __shfl_xor(m, off);
                     m = o > m ? o : m;
                   }
-                  if (lane() == 0) W.pool_rem[(int64_t)pool * d.R + r] -= m;
+                  if (lane() == 0) s_pool[(int64_t)pool * R() + r] -= m;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                wsync();
               }
-              wsync();
               return 1;
             }
           }
@@ -372,7 +430,7 @@ struct Solver {
   }
 
   // --- s.newNodeClaims re-sort (scheduler.go:247) --------------------------------------------------
-  __device__ void sort_claims(int n, int64_t& sorts, int64_t& slow) {
+  __device__ __forceinline__ void sort_claims(int n, int64_t& sorts, int64_t& slow) {
     bool desc = false;
     for (int base = 0; base < n; base += kWave) {
       const int j = base + lane();
@@ -383,67 +441,76 @@ struct Solver {
     if (!desc) return;  // non-decreasing: pdqsort performs no swap
     slow++;
     if (lane() == 0) {
-      GoSortExact g{GoSort{s_okey, s_order}};
+      GoSortExactT<LI32> g{GoSortT<LI32>{s_okey, s_order}};
       g.run(n);
     }
     wsync();
   }
 
-  // --- 64-pod queue window -------------------------------------------------------------------------
-  __device__ void refill(int qhead, int qlen, int P) {
+  // --- 64-pod queue window: one gather per 64 pops ---------------------------------------------
+  __device__ __forceinline__ void refill(int qhead, int qlen, int P) {
+    hbm_release();  // queue pushes / relaxation states / staleness words of this wave have landed
     const int n = qlen < kWave ? qlen : kWave;
     if (lane() < n) {
       int pos = qhead + lane();
       if (pos >= P) pos -= P;
-      const int p = W.queue[pos];
+      const int p = ld_sc1(W.queue + pos);
       const int uid = D.pod_uid[p];
-      const int s = W.pod_state[p];
+      const int s = ld_sc1(W.pod_state + p);
       w_p[lane()] = p;
       w_uid[lane()] = uid;
       w_s[lane()] = s;
-      w_ll[lane()] = W.last_len[uid];
+      w_ll[lane()] = ld_sc1(W.last_len + uid);
       w_flags[lane()] = D.st_flags[s];
       w_tol[2 * lane()] = D.st_tol[2 * s];
       w_tol[2 * lane() + 1] = D.st_tol[2 * s + 1];
-      for (int r = 0; r < d.R; r++) w_req[lane() * d.R + r] = D.pod_req[(int64_t)p * d.R + r];
+      for (int r = 0; r < R(); r++) w_req[lane() * R() + r] = D.pod_req[(int64_t)p * R() + r];
     }
     wsync();
   }
 };
 
+template <int RT>
 __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan pl) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  extern __shared__ __attribute__((aligned(16))) char smem_generic[];
+  char KS_L* smem = (char KS_L*)smem_generic;
   const KsWork W = works[blockIdx.x];
   const KsDims& d = D.d;
-  Solver S(D, W, pl);
-  char* sp = smem;
-  auto take = [&](size_t bytes) { char* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
-  KeyMeta* s_keys = (KeyMeta*)take(sizeof(KeyMeta) * d.NK);
-  S.s_order = (int32_t*)take(4 * (size_t)pl.KO);
-  S.s_okey = (int32_t*)take(4 * (size_t)pl.KO);
-  S.s_ctpl = (int32_t*)take(4 * (size_t)pl.KL);
-  S.s_creq = (int64_t*)take(8 * (size_t)pl.KL * d.R);
-  S.s_cmax = (int64_t*)take(8 * (size_t)pl.KL * d.R);
-  S.s_crem = (uint32_t*)take(4 * (size_t)pl.KL * d.TW);
-  S.s_talloc = (int64_t*)take(pl.talloc ? 8 * (size_t)d.totalTplIts * d.R : 0);
-  S.s_tbeg = (int32_t*)take(4 * (size_t)(d.NTPL + 1));
-  S.s_rs = (uint32_t*)take(4 * (size_t)d.RSW);
-  S.s_rem = (uint32_t*)take(4 * (size_t)d.TW + 8);
-  S.s_cand = (uint32_t*)take(4 * (size_t)d.TW + 8);
-  S.s_req = (int64_t*)take(8 * kMaxR);
-  S.w_p = (int32_t*)take(4 * kWave);
-  S.w_uid = (int32_t*)take(4 * kWave);
-  S.w_s = (int32_t*)take(4 * kWave);
-  S.w_flags = (int32_t*)take(4 * kWave);
-  S.w_ll = (uint64_t*)take(8 * kWave);
-  S.w_tol = (uint64_t*)take(16 * kWave);
-  S.w_req = (int64_t*)take(8 * (size_t)kWave * d.R);
+  Solver<RT> S(D, W, pl);
+  const int R = S.R();
+  char KS_L* sp = smem;
+  auto take = [&](size_t bytes) { char KS_L* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
+  KeyMeta KS_L* s_keys = (KeyMeta KS_L*)take(sizeof(KeyMeta) * d.NK);
+  S.s_order = (LI32)take(4 * (size_t)pl.KO);
+  S.s_okey = (LI32)take(4 * (size_t)pl.KO);
+  S.lc.tpl = (LI32)take(4 * (size_t)pl.KL);
+  S.lc.req = (LI64)take(8 * (size_t)pl.KL * R);
+  S.lc.max = (LI64)take(8 * (size_t)pl.KL * R);
+  S.lc.rem = (LU32)take(4 * (size_t)pl.KL * d.TW);
+  S.s_talloc = (LI64)take(pl.talloc ? 8 * (size_t)d.totalTplIts * R : 0);
+  S.s_tbeg = (LI32)take(4 * (size_t)(d.NTPL + 1));
+  S.s_pool = (LI64)take(8 * (size_t)(d.NPOOL + 1) * R);
+  S.s_rs = (LU32)take(4 * (size_t)d.RSW);
+  S.s_rem = (LU32)take(4 * (size_t)d.TW + 8);
+  S.s_cand = (LU32)take(4 * (size_t)d.TW + 8);
+  S.w_p = (LI32)take(4 * kWave);
+  S.w_uid = (LI32)take(4 * kWave);
+  S.w_s = (LI32)take(4 * kWave);
+  S.w_flags = (LI32)take(4 * kWave);
+  S.w_ll = (LU64)take(8 * kWave);
+  S.w_tol = (LU64)take(16 * kWave);
+  S.w_req = (LI64)take(8 * (size_t)kWave * R);
+  S.gc.tpl = W.c_tpl;
+  S.gc.req = W.c_req;
+  S.gc.max = W.c_max;
+  S.gc.rem = W.c_rem;
   for (int i = lane(); i < d.NK * (int)(sizeof(KeyMeta) / 4); i += kWave)
-    ((uint32_t*)s_keys)[i] = ((const uint32_t*)D.keys)[i];
+    ((uint32_t KS_L*)s_keys)[i] = ((const uint32_t KS_G*)D.keys)[i];
   for (int i = lane(); i <= d.NTPL; i += kWave) S.s_tbeg[i] = D.tpl_it_beg[i];
+  for (int i = lane(); i < d.NPOOL * R; i += kWave) S.s_pool[i] = D.pool_rem0[i];
   if (pl.talloc)
-    for (int i = lane(); i < d.totalTplIts * d.R; i += kWave)
-      S.s_talloc[i] = D.it_alloc[(int64_t)D.tpl_its[i / d.R] * d.R + i % d.R];
+    for (int i = lane(); i < d.totalTplIts * R; i += kWave)
+      S.s_talloc[i] = D.it_alloc[(int64_t)D.tpl_its[i / R] * R + i % R];
   S.L.nkeys = d.NK;
   S.L.W = d.W;
   S.L.NB = d.NB;
@@ -460,12 +527,14 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   uint32_t epoch = 1;
   int qhead = 0, qlen = P;
   int wn = 0, wi = 0;  // window size / next index
-  int64_t pops = 0, sorts = 0, slow = 0, windows = 0;
+  int64_t pops = 0, sorts = 0, slow = 0, windows = 0, fulls = 0, fullFails = 0;
   // Every pop either places a pod, relaxes it, or marks it stale; the reference's queue can cycle
   // O(P^2) in adversarial inputs, far beyond any realistic batch.  Bound it so a logic error ends the
   // kernel with KE_ITER_CAP instead of hanging the device.
   const int64_t popCap = (int64_t)64 * (d.S + P) + 100000;
   int err = KE_OK;
+  int64_t pod[RT > 0 ? RT : kMaxR];
+  int64_t req[RT > 0 ? RT : kMaxR];
 #ifdef KS_PHASE_STATS
   uint64_t cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t tstart = __builtin_amdgcn_s_memtime();
@@ -482,15 +551,19 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     // Queue.Pop (queue.go:46-61)
     const int p = uni(S.w_p[wi]);
     const int uid = uni(S.w_uid[wi]);
-    const uint64_t ll = d.dupUids ? W.last_len[uid] : S.w_ll[wi];
+    uint64_t ll = S.w_ll[wi];
+    if (d.dupUids) {
+      hbm_release();
+      ll = ld_sc1(W.last_len + uid);
+    }
     if ((uint32_t)(ll >> 32) == epoch && (uint32_t)ll == (uint32_t)qlen) break;
     qhead = qhead + 1 == P ? 0 : qhead + 1;
     qlen--;
     if (++pops > popCap) { err = KE_ITER_CAP; break; }
     const int s = uni(S.w_s[wi]);
     const int sflags = uni(S.w_flags[wi]);
-    const int64_t* pod = S.w_req + wi * d.R;
-    const uint64_t* tol = S.w_tol + 2 * wi;
+    for (int r = 0; r < R; r++) pod[r] = uni64(S.w_req[wi * R + r]);
+    const LU64 tol = S.w_tol + 2 * wi;
     wi++;
     PH_END(t0, 0);
     bool placed = false;
@@ -500,12 +573,13 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
       const int n = base + lane();
       const bool ok = n < d.N && S.node_ok(n, s, sflags, pod, tol);
       const uint64_t m = wballot(ok);
-      S.algbytes += (int64_t)min(kWave, d.N - base) * (16 * d.R + 16);
+      S.algbytes += (int64_t)min(kWave, d.N - base) * (16 * R + 16);
       if (m) {
         const int j = base + ctz64(m);
-        if (lane() < d.R) W.n_req[(int64_t)j * d.R + lane()] += pod[lane()];
-        if ((sflags & SF_HAS_KEYS) && lane() == 0)
-          rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+        if (lane() == (j & (kWave - 1))) {  // the owner lane of node j
+          for (int r = 0; r < R; r++) W.n_req[(int64_t)j * R + r] += pod[r];
+          if (sflags & SF_HAS_KEYS) rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+        }
         if (lane() == 0) {
           W.log_pod[nlog] = p;
           W.log_tgt[nlog] = -(j + 1);
@@ -513,8 +587,6 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
         }
         nlog++;
         placed = true;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // n_req / n_rs are re-read by other lanes
-        wsync();
       }
     }
     PH_END(t1, 1);
@@ -526,23 +598,38 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
       for (int base = 0; base < nclaims && !placed; base += kWave) {
         PH_BEGIN(t3);
         const int j = base + lane();
-        const bool q = j < nclaims && S.claim_quick(S.s_order[j], s, sflags, pod, tol);
+        bool q = false;
+        if (j < nclaims) {
+          const int c = S.s_order[j];
+          q = c < pl.KL ? S.template claim_quick<true>(c, s, sflags, pod, tol)
+                        : S.template claim_quick<false>(c, s, sflags, pod, tol);
+        }
         uint64_t m = wballot(q);
-        S.algbytes += (int64_t)min(kWave, nclaims - base) * (16 * d.R + 4);
+        S.algbytes += (int64_t)min(kWave, nclaims - base) * (16 * R + 4);
         PH_END(t3, 3);
         while (m && !placed) {
           const int jj = base + ctz64(m);
           m &= m - 1;
           const int c = uni(S.s_order[jj]);
           PH_BEGIN(t4);
-          const bool ok = S.claim_full(c, s, sflags, pod);
+          const bool inl = c < pl.KL;
+          const bool ok = inl ? S.template claim_full<true>(c, s, sflags, pod, req)
+                              : S.template claim_full<false>(c, s, sflags, pod, req);
+          fulls++;
           PH_END(t4, 4);
+          PH_BEGIN(t5);
           if (ok) {
-            PH_BEGIN(t5);
-            S.commit_claim(c, jj, p, sflags, nlog);
-            PH_END(t5, 5);
+            if (inl) S.template commit_claim<true>(c, jj, p, sflags, req, nlog);
+            else S.template commit_claim<false>(c, jj, p, sflags, req, nlog);
             placed = true;
+          } else {
+            // the quick bound was stale: tighten it to the exact max over the current options
+            fullFails++;
+            const int t = inl ? uni(S.lc.tpl[c]) : uni(W.c_tpl[c]);
+            if (inl) S.template recompute_max<true>(c, S.lc.rem + (int64_t)c * d.TW, t);
+            else S.template recompute_max<false>(c, S.gc.rem + (int64_t)c * d.TW, t);
           }
+          PH_END(t5, 5);
         }
       }
     }
@@ -573,14 +660,12 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     if (lane() == 0) W.queue[tail] = p;
     qlen++;
     if (!relaxed && lane() == 0) W.last_len[uid] = ((uint64_t)epoch << 32) | (uint32_t)qlen;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // queue / pod_state are re-read by the window
-    wsync();
   }
   // write back LDS-resident claim state for the host
   for (int i = lane(); i < nclaims; i += kWave) W.order[i] = S.s_order[i];
   const int kl = nclaims < pl.KL ? nclaims : pl.KL;
-  for (int i = lane(); i < kl * d.R; i += kWave) W.c_req[i] = S.s_creq[i];
-  for (int i = lane(); i < kl * d.TW; i += kWave) W.c_rem[i] = S.s_crem[i];
+  for (int i = lane(); i < kl * R; i += kWave) W.c_req[i] = S.lc.req[i];
+  for (int i = lane(); i < kl * d.TW; i += kWave) W.c_rem[i] = S.lc.rem[i];
   if (lane() == 0) {
     W.counters[CT_NCLAIMS] = nclaims;
     W.counters[CT_NLOG] = nlog;
@@ -590,6 +675,8 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     W.counters[CT_ALGBYTES] = S.algbytes;
     W.counters[CT_SORTS] = sorts;
     W.counters[CT_SORT_SLOW] = slow;
+    W.counters[CT_CLAIM_FULL] = fulls;
+    W.counters[CT_CLAIM_QUICK_FAIL] = fullFails;
     W.counters[CT_WINDOWS] = windows;
 #ifdef KS_PHASE_STATS
     for (int i = 0; i < 7; i++) W.counters[CT_CYC_POP + i] = (int64_t)cyc[i];
@@ -604,17 +691,18 @@ Plan make_plan(const KsDims& d, size_t budget) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   Plan pl{};
   pl.KO = d.Kcap < 8192 ? d.Kcap : 8192;
-  const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(4 * (size_t)d.RSW) +
-                       2 * r16(4 * (size_t)d.TW + 8) + r16(8 * kMaxR) + 4 * r16(4 * kWave) + r16(8 * kWave) +
-                       r16(16 * kWave) + r16(8 * (size_t)kWave * d.R) + 2 * r16(4 * (size_t)pl.KO) + 16 * 8;
-  const size_t perClaim = 4 + 16 * (size_t)d.R + 4 * (size_t)d.TW;
-  const size_t tallocB = r16(8 * (size_t)d.totalTplIts * d.R);
+  const size_t R = d.R;
+  const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + 2 * r16(4 * (size_t)pl.KO) + r16(4 * (size_t)(d.NTPL + 1)) +
+                       r16(8 * (size_t)(d.NPOOL + 1) * R) + r16(4 * (size_t)d.RSW) + 2 * r16(4 * (size_t)d.TW + 8) +
+                       4 * r16(4 * kWave) + r16(8 * kWave) + r16(16 * kWave) + r16(8 * (size_t)kWave * R) + 16 * 16;
+  const size_t perClaim = 4 + 16 * R + 4 * (size_t)d.TW;
+  const size_t tallocB = r16(8 * (size_t)d.totalTplIts * R);
   size_t avail = budget > fixed ? budget - fixed : 0;
   pl.talloc = (tallocB + 64 * perClaim <= avail) ? 1 : 0;
   if (pl.talloc) avail -= tallocB;
-  size_t kl = avail / (perClaim + 16);
+  size_t kl = avail / (perClaim + 64);  // +64: per-array 16-byte rounding slack
   pl.KL = (int)(kl < (size_t)pl.KO ? kl : (size_t)pl.KO);
-  pl.lds = fixed + (pl.talloc ? tallocB : 0) + r16(4 * (size_t)pl.KL) + 2 * r16(8 * (size_t)pl.KL * d.R) +
+  pl.lds = fixed + (pl.talloc ? tallocB : 0) + r16(4 * (size_t)pl.KL) + 2 * r16(8 * (size_t)pl.KL * R) +
            r16(4 * (size_t)pl.KL * d.TW);
   return pl;
 }
@@ -631,7 +719,11 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep, (const int32_t*)qorder);
   if (mid) (void)hipEventRecord(mid, st);
-  hipLaunchKernelGGL(k_solve, dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl);
+  switch (D.d.R) {
+    case 3: hipLaunchKernelGGL(k_solve<3>, dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl); break;
+    case 4: hipLaunchKernelGGL(k_solve<4>, dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl); break;
+    default: hipLaunchKernelGGL(k_solve<0>, dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl); break;
+  }
   return hipGetLastError();
 }
 
