@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile.sh run: per-launch kernel stats + PMC counters for one kernel.
+
+Usage: scripts/pmc_summary.py <tag> [kernel_substring]   (reads gpurun_out/prof_<tag>_*)
+Writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.txt and profiles/traffic_c2.json.
+HBM bytes follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB; on gfx950
+FETCH_SIZE reports half the bytes of a coalesced read, so it is doubled.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1]
+    kname = sys.argv[2] if len(sys.argv) > 2 else "k_solve"
+    out = os.path.join(ROOT, "gpurun_out")
+    prof = os.path.join(ROOT, "profiles")
+    shutil.copy(os.path.join(out, "prof_%s_trace" % tag, "run_kernel_stats.csv"),
+                os.path.join(prof, "%s_kernel_stats.csv" % tag))
+    lines = ["PMC per launch of %s (averaged over the profiled launches)" % kname]
+    vals = {}
+    for grp in ("fetch", "write", "sq"):
+        path = os.path.join(out, "prof_%s_%s" % (tag, grp), "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(path)):
+            if kname in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, v in sorted(agg.items()):
+            vals[k] = sum(v) / len(v)
+            lines.append("  %-22s %16.1f   (%d launches)" % (k, vals[k], len(v)))
+    if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+        rd = 2 * vals["FETCH_SIZE"] * 1024
+        wr = vals["WRITE_SIZE"] * 1024
+        lines.append("HBM bytes per launch: read %.0f (FETCH_SIZE x2 KiB) + write %.0f = %.0f" % (rd, wr, rd + wr))
+        with open(os.path.join(prof, "traffic_c2.json"), "w") as f:
+            json.dump({"tag": tag, "kernel": kname, "hbm_read_bytes_per_launch": rd,
+                       "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr}, f, indent=1)
+    if "SQ_WAVE_CYCLES" in vals and "SQ_BUSY_CYCLES" in vals:
+        lines.append("SQ_WAIT_ANY / SQ_WAVE_CYCLES = %.3f ; SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES = %.3f" % (
+            vals.get("SQ_WAIT_ANY", 0) / vals["SQ_WAVE_CYCLES"], vals.get("SQ_ACTIVE_INST_ANY", 0) / vals["SQ_WAVE_CYCLES"]))
+    txt = "\n".join(lines) + "\n"
+    with open(os.path.join(prof, "%s_pmc.txt" % tag), "w") as f:
+        f.write(txt)
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()
