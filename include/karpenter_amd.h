@@ -40,7 +40,9 @@ typedef struct ks_solve_opts {
   int simulation_mode; /* SchedulerOptions.SimulationMode (scheduler.go:44-47); decisions identical */
   int replicas;        /* >1: solve `replicas` independent copies in one launch (one wavefront each) */
   int timing_only;     /* 1: do not copy results back (counters and timings only); benchmarks */
-  int reserved[4];
+  int lds_budget;      /* bytes of LDS per Solve; 0 = automatic (tests use small budgets to force the
+                          HBM-resident claim path) */
+  int reserved[3];
 } ks_solve_opts;
 
 /* NewScheduler equivalent: parse + encode the snapshot and upload it to HBM.  Replaces the Go

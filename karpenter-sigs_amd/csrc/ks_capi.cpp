@@ -43,7 +43,7 @@ struct Arena {
 };
 
 struct WorkLayout {
-  size_t c_tpl, c_cnt, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
+  size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
       log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, total;
 };
 
@@ -53,6 +53,7 @@ WorkLayout work_layout(const KsDims& d) {
   size_t K = d.Kcap, P = std::max(d.P, 1), N = std::max(d.N, 1);
   w.c_tpl = a.add(4 * K);
   w.c_cnt = a.add(4 * K);
+  w.c_thr = a.add(4 * K * d.R);
   w.c_host = a.add(4 * K);
   w.c_req = a.add(8 * K * d.R);
   w.c_max = a.add(8 * K * d.R);
@@ -81,6 +82,7 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   KsWork k;
   k.c_tpl = (int32_t*)(base + w.c_tpl);
   k.c_cnt = (int32_t*)(base + w.c_cnt);
+  k.c_thr = (int32_t*)(base + w.c_thr);
   k.c_host = (int32_t*)(base + w.c_host);
   k.c_req = (int64_t*)(base + w.c_req);
   k.c_max = (int64_t*)(base + w.c_max);
@@ -141,6 +143,7 @@ struct ks_problem {
   int wreps = 0;
   hipStream_t stream = nullptr;
   int device = -1;
+  int lastKO = 0;  // claim capacity of the last launch plan
   // NewQueue radix-sort workspace
   uint64_t* skeys = nullptr;
   int32_t* svals = nullptr;
@@ -184,6 +187,8 @@ static void upload(ks_problem* pb) {
   size_t o_tb = put(t.tpl_it_beg.data(), t.tpl_it_beg.size() * 4);
   size_t o_ti = put(t.tpl_its.data(), t.tpl_its.size() * 4);
   size_t o_tp = put(t.tpl_pool.data(), t.tpl_pool.size() * 4);
+  size_t o_tsa = put(t.tsort_alloc.data(), t.tsort_alloc.size() * 8);
+  size_t o_tsp = put(t.tsort_pos.data(), t.tsort_pos.size() * 4);
   size_t o_pr = put(t.pool_rem0.data(), t.pool_rem0.size() * 8);
   size_t o_pm = put(t.pool_mask.data(), t.pool_mask.size() * 4);
   size_t o_preq = put(t.pod_req.data(), t.pod_req.size() * 8);
@@ -194,6 +199,7 @@ static void upload(ks_problem* pb) {
   size_t o_sr = put(t.st_rs.data(), t.st_rs.size() * 4);
   size_t o_st = put(t.st_tol.data(), t.st_tol.size() * 8);
   size_t o_sf = put(t.st_flags.data(), t.st_flags.size() * 4);
+  size_t o_stt = put(t.st_toltpl.data(), t.st_toltpl.size() * 4);
   size_t o_na = put(t.n_avail.data(), t.n_avail.size() * 8);
   size_t o_nr = put(t.n_req0.data(), t.n_req0.size() * 8);
   size_t o_nrs = put(t.n_rs0.data(), t.n_rs0.size() * 4);
@@ -222,6 +228,8 @@ static void upload(ks_problem* pb) {
   D.tpl_it_beg = (const int32_t*)(b + o_tb);
   D.tpl_its = (const int32_t*)(b + o_ti);
   D.tpl_pool = (const int32_t*)(b + o_tp);
+  D.tsort_alloc = (const int64_t*)(b + o_tsa);
+  D.tsort_pos = (const int32_t*)(b + o_tsp);
   D.pool_rem0 = (const int64_t*)(b + o_pr);
   D.pool_mask = (const uint32_t*)(b + o_pm);
   D.pod_req = (const int64_t*)(b + o_preq);
@@ -232,6 +240,7 @@ static void upload(ks_problem* pb) {
   D.st_rs = (const uint32_t*)(b + o_sr);
   D.st_tol = (const uint64_t*)(b + o_st);
   D.st_flags = (const int32_t*)(b + o_sf);
+  D.st_toltpl = (const uint32_t*)(b + o_stt);
   D.n_avail = (const int64_t*)(b + o_na);
   D.n_req0 = (const int64_t*)(b + o_nr);
   D.n_rs0 = (const uint32_t*)(b + o_nrs);
@@ -248,7 +257,8 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
   HIPCHK(hipStreamSynchronize(st));
   if (ctr[CT_ERROR] != KE_OK)
     throw KsError(ctr[CT_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
-                  ctr[CT_ERROR] == KE_CLAIM_CAP ? "NodeClaim capacity (8192 per Solve) exceeded"
+                  ctr[CT_ERROR] == KE_CLAIM_CAP ? "NodeClaim capacity (" + std::to_string(pb->lastKO) +
+                                                      " per Solve at this LDS budget) exceeded"
                                                 : "solve kernel iteration cap hit");
   int nc = (int)ctr[CT_NCLAIMS], nl = (int)ctr[CT_NLOG];
   std::vector<int32_t> order, ctpl, chost, logp, logt, status, fstate;
@@ -333,8 +343,12 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
   }
   for (int n = 0; n < d.N; n++) res->nodes.push_back(ks_results::ENode{h.nodes[n].origIndex, h.nodes[n].name, nodePods[n]});
   // PodErrors (scheduler.go:179-183 keeps non-nil errors only)
+  // k_solve records ST_FAILED at each failed attempt and nothing on success: a pod is an error iff
+  // its last recorded attempt failed and it is not in the commit log.
+  std::vector<char> inLog(d.P, 0);
+  for (int i = 0; i < nl; i++) inLog[logp[i]] = 1;
   for (int p = 0; p < d.P; p++) {
-    if (status[p] != ST_FAILED) continue;
+    if (status[p] != ST_FAILED || inLog[p]) continue;
     int s = fstate[p];
     int s0 = h.tab.pod_state0[p];
     const PodState& ps = h.states[p][s - s0];
@@ -468,6 +482,16 @@ int ks_problem_inspect(const char* json, size_t len, char** out) {
   kv("R", d.R); kv("keys", d.NK); kv("W", d.W); kv("NB", d.NB); kv("RSW", d.RSW); kv("T", d.T); kv("templates", d.NTPL);
   kv("pools", d.NPOOL); kv("nodes", d.N); kv("pods", d.P); kv("states", d.S); kv("uids", d.NU); kv("TW", d.TW);
   kv("Kcap", d.Kcap); kv("taints", (long long)h.taints.size());
+  // LDS plans (ks_solve.hip make_plan) at the default and a few reduced budgets
+  o += ",\"plans\":{";
+  const size_t budgets[] = {160 * 1024 - 256, 6000, 9000, 14000, 24000, 40000};
+  for (size_t i = 0; i < sizeof(budgets) / sizeof(budgets[0]); i++) {
+    Plan pl = make_plan(d, budgets[i]);
+    o += (i ? ",\"" : "\"") + std::to_string(budgets[i]) + "\":{\"KO\":" + std::to_string(pl.KO) +
+         ",\"KL\":" + std::to_string(pl.KL) + ",\"talloc\":" + std::to_string(pl.talloc) +
+         ",\"tsort\":" + std::to_string(pl.tsort) + ",\"lds\":" + std::to_string(pl.lds) + "}";
+  }
+  o += "}";
   o += ",\"keyNames\":[";
   for (size_t i = 0; i < h.keyNames.size(); i++) { if (i) o += ","; ksjson::quote(o, h.keyNames[i]); }
   o += "],\"resources\":[";
@@ -490,8 +514,11 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   // one Solve per CU gets the whole 160 KiB; larger batches trade LDS for waves per CU
   size_t budget = 160 * 1024 - 256;
   if (reps > 256) budget = std::max<size_t>(24 * 1024, budget * 256 / reps);
+  if (opts && opts->lds_budget > 0) budget = std::min<size_t>(budget, (size_t)opts->lds_budget);
   Plan pl = make_plan(d, budget);
-  if (pl.lds > 160 * 1024) throw KsError(KS_ERR_CAPACITY, "solve state exceeds 160 KiB of LDS");
+  if (pl.lds > 160 * 1024 || pl.KO < 1)
+    throw KsError(KS_ERR_CAPACITY, "solve state does not fit the LDS budget");
+  pb->lastKO = pl.KO;
   WorkLayout wl = work_layout(d);
   size_t need = wl.total * reps;
   if (need > pb->wbytes || reps != pb->wreps) {

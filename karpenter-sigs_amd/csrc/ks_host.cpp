@@ -663,6 +663,24 @@ void Host::build(const Value& root) {
   dims.maxTplIts = maxIts;
   dims.totalTplIts = (int)tab.tpl_it_beg[NT];
   dims.TW = std::max(1, (maxIts + 31) / 32);
+  // Per template and resource, the template positions ordered by Allocatable ascending: the options a
+  // growing request excludes (resources.go:162-175 Fits) are always a prefix of this order.
+  tab.tsort_alloc.assign((size_t)std::max(dims.totalTplIts, 1) * R, 0);
+  tab.tsort_pos.assign((size_t)std::max(dims.totalTplIts, 1) * R, 0);
+  for (int t = 0; t < NT; t++) {
+    const int tb = tab.tpl_it_beg[t], n = tab.tpl_it_beg[t + 1] - tb;
+    std::vector<int> ord(n);
+    for (int r = 0; r < R; r++) {
+      for (int i = 0; i < n; i++) ord[i] = i;
+      auto al = [&](int i) { return tab.it_alloc[(size_t)tab.tpl_its[tb + i] * R + r]; };
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return al(a) < al(b); });
+      const size_t base = (size_t)tb * R + (size_t)r * n;
+      for (int i = 0; i < n; i++) {
+        tab.tsort_alloc[base + i] = al(ord[i]);
+        tab.tsort_pos[base + i] = ord[i];
+      }
+    }
+  }
 
   // --- existing nodes (NewExistingNode, calculateExistingNodeClaims)
   int N = (int)nodes.size();
@@ -825,6 +843,10 @@ void Host::build(const Value& root) {
     dims.skBits[c] = bits;
   }
   dims.dupUids = (int)uids.size() < P ? 1 : 0;
+  // The threshold filter in k_solve assumes requests only grow (no negative quantities).
+  dims.negReq = 0;
+  for (int64_t v : tab.pod_req) dims.negReq |= v < 0;
+  for (int64_t v : tab.tpl_daemon) dims.negReq |= v < 0;
   {
     std::vector<int> idx(P);
     for (int i = 0; i < P; i++) idx[i] = i;
@@ -838,6 +860,7 @@ void Host::build(const Value& root) {
   tab.st_rs.assign((size_t)dims.S * dims.RSW, 0);
   tab.st_tol.assign((size_t)dims.S * 2, 0);
   tab.st_flags.assign(dims.S, 0);
+  tab.st_toltpl.assign(dims.S, 0);
   int s = 0;
   for (auto& chain : states)
     for (auto& st : chain) {
@@ -847,6 +870,10 @@ void Host::build(const Value& root) {
       tab.st_tol[(size_t)s * 2] = m[0];
       tab.st_tol[(size_t)s * 2 + 1] = m[1];
       uint64_t pres = rs_present(st.rsAll.data());
+      uint32_t tt = 0;
+      for (int t = 0; t < dims.NTPL; t++)
+        if (((tab.tpl_taint[(size_t)t * 2] & ~m[0]) | (tab.tpl_taint[(size_t)t * 2 + 1] & ~m[1])) == 0) tt |= 1u << t;
+      tab.st_toltpl[s] = tt;
       tab.st_flags[s] = (st.hasPreferred ? SF_HAS_PREFERRED : 0) | ((pres & itKeys) ? SF_TOUCHES_IT_KEYS : 0) |
                         (pres ? SF_HAS_KEYS : 0);
       s++;

@@ -99,10 +99,10 @@ struct Host {
 
   // host images of the device tables
   struct Tables {
-    std::vector<int64_t> it_alloc, it_cap, tpl_daemon, pool_rem0, pod_req, pod_sortkey, n_avail, n_req0;
-    std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask;
+    std::vector<int64_t> tsort_alloc, it_alloc, it_cap, tpl_daemon, pool_rem0, pod_req, pod_sortkey, n_avail, n_req0;
+    std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask, st_toltpl;
     std::vector<uint64_t> tpl_taint, st_tol, n_taint;
-    std::vector<int32_t> it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,
+    std::vector<int32_t> tsort_pos, it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,
         st_flags;
   } tab;
 

@@ -55,6 +55,7 @@ struct KsDims {
   int32_t skBits[4];
   int32_t dupUids;     // 1 if two pods share a UID (queue staleness then re-reads last_len)
   int32_t totalTplIts; // sum of template instance-type list lengths
+  int32_t negReq;      // 1 if any pod or daemon request is negative (disables the threshold filter)
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
@@ -62,7 +63,7 @@ struct Plan {
   int32_t KO;      // order/okey capacity = max NodeClaims per solve
   int32_t KL;      // claims [0, KL) keep template/requests/max/options in LDS, the rest in HBM
   int32_t talloc;  // 1: template instance-type Allocatable tables are LDS-resident
-  int32_t pad;
+  int32_t tsort;   // 1: the sorted Allocatable lists (tsort_*) are LDS-resident
   uint64_t lds;    // dynamic LDS bytes
 };
 
@@ -87,6 +88,8 @@ struct KsDev {
   const int32_t KS_G* tpl_it_beg;  // [NTPL+1]
   const int32_t KS_G* tpl_its;     // IT index per template position
   const int32_t KS_G* tpl_pool;    // [NTPL] limit pool or -1
+  const int64_t KS_G* tsort_alloc; // [totalTplIts][R] per template, per resource: Allocatable ascending
+  const int32_t KS_G* tsort_pos;   //   ... and the template position it belongs to (tb*R + r*nIT + i)
   // NodePool limits (remainingResources, scheduler.go:76-78,306-308)
   const int64_t KS_G* pool_rem0;   // [NPOOL][R]
   const uint32_t KS_G* pool_mask;  // [NPOOL] resource names present in the remaining ResourceList
@@ -100,6 +103,7 @@ struct KsDev {
   const uint32_t KS_G* st_rs;      // [S][RSW] NewPodRequirements
   const uint64_t KS_G* st_tol;     // [S][2] tolerated-taint masks
   const int32_t KS_G* st_flags;    // [S]
+  const uint32_t KS_G* st_toltpl;  // [S] bit t: the state tolerates template t's taints
   // existing nodes, in calculateExistingNodeClaims order (scheduler.go:313-321)
   const int64_t KS_G* n_avail;     // [N][R] StateNode.Available()
   const int64_t KS_G* n_req0;      // [N][R] remaining daemon requests (existingnode.go:43-52)
@@ -110,7 +114,8 @@ struct KsDev {
 // Per-solve workspace (one slice per replica / simulation).
 struct KsWork {
   int32_t KS_G* c_tpl;      // [Kcap]
-  int32_t KS_G* c_cnt;      // [Kcap]
+  int32_t KS_G* c_cnt;      // [Kcap] number of remaining options
+  int32_t KS_G* c_thr;      // [Kcap][R] per resource: prefix of tsort already excluded by Fits
   int32_t KS_G* c_host;     // [Kcap] hostname-placeholder ordinal
   int64_t KS_G* c_req;      // [Kcap][R]
   int64_t KS_G* c_max;      // [Kcap][R] per-resource max Allocatable over the remaining options

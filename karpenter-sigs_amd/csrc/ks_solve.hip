@@ -6,20 +6,24 @@
 // parts of each step map onto the 64 lanes:
 //   - existing-node first-fit (scheduler.go:240-244)   lane per node, ballot + ffs picks the first
 //   - in-flight NodeClaim scan (scheduler.go:250-254)  lane per sorted position: a quick reject
-//     (template taints, requests + pod <= max Allocatable of the remaining options, Compatible)
-//     then a wave-cooperative NodeClaim.Add on candidates in order (nodeclaim.go:65-119)
+//     (template taints, pod <= max Allocatable - requests, Compatible) from position-indexed
+//     arrays, then a wave-cooperative NodeClaim.Add on candidates in order (nodeclaim.go:65-119)
 //   - instance-type filter (nodeclaim.go:225-260)      lane per template IT position, ballots build
 //     the remaining-options bitset and the six filterResults flags in one pass
 //   - new NodeClaim per template (scheduler.go:258-283) incl. limits (filterByRemainingResources,
 //     subtractMax)
-// Latency is the bound (the chain is sequential), so everything a step touches lives in LDS: the
-// claim order and pod counts, each claim's template / requests / max-Allocatable / options bitset
-// (for the first Plan::KL claims), the templates' instance-type Allocatable tables, the remaining
-// NodePool limits and a 64-pod window of queue entries gathered once per 64 pops.  Pointers carry
-// explicit address spaces (ks_problem.h) so no access is a flat access, and lanes never hand data
-// to each other through HBM except at the window refill (behind one release fence, read with sc1
-// loads that bypass the L1).  HBM holds the cold state (requirement records, existing nodes,
-// overflow claims) and the write-only commit log.
+// When a pod leaves a claim's requirements unchanged (resource-only pods), NodeClaim.Add's option
+// filter reduces to Fits on growing requests, so the options it drops are a prefix of each
+// resource's Allocatable-ascending order: a per-claim threshold per resource advances over that
+// order and clears exactly the dropped options (no scan of the surviving ones).
+// Latency is the bound (the chain is sequential), so everything a step touches lives in LDS or
+// VGPRs: the 64-pod queue window (one lane per entry, read with readlane), the claim order, pod
+// counts and quick-reject headroom per position, each claim's template / requests / max-Allocatable
+// / options bitset / thresholds (for the first Plan::KL claims), the templates' Allocatable tables
+// and the remaining NodePool limits.  Pointers carry explicit address spaces (ks_problem.h), so no
+// access is a flat access.  Lanes never hand data to each other through HBM except at the window
+// refill (behind one release fence, read with sc1 loads that bypass the L1).  HBM holds the cold
+// state (requirement records, existing nodes, overflow claims) and the write-only commit log.
 // Independent Solves (replicas, consolidation simulations) are independent workgroups, so a launch
 // of thousands of them fills the 256 CUs.  Nothing here is a dense contraction: no MFMA.
 #include <hip/hip_runtime.h>
@@ -33,7 +37,6 @@ namespace ks {
 using LI32 = int32_t KS_L*;
 using LI64 = int64_t KS_L*;
 using LU32 = uint32_t KS_L*;
-using LU64 = uint64_t KS_L*;
 using GI32 = int32_t KS_G*;
 using GI64 = int64_t KS_G*;
 using GU32 = uint32_t KS_G*;
@@ -47,6 +50,11 @@ __device__ __forceinline__ int64_t uni64(int64_t x) {
   return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
                    (uint32_t)__builtin_amdgcn_readfirstlane((int)x));
 }
+__device__ __forceinline__ int rdl(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ int64_t rdl64(int64_t x, int l) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)x, l));
+}
 // Ordering point for LDS traffic between the lanes of the (single) wave: the wave's LDS operations
 // execute in order, so only the compiler must be kept from reordering; no s_waitcnt, no s_barrier.
 __device__ __forceinline__ void wsync() {
@@ -58,6 +66,9 @@ __device__ __forceinline__ void hbm_release() { __builtin_amdgcn_fence(__ATOMIC_
 template <class T>
 __device__ __forceinline__ T ld_sc1(const T KS_G* p) {  // L1-bypassing load of HBM state other lanes wrote
   return __hip_atomic_load((T*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t lds_and(LU32 p, uint32_t v) {  // ds_and_rtn_b32
+  return __hip_atomic_fetch_and(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 #ifdef KS_PHASE_STATS
@@ -94,11 +105,24 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
 // Solve
 // ------------------------------------------------------------------------------------------------
 template <bool INL> struct ClaimView;
-template <> struct ClaimView<true> { LI32 tpl; LI64 req; LI64 max; LU32 rem; };
-template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; };
+template <> struct ClaimView<true> { LI32 tpl; LI64 req; LI64 max; LU32 rem; LI32 thr; LI32 cnt; };
+template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI32 thr; GI32 cnt; };
 
-template <int RT>  // RT > 0: resource count known at compile time (loops unrolled, requests in VGPRs)
+// One queue entry per lane (the 64-pod window), read wave-uniformly with readlane.
+template <int RT>
+struct Window {
+  int p, uid, s, flags, toltpl;
+  uint64_t ll, tol0, tol1;
+  int64_t req[RT > 0 ? RT : kMaxR];
+};
+
+// RT > 0: resource count known at compile time (loops unrolled, requests in VGPRs).
+// TL: the instance-type tables (Allocatable per template position, sorted Allocatable lists) are
+// LDS-resident.  Compile-time, so the hot loops carry no HBM branch (a join of an LDS and an HBM
+// path would wait on vmcnt, i.e. on every outstanding store).
+template <int RT, bool TL>
 struct Solver {
+  static constexpr int RM = RT > 0 ? RT : kMaxR;
   const KsDev& D;
   const KsDims& d;
   const KsWork& W;
@@ -108,15 +132,16 @@ struct Solver {
   ClaimView<false> gc;  // claims [KL, KO)
   LI32 s_order;         // [KO] s.newNodeClaims as claim ids
   LI32 s_okey;          // [KO] len(Pods) of the claim at each position
+  LI32 s_ptpl;          // [KO] template of the claim at each position
+  LI64 s_phead;         // [KO][R] max Allocatable - requests of the claim at each position
   LI64 s_talloc;        // [totalTplIts][R] Allocatable per template position (pl.talloc)
+  LI64 s_tsa;           // tsort_alloc (pl.tsort)
+  LI32 s_tsp;           // tsort_pos (pl.tsort)
   LI32 s_tbeg;          // [NTPL+1]
   LI64 s_pool;          // [NPOOL][R] remaining limits
   LU32 s_rs;            // [RSW] candidate requirements
   LU32 s_rem;           // [TW+2] candidate options
   LU32 s_cand;          // [TW+2] limit-filtered template options
-  LI32 w_p, w_uid, w_s, w_flags;
-  LU64 w_ll, w_tol;
-  LI64 w_req;
   int64_t algbytes = 0;
 
   __device__ Solver(const KsDev& D_, const KsWork& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
@@ -132,7 +157,7 @@ struct Solver {
   __device__ __forceinline__ bool fits(const int64_t* req, P alloc) const {  // resources.go:162-175
     bool ok = true;
 #pragma unroll
-    for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+    for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
       const int64_t a = alloc[r];
       ok &= (a >= 0) & (req[r] <= a);
@@ -140,12 +165,43 @@ struct Solver {
     return ok;
   }
   __device__ __forceinline__ bool fits_pos(const int64_t* req, int gpos) const {
-    if (pl.talloc) return fits(req, s_talloc + (int64_t)gpos * R());
-    return fits(req, D.it_alloc + (int64_t)D.tpl_its[gpos] * R());
+    if constexpr (TL) return fits(req, s_talloc + (int64_t)gpos * R());
+    else return fits(req, D.it_alloc + (int64_t)D.tpl_its[gpos] * R());
   }
   __device__ __forceinline__ int64_t alloc_pos(int gpos, int r) const {
-    if (pl.talloc) return s_talloc[(int64_t)gpos * R() + r];
-    return D.it_alloc[(int64_t)D.tpl_its[gpos] * R() + r];
+    if constexpr (TL) return s_talloc[(int64_t)gpos * R() + r];
+    else return D.it_alloc[(int64_t)D.tpl_its[gpos] * R() + r];
+  }
+  __device__ __forceinline__ int64_t tsort_a(int64_t i) const {
+    if constexpr (TL) return s_tsa[i];
+    else return D.tsort_alloc[i];
+  }
+  __device__ __forceinline__ int tsort_p(int64_t i) const {
+    if constexpr (TL) return s_tsp[i];
+    else return D.tsort_pos[i];
+  }
+
+  // Commit log (scheduler.go:253/274 placements in order): lane (i & 63) holds entry i until 64 are
+  // buffered, then one coalesced store.  Per-pod global stores would make the next global load wait
+  // for their write acknowledgements (vmcnt counts stores on gfx9).
+  int lg_p = 0, lg_t = 0;
+  __device__ __forceinline__ void log_commit(int p, int tgt, int& nlog) {
+    if (lane() == (nlog & (kWave - 1))) {
+      lg_p = p;
+      lg_t = tgt;
+    }
+    nlog++;
+    if ((nlog & (kWave - 1)) == 0) {
+      W.log_pod[nlog - kWave + lane()] = lg_p;
+      W.log_tgt[nlog - kWave + lane()] = lg_t;
+    }
+  }
+  __device__ __forceinline__ void log_flush(int nlog) {
+    const int k = nlog & (kWave - 1);
+    if (lane() < k) {
+      W.log_pod[nlog - k + lane()] = lg_p;
+      W.log_tgt[nlog - k + lane()] = lg_t;
+    }
   }
   template <class PR>
   __device__ __forceinline__ bool has_offering(int it, PR rs) const {  // nodeclaim.go:270-278
@@ -153,10 +209,6 @@ struct Solver {
     for (int o = b; o < e; o++)
       if (rs_member(L, rs, d.zoneKey, D.off_zone[o]) && rs_member(L, rs, d.ctKey, D.off_ct[o])) return true;
     return false;
-  }
-  template <class PT, class PL>
-  __device__ static bool tolerates(PT taint, PL tol) {
-    return ((taint[0] & ~tol[0]) | (taint[1] & ~tol[1])) == 0;
   }
   template <class PD, class PS>
   __device__ void copy_words(PD dst, PS src, int n) const {
@@ -168,16 +220,24 @@ struct Solver {
       if ((base >> 5) + 1 < d.TW) dst[(base >> 5) + 1] = (uint32_t)(m >> 32);
     }
   }
+  __device__ int popc_words(LU32 w, int n) const {
+    int c = 0;
+    for (int i = lane(); i < n; i += kWave) c += __popc(w[i]);
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
+    return uni(c);
+  }
 
   // --- existing nodes (ExistingNode.Add, existingnode.go:64-124) -------------------------------
   // Lane (n & 63) is the only lane that ever reads or writes node n's mutable state.
-  __device__ __forceinline__ bool node_ok(int n, int s, int sflags, const int64_t* pod, LU64 tol) const {
-    if (!tolerates(D.n_taint + 2 * n, tol)) return false;
+  __device__ __forceinline__ bool node_ok(int n, int s, int sflags, const int64_t* pod, uint64_t tol0,
+                                          uint64_t tol1) const {
+    const uint64_t KS_G* nt = D.n_taint + 2 * n;
+    if (((nt[0] & ~tol0) | (nt[1] & ~tol1)) != 0) return false;
     const int64_t KS_G* av = D.n_avail + (int64_t)n * R();
     const int64_t KS_G* rq = W.n_req + (int64_t)n * R();
     bool ok = true;
 #pragma unroll
-    for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+    for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
       const int64_t a = av[r];
       ok &= (a >= 0) & (rq[r] + pod[r] <= a);
@@ -187,26 +247,25 @@ struct Solver {
     return ok;
   }
 
-  // --- NodeClaim quick reject: necessary conditions of NodeClaim.Add ----------------------------
-  template <bool INL>
-  __device__ __forceinline__ bool claim_quick(int c, int s, int sflags, const int64_t* pod, LU64 tol) const {
-    const ClaimView<INL>& v = cv<INL>();
-    const int t = v.tpl[c];
-    if (!tolerates(D.tpl_taint + 2 * t, tol)) return false;
+  // --- NodeClaim quick reject at sorted position j: necessary conditions of NodeClaim.Add ------
+  __device__ __forceinline__ bool claim_quick(int j, int s, int sflags, uint32_t toltpl, const int64_t* pod) const {
+    if (!((toltpl >> s_ptpl[j]) & 1u)) return false;  // Taints.Tolerates (nodeclaim.go:68-71)
     bool ok = true;
 #pragma unroll
-    for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+    for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
-      ok &= v.req[(int64_t)c * R() + r] + pod[r] <= v.max[(int64_t)c * R() + r];
+      ok &= pod[r] <= s_phead[(int64_t)j * R() + r];
     }
     if (ok && (sflags & SF_HAS_KEYS))
-      ok = rs_compatible(L, W.c_rs + (int64_t)c * d.RSW, D.st_rs + (int64_t)s * d.RSW, d.allowWK);
+      ok = rs_compatible(L, W.c_rs + (int64_t)s_order[j] * d.RSW, D.st_rs + (int64_t)s * d.RSW, d.allowWK);
     return ok;
   }
 
-  // --- wave-cooperative NodeClaim.Add on claim c: builds s_rs / s_rem and the new requests --------
+  // --- wave-cooperative NodeClaim.Add on claim c -------------------------------------------------
+  // Builds s_rs / s_rem, the new requests, thresholds and option count.  Returns options left > 0.
   template <bool INL>
-  __device__ __forceinline__ bool claim_full(int c, int s, int sflags, const int64_t* pod, int64_t* req) {
+  __device__ __forceinline__ bool claim_full(int c, int s, int sflags, const int64_t* pod, int64_t* req, int* nthr,
+                                             int& ncnt) {
     const ClaimView<INL>& v = cv<INL>();
     bool changed = false;
     if (sflags & SF_HAS_KEYS) {
@@ -220,17 +279,49 @@ struct Solver {
     }
     const int t = uni(v.tpl[c]);
 #pragma unroll
-    for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+    for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
       req[r] = v.req[(int64_t)c * R() + r] + pod[r];
+      nthr[r] = uni(v.thr[(int64_t)c * R() + r]);
     }
     const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
-    uint64_t any = 0;
-    int scanned = 0;
+    copy_words(s_rem, v.rem + (int64_t)c * d.TW, d.TW);
+    wsync();
+    if (!changed && !d.negReq) {
+      // Requirements unchanged: the options dropped are exactly those some growing request no longer
+      // fits, a prefix of each resource's Allocatable-ascending order beyond its threshold.
+      int removed = 0, examined = 0;
+      for (int r = 0; r < R(); r++) {
+        const int64_t base = (int64_t)tb * R() + (int64_t)r * nIT;
+        int k = nthr[r];
+        while (k < nIT) {
+          const int i = k + lane();
+          const bool ex = i < nIT && tsort_a(base + i) < req[r];
+          const uint64_t m = wballot(ex);
+          if (m == 0) break;
+          bool was = false;
+          if (ex) {
+            const int pos = tsort_p(base + i);
+            const uint32_t bit = 1u << (pos & 31);
+            was = (lds_and(s_rem + (pos >> 5), ~bit) & bit) != 0;
+          }
+          removed += __popcll(wballot(was));
+          const int nm = __popcll(m);
+          k += nm;
+          examined += nm;
+          if (nm < kWave) break;
+        }
+        nthr[r] = k;
+      }
+      ncnt = uni(v.cnt[c]) - removed;
+      algbytes += 8 * d.TW + 16 * R() + 4 * R() + (int64_t)examined * 12;
+      wsync();
+      return ncnt > 0;
+    }
+    int cnt = 0, scanned = 0;
     for (int base = 0; base < nIT; base += kWave) {
       const int wi = base >> 5;
-      const uint64_t bits = (uint64_t)v.rem[(int64_t)c * d.TW + wi] |
-                            (wi + 1 < d.TW ? (uint64_t)v.rem[(int64_t)c * d.TW + wi + 1] << 32 : 0ull);
+      const uint64_t bits = (uint64_t)s_rem[wi] | (wi + 1 < d.TW ? (uint64_t)s_rem[wi + 1] << 32 : 0ull);
       uint64_t m = 0;
       if (bits) {
         const int gpos = tb + base + lane();
@@ -243,65 +334,75 @@ struct Solver {
         m = wballot(ok);
         scanned += __popcll(bits);
       }
+      wsync();
       store_bits(s_rem, base, m);
-      any |= m;
+      cnt += __popcll(m);
     }
-    algbytes += 4 * d.TW + 16 * R() + (int64_t)scanned * 8 * R();
+    ncnt = cnt;
+    algbytes += 8 * d.TW + 16 * R() + (int64_t)scanned * 8 * R();
     wsync();
-    return any != 0;
+    return cnt > 0;
   }
 
-  // exact max Allocatable per resource over the options (quick-reject bound)
+  // exact max Allocatable per resource over the options (quick-reject bound); refreshes the
+  // headroom of the claim's sorted position `pos` (-1: none yet)
   template <bool INL, class PB>
-  __device__ __forceinline__ void recompute_max(int c, PB bits, int t) {
+  __device__ __forceinline__ void recompute_max(int c, PB bits, int t, int pos) {
     const ClaimView<INL>& v = cv<INL>();
     const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
     for (int r = 0; r < R(); r++) {
       int64_t m = INT64_MIN;
-      for (int pos = lane(); pos < nIT; pos += kWave)
-        if ((bits[pos >> 5] >> (pos & 31)) & 1u) {
-          const int64_t a = alloc_pos(tb + pos, r);
+      for (int q = lane(); q < nIT; q += kWave)
+        if ((bits[q >> 5] >> (q & 31)) & 1u) {
+          const int64_t a = alloc_pos(tb + q, r);
           m = a > m ? a : m;
         }
       for (int off = 32; off >= 1; off >>= 1) {
         const int64_t o = __shfl_xor(m, off);
         m = o > m ? o : m;
       }
-      if (lane() == 0) v.max[(int64_t)c * R() + r] = m;
+      if (lane() == 0) {
+        v.max[(int64_t)c * R() + r] = m;
+        if (pos >= 0) s_phead[(int64_t)pos * R() + r] = m - v.req[(int64_t)c * R() + r];
+      }
     }
+    if (!INL) hbm_release();
     wsync();
   }
 
+  // Returns whether s.newNodeClaims is still non-decreasing after the increment at `pos`.
   template <bool INL>
-  __device__ __forceinline__ void commit_claim(int c, int pos, int p, int sflags, const int64_t* req, int& nlog) {
+  __device__ __forceinline__ bool commit_claim(int c, int pos, int n, int p, int sflags, const int64_t* pod,
+                                               const int64_t* req, const int* nthr, int ncnt, int& nlog) {
     const ClaimView<INL>& v = cv<INL>();
+    const int okNew = uni(s_okey[pos]) + 1;
+    const bool srt = pos + 1 >= n || okNew <= uni(s_okey[pos + 1]);
     if (lane() == 0) {
 #pragma unroll
-      for (int r = 0; r < (RT > 0 ? RT : kMaxR); r++) {
+      for (int r = 0; r < RM; r++) {
         if (RT == 0 && r >= d.R) break;
         v.req[(int64_t)c * R() + r] = req[r];
+        v.thr[(int64_t)c * R() + r] = nthr[r];
+        s_phead[(int64_t)pos * R() + r] -= pod[r];
       }
+      v.cnt[c] = ncnt;
+      s_okey[pos] = okNew;
     }
     if (sflags & SF_HAS_KEYS) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
     copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
-    if (lane() == 0) {
-      s_okey[pos] += 1;
-      W.log_pod[nlog] = p;
-      W.log_tgt[nlog] = c;
-      W.pod_status[p] = ST_SCHEDULED;
-    }
-    nlog++;
+    log_commit(p, c, nlog);
     // The max bound stays valid as the options only shrink; it is tightened lazily when a full check
     // fails.  HBM-resident claim state is re-read by other lanes: drain the stores first.
     if ((sflags & SF_HAS_KEYS) || !INL) hbm_release();
     wsync();
-    algbytes += 16 * R() + 4 * d.TW;
+    algbytes += 24 * R() + 4 * d.TW + 8;
+    return srt;
   }
 
   // --- new NodeClaim from each template in order (scheduler.go:258-283) -----------------------
   // Returns 1 placed, 0 failed (fail codes recorded), 2 no templates (add() returns nil), -1 cap.
-  __device__ __forceinline__ int try_templates(int p, int s, int sflags, const int64_t* pod, LU64 tol, int& nclaims, int& nlog,
-                               int& hostCtr) {
+  __device__ __forceinline__ int try_templates(int p, int s, int sflags, uint32_t toltpl, const int64_t* pod,
+                                               int& nclaims, int& nlog, int& hostCtr, bool& srt) {
     if (d.NTPL == 0) return 2;
     for (int t = 0; t < d.NTPL; t++) {
       uint32_t code = FC_NONE;
@@ -328,7 +429,7 @@ struct Solver {
         code = FC_LIMITS;
       } else {
         hostid = ++hostCtr;  // NewNodeClaim: atomic.AddInt64(&nodeID, 1) (nodeclaim.go:48)
-        if (!tolerates(D.tpl_taint + 2 * t, tol)) {
+        if (!((toltpl >> t) & 1u)) {
           code = FC_TAINTS;
         } else {
           copy_words(s_rs, D.tpl_rs + (int64_t)t * d.RSW, d.RSW);
@@ -342,7 +443,7 @@ struct Solver {
           if (!ok) {
             code = FC_COMPAT;
           } else {
-            int64_t req[RT > 0 ? RT : kMaxR];
+            int64_t req[RM];
             for (int r = 0; r < R(); r++) req[r] = D.tpl_daemon[(int64_t)t * R() + r] + pod[r];
             uint32_t flags = 0;
             uint64_t any = 0;
@@ -373,31 +474,48 @@ struct Solver {
             } else {
               if (nclaims >= pl.KO) return -1;
               const int c = nclaims++;
+              const bool inl = c < pl.KL;
               copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
-              if (c < pl.KL) {
-                copy_words(lc.rem + (int64_t)c * d.TW, s_rem, d.TW);
-              } else {
-                copy_words(gc.rem + (int64_t)c * d.TW, s_rem, d.TW);
+              if (inl) copy_words(lc.rem + (int64_t)c * d.TW, s_rem, d.TW);
+              else copy_words(gc.rem + (int64_t)c * d.TW, s_rem, d.TW);
+              // thresholds: how much of each resource's ascending Allocatable order req excludes
+              int thr[RM];
+              for (int r = 0; r < R(); r++) {
+                const int64_t b = (int64_t)tb * R() + (int64_t)r * nIT;
+                int k = 0;
+                for (int q = 0; q < nIT; q += kWave)
+                  k += __popcll(wballot(q + lane() < nIT && tsort_a(b + q + lane()) < req[r]));
+                thr[r] = k;
               }
+              const int cnt = popc_words(s_rem, d.TW);
               if (lane() == 0) {
                 for (int r = 0; r < R(); r++) {
-                  if (c < pl.KL) lc.req[(int64_t)c * R() + r] = req[r];
-                  else gc.req[(int64_t)c * R() + r] = req[r];
+                  if (inl) {
+                    lc.req[(int64_t)c * R() + r] = req[r];
+                    lc.thr[(int64_t)c * R() + r] = thr[r];
+                  } else {
+                    gc.req[(int64_t)c * R() + r] = req[r];
+                    gc.thr[(int64_t)c * R() + r] = thr[r];
+                  }
                 }
-                if (c < pl.KL) lc.tpl[c] = t;
+                if (inl) {
+                  lc.tpl[c] = t;
+                  lc.cnt[c] = cnt;
+                } else {
+                  gc.cnt[c] = cnt;
+                }
                 W.c_tpl[c] = t;
                 W.c_host[c] = hostid;
                 s_order[c] = c;
                 s_okey[c] = 1;
-                W.log_pod[nlog] = p;
-                W.log_tgt[nlog] = c;
-                W.pod_status[p] = ST_SCHEDULED;
+                s_ptpl[c] = t;
               }
-              nlog++;
+              srt = c == 0 || uni(s_okey[c - 1]) <= 1;
+              log_commit(p, c, nlog);
               hbm_release();  // c_rs / c_tpl / overflow state are read by other lanes later
               wsync();
-              if (c < pl.KL) recompute_max<true>(c, s_rem, t);
-              else recompute_max<false>(c, s_rem, t);
+              if (inl) recompute_max<true>(c, s_rem, t, c);
+              else recompute_max<false>(c, s_rem, t, c);
               if (pool >= 0) {  // subtractMax (scheduler.go:347-362)
                 const uint32_t mask = D.pool_mask[pool];
                 for (int r = 0; r < R(); r++) {
@@ -430,87 +548,100 @@ struct Solver {
   }
 
   // --- s.newNodeClaims re-sort (scheduler.go:247) --------------------------------------------------
-  __device__ __forceinline__ void sort_claims(int n, int64_t& sorts, int64_t& slow) {
-    bool desc = false;
-    for (int base = 0; base < n; base += kWave) {
-      const int j = base + lane();
-      const bool dd = j > 0 && j < n && s_okey[j] < s_okey[j - 1];
-      desc |= wballot(dd) != 0;
-    }
-    sorts++;
-    if (!desc) return;  // non-decreasing: pdqsort performs no swap
-    slow++;
+  // Called only when the array is not non-decreasing (a non-decreasing array is provably left
+  // untouched by pdqsort).  Lane 0 replays Go's pdqsort_func; the position-indexed quick-reject
+  // arrays are then regathered from the claims.
+  __device__ __forceinline__ void sort_claims(int n) {
     if (lane() == 0) {
       GoSortExactT<LI32> g{GoSortT<LI32>{s_okey, s_order}};
       g.run(n);
     }
     wsync();
+    for (int j = lane(); j < n; j += kWave) {
+      const int c = s_order[j];
+      const bool inl = c < pl.KL;
+      s_ptpl[j] = inl ? lc.tpl[c] : W.c_tpl[c];
+      for (int r = 0; r < R(); r++) {
+        const int64_t i = (int64_t)c * R() + r;
+        s_phead[(int64_t)j * R() + r] = inl ? lc.max[i] - lc.req[i] : gc.max[i] - gc.req[i];
+      }
+    }
+    wsync();
+    algbytes += (int64_t)n * (8 + 16 * R());
   }
 
-  // --- 64-pod queue window: one gather per 64 pops ---------------------------------------------
-  __device__ __forceinline__ void refill(int qhead, int qlen, int P) {
-    hbm_release();  // queue pushes / relaxation states / staleness words of this wave have landed
+  // --- 64-pod queue window: one gather per 64 pops, one entry per lane ------------------------
+  __device__ __forceinline__ void refill(Window<RT>& w, int qhead, int qlen, int P, bool pushed) {
+    if (pushed) hbm_release();  // queue pushes / relaxation states / staleness words have landed
     const int n = qlen < kWave ? qlen : kWave;
     if (lane() < n) {
       int pos = qhead + lane();
       if (pos >= P) pos -= P;
-      const int p = ld_sc1(W.queue + pos);
-      const int uid = D.pod_uid[p];
-      const int s = ld_sc1(W.pod_state + p);
-      w_p[lane()] = p;
-      w_uid[lane()] = uid;
-      w_s[lane()] = s;
-      w_ll[lane()] = ld_sc1(W.last_len + uid);
-      w_flags[lane()] = D.st_flags[s];
-      w_tol[2 * lane()] = D.st_tol[2 * s];
-      w_tol[2 * lane() + 1] = D.st_tol[2 * s + 1];
-      for (int r = 0; r < R(); r++) w_req[lane() * R() + r] = D.pod_req[(int64_t)p * R() + r];
+      w.p = ld_sc1(W.queue + pos);
+      w.uid = D.pod_uid[w.p];
+      w.s = ld_sc1(W.pod_state + w.p);
+      w.ll = ld_sc1(W.last_len + w.uid);
+      w.flags = D.st_flags[w.s];
+      w.toltpl = D.st_toltpl[w.s];
+      w.tol0 = D.st_tol[2 * w.s];
+      w.tol1 = D.st_tol[2 * w.s + 1];
+#pragma unroll
+      for (int r = 0; r < RM; r++) {
+        if (RT == 0 && r >= d.R) break;
+        w.req[r] = D.pod_req[(int64_t)w.p * R() + r];
+      }
     }
-    wsync();
   }
 };
 
-template <int RT>
+template <int RT, bool TL>
 __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan pl) {
+  constexpr int RM = Solver<RT, TL>::RM;
   extern __shared__ __attribute__((aligned(16))) char smem_generic[];
   char KS_L* smem = (char KS_L*)smem_generic;
   const KsWork W = works[blockIdx.x];
   const KsDims& d = D.d;
-  Solver<RT> S(D, W, pl);
+  Solver<RT, TL> S(D, W, pl);
   const int R = S.R();
   char KS_L* sp = smem;
   auto take = [&](size_t bytes) { char KS_L* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
   KeyMeta KS_L* s_keys = (KeyMeta KS_L*)take(sizeof(KeyMeta) * d.NK);
   S.s_order = (LI32)take(4 * (size_t)pl.KO);
   S.s_okey = (LI32)take(4 * (size_t)pl.KO);
+  S.s_ptpl = (LI32)take(4 * (size_t)pl.KO);
+  S.s_phead = (LI64)take(8 * (size_t)pl.KO * R);
   S.lc.tpl = (LI32)take(4 * (size_t)pl.KL);
   S.lc.req = (LI64)take(8 * (size_t)pl.KL * R);
   S.lc.max = (LI64)take(8 * (size_t)pl.KL * R);
   S.lc.rem = (LU32)take(4 * (size_t)pl.KL * d.TW);
-  S.s_talloc = (LI64)take(pl.talloc ? 8 * (size_t)d.totalTplIts * R : 0);
+  S.lc.thr = (LI32)take(4 * (size_t)pl.KL * R);
+  S.lc.cnt = (LI32)take(4 * (size_t)pl.KL);
+  S.s_talloc = (LI64)take(TL ? 8 * (size_t)d.totalTplIts * R : 0);
+  S.s_tsa = (LI64)take(TL && pl.tsort ? 8 * (size_t)d.totalTplIts * R : 0);
+  S.s_tsp = (LI32)take(TL && pl.tsort ? 4 * (size_t)d.totalTplIts * R : 0);
   S.s_tbeg = (LI32)take(4 * (size_t)(d.NTPL + 1));
   S.s_pool = (LI64)take(8 * (size_t)(d.NPOOL + 1) * R);
   S.s_rs = (LU32)take(4 * (size_t)d.RSW);
   S.s_rem = (LU32)take(4 * (size_t)d.TW + 8);
   S.s_cand = (LU32)take(4 * (size_t)d.TW + 8);
-  S.w_p = (LI32)take(4 * kWave);
-  S.w_uid = (LI32)take(4 * kWave);
-  S.w_s = (LI32)take(4 * kWave);
-  S.w_flags = (LI32)take(4 * kWave);
-  S.w_ll = (LU64)take(8 * kWave);
-  S.w_tol = (LU64)take(16 * kWave);
-  S.w_req = (LI64)take(8 * (size_t)kWave * R);
   S.gc.tpl = W.c_tpl;
   S.gc.req = W.c_req;
   S.gc.max = W.c_max;
   S.gc.rem = W.c_rem;
+  S.gc.thr = W.c_thr;
+  S.gc.cnt = W.c_cnt;
   for (int i = lane(); i < d.NK * (int)(sizeof(KeyMeta) / 4); i += kWave)
     ((uint32_t KS_L*)s_keys)[i] = ((const uint32_t KS_G*)D.keys)[i];
   for (int i = lane(); i <= d.NTPL; i += kWave) S.s_tbeg[i] = D.tpl_it_beg[i];
   for (int i = lane(); i < d.NPOOL * R; i += kWave) S.s_pool[i] = D.pool_rem0[i];
-  if (pl.talloc)
+  if (TL)
     for (int i = lane(); i < d.totalTplIts * R; i += kWave)
       S.s_talloc[i] = D.it_alloc[(int64_t)D.tpl_its[i / R] * R + i % R];
+  if (TL && pl.tsort)
+    for (int i = lane(); i < d.totalTplIts * R; i += kWave) {
+      S.s_tsa[i] = D.tsort_alloc[i];
+      S.s_tsp[i] = D.tsort_pos[i];
+    }
   S.L.nkeys = d.NK;
   S.L.W = d.W;
   S.L.NB = d.NB;
@@ -524,6 +655,8 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
 
   const int P = d.P;
   int nclaims = 0, nlog = 0, hostCtr = d.hostnameSeed;
+  bool srt = true;      // s.newNodeClaims non-decreasing in len(Pods)
+  bool pushed = false;  // a failed pod was pushed back since the last window refill
   uint32_t epoch = 1;
   int qhead = 0, qlen = P;
   int wn = 0, wi = 0;  // window size / next index
@@ -533,8 +666,10 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   // kernel with KE_ITER_CAP instead of hanging the device.
   const int64_t popCap = (int64_t)64 * (d.S + P) + 100000;
   int err = KE_OK;
-  int64_t pod[RT > 0 ? RT : kMaxR];
-  int64_t req[RT > 0 ? RT : kMaxR];
+  Window<RT> w;
+  int64_t pod[RM];
+  int64_t req[RM];
+  int nthr[RM];
 #ifdef KS_PHASE_STATS
   uint64_t cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t tstart = __builtin_amdgcn_s_memtime();
@@ -543,27 +678,33 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   while (qlen > 0) {
     PH_BEGIN(t0);
     if (wi == wn) {
-      S.refill(qhead, qlen, P);
+      S.refill(w, qhead, qlen, P, pushed);
+      pushed = false;
       wn = qlen < kWave ? qlen : kWave;
       wi = 0;
       windows++;
     }
     // Queue.Pop (queue.go:46-61)
-    const int p = uni(S.w_p[wi]);
-    const int uid = uni(S.w_uid[wi]);
-    uint64_t ll = S.w_ll[wi];
+    const int p = rdl(w.p, wi);
+    const int uid = rdl(w.uid, wi);
+    uint64_t ll = (uint64_t)rdl64((int64_t)w.ll, wi);
     if (d.dupUids) {
       hbm_release();
-      ll = ld_sc1(W.last_len + uid);
+      ll = uni64((int64_t)ld_sc1(W.last_len + uid));
     }
     if ((uint32_t)(ll >> 32) == epoch && (uint32_t)ll == (uint32_t)qlen) break;
     qhead = qhead + 1 == P ? 0 : qhead + 1;
     qlen--;
     if (++pops > popCap) { err = KE_ITER_CAP; break; }
-    const int s = uni(S.w_s[wi]);
-    const int sflags = uni(S.w_flags[wi]);
-    for (int r = 0; r < R; r++) pod[r] = uni64(S.w_req[wi * R + r]);
-    const LU64 tol = S.w_tol + 2 * wi;
+    const int s = rdl(w.s, wi);
+    const int sflags = rdl(w.flags, wi);
+    const uint32_t toltpl = (uint32_t)rdl((int)w.toltpl, wi);
+    const uint64_t tol0 = (uint64_t)rdl64((int64_t)w.tol0, wi), tol1 = (uint64_t)rdl64((int64_t)w.tol1, wi);
+#pragma unroll
+    for (int r = 0; r < RM; r++) {
+      if (RT == 0 && r >= R) break;
+      pod[r] = rdl64(w.req[r], wi);
+    }
     wi++;
     PH_END(t0, 0);
     bool placed = false;
@@ -571,7 +712,7 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     PH_BEGIN(t1);
     for (int base = 0; base < d.N && !placed; base += kWave) {
       const int n = base + lane();
-      const bool ok = n < d.N && S.node_ok(n, s, sflags, pod, tol);
+      const bool ok = n < d.N && S.node_ok(n, s, sflags, pod, tol0, tol1);
       const uint64_t m = wballot(ok);
       S.algbytes += (int64_t)min(kWave, d.N - base) * (16 * R + 16);
       if (m) {
@@ -580,12 +721,7 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
           for (int r = 0; r < R; r++) W.n_req[(int64_t)j * R + r] += pod[r];
           if (sflags & SF_HAS_KEYS) rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
         }
-        if (lane() == 0) {
-          W.log_pod[nlog] = p;
-          W.log_tgt[nlog] = -(j + 1);
-          W.pod_status[p] = ST_SCHEDULED;
-        }
-        nlog++;
+        S.log_commit(p, -(j + 1), nlog);
         placed = true;
       }
     }
@@ -593,19 +729,19 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     // 2) in-flight NodeClaims, sorted by pod count
     if (!placed && nclaims > 0) {
       PH_BEGIN(t2);
-      S.sort_claims(nclaims, sorts, slow);
+      sorts++;
+      if (!srt) {
+        S.sort_claims(nclaims);
+        slow++;
+        srt = true;
+      }
       PH_END(t2, 2);
       for (int base = 0; base < nclaims && !placed; base += kWave) {
         PH_BEGIN(t3);
         const int j = base + lane();
-        bool q = false;
-        if (j < nclaims) {
-          const int c = S.s_order[j];
-          q = c < pl.KL ? S.template claim_quick<true>(c, s, sflags, pod, tol)
-                        : S.template claim_quick<false>(c, s, sflags, pod, tol);
-        }
+        const bool q = j < nclaims && S.claim_quick(j, s, sflags, toltpl, pod);
         uint64_t m = wballot(q);
-        S.algbytes += (int64_t)min(kWave, nclaims - base) * (16 * R + 4);
+        S.algbytes += (int64_t)min(kWave, nclaims - base) * (8 * R + 4);
         PH_END(t3, 3);
         while (m && !placed) {
           const int jj = base + ctz64(m);
@@ -613,21 +749,22 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
           const int c = uni(S.s_order[jj]);
           PH_BEGIN(t4);
           const bool inl = c < pl.KL;
-          const bool ok = inl ? S.template claim_full<true>(c, s, sflags, pod, req)
-                              : S.template claim_full<false>(c, s, sflags, pod, req);
+          int ncnt = 0;
+          const bool ok = inl ? S.template claim_full<true>(c, s, sflags, pod, req, nthr, ncnt)
+                              : S.template claim_full<false>(c, s, sflags, pod, req, nthr, ncnt);
           fulls++;
           PH_END(t4, 4);
           PH_BEGIN(t5);
           if (ok) {
-            if (inl) S.template commit_claim<true>(c, jj, p, sflags, req, nlog);
-            else S.template commit_claim<false>(c, jj, p, sflags, req, nlog);
+            srt = inl ? S.template commit_claim<true>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog)
+                      : S.template commit_claim<false>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog);
             placed = true;
           } else {
             // the quick bound was stale: tighten it to the exact max over the current options
             fullFails++;
             const int t = inl ? uni(S.lc.tpl[c]) : uni(W.c_tpl[c]);
-            if (inl) S.template recompute_max<true>(c, S.lc.rem + (int64_t)c * d.TW, t);
-            else S.template recompute_max<false>(c, S.gc.rem + (int64_t)c * d.TW, t);
+            if (inl) S.template recompute_max<true>(c, S.lc.rem + (int64_t)c * d.TW, t, jj);
+            else S.template recompute_max<false>(c, S.gc.rem + (int64_t)c * d.TW, t, jj);
           }
           PH_END(t5, 5);
         }
@@ -636,7 +773,7 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     // 3) new NodeClaim per template
     if (!placed) {
       PH_BEGIN(t6);
-      const int r = S.try_templates(p, s, sflags, pod, tol, nclaims, nlog, hostCtr);
+      const int r = S.try_templates(p, s, sflags, toltpl, pod, nclaims, nlog, hostCtr, srt);
       PH_END(t6, 6);
       if (r < 0) { err = KE_CLAIM_CAP; break; }
       if (r == 1) placed = true;
@@ -659,8 +796,10 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     if (tail >= P) tail -= P;
     if (lane() == 0) W.queue[tail] = p;
     qlen++;
+    pushed = true;
     if (!relaxed && lane() == 0) W.last_len[uid] = ((uint64_t)epoch << 32) | (uint32_t)qlen;
   }
+  S.log_flush(nlog);
   // write back LDS-resident claim state for the host
   for (int i = lane(); i < nclaims; i += kWave) W.order[i] = S.s_order[i];
   const int kl = nclaims < pl.KL ? nclaims : pl.KL;
@@ -685,25 +824,39 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   }
 }
 
-// LDS plan: put as much claim state in LDS as `budget` allows (one-Solve launches use the whole
-// 160 KiB of a CU; batched simulations pass a smaller budget to keep several waves per CU).
+// LDS plan.  Position-indexed state (order, pod count, template, headroom) bounds the NodeClaims
+// per Solve (KO); claims [0, KL) also keep their template/requests/max/options/thresholds in LDS,
+// the rest in HBM.  The instance-type tables go to LDS first when they leave room for 64 claims.
+// One-Solve launches use the whole 160 KiB of a CU; batched simulations pass a smaller budget.
 Plan make_plan(const KsDims& d, size_t budget) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   Plan pl{};
-  pl.KO = d.Kcap < 8192 ? d.Kcap : 8192;
-  const size_t R = d.R;
-  const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + 2 * r16(4 * (size_t)pl.KO) + r16(4 * (size_t)(d.NTPL + 1)) +
-                       r16(8 * (size_t)(d.NPOOL + 1) * R) + r16(4 * (size_t)d.RSW) + 2 * r16(4 * (size_t)d.TW + 8) +
-                       4 * r16(4 * kWave) + r16(8 * kWave) + r16(16 * kWave) + r16(8 * (size_t)kWave * R) + 16 * 16;
-  const size_t perClaim = 4 + 16 * R + 4 * (size_t)d.TW;
-  const size_t tallocB = r16(8 * (size_t)d.totalTplIts * R);
-  size_t avail = budget > fixed ? budget - fixed : 0;
-  pl.talloc = (tallocB + 64 * perClaim <= avail) ? 1 : 0;
-  if (pl.talloc) avail -= tallocB;
-  size_t kl = avail / (perClaim + 64);  // +64: per-array 16-byte rounding slack
-  pl.KL = (int)(kl < (size_t)pl.KO ? kl : (size_t)pl.KO);
-  pl.lds = fixed + (pl.talloc ? tallocB : 0) + r16(4 * (size_t)pl.KL) + 2 * r16(8 * (size_t)pl.KL * R) +
-           r16(4 * (size_t)pl.KL * d.TW);
+  const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
+  const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
+                       r16(4 * (size_t)d.RSW) + 2 * r16(4 * TW + 8) + 16 * 16;
+  const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)
+  const size_t clmB = 16 + 16 * R + 4 * TW + 4 * R;      // tpl, cnt, req, max, rem, thr (+ rounding)
+  const size_t slack = 10 * 16;                          // per-array 16-byte rounding
+  const size_t tallocB = r16(8 * tot * R);
+  const size_t tsortB = r16(8 * tot * R) + r16(4 * tot * R);
+  size_t avail = budget > fixed + slack ? budget - fixed - slack : 0;
+  // The threshold filter needs the sorted lists only without negative requests.
+  const size_t tablesB = tallocB + (d.negReq ? 0 : tsortB);
+  pl.talloc = (tablesB + 64 * (posB + clmB) <= avail) ? 1 : 0;
+  pl.tsort = pl.talloc && !d.negReq;
+  if (pl.talloc) avail -= tablesB;
+  const size_t kAll = avail / (posB + clmB);
+  size_t ko, kl;
+  if (kAll >= (size_t)d.Kcap) {
+    ko = kl = d.Kcap;
+  } else {  // half the LDS to positions, half to claim state
+    ko = std::min((size_t)d.Kcap, std::max(kAll, avail / 2 / posB));
+    kl = std::min(ko, (avail - ko * posB) / clmB);
+  }
+  pl.KO = (int)ko;
+  pl.KL = (int)kl;
+  pl.lds = fixed + 3 * r16(4 * ko) + r16(8 * ko * R) + 2 * r16(4 * kl) + 2 * r16(8 * kl * R) + r16(4 * kl * TW) +
+           r16(4 * kl * R) + (pl.tsort ? tsortB : 0) + (pl.talloc ? tallocB : 0);
   return pl;
 }
 
@@ -719,11 +872,14 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep, (const int32_t*)qorder);
   if (mid) (void)hipEventRecord(mid, st);
+#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_>), dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl)
+  const bool tl = pl.talloc != 0;
   switch (D.d.R) {
-    case 3: hipLaunchKernelGGL(k_solve<3>, dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl); break;
-    case 4: hipLaunchKernelGGL(k_solve<4>, dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl); break;
-    default: hipLaunchKernelGGL(k_solve<0>, dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl); break;
+    case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;
+    case 4: if (tl) KS_LAUNCH(4, true); else KS_LAUNCH(4, false); break;
+    default: if (tl) KS_LAUNCH(0, true); else KS_LAUNCH(0, false); break;
   }
+#undef KS_LAUNCH
   return hipGetLastError();
 }
 

@@ -29,7 +29,8 @@ class KsError(RuntimeError):
 
 class _Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("simulation_mode", ctypes.c_int), ("replicas", ctypes.c_int),
-                ("timing_only", ctypes.c_int), ("reserved", ctypes.c_int * 4)]
+                ("timing_only", ctypes.c_int), ("lds_budget", ctypes.c_int),
+                ("reserved", ctypes.c_int * 3)]
 
 
 def library_path():
@@ -115,10 +116,10 @@ class Scheduler:
         _check(lib().ks_problem_create(b, len(b), ctypes.byref(h)))
         self._h = h
 
-    def solve(self, replicas=1, device=-1, simulation_mode=True, timing_only=False):
+    def solve(self, replicas=1, device=-1, simulation_mode=True, timing_only=False, lds_budget=0):
         """Solve(ctx, pods) with fresh scheduler state; replicas>1 runs that many independent copies
         of the same Solve in one launch (one wavefront each) and returns replica 0's results."""
-        o = _Opts(device, 1 if simulation_mode else 0, replicas, 1 if timing_only else 0)
+        o = _Opts(device, 1 if simulation_mode else 0, replicas, 1 if timing_only else 0, lds_budget)
         r = ctypes.c_void_p()
         _check(lib().ks_solve(self._h, ctypes.byref(o), ctypes.byref(r)))
         try:

@@ -103,3 +103,29 @@ def test_reference_scenarios_gpu(scn):
     want, got = _solve_both(scn["snapshot"])
     assert scenario_check.check(scn, got.canonical()) == []
     assert _diff(want, got) is None
+
+
+# (seed, budget): claims exceed Plan::KL (checked below via ks_problem_inspect's plans)
+@pytest.mark.parametrize("seed,budget", [(201, 6000), (203, 14000), (206, 6000), (242, 9000), (251, 9000),
+                                         (251, 14000)])
+def test_small_lds_budget_parity(seed, budget):
+    """Small LDS budgets move claim state past Plan::KL to HBM and the instance-type tables out of
+    LDS; decisions must not change."""
+    snap = problems.random_problem(seed, n_pods=400, n_its=30, n_nodes=5)
+    from karpenter_amd import inspect
+    plan = inspect(snap)["plans"][str(budget)]
+    s = json.dumps(snap)
+    want, _ = bridge.solve(s)
+    assert plan["KL"] < len(want["newNodeClaims"]) <= plan["KO"]
+    got = Scheduler(s).solve(lds_budget=budget)
+    d = _diff(problems.canonical(want), got)
+    assert d is None, d
+
+
+def test_small_lds_budget_config2_overflow():
+    """C2 at 10k with ~6 KB of LDS: claims past KL=19 live in HBM, sorted Allocatable lists too."""
+    s = json.dumps(synth.config2(10000))
+    want, _ = bridge.solve(s)
+    assert len(want["newNodeClaims"]) > 19
+    got = Scheduler(s).solve(lds_budget=6000)
+    assert _diff(problems.canonical(want), got) is None
