@@ -185,3 +185,92 @@ def config1(seed=42):
 def config2(n_pods=50000, seed=42):
     """C2: 50k resource-only pods x 400 fake instance types, 1 template, no limits."""
     return benchmark_snapshot(n_pods, 400, seed, diverse=False)
+
+
+def _fmt_time(sec):
+    import datetime
+    return datetime.datetime.fromtimestamp(int(sec), tz=datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+NOW = 1760000000  # fixed "now" for lifetimeRemaining (types.go:136-145)
+
+
+def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, spot_frac=0.3, it_range=(15, 40),
+                     uninitialized_frac=0.0, not_ready_frac=0.0, expire_after="720h", pod_selectors=False,
+                     limits=None):
+    """A consolidation snapshot: an existing cluster of `n_nodes` nodes launched from one
+    WhenUnderutilized NodePool over fake.InstanceTypes(n_its), each running `pods_per_node` bound pods
+    (C1 cpu/memory distributions, distinct pod-deletion-cost annotations so candidate costs are
+    distinct), plus `n_pending` pending pods.  Every node is listed as a candidate; the host applies
+    NewCandidate / filterCandidates / the disruption-cost sort.  Schema: INTEGRATION.md §5."""
+    rng = np.random.default_rng(seed)
+    its = fake_instance_types(n_its)
+    pool = node_pool("default", limits=limits)
+    pool["spec"]["disruption"] = {"consolidationPolicy": "WhenUnderutilized", "expireAfter": expire_after}
+    cpu_m = [100, 250, 500, 1000, 1500]
+    mem_mi = [100, 256, 512, 1024, 2048, 4096]
+    nodes, cands = [], []
+    pid = 0
+    for j in range(n_nodes):
+        i = int(rng.integers(it_range[0], it_range[1]))
+        it = its[i]
+        alloc_cpu_m = (i + 1) * 1000 - 100
+        alloc_mem = 2 * (i + 1) * GI - 10 * (1 << 20)
+        alloc_pods = 10 * (i + 1)
+        offers = [o for o in it["offerings"] if o["available"]]
+        spot = rng.random() < spot_frac
+        cands_off = [o for o in offers if o["capacityType"] == ("spot" if spot else "on-demand")]
+        off = cands_off[int(rng.integers(len(cands_off)))]
+        used_cpu, used_mem, pods = 0, 0, []
+        for _ in range(pods_per_node):
+            c = cpu_m[int(rng.integers(5))]
+            m = mem_mi[int(rng.integers(6))] << 20
+            if used_cpu + c > alloc_cpu_m or used_mem + m > alloc_mem or len(pods) + 1 > alloc_pods:
+                continue
+            used_cpu += c
+            used_mem += m
+            p = pod(pid, cpu="%dm" % c, mem="%dMi" % (m >> 20), labels={"my-label": LABEL_VALUES[rng.integers(7)]})
+            if pod_selectors and rng.random() < 0.2:
+                p["spec"]["nodeSelector"] = {ARCH: "amd64"}
+            p["metadata"]["annotations"] = {"controller.kubernetes.io/pod-deletion-cost": str(int(rng.integers(-1000, 1000000)))}
+            p["spec"]["nodeName"] = "node-%05d" % j
+            p["status"] = {"phase": "Running", "conditions": [{"type": "PodScheduled", "status": "True"}]}
+            pods.append(p)
+            pid += 1
+        name = "node-%05d" % j
+        labels = {NODEPOOL: "default", IT_LABEL: it["name"], ZONE: off["zone"], CT: off["capacityType"],
+                  HOSTNAME: name, ARCH: "amd64", OS: "linux", "testing/cluster": "unspecified"}
+        nodes.append({
+            "name": name, "hostName": name, "labels": labels, "taints": [],
+            "capacity": dict(it["capacity"]),
+            "available": {"cpu": "%dm" % (alloc_cpu_m - used_cpu), "memory": str(alloc_mem - used_mem),
+                          "pods": str(alloc_pods - len(pods))},
+            "daemonSetRequests": {},
+            "initialized": bool(rng.random() >= uninitialized_frac),
+            "ready": bool(rng.random() >= not_ready_frac),
+            "creationTimestamp": _fmt_time(NOW - int(rng.integers(0, 30 * 86400))),
+            "pods": pods,
+        })
+        cands.append(name)
+    pending = []
+    for _ in range(n_pending):
+        pending.append(pod(pid, cpu=CPU_CHOICES[rng.integers(5)], mem=MEM_CHOICES[rng.integers(6)]))
+        pid += 1
+    return {
+        "wellKnownLabels": FAKE_WELL_KNOWN,
+        "instanceTypes": its,
+        "instanceTypesByNodePool": {"default": list(range(n_its))},
+        "nodeClaimTemplates": [pool],
+        "nodePools": [pool],
+        "daemonSetPods": [],
+        "stateNodes": nodes,
+        "pendingPods": pending,
+        "candidates": cands,
+        "now": _fmt_time(NOW),
+        "hostnameSeed": 0,
+    }
+
+
+def config5(n_nodes=5000, pods_per_node=20, seed=4205):
+    """C5: multi-node + single-node consolidation over a 5k-node / 100k-pod cluster."""
+    return cluster_snapshot(n_nodes, pods_per_node, 400, seed)

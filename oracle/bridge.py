@@ -25,6 +25,9 @@ def lib():
         l.oref_time_solve.restype = ctypes.c_int
         l.oref_eval_ops.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
         l.oref_eval_ops.restype = ctypes.c_int
+        l.oref_consolidate_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.POINTER(ctypes.c_double)]
+        l.oref_consolidate_json.restype = ctypes.c_int
         l.oref_last_error.restype = ctypes.c_char_p
         l.oref_free.argtypes = [ctypes.c_void_p]
         _lib = l
@@ -56,6 +59,18 @@ def time_solve(snapshot, reps):
     if l.oref_time_solve(s.encode(), reps, ctypes.byref(secs)) != 0:
         raise RuntimeError("oracle: " + l.oref_last_error().decode())
     return secs.value
+
+
+def consolidate(snapshot, all_sims=False):
+    """Oracle multi-node then single-node consolidation over a cluster snapshot; returns (doc, seconds).
+    all_sims: simulate every candidate / prefix (what the GPU computes) and report each outcome."""
+    l = lib()
+    s = snapshot if isinstance(snapshot, str) else json.dumps(snapshot)
+    out = ctypes.c_void_p()
+    secs = ctypes.c_double()
+    if l.oref_consolidate_json(s.encode(), 1 if all_sims else 0, ctypes.byref(out), ctypes.byref(secs)) != 0:
+        raise RuntimeError("oracle: " + l.oref_last_error().decode())
+    return json.loads(_take(out)), secs.value
 
 
 def eval_ops(ops, well_known=None):

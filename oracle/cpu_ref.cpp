@@ -17,7 +17,11 @@
 //
 // Go map-iteration-order choices are made canonically (sorted keys); see DESIGN.md §Parity.
 #include <algorithm>
+#include <cctype>
 #include <chrono>
+#include <cmath>
+#include <limits>
+#include <memory>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -381,6 +385,9 @@ struct Pod {
   bool hasOverhead = false;
   ResourceList overhead;
   vector<string> tscWhen;  // topologySpreadConstraints whenUnsatisfiable (inert with an empty Topology)
+  map<string, string> annotations;
+  bool hasPriority = false;
+  int32_t priority = 0;
 };
 
 // pkg/utils/pod/scheduling.go:28-34
@@ -648,6 +655,7 @@ static Pod parsePod(const ojson::Value& v) {
     if (auto* x = md->get("namespace")) p.ns = x->str();
     if (auto* x = md->get("uid")) p.uid = x->str();
     p.labels = strMap(md->get("labels"));
+    p.annotations = strMap(md->get("annotations"));
     if (auto* x = md->get("creationTimestamp")) p.created = parseTime(x->str());
     if (auto* x = md->get("deletionTimestamp")) p.deleting = !x->is_null();
     if (auto* ors = md->get("ownerReferences"))
@@ -661,6 +669,7 @@ static Pod parsePod(const ojson::Value& v) {
   const ojson::Value* sp = v.get("spec");
   if (sp) {
     if (auto* x = sp->get("nodeName")) p.nodeName = x->str();
+    if (auto* x = sp->get("priority"); x && !x->is_null()) { p.hasPriority = true; p.priority = (int32_t)x->i64(); }
     p.nodeSelector = strMap(sp->get("nodeSelector"));
     if (auto* af = sp->get("affinity"); af && !af->is_null()) {
       p.hasAffinity = true;
@@ -966,6 +975,13 @@ class Scheduler {
   }
 
   string ResultsJSON() const;
+
+  // Results accessors for the consolidation restatement (read after Solve)
+  int numNewNodeClaims() const { return (int)order_.size(); }
+  const NodeClaim& newNodeClaim(int k) const { return claims_[order_[k]]; }
+  const vector<ExistingNode>& existingNodes() const { return existing_; }
+  bool podError(int p) const { return attempted_[p] && !errors_[p].ok; }
+  int64_t nodeIDCounter() const { return nodeID_; }
 
   long long attempts = 0;  // statistics: NodeClaim.Add calls
 
@@ -1290,6 +1306,8 @@ string Scheduler::ResultsJSON() const {
   return o;
 }
 
+#include "consolidation.inc"
+
 // ---------------------------------------------------------------------------------------------
 // Requirement-algebra evaluator for the reference's golden vectors (requirement_test.go,
 // requirements_test.go).  Input: {"ops":[{"op":..., ...}]}; output {"results":[...]}.
@@ -1406,6 +1424,23 @@ int oref_time_solve(const char* snapshot, int reps, double* seconds) {
       total += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     *seconds = total;
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// Consolidation (single- and multi-node) over a cluster snapshot.  all_sims=1 simulates every
+// candidate and every multi-node prefix and reports each outcome.
+int oref_consolidate_json(const char* snapshot, int all_sims, char** out, double* seconds) {
+  try {
+    ojson::Value root = ojson::parse(snapshot);
+    oref::ConsProblem cp = oref::parseConsProblem(root);
+    auto t0 = std::chrono::steady_clock::now();
+    std::string r = oref::consolidateJSON(cp, all_sims != 0);
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (out) *out = dupstr(r);
     return 0;
   } catch (const std::exception& e) {
     g_err = e.what();

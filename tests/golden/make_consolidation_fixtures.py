@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Known-answer consolidation scenarios hand-transcribed from the reference's Go tests.
+
+Source: pkg/controllers/disruption/consolidation_test.go, with the suite setup of
+pkg/controllers/disruption/suite_test.go:95-130 (fake.InstanceTypesAssorted(), on-demand types
+sorted by cheapest price -> leastExpensiveInstance / mostExpensiveInstance) and the test.NodePool()
+defaults (WhenUnderutilized, expireAfter 720h; clock stepped 10 minutes past node creation).
+
+Each scenario is {"name", "source", "snapshot", "expect"}; `expect` holds the Go test's assertion on
+the command the disruption controller would execute (multi-node consolidation runs before
+single-node consolidation; the first non-no-op wins):
+  action      : "delete" | "replace" | "no-op"
+  candidates  : node names removed by the command (set)
+  replacement_excludes : an instance type the replacement must not offer
+Validation (the 15 s re-check) and PDBs are outside the restated path.
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "karpenter-sigs_amd"))
+from karpenter_amd import synth  # noqa: E402
+
+NOW = synth.NOW
+
+
+def assorted():
+    """fake.InstanceTypesAssorted (fake/instancetype.go:111-145)."""
+    out = []
+    for cpu in [1, 2, 4, 8, 16, 32, 64]:
+        for mem in [1, 2, 4, 8, 16, 32, 64, 128]:
+            for zone in ["test-zone-1", "test-zone-2", "test-zone-3"]:
+                for ct in ["spot", "on-demand"]:
+                    for os_ in ["linux", "windows"]:
+                        for arch in ["amd64", "arm64"]:
+                            name = "%d-cpu-%d-mem-%s-%s-%s-%s" % (cpu, mem, arch, os_, zone, ct)
+                            price = synth.price_from_resources(cpu, mem * synth.GI)
+                            out.append(synth.fake_instance_type(
+                                name, cpu, mem, pods=None, arch=arch, oses=(os_,),
+                                offerings=[{"capacityType": ct, "zone": zone, "price": price, "available": True}]))
+    return out
+
+
+def cheapest_price(it):
+    return min(o["price"] for o in it["offerings"])
+
+
+def od_sorted(its):
+    # suite_test.go:116-128; price ties keep list order here (Go's sort.Slice tie order is unpinned,
+    # and no assertion below depends on which tied type is picked)
+    ods = [it for it in its if any(o["capacityType"] == "on-demand" for o in it["offerings"])]
+    return sorted(ods, key=cheapest_price)
+
+
+def nodepool(requirements=None):
+    np_ = synth.node_pool("default", requirements=requirements)
+    np_["spec"]["disruption"] = {"consolidationPolicy": "WhenUnderutilized", "expireAfter": "720h"}
+    return np_
+
+
+def rs_pod(i, cpu=None, bound_to=None, annotations=None, pending=False):
+    """test.Pod owned by a ReplicaSet (consolidation_test.go), bound with ExpectManualBinding."""
+    p = synth.pod(i, cpu=cpu)
+    p["metadata"]["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "rs", "uid": "rs-uid"}]
+    p["metadata"]["labels"] = {"app": "test"}
+    if annotations:
+        p["metadata"]["annotations"] = annotations
+    if bound_to:
+        p["spec"]["nodeName"] = bound_to
+        p["status"] = {"phase": "Running", "conditions": [{"type": "PodScheduled", "status": "True"}]}
+    return p
+
+
+def node(name, it, alloc, pods, initialized=True):
+    """test.NodeClaimAndNode with the NodeClaim's labels and Status.Allocatable."""
+    off = it["offerings"][0]
+    labels = {synth.NODEPOOL: "default", synth.IT_LABEL: it["name"], synth.CT: off["capacityType"],
+              synth.ZONE: off["zone"], synth.HOSTNAME: name}
+    avail = dict(alloc)
+    if "pods" in avail:
+        avail["pods"] = str(int(avail["pods"]) - len(pods))
+    if "cpu" in avail:
+        used_m = 0
+        for p in pods:
+            c = p["spec"]["containers"][0]["resources"]["requests"].get("cpu")
+            if c:
+                used_m += int(float(c) * 1000) if not c.endswith("m") else int(c[:-1])
+        total_m = int(float(alloc["cpu"]) * 1000)
+        avail["cpu"] = "%dm" % (total_m - used_m)
+    return {"name": name, "hostName": name, "labels": labels, "taints": [], "capacity": dict(alloc),
+            "available": avail, "daemonSetRequests": {}, "initialized": initialized, "ready": initialized,
+            "creationTimestamp": synth._fmt_time(NOW - 600), "pods": pods}
+
+
+def snapshot(its, nodes, pending=(), requirements=None):
+    np_ = nodepool(requirements)
+    return {"wellKnownLabels": synth.FAKE_WELL_KNOWN, "instanceTypes": its,
+            "instanceTypesByNodePool": {"default": list(range(len(its)))},
+            "nodeClaimTemplates": [np_], "nodePools": [np_], "daemonSetPods": [],
+            "stateNodes": nodes, "pendingPods": list(pending), "candidates": [n["name"] for n in nodes],
+            "now": synth._fmt_time(NOW), "hostnameSeed": 0}
+
+
+def scenarios():
+    src = "pkg/controllers/disruption/consolidation_test.go"
+    its = assorted()
+    ods = od_sorted(its)
+    least, most = ods[0], ods[-1]
+    S = []
+    # Replace / "can replace node" (:209-266)
+    n = node("node-a", most, {"cpu": "32"}, [rs_pod(0, bound_to="node-a")])
+    S.append({"name": "can-replace-node", "source": src + ":209-266", "snapshot": snapshot(its, [n]),
+              "expect": {"action": "replace", "candidates": ["node-a"], "replacement_excludes": most["name"]}})
+    # "won't replace node if any spot replacement is more expensive" (:851-945)
+    cur = synth.fake_instance_type("current-on-demand", 4, 4, offerings=[
+        {"capacityType": "on-demand", "zone": "test-zone-1a", "price": 0.5, "available": False}])
+    rep = synth.fake_instance_type("potential-spot-replacement", 4, 4, offerings=[
+        {"capacityType": "spot", "zone": "test-zone-1a", "price": 1.0, "available": True},
+        {"capacityType": "spot", "zone": "test-zone-1b", "price": 0.2, "available": True},
+        {"capacityType": "spot", "zone": "test-zone-1c", "price": 0.4, "available": True}])
+    n = node("node-a", cur, {"cpu": "32"}, [rs_pod(0, bound_to="node-a")])
+    S.append({"name": "spot-replacement-more-expensive", "source": src + ":851-945",
+              "snapshot": snapshot([cur, rep], [n]), "expect": {"action": "no-op", "candidates": []}})
+    # "won't replace on-demand node if on-demand replacement is more expensive" (:946-1040)
+    rep = synth.fake_instance_type("on-demand-replacement", 4, 4, offerings=[
+        {"capacityType": "on-demand", "zone": "test-zone-1a", "price": 0.6, "available": True},
+        {"capacityType": "on-demand", "zone": "test-zone-1b", "price": 0.6, "available": True},
+        {"capacityType": "spot", "zone": "test-zone-1b", "price": 0.2, "available": True},
+        {"capacityType": "spot", "zone": "test-zone-1c", "price": 0.3, "available": True}])
+    n = node("node-a", cur, {"cpu": "32"}, [rs_pod(0, bound_to="node-a")])
+    S.append({"name": "on-demand-replacement-more-expensive", "source": src + ":946-1040",
+              "snapshot": snapshot([cur, rep], [n], requirements=[
+                  {"key": synth.CT, "operator": "In", "values": ["on-demand"]}]),
+              "expect": {"action": "no-op", "candidates": []}})
+    # Delete / "can delete nodes" (:1098-1145)
+    alloc = {"cpu": "32", "pods": "100"}
+    n1 = node("node-a", least, alloc, [rs_pod(0, bound_to="node-a"), rs_pod(1, bound_to="node-a")])
+    n2 = node("node-b", least, alloc, [rs_pod(2, bound_to="node-b")])
+    S.append({"name": "can-delete-nodes", "source": src + ":1098-1145", "snapshot": snapshot(its, [n1, n2]),
+              "expect": {"action": "delete", "candidates": ["node-b"]}})
+    # "won't delete node if it would require pods to schedule on an un-initialized node" (:1582-1631)
+    n1 = node("node-a", least, alloc, [rs_pod(0, bound_to="node-a"), rs_pod(1, bound_to="node-a")],
+              initialized=False)
+    n2 = node("node-b", least, alloc, [rs_pod(2, bound_to="node-b")])
+    S.append({"name": "no-delete-onto-uninitialized", "source": src + ":1582-1631",
+              "snapshot": snapshot(its, [n1, n2]), "expect": {"action": "no-op", "candidates": []}})
+    # "can replace nodes, considers karpenter.sh/do-not-disrupt on pods" (:772-850)
+    n = node("node-a", most, {"cpu": "32"},
+             [rs_pod(0, bound_to="node-a", annotations={"karpenter.sh/do-not-disrupt": "true"})])
+    S.append({"name": "do-not-disrupt-pod", "source": src + ":772-850", "snapshot": snapshot(its, [n]),
+              "expect": {"action": "no-op", "candidates": []}})
+    # "considers pending pods when consolidating" (:148-208)
+    large = sorted([it for it in its if int(it["capacity"]["cpu"]) >= 64], key=lambda it: it["offerings"][0]["price"])[0]
+    bound = rs_pod(0, cpu="1", bound_to="node-a")
+    bound["metadata"].pop("ownerReferences")
+    unsched = synth.pod(1, cpu="62")
+    n = node("node-a", large, {"cpu": large["capacity"]["cpu"], "pods": large["capacity"]["pods"]}, [bound])
+    S.append({"name": "considers-pending-pods", "source": src + ":148-208",
+              "snapshot": snapshot(its, [n], pending=[unsched]), "expect": {"action": "no-op", "candidates": []}})
+    # Multi-NodeClaim / "can merge 3 nodes into 1" (:2799-2848)
+    ns = [node("node-%s" % c, most, alloc, [rs_pod(i, bound_to="node-%s" % c)]) for i, c in enumerate("abc")]
+    S.append({"name": "merge-3-into-1", "source": src + ":2799-2848", "snapshot": snapshot(its, ns),
+              "expect": {"action": "replace", "candidates": ["node-a", "node-b", "node-c"]}})
+    # "won't merge 2 nodes into 1 of the same type" (:2849-2926)
+    n1 = node("node-a", least, alloc, [rs_pod(0, bound_to="node-a")])
+    n2 = node("node-b", least, alloc, [rs_pod(1, bound_to="node-b"), rs_pod(2, bound_to="node-b")])
+    S.append({"name": "no-merge-same-type", "source": src + ":2849-2926", "snapshot": snapshot(its, [n1, n2]),
+              "expect": {"action": "delete", "candidates": ["node-a"]}})
+    return S
+
+
+def main():
+    # The snapshots (1344 instance types each) are rebuilt from this script by the tests; the fixture
+    # keeps the transcribed expectations.
+    out = [{"name": s["name"], "source": s["source"], "expect": s["expect"]} for s in scenarios()]
+    with open(os.path.join(HERE, "consolidation_scenarios.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print("%d scenarios" % len(out))
+
+
+if __name__ == "__main__":
+    main()
