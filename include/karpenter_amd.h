@@ -82,6 +82,32 @@ double ks_results_solve_kernel_ms(const ks_results* r);
 /* Algorithmic bytes the solve scanned (SURVEY.md §8d formula, counted by the kernel). */
 double ks_results_algorithmic_bytes(const ks_results* r);
 
+/* ---- Consolidation (pkg/controllers/disruption) ------------------------------------------------
+ * ks_cons_create replaces the per-simulation NewScheduler calls of simulateScheduling
+ * (helpers.go:73-127) for one disruption pass: the cluster snapshot (state nodes
+ * with their pods, pending pods, candidate node names, NodePools, instance types) is encoded once.
+ * Candidates are built and ordered like NewCandidate + sortAndFilterCandidates (types.go:54-113,
+ * consolidation.go:73-83).  The simulations are every multi-node prefix firstNConsolidationOption
+ * can probe (multinodeconsolidation.go:87-137) and one per candidate (singlenodeconsolidation.go:
+ * 42-88); each ends in the computeConsolidation decision (consolidation.go:113-194) on the GPU. */
+typedef struct ks_cons ks_cons;
+int ks_cons_create(const char* snapshot_json, size_t len, ks_cons** out);
+void ks_cons_free(ks_cons* c);
+int ks_cons_num_candidates(const ks_cons* c);
+int ks_cons_num_sims(const ks_cons* c);
+int ks_cons_record_bytes(const ks_cons* c);           /* fixed size of one simulation record */
+int ks_cons_records_per_rank(const ks_cons* c, int world);
+/* Run the simulations s with s % world == rank on the current (or opts->device) GPU and write their
+ * records, in order of s, to `records` (records_per_rank * record_bytes bytes; a device pointer when
+ * records_on_device, so an all-gather over RCCL can collect them).  kernel_ms: HIP-event time of the
+ * queue sort + simulation kernel on the stream they ran on. */
+int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void* records, int records_on_device,
+                double* kernel_ms);
+/* Replay the reference's sequential choice over the gathered records ([rank][slot] layout):
+ * JSON {"candidates":[{name, disruptionCost}], "multi":{"command", "sims"}, "single":{"command", "sims"}}.
+ * all_sims: report every simulation (otherwise only those the reference would have run). */
+int ks_cons_decide(const ks_cons* c, const void* records, int world, int all_sims, char** json_out);
+
 void ks_free(void* p);
 const char* ks_last_error(void);
 int ks_device_count(void);

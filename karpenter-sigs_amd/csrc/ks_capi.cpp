@@ -10,37 +10,16 @@
 
 #include "../../include/karpenter_amd.h"
 #include "ks_host.h"
-
-namespace ks {
-hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
-                        uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
-                        hipEvent_t mid);
-Plan make_plan(const KsDims& d, size_t budget);
-size_t queue_sort_temp_bytes(int n);
-}  // namespace ks
+#include "ks_runtime.h"
 
 using namespace ks;
 
 static thread_local std::string g_err;
-
-#define HIPCHK(x)                                                                                   \
-  do {                                                                                              \
-    hipError_t e_ = (x);                                                                            \
-    if (e_ != hipSuccess) throw KsError(KS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
-  } while (0)
+namespace ks {
+void set_last_error(const std::string& m) { g_err = m; }
+}  // namespace ks
 
 namespace {
-
-// One hipMalloc carved into 256-byte aligned arrays.
-struct Arena {
-  std::vector<std::pair<size_t, size_t>> parts;  // offset, bytes
-  size_t total = 0;
-  size_t add(size_t bytes) {
-    size_t off = total;
-    total += (bytes + 255) & ~(size_t)255;
-    return off;
-  }
-};
 
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
@@ -133,34 +112,7 @@ struct ks_results {
   std::vector<int64_t> counters;
 };
 
-struct ks_problem {
-  Host host;
-  KsDev dev{};
-  void* dbuf = nullptr;
-  void* wbuf = nullptr;
-  size_t wbytes = 0;
-  KsWork* works_dev = nullptr;
-  int wreps = 0;
-  hipStream_t stream = nullptr;
-  int device = -1;
-  int lastKO = 0;  // claim capacity of the last launch plan
-  // NewQueue radix-sort workspace
-  uint64_t* skeys = nullptr;
-  int32_t* svals = nullptr;
-  void* stemp = nullptr;
-  size_t stempBytes = 0;
-  ~ks_problem() {
-    if (skeys) (void)hipFree(skeys);
-    if (svals) (void)hipFree(svals);
-    if (stemp) (void)hipFree(stemp);
-    if (dbuf) (void)hipFree(dbuf);
-    if (wbuf) (void)hipFree(wbuf);
-    if (works_dev) (void)hipFree(works_dev);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-};
-
-static void upload(ks_problem* pb) {
+void ks_upload(ks_problem* pb) {
   Host& h = pb->host;
   auto& t = h.tab;
   Arena a;
@@ -204,6 +156,9 @@ static void upload(ks_problem* pb) {
   size_t o_nr = put(t.n_req0.data(), t.n_req0.size() * 8);
   size_t o_nrs = put(t.n_rs0.data(), t.n_rs0.size() * 4);
   size_t o_nt = put(t.n_taint.data(), t.n_taint.size() * 8);
+  size_t o_nf = put(t.n_flags.data(), t.n_flags.size() * 4);
+  size_t o_pf = put(t.pod_flags.data(), t.pod_flags.size() * 4);
+  size_t o_op = put(t.off_price.data(), t.off_price.size() * 8);
   HIPCHK(hipMalloc(&pb->dbuf, a.total));
   std::vector<char> staging(a.total, 0);
   for (auto& it : items)
@@ -245,6 +200,9 @@ static void upload(ks_problem* pb) {
   D.n_req0 = (const int64_t*)(b + o_nr);
   D.n_rs0 = (const uint32_t*)(b + o_nrs);
   D.n_taint = (const uint64_t*)(b + o_nt);
+  D.n_flags = (const int32_t*)(b + o_nf);
+  D.pod_flags = (const int32_t*)(b + o_pf);
+  D.off_price = (const double*)(b + o_op);
 }
 
 // Rebuild Results from the replica-0 workspace.
@@ -422,18 +380,6 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
   return res;
 }
 
-#define API_TRY try {
-#define API_CATCH                                  \
-  }                                                \
-  catch (const KsError& e) {                       \
-    g_err = e.what();                              \
-    return e.code;                                 \
-  }                                                \
-  catch (const std::exception& e) {                \
-    g_err = e.what();                              \
-    return KS_ERR_PARSE;                           \
-  }
-
 extern "C" {
 
 const char* ks_last_error(void) { return g_err.c_str(); }
@@ -456,7 +402,7 @@ int ks_problem_create(const char* json, size_t len, ks_problem** out) {
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw KsError(KS_ERR_HIP, "no HIP device visible");
   HIPCHK(hipGetDevice(&pb->device));
   HIPCHK(hipStreamCreateWithFlags(&pb->stream, hipStreamNonBlocking));
-  upload(pb.get());
+  ks_upload(pb.get());
   {
     size_t n = std::max(pb->host.dims.P, 1);
     HIPCHK(hipMalloc(&pb->skeys, 2 * n * sizeof(uint64_t)));

@@ -1,0 +1,775 @@
+// ks_cons.cpp — consolidation (pkg/controllers/disruption) on the GPU.
+//
+//   host   : the cluster snapshot -> one resident scheduling problem holding every pod any simulation
+//            schedules (pending pods, the candidates' reschedulable pods, the deleting nodes' pods)
+//            and every active node; candidate construction and ordering; per-simulation views
+//   device : every candidate-deletion simulation (simulateScheduling helpers.go:73-127 + the
+//            computeConsolidation decision consolidation.go:113-194) as one wavefront of k_solve<SIM>,
+//            a whole batch per launch, sharded across GPUs by simulation index
+//   host   : the reference's sequential selection replayed over the gathered records
+//            (MultiNodeConsolidation.firstNConsolidationOption multinodeconsolidation.go:87-137,
+//            SingleNodeConsolidation.ComputeCommand singlenodeconsolidation.go:42-88)
+//
+// Candidate construction follows NewCandidate (types.go:54-113) for the listed nodes, disruptionCost /
+// GetPodEvictionCost / lifetimeRemaining (helpers.go:137-177, types.go:136-145), filterCandidates'
+// do-not-disrupt rule (helpers.go:47-71; PDBs are the caller's filter) and the cost sort of
+// sortAndFilterCandidates (consolidation.go:73-83, Go sort.Slice emulated exactly).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <ctime>
+#include <limits>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/karpenter_amd.h"
+#include "ks_gosort.h"
+#include "ks_host.h"
+#include "ks_runtime.h"
+
+using namespace ks;
+using ksjson::Value;
+
+namespace {
+
+const char* kCTKey = "karpenter.sh/capacity-type";
+const char* kZoneKey = "topology.kubernetes.io/zone";
+const char* kPoolKey = "karpenter.sh/nodepool";
+const char* kITKey = "node.kubernetes.io/instance-type";
+
+std::string jstr(const Value* v, const char* k, const std::string& d = "") {
+  if (!v) return d;
+  const Value* x = v->get(k);
+  return x && x->is_str() ? x->str() : d;
+}
+
+int64_t parse_rfc3339(const std::string& s) {  // seconds; the snapshot uses "YYYY-MM-DDTHH:MM:SSZ"
+  if (s.size() < 19) return 0;
+  struct tm t{};
+  t.tm_year = std::atoi(s.substr(0, 4).c_str()) - 1900;
+  t.tm_mon = std::atoi(s.substr(5, 2).c_str()) - 1;
+  t.tm_mday = std::atoi(s.substr(8, 2).c_str());
+  t.tm_hour = std::atoi(s.substr(11, 2).c_str());
+  t.tm_min = std::atoi(s.substr(14, 2).c_str());
+  t.tm_sec = std::atoi(s.substr(17, 2).c_str());
+  return (int64_t)timegm(&t);
+}
+
+// time.ParseDuration for the forms NodePool durations take ("720h", "1h30m", "90s", "1.5h")
+bool go_duration(const std::string& s, int64_t& ns) {
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '-' || s[0] == '+') neg = s[i++] == '-';
+  if (s.substr(i) == "0") { ns = 0; return true; }
+  long double total = 0;
+  while (i < s.size()) {
+    size_t j = i;
+    while (j < s.size() && (std::isdigit((unsigned char)s[j]) || s[j] == '.')) j++;
+    if (j == i) return false;
+    const long double v = std::stold(s.substr(i, j - i));
+    size_t k = j;
+    while (k < s.size() && !std::isdigit((unsigned char)s[k]) && s[k] != '.') k++;
+    const std::string u = s.substr(j, k - j);
+    long double mul;
+    if (u == "ns") mul = 1;
+    else if (u == "us" || u == "\xC2\xB5s" || u == "\xCE\xBCs") mul = 1e3;
+    else if (u == "ms") mul = 1e6;
+    else if (u == "s") mul = 1e9;
+    else if (u == "m") mul = 60e9;
+    else if (u == "h") mul = 3600e9;
+    else return false;
+    total += v * mul;
+    i = k;
+  }
+  ns = (int64_t)(neg ? -total : total);
+  return true;
+}
+
+double dur_seconds(int64_t d) { return (double)(d / 1000000000) + (double)(d % 1000000000) / 1e9; }
+double clampf(double lo, double v, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+double eviction_cost(const PodH& p) {  // GetPodEvictionCost helpers.go:137-159
+  double cost = 1.0;
+  auto a = p.annotations.find("controller.kubernetes.io/pod-deletion-cost");
+  if (a != p.annotations.end() && !a->second.empty() && !std::isspace((unsigned char)a->second[0])) {
+    char* end = nullptr;
+    const double c = std::strtod(a->second.c_str(), &end);
+    if (end && *end == 0) cost += c / std::pow(2.0, 27.0);  // a ParseFloat error is logged and ignored
+  }
+  if (p.hasPriority) cost += (double)p.priority / std::pow(2.0, 25.0);
+  return clampf(-10.0, cost, 10.0);
+}
+
+bool do_not_disrupt(const PodH& p) {  // pkg/utils/pod/scheduling.go:85-92
+  auto a = p.annotations.find("karpenter.sh/do-not-evict");
+  auto b = p.annotations.find("karpenter.sh/do-not-disrupt");
+  return (a != p.annotations.end() && a->second == "true") || (b != p.annotations.end() && b->second == "true");
+}
+
+}  // namespace
+
+struct ks_cons {
+  struct Cand {
+    int node = -1;  // index into host.nodes (calculateExistingNodeClaims order)
+    std::string name, pool, ct, zone;
+    int it = -1;
+    double cost = 0;
+    std::vector<int> pods;  // global pod indices (GetNodePods)
+  };
+  struct Sim {
+    std::vector<int> cands;  // indices into cands
+    bool multi = false;
+  };
+  std::unique_ptr<ks_problem> pb;
+  std::vector<Cand> cands;
+  std::vector<Sim> sims;  // multi-node prefixes first (largest first), then one per candidate
+  int multiHi = 0;        // multi-node prefix lengths mid+1 for mid in [1, multiHi]
+  std::vector<int> pending, deleting;
+  int64_t hostnameSeed = 0;
+  int recWords = 0;
+
+  // cached launch for (rank, world)
+  int lrank = -1, lworld = -1;
+  std::vector<int> lsims;  // simulation ids of this rank, launch order
+  void* lbuf = nullptr;    // workspaces + pod maps + views
+  KsWork* lworks = nullptr;
+  int32_t* lrec = nullptr;
+  int32_t* lentries = nullptr;
+  int32_t* lentrySim = nullptr;
+  int32_t* lpodmap = nullptr;
+  uint64_t* lkeys = nullptr;
+  int32_t* lvals = nullptr;
+  void* ltemp = nullptr;
+  size_t ltempBytes = 0;
+  int lnent = 0, lrbits = 0, lsbits = 0;
+  Plan lplan{};
+  int32_t* rank = nullptr;  // global NewQueue rank of every pod
+
+  int sim_of_multi(int mid) const { return multiHi - mid; }  // mid in [1, multiHi]
+  int sim_of_single(int i) const { return multiHi + i; }
+  int per_rank(int world) const { return ((int)sims.size() + world - 1) / world; }
+
+  void free_launch() {
+    for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
+                    (void*)lkeys, (void*)lvals, ltemp})
+      if (p) (void)hipFree(p);
+    lbuf = nullptr;
+    lworks = nullptr;
+    lrec = lentries = lentrySim = lpodmap = nullptr;
+    lkeys = nullptr;
+    lvals = nullptr;
+    ltemp = nullptr;
+    lrank = lworld = -1;
+  }
+  ~ks_cons() {
+    if (pb) (void)hipSetDevice(pb->device);
+    free_launch();
+    if (rank) (void)hipFree(rank);
+  }
+};
+
+namespace {
+
+// Parse the cluster snapshot into the resident problem + candidates + sims.
+void build_cons(ks_cons& c, const Value& root) {
+  if (!root.is_obj()) throw KsError(KS_ERR_PARSE, "snapshot is not an object");
+  const Value* nodesV = root.get("stateNodes");
+  // Active nodes (nodes.Active(): not marked for deletion) enter the problem; the deleting ones only
+  // contribute their pods (deletingNodes.Pods, helpers.go:91-95).
+  auto sub = std::make_shared<ksjson::Array>();
+  auto pods = std::make_shared<ksjson::Array>();
+  std::vector<std::vector<int>> nodePods;  // per snapshot node: global pod indices (GetNodePods)
+  std::vector<PodH> podMeta;
+  if (const Value* pv = root.get("pendingPods"))
+    for (auto& v : pv->arr()) {
+      c.pending.push_back((int)pods->size());
+      pods->push_back(v);
+      podMeta.push_back(parse_pod(v));
+    }
+  std::map<std::string, int> nodeByName;
+  std::vector<char> deletingNode;
+  int ni = 0;
+  for (auto& nv : nodesV ? nodesV->arr() : ksjson::Array{}) {
+    const std::string name = jstr(&nv, "name");
+    const bool del = nv.get("markedForDeletion") ? nv.get("markedForDeletion")->boolean(false) : false;
+    nodeByName[name] = ni++;
+    deletingNode.push_back(del);
+    if (!del) sub->push_back(nv);
+    std::vector<int> mine;
+    if (const Value* ps = nv.get("pods"))
+      for (auto& pv : ps->arr()) {
+        PodH p = parse_pod(pv);
+        if (p.ownedByNode || p.ownedByDaemonSet || p.terminal || p.deleting) continue;  // node.go:32-53
+        mine.push_back((int)pods->size());
+        pods->push_back(pv);
+        podMeta.push_back(std::move(p));
+      }
+    nodePods.push_back(mine);
+  }
+  for (size_t i = 0; i < nodePods.size(); i++)
+    if (deletingNode[i]) for (int p : nodePods[i]) c.deleting.push_back(p);
+
+  // the Solve snapshot the problem is encoded from
+  Value solveRoot;
+  solveRoot.kind = Value::Obj;
+  solveRoot.o = std::make_shared<ksjson::Object>(root.obj());
+  Value a1, a2;
+  a1.kind = a2.kind = Value::Arr;
+  a1.a = sub;
+  a2.a = pods;
+  (*solveRoot.o)["stateNodes"] = a1;
+  (*solveRoot.o)["pods"] = a2;
+  c.pb.reset(new ks_problem());
+  Host& h = c.pb->host;
+  h.build(solveRoot);
+  if (h.dims.dupUids) throw KsError(KS_ERR_UNSUPPORTED, "consolidation snapshot has duplicate pod UIDs");
+  c.hostnameSeed = h.hostnameSeed;
+  std::map<std::string, int> hostNode;  // node name -> host.nodes index (sorted order)
+  for (size_t i = 0; i < h.nodes.size(); i++) hostNode[h.nodes[i].name] = (int)i;
+
+  // NodePools: expireAfter for lifetimeRemaining
+  std::map<std::string, int64_t> expire;
+  std::set<std::string> poolNames;
+  if (const Value* ps = root.get("nodePools"))
+    for (auto& v : ps->arr()) {
+      const std::string name = jstr(v.get("metadata"), "name");
+      poolNames.insert(name);
+      const Value* d = v.get("spec") ? v.get("spec")->get("disruption") : nullptr;
+      int64_t ns = 0;
+      if (d && d->get("expireAfter") && d->get("expireAfter")->is_str() && go_duration(d->get("expireAfter")->str(), ns))
+        expire[name] = ns;
+    }
+  std::map<std::string, std::map<std::string, int>> poolTypes;
+  if (const Value* bp = root.get("instanceTypesByNodePool"))
+    for (auto& kv : bp->obj())
+      for (auto& x : kv.second.arr()) {
+        const int64_t i = x.i64();
+        if (i < 0 || i >= (int64_t)h.its.size()) throw KsError(KS_ERR_PARSE, "instanceTypesByNodePool index out of range");
+        poolTypes[kv.first][h.its[(size_t)i].name] = (int)i;
+      }
+  const int64_t nowNs = parse_rfc3339(jstr(&root, "now")) * 1000000000;
+
+  // NewCandidate for the listed nodes; nodes that would fail it are not candidates
+  std::vector<ks_cons::Cand> cands;
+  if (const Value* cs = root.get("candidates"))
+    for (auto& v : cs->arr()) {
+      const std::string name = v.str();
+      auto it = nodeByName.find(name);
+      if (it == nodeByName.end()) continue;
+      const Value& nv = nodesV->arr()[(size_t)it->second];
+      if (deletingNode[(size_t)it->second]) continue;
+      auto hn = hostNode.find(name);
+      if (hn == hostNode.end()) continue;
+      const Host::Node& n = h.nodes[(size_t)hn->second];
+      if (!n.initialized) continue;
+      auto lct = n.labels.find(kCTKey), lz = n.labels.find(kZoneKey), lp = n.labels.find(kPoolKey);
+      if (lct == n.labels.end() || lz == n.labels.end() || lp == n.labels.end()) continue;
+      auto pt = poolTypes.find(lp->second);
+      if (!poolNames.count(lp->second) || pt == poolTypes.end()) continue;
+      auto lit = n.labels.find(kITKey);
+      if (lit == n.labels.end() || !pt->second.count(lit->second)) continue;
+      ks_cons::Cand k;
+      k.node = hn->second;
+      k.name = name;
+      k.pool = lp->second;
+      k.ct = lct->second;
+      k.zone = lz->second;
+      k.it = pt->second.at(lit->second);
+      k.pods = nodePods[(size_t)it->second];
+      double cost = 0;
+      for (int p : k.pods) cost += eviction_cost(podMeta[(size_t)p]);  // disruptionCost helpers.go:170-176
+      double remaining = 1.0;                                           // lifetimeRemaining types.go:136-145
+      auto ex = expire.find(k.pool);
+      if (ex != expire.end()) {
+        const int64_t created = parse_rfc3339(jstr(&nv, "creationTimestamp")) * 1000000000;
+        const double age = dur_seconds(nowNs - created), total = dur_seconds(ex->second);
+        remaining = clampf(0.0, (total - age) / total, 1.0);
+      }
+      k.cost = cost * remaining;
+      bool blocked = false;
+      for (int p : k.pods) blocked = blocked || do_not_disrupt(podMeta[(size_t)p]);
+      if (!blocked) cands.push_back(std::move(k));
+    }
+  // sort.Slice(candidates, disruptionCost <): pdqsort only observes less(), so the costs' dense ranks
+  // reproduce its swap sequence exactly.
+  {
+    const int n = (int)cands.size();
+    std::vector<double> vals;
+    for (auto& k : cands) vals.push_back(k.cost);
+    std::sort(vals.begin(), vals.end());
+    std::vector<int32_t> key(n), idx(n);
+    for (int i = 0; i < n; i++) {
+      key[i] = (int32_t)(std::lower_bound(vals.begin(), vals.end(), cands[i].cost) - vals.begin());
+      idx[i] = i;
+    }
+    GoSortExact g{GoSort{key.data(), idx.data()}};
+    g.run(n);
+    for (int i = 0; i < n; i++) c.cands.push_back(cands[(size_t)idx[i]]);
+  }
+  // the simulations: multi-node prefixes (firstNConsolidationOption's search space) and single nodes
+  const int n = (int)c.cands.size();
+  if (n >= 2) {
+    int hi = std::min(n, 100);
+    if (n <= hi) hi = n - 1;
+    c.multiHi = hi;
+  }
+  for (int mid = c.multiHi; mid >= 1; mid--) {
+    ks_cons::Sim s;
+    s.multi = true;
+    for (int i = 0; i <= mid; i++) s.cands.push_back(i);
+    c.sims.push_back(s);
+  }
+  for (int i = 0; i < n; i++) {
+    ks_cons::Sim s;
+    s.cands.push_back(i);
+    c.sims.push_back(s);
+  }
+  c.recWords = rec_words(h.dims.TW, h.dims.RSW);
+}
+
+// Offerings.Get(capacityType, zone) (all offerings, available or not): first match
+bool offering_price(const Host::IT& it, const std::string& ct, const std::string& zone, double& price) {
+  for (auto& o : it.all)
+    if (o.ct == ct && o.zone == zone) {
+      price = o.price;
+      return true;
+    }
+  return false;
+}
+
+// Build and upload the launch of this rank's simulations (cached per (rank, world)).
+void prepare_launch(ks_cons& c, int rank, int world) {
+  if (c.lrank == rank && c.lworld == world) return;
+  c.free_launch();
+  ks_problem& pb = *c.pb;
+  Host& h = pb.host;
+  const KsDims& d = h.dims;
+  const int R = d.R, N = std::max(d.N, 1), NT = std::max(d.NTPL, 1), NP = std::max(d.NPOOL, 1);
+  std::vector<int> mine;
+  for (int s = rank; s < (int)c.sims.size(); s += world) mine.push_back(s);
+  const int ns = (int)mine.size();
+  c.lsims = mine;
+  // per-node capacity in device units (limits are restored for the removed candidates)
+  auto nodeCap = [&](int node, int r) -> int64_t {
+    auto it = h.nodes[(size_t)node].capacity.find(h.resNames[(size_t)r]);
+    return it == h.nodes[(size_t)node].capacity.end() ? 0 : h.toDev(r, it->second);
+  };
+  Arena a;
+  struct Off {
+    size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
+        last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price;
+  };
+  std::vector<Off> offs(ns);
+  std::vector<int> simP(ns), entBeg(ns + 1, 0);
+  std::vector<int32_t> entries, entrySim;
+  int maxP = 1;
+  for (int k = 0; k < ns; k++) {
+    const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
+    std::vector<int> pods = c.pending;
+    for (int ci : sm.cands) pods.insert(pods.end(), c.cands[(size_t)ci].pods.begin(), c.cands[(size_t)ci].pods.end());
+    pods.insert(pods.end(), c.deleting.begin(), c.deleting.end());
+    simP[k] = (int)pods.size();
+    maxP = std::max(maxP, simP[k]);
+    for (int p : pods) {
+      entries.push_back(p);
+      entrySim.push_back(k);
+    }
+    entBeg[k + 1] = (int)entries.size();
+    const size_t P = std::max(simP[k], 1), K = P;
+    Off& o = offs[k];
+    o.c_tpl = a.add(4 * K);
+    o.c_cnt = a.add(4 * K);
+    o.c_thr = a.add(4 * K * R);
+    o.c_host = a.add(4 * K);
+    o.c_req = a.add(8 * K * R);
+    o.c_max = a.add(8 * K * R);
+    o.c_rs = a.add(4 * K * d.RSW);
+    o.c_rem = a.add(4 * K * d.TW);
+    o.order = a.add(4 * K);
+    o.n_req = a.add(8 * P * R);
+    o.n_rs = a.add(4 * P * d.RSW);
+    o.n_slot = a.add(4 * (size_t)N);
+    o.queue = a.add(4 * P);
+    o.pod_state = a.add(4 * P);
+    o.last_len = a.add(8 * P);
+    o.log_pod = a.add(4 * P);
+    o.log_tgt = a.add(4 * P);
+    o.pod_status = a.add(4 * P);
+    o.pod_fstate = a.add(4 * P);
+    o.fail_code = a.add(4 * P * NT);
+    o.fail_host = a.add(4 * P * NT);
+    o.counters = a.add(8 * CT_NCOUNTERS);
+    o.rm = a.add(4 * std::max<size_t>(sm.cands.size(), 1));
+    o.pool0 = a.add(8 * (size_t)NP * R);
+    o.st_price = sm.multi ? a.add(8 * (size_t)std::max(d.T, 1)) : 0;
+  }
+  c.lnent = (int)entries.size();
+  HIPCHK(hipMalloc(&c.lbuf, std::max<size_t>(a.total, 256)));
+  char* base = (char*)c.lbuf;
+  HIPCHK(hipMalloc(&c.lworks, sizeof(KsWork) * std::max(ns, 1)));
+  HIPCHK(hipMalloc(&c.lrec, 4 * (size_t)c.recWords * std::max(ns, 1)));
+  HIPCHK(hipMalloc(&c.lentries, 4 * (size_t)std::max(c.lnent, 1)));
+  HIPCHK(hipMalloc(&c.lentrySim, 4 * (size_t)std::max(c.lnent, 1)));
+  HIPCHK(hipMalloc(&c.lpodmap, 4 * (size_t)std::max(c.lnent, 1)));
+  HIPCHK(hipMalloc(&c.lkeys, 16 * (size_t)std::max(c.lnent, 1)));
+  HIPCHK(hipMalloc(&c.lvals, 8 * (size_t)std::max(c.lnent, 1)));
+  c.ltempBytes = std::max<size_t>(queue_sort_temp_bytes(std::max(c.lnent, 1)), 256);
+  HIPCHK(hipMalloc(&c.ltemp, c.ltempBytes));
+  if (c.lnent) {
+    HIPCHK(hipMemcpy(c.lentries, entries.data(), 4 * entries.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c.lentrySim, entrySim.data(), 4 * entrySim.size(), hipMemcpyHostToDevice));
+  }
+  c.lrbits = 1;
+  while ((1ll << c.lrbits) < std::max(d.P, 2)) c.lrbits++;
+  c.lsbits = 1;
+  while ((1ll << c.lsbits) < std::max(ns, 2)) c.lsbits++;
+
+  // per-simulation inputs: removed nodes, limits, prices
+  std::vector<char> stage(a.total, 0);
+  std::vector<KsWork> works(ns);
+  for (int k = 0; k < ns; k++) {
+    const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
+    const Off& o = offs[k];
+    std::vector<int32_t> rm;
+    for (int ci : sm.cands) rm.push_back(c.cands[(size_t)ci].node);
+    std::sort(rm.begin(), rm.end());
+    memcpy(stage.data() + o.rm, rm.data(), 4 * rm.size());
+    std::vector<int64_t> pool0(h.tab.pool_rem0.begin(), h.tab.pool_rem0.begin() + (size_t)NP * R);
+    for (int p = 0; p < d.NPOOL; p++)
+      for (int node : rm) {
+        auto l = h.nodes[(size_t)node].labels.find(kPoolKey);
+        if (l == h.nodes[(size_t)node].labels.end() || l->second != h.pools[(size_t)p].name) continue;
+        for (int r = 0; r < R; r++)
+          if ((h.tab.pool_mask[(size_t)p] >> r) & 1u) pool0[(size_t)p * R + r] += nodeCap(node, r);
+      }
+    memcpy(stage.data() + o.pool0, pool0.data(), 8 * pool0.size());
+    KsWork w{};
+    // getCandidatePrices (consolidation.go:197-207): float64 sum in candidate order
+    double price = 0;
+    int cflags = 0;
+    bool allSpot = true;
+    for (int ci : sm.cands) {
+      const ks_cons::Cand& k = c.cands[(size_t)ci];
+      double pr;
+      if (!offering_price(h.its[(size_t)k.it], k.ct, k.zone, pr)) {
+        cflags |= CF_PRICE_ERR;
+        break;
+      }
+      price += pr;
+    }
+    for (int ci : sm.cands) allSpot = allSpot && c.cands[(size_t)ci].ct == "spot";
+    if (allSpot) cflags |= CF_ALL_SPOT;
+    if (sm.multi) {
+      cflags |= CF_MULTI;
+      // filterOutSameType: the cheapest candidate offering per candidate instance type (by name)
+      std::set<std::string> existing;
+      std::map<std::string, double> prices;
+      for (int ci : sm.cands) {
+        const ks_cons::Cand& k = c.cands[(size_t)ci];
+        const Host::IT& it = h.its[(size_t)k.it];
+        existing.insert(it.name);
+        double pr;
+        if (!offering_price(it, k.ct, k.zone, pr)) continue;
+        auto f = prices.find(it.name);
+        const double cur = f == prices.end() ? std::numeric_limits<double>::max() : f->second;
+        if (pr < cur) prices[it.name] = pr;
+      }
+      std::vector<double> st(std::max(d.T, 1), std::numeric_limits<double>::quiet_NaN());
+      for (int t = 0; t < d.T; t++)
+        if (existing.count(h.its[(size_t)t].name)) {
+          auto f = prices.find(h.its[(size_t)t].name);
+          st[(size_t)t] = f == prices.end() ? 0.0 : f->second;  // a missing map entry reads as 0
+        }
+      memcpy(stage.data() + o.st_price, st.data(), 8 * st.size());
+      w.st_price = (const double*)(base + o.st_price);
+    }
+    w.c_tpl = (int32_t*)(base + o.c_tpl);
+    w.c_cnt = (int32_t*)(base + o.c_cnt);
+    w.c_thr = (int32_t*)(base + o.c_thr);
+    w.c_host = (int32_t*)(base + o.c_host);
+    w.c_req = (int64_t*)(base + o.c_req);
+    w.c_max = (int64_t*)(base + o.c_max);
+    w.c_rs = (uint32_t*)(base + o.c_rs);
+    w.c_rem = (uint32_t*)(base + o.c_rem);
+    w.order = (int32_t*)(base + o.order);
+    w.n_req = (int64_t*)(base + o.n_req);
+    w.n_rs = (uint32_t*)(base + o.n_rs);
+    w.n_slot = (int32_t*)(base + o.n_slot);
+    w.queue = (int32_t*)(base + o.queue);
+    w.qorder = nullptr;
+    w.pod_state = (int32_t*)(base + o.pod_state);
+    w.last_len = (uint64_t*)(base + o.last_len);
+    w.log_pod = (int32_t*)(base + o.log_pod);
+    w.log_tgt = (int32_t*)(base + o.log_tgt);
+    w.pod_status = (int32_t*)(base + o.pod_status);
+    w.pod_fstate = (int32_t*)(base + o.pod_fstate);
+    w.fail_code = (uint32_t*)(base + o.fail_code);
+    w.fail_host = (int32_t*)(base + o.fail_host);
+    w.pool_rem = nullptr;
+    w.counters = (int64_t*)(base + o.counters);
+    w.pod_map = c.lpodmap + entBeg[k];
+    w.P = simP[k];
+    w.nrm = (int32_t)rm.size();
+    w.rm = (const int32_t*)(base + o.rm);
+    w.pool0 = (const int64_t*)(base + o.pool0);
+    w.rec = c.lrec + (size_t)k * c.recWords;
+    w.price = price;
+    w.cflags = cflags;
+    works[k] = w;
+  }
+  HIPCHK(hipMemcpy(c.lbuf, stage.data(), a.total, hipMemcpyHostToDevice));
+  if (ns) HIPCHK(hipMemcpy(c.lworks, works.data(), sizeof(KsWork) * ns, hipMemcpyHostToDevice));
+  // LDS plan: a small budget per simulation so several simulations share a CU
+  KsDims dd = d;
+  dd.Kcap = std::max(1, std::min(maxP, 16384));
+  c.lplan = make_plan(dd, 40 * 1024, true);
+  if (c.lplan.lds > 64 * 1024 || c.lplan.KO < 1) c.lplan = make_plan(dd, 160 * 1024 - 256, true);
+  if (c.lplan.lds > 160 * 1024 || c.lplan.KO < 1) throw KsError(KS_ERR_CAPACITY, "simulation state does not fit in LDS");
+  c.lrank = rank;
+  c.lworld = world;
+}
+
+std::string names_json(const Host& h, const std::vector<int>& its) {
+  std::string o = "[";
+  for (size_t i = 0; i < its.size(); i++) {
+    if (i) o += ",";
+    ksjson::quote(o, h.its[(size_t)its[i]].name);
+  }
+  return o + "]";
+}
+
+std::vector<int> bits_to_its(const Host& h, int tpl, const int32_t* bits) {
+  std::vector<int> out;
+  const Host::Tpl& t = h.tpls[(size_t)tpl];
+  for (int pos = 0; pos < (int)t.its.size(); pos++)
+    if (((uint32_t)bits[pos >> 5] >> (pos & 31)) & 1u) out.push_back(t.its[(size_t)pos]);
+  return out;
+}
+
+// The reference's sequential selection over the simulation records.
+std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool allSims) {
+  const Host& h = c.pb->host;
+  const KsDims& d = h.dims;
+  const int per = c.per_rank(world);
+  auto rec = [&](int sim) -> const int32_t* {
+    return recs + ((size_t)(sim % world) * per + (size_t)(sim / world)) * c.recWords;
+  };
+  for (size_t s = 0; s < c.sims.size(); s++)
+    if (rec((int)s)[RF_ERROR] != KE_OK)
+      throw KsError(rec((int)s)[RF_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
+                    "simulation " + std::to_string(s) + " reported kernel error " + std::to_string(rec((int)s)[RF_ERROR]));
+  const int n = (int)c.cands.size();
+  int64_t counter = c.hostnameSeed;
+  std::map<int, int64_t> before;  // sim -> hostname counter before it ran
+  auto run = [&](int sim) {
+    if (before.count(sim)) return;
+    before[sim] = counter;
+    counter += rec(sim)[RF_HOSTINCR];
+  };
+  auto candNames = [&](const std::vector<int>& cs) {
+    std::string o = "[";
+    for (size_t i = 0; i < cs.size(); i++) {
+      if (i) o += ",";
+      ksjson::quote(o, c.cands[(size_t)cs[i]].name);
+    }
+    return o + "]";
+  };
+  auto simJSON = [&](int sim) {
+    const int32_t* r = rec(sim);
+    std::string o = "{\"candidates\":" + candNames(c.sims[(size_t)sim].cands) + ",\"allNonPendingScheduled\":" +
+                    ((r[RF_FLAGS] & RB_ALL_SCHEDULED) ? "true" : "false") +
+                    ",\"newNodeClaims\":" + std::to_string(r[RF_NCLAIMS]);
+    if (r[RF_NCLAIMS] > 0) {
+      o += ",\"claim0\":{\"nodePoolName\":";
+      ksjson::quote(o, h.tpls[(size_t)r[RF_TPL]].pool);
+      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR));
+      o += ",\"requirementsString\":";
+      ksjson::quote(o, h.reqsString((const uint32_t*)(r + RF_HDR + 3 * d.TW), before.at(sim) + r[RF_HOST]));
+      o += "}";
+    }
+    return o + "}";
+  };
+  // commandJSON: action, candidates, replacement (multi: filterOutSameType's options)
+  auto cmdJSON = [&](int sim, bool err) {
+    if (sim < 0) return std::string("{\"action\":\"no-op\",\"candidates\":[]") + (err ? ",\"error\":true}" : "}");
+    const int32_t* r = rec(sim);
+    static const char* act[] = {"no-op", "delete", "replace", "no-op"};
+    std::string o = std::string("{\"action\":\"") + act[r[RF_ACTION]] + "\",\"candidates\":" +
+                    (r[RF_ACTION] == CA_NOOP || r[RF_ACTION] == CA_ERROR ? std::string("[]") : candNames(c.sims[(size_t)sim].cands));
+    if (r[RF_ACTION] == CA_REPLACE) {
+      const bool multi = c.sims[(size_t)sim].multi;
+      std::vector<uint32_t> rs((const uint32_t*)(r + RF_HDR + 3 * d.TW), (const uint32_t*)(r + RF_HDR + 3 * d.TW) + d.RSW);
+      if (r[RF_FLAGS] & RB_NARROWED) {
+        std::vector<uint32_t> spot = h.emptyRec();
+        h.addNSR(spot, kCTKey, "In", {"spot"});
+        rs_add(h.L, rs.data(), spot.data());
+      }
+      o += ",\"replacement\":{\"nodePoolName\":";
+      ksjson::quote(o, h.tpls[(size_t)r[RF_TPL]].pool);
+      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR + (multi ? 2 : 1) * d.TW));
+      o += ",\"requirements\":[";
+      const uint64_t pr = rs_present(rs.data());
+      bool first = true;
+      for (int k = 0; k < d.NK; k++) {  // FinalizeScheduling dropped the hostname requirement
+        if (!bit(pr, k) || k == h.hostKey) continue;
+        if (!first) o += ",";
+        first = false;
+        ksjson::quote(o, h.reqString(rs.data(), k, true, before.at(sim) + r[RF_HOST]));
+      }
+      o += "]}";
+    }
+    if (err) o += ",\"error\":true";
+    return o + "}";
+  };
+
+  std::string o = "{\"candidates\":[";
+  for (int i = 0; i < n; i++) {
+    if (i) o += ",";
+    o += "{\"name\":";
+    ksjson::quote(o, c.cands[(size_t)i].name);
+    char buf[64];
+    snprintf(buf, sizeof buf, ",\"disruptionCost\":%.17g}", c.cands[(size_t)i].cost);
+    o += buf;
+  }
+  // MultiNodeConsolidation.firstNConsolidationOption: binary search over the prefix length
+  int multiSim = -1;
+  bool multiErr = false;
+  std::set<int> multiRan;
+  if (c.multiHi >= 1) {
+    int lo = 1, hi = c.multiHi;
+    if (allSims)
+      for (int mid = 1; mid <= c.multiHi; mid++) {
+        run(c.sim_of_multi(mid));
+        multiRan.insert(mid);
+      }
+    while (lo <= hi) {
+      const int mid = (lo + hi) / 2;
+      const int sim = c.sim_of_multi(mid);
+      run(sim);
+      multiRan.insert(mid);
+      const int32_t* r = rec(sim);
+      if (r[RF_ACTION] == CA_ERROR) {
+        multiErr = true;
+        multiSim = -1;
+        break;
+      }
+      const bool validReplace = r[RF_ACTION] == CA_REPLACE && r[RF_NSAME] > 0;
+      if (validReplace || r[RF_ACTION] == CA_DELETE) {
+        multiSim = sim;
+        lo = mid + 1;
+      } else {
+        hi = mid - 1;
+      }
+    }
+  }
+  std::string multiSims;
+  for (int mid : multiRan) multiSims += (multiSims.empty() ? "" : ",") + simJSON(c.sim_of_multi(mid));
+  // SingleNodeConsolidation.ComputeCommand: the first candidate whose simulation yields an action
+  int singleSim = -1;
+  std::string singleSims;
+  for (int i = 0; i < n; i++) {
+    if (singleSim >= 0 && !allSims) break;
+    const int sim = c.sim_of_single(i);
+    run(sim);
+    singleSims += (i ? "," : "") + simJSON(sim);
+    const int a = rec(sim)[RF_ACTION];
+    if (singleSim >= 0 || a == CA_ERROR || a == CA_NOOP) continue;
+    singleSim = sim;
+  }
+  o += "],\"multi\":{\"command\":" + cmdJSON(multiSim, multiErr) + ",\"sims\":[" + multiSims + "]}";
+  o += ",\"single\":{\"command\":" + cmdJSON(singleSim, false) + ",\"sims\":[" + singleSims + "]}}";
+  return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ks_cons_create(const char* json, size_t len, ks_cons** out) {
+  API_TRY
+  if (!json || !out) throw KsError(KS_ERR_ARG, "null argument");
+  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  std::unique_ptr<ks_cons> c(new ks_cons());
+  build_cons(*c, root);
+  ks_problem& pb = *c->pb;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw KsError(KS_ERR_HIP, "no HIP device visible");
+  HIPCHK(hipGetDevice(&pb.device));
+  HIPCHK(hipStreamCreateWithFlags(&pb.stream, hipStreamNonBlocking));
+  ks_upload(&pb);
+  // global NewQueue rank of every pod (each simulation's queue is this order restricted to its pods)
+  const int P = pb.host.dims.P;
+  const size_t np = std::max(P, 1);
+  HIPCHK(hipMalloc(&pb.skeys, 2 * np * sizeof(uint64_t)));
+  HIPCHK(hipMalloc(&pb.svals, 2 * np * sizeof(int32_t)));
+  pb.stempBytes = std::max<size_t>(queue_sort_temp_bytes((int)np), 256);
+  HIPCHK(hipMalloc(&pb.stemp, pb.stempBytes));
+  int32_t* order = nullptr;
+  HIPCHK(hipMalloc(&order, 4 * np));
+  HIPCHK(hipMalloc(&c->rank, 4 * np));
+  HIPCHK(queue_sort(pb.dev, pb.skeys, pb.svals, pb.stemp, pb.stempBytes, order, pb.stream));
+  HIPCHK(rank_from_order(order, c->rank, P, pb.stream));
+  HIPCHK(hipStreamSynchronize(pb.stream));
+  (void)hipFree(order);
+  *out = c.release();
+  return KS_OK;
+  API_CATCH
+}
+
+void ks_cons_free(ks_cons* c) { delete c; }
+
+int ks_cons_num_candidates(const ks_cons* c) { return c ? (int)c->cands.size() : 0; }
+int ks_cons_num_sims(const ks_cons* c) { return c ? (int)c->sims.size() : 0; }
+int ks_cons_record_bytes(const ks_cons* c) { return c ? 4 * c->recWords : 0; }
+int ks_cons_records_per_rank(const ks_cons* c, int world) { return c && world > 0 ? c->per_rank(world) : 0; }
+
+int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void* records, int records_on_device,
+                double* kernel_ms) {
+  API_TRY
+  if (!c || !records || world < 1 || rank < 0 || rank >= world) throw KsError(KS_ERR_ARG, "bad argument");
+  if (opts && opts->device >= 0) HIPCHK(hipSetDevice(opts->device));
+  prepare_launch(*c, rank, world);
+  ks_problem& pb = *c->pb;
+  const int ns = (int)c->lsims.size();
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, pb.stream));
+  HIPCHK(sim_queue_sort(c->rank, c->lentries, c->lentrySim, c->lnent, c->lrbits, c->lsbits, c->lkeys, c->lvals,
+                        c->ltemp, c->ltempBytes, c->lpodmap, pb.stream));
+  HIPCHK(launch_sims(pb.dev, c->lworks, ns, c->lplan, pb.stream));
+  HIPCHK(hipEventRecord(e1, pb.stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  const size_t bytes = 4 * (size_t)c->recWords * ns, all = 4 * (size_t)c->recWords * c->per_rank(world);
+  if (records_on_device) {
+    HIPCHK(hipMemsetAsync(records, 0, all, pb.stream));
+    if (bytes) HIPCHK(hipMemcpyAsync(records, c->lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
+  } else {
+    memset(records, 0, all);
+    if (bytes) HIPCHK(hipMemcpyAsync(records, c->lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
+  }
+  HIPCHK(hipStreamSynchronize(pb.stream));
+  if (kernel_ms) *kernel_ms = ms;
+  return KS_OK;
+  API_CATCH
+}
+
+int ks_cons_decide(const ks_cons* c, const void* records, int world, int all_sims, char** json_out) {
+  API_TRY
+  if (!c || !records || !json_out || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
+  *json_out = strdup(decide_json(*c, (const int32_t*)records, world, all_sims != 0).c_str());
+  return KS_OK;
+  API_CATCH
+}
+
+}  // extern "C"

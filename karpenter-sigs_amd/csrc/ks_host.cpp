@@ -179,16 +179,41 @@ static QList podRequests(const Value& pod, bool& hostPorts, bool& volumes) {
   return req;
 }
 
-static PodH parsePod(const Value& v) {
+PodH parse_pod(const Value& v) {
   PodH p;
   const Value* md = v.get("metadata");
   p.name = jstr(md, "name");
   p.ns = jstr(md, "namespace");
   p.uid = jstr(md, "uid");
   p.created = jtime(jstr(md, "creationTimestamp"));
-  if (md) p.labels = jmap(md->get("labels"));
+  std::string nodeName, nominated;
+  bool failedToSchedule = false;
+  if (md) {
+    p.labels = jmap(md->get("labels"));
+    p.annotations = jmap(md->get("annotations"));
+    if (auto* x = md->get("deletionTimestamp")) p.deleting = !x->is_null();
+    if (auto* ors = md->get("ownerReferences"))
+      for (auto& o : ors->arr()) {
+        const std::string av = jstr(&o, "apiVersion"), kind = jstr(&o, "kind");
+        if (av == "apps/v1" && kind == "DaemonSet") p.ownedByDaemonSet = true;
+        if (av == "v1" && kind == "Node") p.ownedByNode = true;
+      }
+  }
+  if (auto* st = v.get("status")) {
+    const std::string ph = jstr(st, "phase");
+    p.terminal = ph == "Failed" || ph == "Succeeded";
+    nominated = jstr(st, "nominatedNodeName");
+    if (auto* cs = st->get("conditions"))
+      for (auto& c : cs->arr())
+        if (jstr(&c, "type") == "PodScheduled" && jstr(&c, "reason") == "Unschedulable") failedToSchedule = true;
+  }
   const Value* sp = v.get("spec");
   if (sp) {
+    nodeName = jstr(sp, "nodeName");
+    if (auto* x = sp->get("priority"); x && !x->is_null()) {
+      p.hasPriority = true;
+      p.priority = (int32_t)x->i64();
+    }
     p.nodeSelector = jmap(sp->get("nodeSelector"));
     if (auto* af = sp->get("affinity"); af && !af->is_null()) {
       p.hasAffinity = true;
@@ -220,6 +245,7 @@ static PodH parsePod(const Value& v) {
       for (auto& t : ts->arr()) p.tscWhen.push_back(jstr(&t, "whenUnsatisfiable"));
   }
   p.requests = podRequests(v, p.hostPorts, p.volumes);
+  p.provisionable = nodeName.empty() && nominated.empty() && failedToSchedule && !p.ownedByDaemonSet && !p.ownedByNode;
   return p;
 }
 
@@ -373,7 +399,12 @@ void Host::build(const Value& root) {
       if (auto* os = e.get("offerings"))
         for (auto& o : os->arr()) {
           bool avail = o.get("available") ? o.get("available")->boolean(true) : true;
-          if (avail) it.offers.push_back({jstr(&o, "zone"), jstr(&o, "capacityType")});
+          const double price = o.get("price") ? o.get("price")->f64() : 0.0;
+          it.all.push_back(Offer{jstr(&o, "zone"), jstr(&o, "capacityType"), price, avail});
+          if (avail) {
+            it.offers.push_back({jstr(&o, "zone"), jstr(&o, "capacityType")});
+            it.prices.push_back(price);
+          }
         }
       its.push_back(std::move(it));
     }
@@ -425,6 +456,7 @@ void Host::build(const Value& root) {
       n.capacity = jqlist(e.get("capacity"));
       n.dsRequests = jqlist(e.get("daemonSetRequests"));
       n.initialized = e.get("initialized") ? e.get("initialized")->boolean(true) : true;
+      n.ready = e.get("ready") ? e.get("ready")->boolean(true) : true;
       n.origIndex = (int)nodes.size();
       nodes.push_back(std::move(n));
     }
@@ -432,8 +464,8 @@ void Host::build(const Value& root) {
     if (a.initialized != b.initialized) return a.initialized;
     return a.name < b.name;
   });
-  if (auto* v = root.get("daemonSetPods")) for (auto& e : v->arr()) daemons.push_back(parsePod(e));
-  if (auto* v = root.get("pods")) for (auto& e : v->arr()) pods.push_back(parsePod(e));
+  if (auto* v = root.get("daemonSetPods")) for (auto& e : v->arr()) daemons.push_back(parse_pod(e));
+  if (auto* v = root.get("pods")) for (auto& e : v->arr()) pods.push_back(parse_pod(e));
   for (auto& p : pods) {
     if (p.hostPorts) throw KsError(-2, "pod " + p.ns + "/" + p.name + " uses hostPorts (not encoded by this build)");
     if (p.volumes) throw KsError(-2, "pod " + p.ns + "/" + p.name + " mounts PVC volumes (not encoded by this build)");
@@ -443,6 +475,8 @@ void Host::build(const Value& root) {
   internKey(kHostname);
   internKey(kZone);
   internKey(kCT);
+  intern(kCT, "spot");  // worstLaunchPrice asks Has(spot) / Has(on-demand) of every requirement set
+  intern(kCT, "on-demand");
   std::set<std::string> bounded;
   auto visitNSR = [&](const std::vector<NSR>& v) {
     for (auto& n : v) {
@@ -598,14 +632,15 @@ void Host::build(const Value& root) {
     for (auto& n : its[i].reqs) addNSR(rs, n.key, n.op, n.values);
     std::copy(rs.begin(), rs.end(), tab.it_rs.begin() + (size_t)i * dims.RSW);
     itKeys |= rs_present(rs.data());
-    for (auto& o : its[i].offers) {
-      tab.off_zone.push_back(valueId[zoneKey].at(o.first));
-      tab.off_ct.push_back(valueId[ctKey].at(o.second));
+    for (size_t o = 0; o < its[i].offers.size(); o++) {
+      tab.off_zone.push_back(valueId[zoneKey].at(its[i].offers[o].first));
+      tab.off_ct.push_back(valueId[ctKey].at(its[i].offers[o].second));
+      tab.off_price.push_back(its[i].prices[o]);
     }
     tab.it_off_beg[i + 1] = (int)tab.off_zone.size();
   }
   itKeys |= (1ull << zoneKey) | (1ull << ctKey);
-  if (tab.off_zone.empty()) { tab.off_zone.push_back(0); tab.off_ct.push_back(0); }
+  if (tab.off_zone.empty()) { tab.off_zone.push_back(0); tab.off_ct.push_back(0); tab.off_price.push_back(0); }
 
   // --- templates: requirements, daemon overhead (getDaemonOverhead scheduler.go:324-341)
   int NT = (int)tpls.size();
@@ -689,8 +724,10 @@ void Host::build(const Value& root) {
   tab.n_req0.assign((size_t)std::max(N, 1) * R, 0);
   tab.n_rs0.assign((size_t)std::max(N, 1) * dims.RSW, 0);
   tab.n_taint.assign((size_t)std::max(N, 1) * 2, 0);
+  tab.n_flags.assign(std::max(N, 1), 0);
   for (int i = 0; i < N; i++) {
     Node& n = nodes[i];
+    tab.n_flags[i] = (!n.initialized || !n.ready) ? NF_UNUSABLE : 0;
     std::vector<uint32_t> lab = emptyRec();
     addLabels(lab, n.labels);
     QList dreq;
@@ -757,6 +794,8 @@ void Host::build(const Value& root) {
   tab.pod_state0.assign(std::max(P, 1), 0);
   tab.pod_nstate.assign(std::max(P, 1), 0);
   tab.pod_uid.assign(std::max(P, 1), 0);
+  tab.pod_flags.assign(std::max(P, 1), 0);
+  for (int i = 0; i < P; i++) tab.pod_flags[i] = pods[i].provisionable ? PF_PROVISIONABLE : 0;
   std::map<std::string, int> uids;
   for (auto& p : pods) uids[p.uid] = 0;
   int u = 0;
@@ -881,6 +920,8 @@ void Host::build(const Value& root) {
   dims.zoneKey = zoneKey;
   dims.ctKey = ctKey;
   dims.hostKey = hostKey;
+  dims.spotBit = valueId[ctKey].at("spot");
+  dims.odBit = valueId[ctKey].at("on-demand");
   dims.allowWK = allowWK;
   dims.itKeys = itKeys;
   dims.hostnameSeed = (int32_t)hostnameSeed;

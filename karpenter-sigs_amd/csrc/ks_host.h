@@ -41,8 +41,14 @@ struct PodH {
   std::vector<TolH> tols;
   QList requests;  // RequestsForPods(pod) incl. pods=1
   bool hostPorts = false, volumes = false;
-  bool provisionable = true;
+  bool provisionable = true;  // IsProvisionable (pkg/utils/pod/scheduling.go:28-34)
+  // fields the disruption path reads (node.go:32-53 GetNodePods, helpers.go:137-159, scheduling.go:85-92)
+  bool ownedByNode = false, ownedByDaemonSet = false, terminal = false, deleting = false;
+  std::map<std::string, std::string> annotations;
+  bool hasPriority = false;
+  int32_t priority = 0;
 };
+PodH parse_pod(const ksjson::Value& v);
 
 struct PodState {  // one point of the relaxation chain
   std::vector<uint32_t> rsAll, rsStrict;
@@ -70,7 +76,9 @@ struct Host {
   // taints
   std::vector<TaintH> taints;
   // instance types
-  struct IT { std::string name; std::vector<NSR> reqs; QList capacity, alloc; std::vector<std::pair<std::string, std::string>> offers; };
+  struct Offer { std::string zone, ct; double price = 0; bool available = true; };
+  struct IT { std::string name; std::vector<NSR> reqs; QList capacity, alloc; std::vector<std::pair<std::string, std::string>> offers;
+              std::vector<double> prices; std::vector<Offer> all; };
   std::vector<IT> its;
   // templates
   struct Tpl {
@@ -89,7 +97,7 @@ struct Host {
   bool toleratePreferNoSchedule = false;
   // existing nodes (sorted)
   struct Node { std::string name, hostName; std::map<std::string, std::string> labels; std::vector<TaintH> taints;
-                QList available, capacity, dsRequests, req0; bool initialized = true; int origIndex = 0; };
+                QList available, capacity, dsRequests, req0; bool initialized = true, ready = true; int origIndex = 0; };
   std::vector<Node> nodes;
   std::vector<PodH> daemons;
   std::vector<PodH> pods;
@@ -100,6 +108,8 @@ struct Host {
   // host images of the device tables
   struct Tables {
     std::vector<int64_t> tsort_alloc, it_alloc, it_cap, tpl_daemon, pool_rem0, pod_req, pod_sortkey, n_avail, n_req0;
+    std::vector<double> off_price;
+    std::vector<int32_t> n_flags, pod_flags;
     std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask, st_toltpl;
     std::vector<uint64_t> tpl_taint, st_tol, n_taint;
     std::vector<int32_t> tsort_pos, it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,

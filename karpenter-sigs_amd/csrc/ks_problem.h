@@ -56,6 +56,7 @@ struct KsDims {
   int32_t dupUids;     // 1 if two pods share a UID (queue staleness then re-reads last_len)
   int32_t totalTplIts; // sum of template instance-type list lengths
   int32_t negReq;      // 1 if any pod or daemon request is negative (disables the threshold filter)
+  int32_t spotBit, odBit;  // capacity-type value bits of "spot" / "on-demand" (always interned)
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
@@ -109,7 +110,33 @@ struct KsDev {
   const int64_t KS_G* n_req0;      // [N][R] remaining daemon requests (existingnode.go:43-52)
   const uint32_t KS_G* n_rs0;      // [N][RSW] node labels + hostname
   const uint64_t KS_G* n_taint;    // [N][2]
+  const int32_t KS_G* n_flags;     // [N] NF_UNUSABLE: not initialized or not Ready (helpers.go:118-124)
+  const int32_t KS_G* pod_flags;   // [P] PF_PROVISIONABLE (pkg/utils/pod/scheduling.go IsProvisionable)
+  const double KS_G* off_price;    // available offerings' prices (worstLaunchPrice, helpers.go:235-258)
 };
+
+enum NodeFlag : int32_t { NF_UNUSABLE = 1 };
+enum PodFlag : int32_t { PF_PROVISIONABLE = 1 };
+enum ConsFlag : int32_t { CF_PRICE_ERR = 1, CF_ALL_SPOT = 2, CF_MULTI = 4 };
+enum ConsAction : int32_t { CA_NOOP = 0, CA_DELETE = 1, CA_REPLACE = 2, CA_ERROR = 3 };
+
+// Consolidation simulation record (one per simulateScheduling + computeConsolidation, written by the
+// SIM epilogue of k_solve), int32 words; gathered across GPUs as fixed-size records.
+enum RecField {
+  RF_FLAGS = 0,     // RB_* bits
+  RF_NCLAIMS,       // len(results.NewNodeClaims)
+  RF_HOSTINCR,      // NewNodeClaim calls (global nodeID counter increments, nodeclaim.go:44-48)
+  RF_TPL,           // NewNodeClaims[0] template
+  RF_HOST,          // NewNodeClaims[0] hostname ordinal (relative to the simulation's first)
+  RF_ACTION,        // ConsAction of computeConsolidation (consolidation.go:113-194)
+  RF_NOPT,          // len(NewNodeClaims[0].InstanceTypeOptions)
+  RF_NPRICE,        // options left by filterByPrice
+  RF_NSAME,         // options left by filterOutSameType (multi-node only)
+  RF_ERROR,         // KernelError of the simulation's Solve
+  RF_HDR = 16,      // then: [TW] options, [TW] after filterByPrice, [TW] after filterOutSameType, [RSW] requirements
+};
+enum RecBit { RB_ALL_SCHEDULED = 1, RB_NARROWED = 2, RB_HAS_SPOT = 4, RB_HAS_OD = 8 };
+KS_HD int rec_words(int TW, int RSW) { return RF_HDR + 3 * TW + RSW; }
 
 // Per-solve workspace (one slice per replica / simulation).
 struct KsWork {
@@ -136,6 +163,18 @@ struct KsWork {
   int32_t KS_G* fail_host;  // [P][NTPL]
   int64_t KS_G* pool_rem;   // [NPOOL][R]
   int64_t KS_G* counters;   // [16]
+  // consolidation simulations only (k_solve<.., SIM=true>): this simulation's view of the shared
+  // cluster problem (helpers.go:73-127 — candidates removed, their pods added to the pending ones)
+  const int32_t KS_G* pod_map;  // [P] local -> global pod, in NewQueue order (k_sim_keys + sort)
+  int32_t P;                    // pods in this simulation
+  int32_t nrm;                  // removed (candidate) nodes
+  const int32_t KS_G* rm;       // [nrm] their indices in calculateExistingNodeClaims order
+  const int64_t KS_G* pool0;    // [NPOOL][R] remaining limits with the candidates' capacity not subtracted
+  const double KS_G* st_price;  // [T] filterOutSameType price per instance type, NaN: not a candidate type
+  int32_t KS_G* rec;            // [rec_words] output record
+  int32_t KS_G* n_slot;         // [N] compact state slot of a touched node (valid where s_tch is set)
+  double price;                 // getCandidatePrices (consolidation.go:197-207), summed in candidate order
+  int32_t cflags;               // ConsFlag
 };
 
 enum Counter {

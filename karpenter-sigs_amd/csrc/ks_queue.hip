@@ -68,4 +68,39 @@ hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp,
   return hipGetLastError();
 }
 
+// Per-simulation NewQueue (queue.go:37-43) for a batch of consolidation simulations.  Each
+// simulation's pods are a subset of the cluster problem's pods, and byCPUAndMemoryDescending is a
+// strict total order on them, so a simulation's queue is the global queue order restricted to its
+// subset: one radix sort of (simulation, global rank) keys orders every simulation at once and the
+// stable sort keeps each simulation's entries at its own CSR offsets.
+__global__ void k_sim_keys(const int32_t* rank, const int32_t* entries, const int32_t* entry_sim, int rbits,
+                           uint64_t* keys, int32_t* vals, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int p = entries[i];
+  keys[i] = ((uint64_t)entry_sim[i] << rbits) | (uint64_t)rank[p];
+  vals[i] = p;
+}
+
+__global__ void k_rank(const int32_t* order, int32_t* rank, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) rank[order[i]] = i;
+}
+
+hipError_t rank_from_order(const int32_t* order, int32_t* rank, int n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rank, dim3((n + 255) / 256), dim3(256), 0, st, order, rank, n);
+  return hipGetLastError();
+}
+
+// keys: 2*n u64, vals: 2*n i32, temp: queue_sort_temp_bytes(n).  Sorted global pod indices -> out.
+hipError_t sim_queue_sort(const int32_t* rank, const int32_t* entries, const int32_t* entry_sim, int n, int rbits,
+                          int sbits, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
+                          hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sim_keys, dim3((n + 255) / 256), dim3(256), 0, st, rank, entries, entry_sim, rbits, keys, vals, n);
+  size_t tb = tempBytes;
+  return hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys + n, vals, out, n, 0, rbits + sbits, st);
+}
+
 }  // namespace ks

@@ -1,0 +1,86 @@
+// ks_runtime.h — internals shared by the C-ABI translation units (ks_capi.cpp: Solve,
+// ks_cons.cpp: consolidation): the resident problem, device arena helper and kernel launchers.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/karpenter_amd.h"
+#include "ks_host.h"
+
+namespace ks {
+hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
+                        uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
+                        hipEvent_t mid);
+hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st);
+Plan make_plan(const KsDims& d, size_t budget, bool sim = false);
+size_t queue_sort_temp_bytes(int n);
+hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
+                      hipStream_t st);
+hipError_t rank_from_order(const int32_t* order, int32_t* rank, int n, hipStream_t st);
+hipError_t sim_queue_sort(const int32_t* rank, const int32_t* entries, const int32_t* entry_sim, int n, int rbits,
+                          int sbits, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
+                          hipStream_t st);
+
+// One hipMalloc carved into 256-byte aligned arrays.
+struct Arena {
+  size_t total = 0;
+  size_t add(size_t bytes) {
+    size_t off = total;
+    total += (bytes + 255) & ~(size_t)255;
+    return off;
+  }
+};
+
+void set_last_error(const std::string& m);
+}  // namespace ks
+
+#define HIPCHK(x)                                                                                         \
+  do {                                                                                                    \
+    hipError_t e_ = (x);                                                                                  \
+    if (e_ != hipSuccess) throw ks::KsError(KS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// The encoded problem resident in HBM (ks_problem_create = NewScheduler).
+struct ks_problem {
+  ks::Host host;
+  ks::KsDev dev{};
+  void* dbuf = nullptr;
+  void* wbuf = nullptr;
+  size_t wbytes = 0;
+  ks::KsWork* works_dev = nullptr;
+  int wreps = 0;
+  hipStream_t stream = nullptr;
+  int device = -1;
+  int lastKO = 0;  // claim capacity of the last launch plan
+  // NewQueue radix-sort workspace
+  uint64_t* skeys = nullptr;
+  int32_t* svals = nullptr;
+  void* stemp = nullptr;
+  size_t stempBytes = 0;
+  ~ks_problem() {
+    if (skeys) (void)hipFree(skeys);
+    if (svals) (void)hipFree(svals);
+    if (stemp) (void)hipFree(stemp);
+    if (dbuf) (void)hipFree(dbuf);
+    if (wbuf) (void)hipFree(wbuf);
+    if (works_dev) (void)hipFree(works_dev);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+// Upload the host tables to one HBM allocation and point pb->dev at them.
+void ks_upload(ks_problem* pb);
+
+#define API_TRY try {
+#define API_CATCH                                  \
+  }                                                \
+  catch (const ks::KsError& e) {                   \
+    ks::set_last_error(e.what());                  \
+    return e.code;                                 \
+  }                                                \
+  catch (const std::exception& e) {                \
+    ks::set_last_error(e.what());                  \
+    return KS_ERR_PARSE;                           \
+  }

@@ -111,7 +111,7 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 // One queue entry per lane (the 64-pod window), read wave-uniformly with readlane.
 template <int RT>
 struct Window {
-  int p, uid, s, flags, toltpl;
+  int p, g, uid, s, flags, toltpl;
   uint64_t ll, tol0, tol1;
   int64_t req[RT > 0 ? RT : kMaxR];
 };
@@ -120,7 +120,10 @@ struct Window {
 // TL: the instance-type tables (Allocatable per template position, sorted Allocatable lists) are
 // LDS-resident.  Compile-time, so the hot loops carry no HBM branch (a join of an LDS and an HBM
 // path would wait on vmcnt, i.e. on every outstanding store).
-template <int RT, bool TL>
+// SIM: a consolidation simulation (helpers.go:73-127) over the shared cluster problem: pods are
+// the simulation's local subset (W.pod_map), the candidates' nodes are masked out, and existing
+// node state is copy-on-write (a node's HBM slot is initialised the first time a pod lands on it).
+template <int RT, bool TL, bool SIM>
 struct Solver {
   static constexpr int RM = RT > 0 ? RT : kMaxR;
   const KsDev& D;
@@ -142,6 +145,8 @@ struct Solver {
   LU32 s_rs;            // [RSW] candidate requirements
   LU32 s_rem;           // [TW+2] candidate options
   LU32 s_cand;          // [TW+2] limit-filtered template options
+  LU32 s_rmv;           // SIM: [ceil(N/32)] nodes removed by the simulation (the candidates)
+  LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose mutable state lives in W.n_req / W.n_rs
   int64_t algbytes = 0;
 
   __device__ Solver(const KsDev& D_, const KsWork& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
@@ -229,12 +234,16 @@ struct Solver {
 
   // --- existing nodes (ExistingNode.Add, existingnode.go:64-124) -------------------------------
   // Lane (n & 63) is the only lane that ever reads or writes node n's mutable state.
+  __device__ __forceinline__ bool tbit(LU32 m, int n) const { return (m[n >> 5] >> (n & 31)) & 1u; }
   __device__ __forceinline__ bool node_ok(int n, int s, int sflags, const int64_t* pod, uint64_t tol0,
                                           uint64_t tol1) const {
+    if (SIM && tbit(s_rmv, n)) return false;
+    const bool own = !SIM || tbit(s_tch, n);
     const uint64_t KS_G* nt = D.n_taint + 2 * n;
     if (((nt[0] & ~tol0) | (nt[1] & ~tol1)) != 0) return false;
     const int64_t KS_G* av = D.n_avail + (int64_t)n * R();
-    const int64_t KS_G* rq = W.n_req + (int64_t)n * R();
+    const int slot = SIM && own ? W.n_slot[n] : n;
+    const int64_t KS_G* rq = own ? W.n_req + (int64_t)slot * R() : D.n_req0 + (int64_t)n * R();
     bool ok = true;
 #pragma unroll
     for (int r = 0; r < RM; r++) {
@@ -243,8 +252,28 @@ struct Solver {
       ok &= (a >= 0) & (rq[r] + pod[r] <= a);
     }
     if (ok && (sflags & SF_HAS_KEYS))  // strict Compatible: no AllowUndefinedWellKnownLabels
-      ok = rs_compatible(L, W.n_rs + (int64_t)n * d.RSW, D.st_rs + (int64_t)s * d.RSW, 0);
+      ok = rs_compatible(L, own ? W.n_rs + (int64_t)slot * d.RSW : D.n_rs0 + (int64_t)n * d.RSW,
+                         D.st_rs + (int64_t)s * d.RSW, 0);
     return ok;
+  }
+  // commit of a pod to node j, by j's owner lane.  SIM: copy-on-write — the first pod to land on a
+  // node moves its state into the next compact slot (`fresh`, wave-uniform), so a simulation's
+  // node workspace is proportional to its pods, not to the cluster.
+  __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod, int fresh) {
+    int slot = j;
+    if constexpr (SIM) {
+      if (!tbit(s_tch, j)) {
+        slot = fresh;
+        W.n_slot[j] = slot;
+        for (int r = 0; r < R(); r++) W.n_req[(int64_t)slot * R() + r] = D.n_req0[(int64_t)j * R() + r];
+        for (int i = 0; i < d.RSW; i++) W.n_rs[(int64_t)slot * d.RSW + i] = D.n_rs0[(int64_t)j * d.RSW + i];
+        s_tch[j >> 5] |= 1u << (j & 31);
+      } else {
+        slot = W.n_slot[j];
+      }
+    }
+    for (int r = 0; r < R(); r++) W.n_req[(int64_t)slot * R() + r] += pod[r];
+    if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)slot * d.RSW, D.st_rs + (int64_t)s * d.RSW);
   }
 
   // --- NodeClaim quick reject at sorted position j: necessary conditions of NodeClaim.Add ------
@@ -570,6 +599,128 @@ struct Solver {
     algbytes += (int64_t)n * (8 + 16 * R());
   }
 
+  // --- consolidation decision for this simulation (SIM epilogue) -------------------------------
+  // worstLaunchPrice (helpers.go:235-258): the max price over the available offerings of the
+  // preferred capacity type (spot first) whose zone the requirements allow.
+  template <class PR>
+  __device__ __forceinline__ double worst_price(int it, PR rs, bool spot, bool od) const {
+    const int b = D.it_off_beg[it], e = D.it_off_beg[it + 1];
+    for (int pass = 0; pass < 2; pass++) {
+      if (!(pass == 0 ? spot : od)) continue;
+      const int want = pass == 0 ? d.spotBit : d.odBit;
+      bool any = false;
+      double w = 0;
+      for (int o = b; o < e; o++)
+        if (D.off_ct[o] == want && rs_member(L, rs, d.zoneKey, D.off_zone[o])) {
+          const double pr = D.off_price[o];
+          if (!any || pr > w) w = pr;
+          any = true;
+        }
+      if (any) return w;
+    }
+    return __DBL_MAX__;
+  }
+  // filterByPrice (helpers.go:160-169) over the options bitset `in` of template t -> `out`
+  template <class PI, class PO, class PR>
+  __device__ __forceinline__ int price_filter(PI in, PO out, int t, PR rs, bool spot, bool od, double price) const {
+    const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
+    int cnt = 0;
+    for (int base = 0; base < nIT; base += kWave) {
+      const int pos = base + lane();
+      bool keep = pos < nIT && ((in[pos >> 5] >> (pos & 31)) & 1u);
+      if (keep) keep = worst_price(D.tpl_its[tb + pos], rs, spot, od) < price;
+      const uint64_t m = wballot(keep);
+      if (lane() == 0) {
+        out[base >> 5] = (uint32_t)m;
+        if ((base >> 5) + 1 < d.TW) out[(base >> 5) + 1] = (uint32_t)(m >> 32);
+      }
+      cnt += __popcll(m);
+    }
+    return cnt;
+  }
+  // simulateScheduling's post-check (helpers.go:115-124) + computeConsolidation (consolidation.go:
+  // 113-194) + filterOutSameType (multinodeconsolidation.go:155-188), into the record W.rec
+  __device__ void sim_record(int P, int nclaims, int hostCtr, bool allSched, int err) {
+    hbm_release();  // pod statuses written by lane 0
+    bool bad = false;
+    for (int i = lane(); i < P; i += kWave)
+      bad |= ld_sc1(W.pod_status + i) == ST_FAILED && !(D.pod_flags[W.pod_map[i]] & PF_PROVISIONABLE);
+    allSched = allSched && wballot(bad) == 0;
+    int32_t KS_G* rec = W.rec;
+    const int TW = d.TW;
+    int32_t KS_G* o_opt = rec + RF_HDR;
+    int32_t KS_G* o_price = o_opt + TW;
+    int32_t KS_G* o_same = o_price + TW;
+    int32_t KS_G* o_rs = o_same + TW;
+    for (int i = lane(); i < 3 * TW; i += kWave) o_opt[i] = 0;
+    int flags = allSched ? RB_ALL_SCHEDULED : 0, tpl = -1, host = -1, nopt = 0, nprice = 0, nsame = 0;
+    int action = CA_NOOP;
+    if (nclaims > 0 && err == KE_OK) {
+      const int c = uni(s_order[0]);
+      const bool inl = c < pl.KL;
+      tpl = inl ? uni(lc.tpl[c]) : uni(W.c_tpl[c]);
+      host = W.c_host[c];
+      const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
+      wsync();
+      for (int i = lane(); i < TW; i += kWave) o_opt[i] = inl ? lc.rem[(int64_t)c * TW + i] : gc.rem[(int64_t)c * TW + i];
+      for (int i = lane(); i < d.RSW; i += kWave) o_rs[i] = crs[i];
+      {
+        int cc = 0;
+        for (int i = lane(); i < TW; i += kWave) cc += __popc(inl ? lc.rem[(int64_t)c * TW + i] : gc.rem[(int64_t)c * TW + i]);
+        for (int off = 32; off >= 1; off >>= 1) cc += __shfl_xor(cc, off);
+        nopt = uni(cc);
+      }
+      const bool spot = rs_member(L, crs, d.ctKey, d.spotBit), od = rs_member(L, crs, d.ctKey, d.odBit);
+      flags |= (spot ? RB_HAS_SPOT : 0) | (od ? RB_HAS_OD : 0);
+      if (allSched && nclaims == 1) {
+        if (W.cflags & CF_PRICE_ERR) {
+          action = CA_ERROR;
+        } else {
+          // filterByPrice into LDS scratch (s_cand), then filterOutSameType into s_rem
+          nprice = inl ? price_filter(lc.rem + (int64_t)c * TW, s_cand, tpl, crs, spot, od, W.price)
+                       : price_filter(gc.rem + (int64_t)c * TW, s_cand, tpl, crs, spot, od, W.price);
+          wsync();
+          for (int i = lane(); i < TW; i += kWave) o_price[i] = s_cand[i];
+          if (nprice > 0 && !((W.cflags & CF_ALL_SPOT) && spot)) {
+            action = CA_REPLACE;
+            const bool narrowed = spot && od;  // [spot, on-demand] -> spot (consolidation.go:183-188)
+            if (narrowed) flags |= RB_NARROWED;
+            if (W.cflags & CF_MULTI) {
+              const int tb = s_tbeg[tpl], nIT = s_tbeg[tpl + 1] - tb;
+              double mx = __DBL_MAX__;
+              for (int pos = lane(); pos < nIT; pos += kWave)
+                if ((s_cand[pos >> 5] >> (pos & 31)) & 1u) {
+                  const double v = W.st_price[D.tpl_its[tb + pos]];
+                  if (v == v && v < mx) mx = v;
+                }
+              for (int off = 32; off >= 1; off >>= 1) {
+                const double x = __shfl_xor(mx, off);
+                mx = x < mx ? x : mx;
+              }
+              nsame = price_filter(s_cand, s_rem, tpl, crs, spot, od && !narrowed, mx);
+              wsync();
+              for (int i = lane(); i < TW; i += kWave) o_same[i] = s_rem[i];
+            }
+          }
+        }
+      }
+    } else if (allSched && nclaims == 0 && err == KE_OK) {
+      action = CA_DELETE;
+    }
+    if (lane() == 0) {
+      rec[RF_FLAGS] = flags;
+      rec[RF_NCLAIMS] = nclaims;
+      rec[RF_HOSTINCR] = hostCtr;
+      rec[RF_TPL] = tpl;
+      rec[RF_HOST] = host;
+      rec[RF_ACTION] = action;
+      rec[RF_NOPT] = nopt;
+      rec[RF_NPRICE] = nprice;
+      rec[RF_NSAME] = nsame;
+      rec[RF_ERROR] = err;
+    }
+  }
+
   // --- 64-pod queue window: one gather per 64 pops, one entry per lane ------------------------
   __device__ __forceinline__ void refill(Window<RT>& w, int qhead, int qlen, int P, bool pushed) {
     if (pushed) hbm_release();  // queue pushes / relaxation states / staleness words have landed
@@ -578,7 +729,8 @@ struct Solver {
       int pos = qhead + lane();
       if (pos >= P) pos -= P;
       w.p = ld_sc1(W.queue + pos);
-      w.uid = D.pod_uid[w.p];
+      w.g = SIM ? W.pod_map[w.p] : w.p;
+      w.uid = SIM ? w.p : D.pod_uid[w.p];  // simulations reject duplicate UIDs: local index == UID
       w.s = ld_sc1(W.pod_state + w.p);
       w.ll = ld_sc1(W.last_len + w.uid);
       w.flags = D.st_flags[w.s];
@@ -588,20 +740,20 @@ struct Solver {
 #pragma unroll
       for (int r = 0; r < RM; r++) {
         if (RT == 0 && r >= d.R) break;
-        w.req[r] = D.pod_req[(int64_t)w.p * R() + r];
+        w.req[r] = D.pod_req[(int64_t)w.g * R() + r];
       }
     }
   }
 };
 
-template <int RT, bool TL>
+template <int RT, bool TL, bool SIM>
 __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan pl) {
-  constexpr int RM = Solver<RT, TL>::RM;
+  constexpr int RM = Solver<RT, TL, SIM>::RM;
   extern __shared__ __attribute__((aligned(16))) char smem_generic[];
   char KS_L* smem = (char KS_L*)smem_generic;
   const KsWork W = works[blockIdx.x];
   const KsDims& d = D.d;
-  Solver<RT, TL> S(D, W, pl);
+  Solver<RT, TL, SIM> S(D, W, pl);
   const int R = S.R();
   char KS_L* sp = smem;
   auto take = [&](size_t bytes) { char KS_L* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
@@ -624,6 +776,9 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   S.s_rs = (LU32)take(4 * (size_t)d.RSW);
   S.s_rem = (LU32)take(4 * (size_t)d.TW + 8);
   S.s_cand = (LU32)take(4 * (size_t)d.TW + 8);
+  const int NWN = (d.N + 31) >> 5;
+  S.s_rmv = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
+  S.s_tch = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.gc.tpl = W.c_tpl;
   S.gc.req = W.c_req;
   S.gc.max = W.c_max;
@@ -633,7 +788,30 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   for (int i = lane(); i < d.NK * (int)(sizeof(KeyMeta) / 4); i += kWave)
     ((uint32_t KS_L*)s_keys)[i] = ((const uint32_t KS_G*)D.keys)[i];
   for (int i = lane(); i <= d.NTPL; i += kWave) S.s_tbeg[i] = D.tpl_it_beg[i];
-  for (int i = lane(); i < d.NPOOL * R; i += kWave) S.s_pool[i] = D.pool_rem0[i];
+  for (int i = lane(); i < d.NPOOL * R; i += kWave) S.s_pool[i] = SIM ? W.pool0[i] : D.pool_rem0[i];
+  const int P = SIM ? W.P : d.P;
+  if constexpr (SIM) {
+    // the simulation's fresh Scheduler state (what k_init does for plain Solves): NewQueue order is
+    // the local order (pod_map is sorted), nothing placed, no staleness marks
+    for (int i = lane(); i < NWN; i += kWave) {
+      S.s_rmv[i] = 0;
+      S.s_tch[i] = 0;
+    }
+    for (int i = lane(); i < P; i += kWave) {
+      W.queue[i] = i;
+      W.pod_state[i] = D.pod_state0[W.pod_map[i]];
+      W.pod_status[i] = ST_PENDING;
+      W.pod_fstate[i] = -1;
+      W.last_len[i] = 0;
+    }
+    wsync();
+    if (lane() == 0)
+      for (int i = 0; i < W.nrm; i++) {
+        const int n = W.rm[i];
+        S.s_rmv[n >> 5] |= 1u << (n & 31);
+      }
+    hbm_release();
+  }
   if (TL)
     for (int i = lane(); i < d.totalTplIts * R; i += kWave)
       S.s_talloc[i] = D.it_alloc[(int64_t)D.tpl_its[i / R] * R + i % R];
@@ -653,8 +831,9 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   S.L.vInt = D.vInt;
   wsync();
 
-  const int P = d.P;
-  int nclaims = 0, nlog = 0, hostCtr = d.hostnameSeed;
+  int nclaims = 0, nlog = 0, hostCtr = SIM ? 0 : d.hostnameSeed;
+  bool allSched = true;  // SIM: AllNonPendingPodsScheduled so far (pods placed on unusable nodes)
+  int ntouched = 0;      // SIM: compact node-state slots in use
   bool srt = true;      // s.newNodeClaims non-decreasing in len(Pods)
   bool pushed = false;  // a failed pod was pushed back since the last window refill
   uint32_t epoch = 1;
@@ -686,6 +865,7 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     }
     // Queue.Pop (queue.go:46-61)
     const int p = rdl(w.p, wi);
+    const int g = SIM ? rdl(w.g, wi) : p;
     const int uid = rdl(w.uid, wi);
     uint64_t ll = (uint64_t)rdl64((int64_t)w.ll, wi);
     if (d.dupUids) {
@@ -717,10 +897,15 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
       S.algbytes += (int64_t)min(kWave, d.N - base) * (16 * R + 16);
       if (m) {
         const int j = base + ctz64(m);
-        if (lane() == (j & (kWave - 1))) {  // the owner lane of node j
-          for (int r = 0; r < R; r++) W.n_req[(int64_t)j * R + r] += pod[r];
-          if (sflags & SF_HAS_KEYS) rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+        if constexpr (SIM) {
+          const bool fresh = !S.tbit(S.s_tch, j);
+          wsync();
+          if (lane() == (j & (kWave - 1))) S.node_commit(j, s, sflags, pod, ntouched);  // j's owner lane
+          ntouched += fresh ? 1 : 0;
+        } else {
+          if (lane() == (j & (kWave - 1))) S.node_commit(j, s, sflags, pod, 0);
         }
+        if (SIM && (D.n_flags[j] & NF_UNUSABLE) && !(D.pod_flags[g] & PF_PROVISIONABLE)) allSched = false;
         S.log_commit(p, -(j + 1), nlog);
         placed = true;
       }
@@ -782,9 +967,12 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
         placed = true;
       }
     }
-    if (placed) continue;
+    if (placed) {
+      if (SIM && lane() == 0) W.pod_status[p] = ST_SCHEDULED;
+      continue;
+    }
     // failure: Preferences.Relax (preferences.go:38) + Queue.Push (queue.go:64-71)
-    const int s0 = D.pod_state0[p], ns = D.pod_nstate[p];
+    const int s0 = D.pod_state0[g], ns = D.pod_nstate[g];
     const bool relaxed = s - s0 + 1 < ns;
     if (lane() == 0) {
       W.pod_status[p] = ST_FAILED;
@@ -822,18 +1010,20 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     W.counters[CT_CYC_TOTAL] = (int64_t)(__builtin_amdgcn_s_memtime() - tstart);
 #endif
   }
+  if constexpr (SIM) S.sim_record(P, nclaims, hostCtr, allSched, err);
 }
 
 // LDS plan.  Position-indexed state (order, pod count, template, headroom) bounds the NodeClaims
 // per Solve (KO); claims [0, KL) also keep their template/requests/max/options/thresholds in LDS,
 // the rest in HBM.  The instance-type tables go to LDS first when they leave room for 64 claims.
 // One-Solve launches use the whole 160 KiB of a CU; batched simulations pass a smaller budget.
-Plan make_plan(const KsDims& d, size_t budget) {
+Plan make_plan(const KsDims& d, size_t budget, bool sim) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   Plan pl{};
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
-                       r16(4 * (size_t)d.RSW) + 2 * r16(4 * TW + 8) + 16 * 16;
+                       r16(4 * (size_t)d.RSW) + 2 * r16(4 * TW + 8) + 16 * 16 +
+                       (sim ? 2 * r16(4 * (size_t)((d.N + 31) / 32)) : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)
   const size_t clmB = 16 + 16 * R + 4 * TW + 4 * R;      // tpl, cnt, req, max, rem, thr (+ rounding)
   const size_t slack = 10 * 16;                          // per-array 16-byte rounding
@@ -872,7 +1062,23 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep, (const int32_t*)qorder);
   if (mid) (void)hipEventRecord(mid, st);
-#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_>), dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl)
+#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, false>), dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl)
+  const bool tl = pl.talloc != 0;
+  switch (D.d.R) {
+    case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;
+    case 4: if (tl) KS_LAUNCH(4, true); else KS_LAUNCH(4, false); break;
+    default: if (tl) KS_LAUNCH(0, true); else KS_LAUNCH(0, false); break;
+  }
+#undef KS_LAUNCH
+  return hipGetLastError();
+}
+
+// A batch of consolidation simulations (one wavefront each); their pod_map lists must already be
+// in NewQueue order (sim_queue_sort).
+hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st) {
+  if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
+  if (nsims <= 0) return hipSuccess;
+#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, true>), dim3(nsims), dim3(kWave), pl.lds, st, D, works_dev, pl)
   const bool tl = pl.talloc != 0;
   switch (D.d.R) {
     case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;

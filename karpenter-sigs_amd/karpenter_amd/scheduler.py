@@ -145,3 +145,82 @@ class Scheduler:
             self.close()
         except Exception:
             pass
+
+
+def _cons_lib():
+    l = lib()
+    if not getattr(l, "_cons_ready", False):
+        vp = ctypes.c_void_p
+        l.ks_cons_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
+        l.ks_cons_free.argtypes = [vp]
+        for f in ("ks_cons_num_candidates", "ks_cons_num_sims", "ks_cons_record_bytes"):
+            getattr(l, f).argtypes = [vp]
+        l.ks_cons_records_per_rank.argtypes = [vp, ctypes.c_int]
+        l.ks_cons_run.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_Opts), vp, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_double)]
+        l.ks_cons_decide.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        l._cons_ready = True
+    return l
+
+
+class Consolidator:
+    """One disruption pass of consolidation on the GPU (pkg/controllers/disruption).
+
+    Mirrors MultiNodeConsolidation / SingleNodeConsolidation.ComputeCommand over a cluster snapshot
+    (INTEGRATION.md §5): every candidate-deletion simulation (simulateScheduling, helpers.go:73-127)
+    runs on the GPU with its computeConsolidation decision; `decide` replays the reference's
+    sequential choice.  Sharding: rank r of `world` runs simulations s with s % world == r."""
+
+    def __init__(self, snapshot):
+        l = _cons_lib()
+        b = _encode(snapshot)
+        h = ctypes.c_void_p()
+        _check(l.ks_cons_create(b, len(b), ctypes.byref(h)))
+        self._h = h
+        self.num_candidates = l.ks_cons_num_candidates(h)
+        self.num_sims = l.ks_cons_num_sims(h)
+        self.record_bytes = l.ks_cons_record_bytes(h)
+
+    def records_per_rank(self, world=1):
+        return _cons_lib().ks_cons_records_per_rank(self._h, world)
+
+    def run(self, rank=0, world=1, device=-1, out_ptr=None):
+        """Run this rank's simulations.  out_ptr: device pointer for records_per_rank*record_bytes
+        bytes (e.g. a torch tensor's data_ptr()); None returns the records as host bytes.
+        Returns (records bytes or None, kernel ms)."""
+        l = _cons_lib()
+        o = _Opts(device, 1, 1, 0, 0)
+        ms = ctypes.c_double()
+        if out_ptr is None:
+            buf = ctypes.create_string_buffer(self.records_per_rank(world) * self.record_bytes)
+            _check(l.ks_cons_run(self._h, rank, world, ctypes.byref(o), ctypes.cast(buf, ctypes.c_void_p), 0,
+                                 ctypes.byref(ms)))
+            return buf.raw, ms.value
+        _check(l.ks_cons_run(self._h, rank, world, ctypes.byref(o), ctypes.c_void_p(out_ptr), 1, ctypes.byref(ms)))
+        return None, ms.value
+
+    def decide(self, records, world=1, all_sims=False):
+        """Sequential selection over the gathered records ([rank][slot] layout, bytes)."""
+        l = _cons_lib()
+        buf = ctypes.create_string_buffer(bytes(records), len(records))
+        js = ctypes.c_void_p()
+        _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, 1 if all_sims else 0,
+                                ctypes.byref(js)))
+        return json.loads(_take_str(js))
+
+    def consolidate(self, all_sims=False, device=-1):
+        recs, ms = self.run(0, 1, device)
+        doc = self.decide(recs, 1, all_sims)
+        doc["kernel_ms"] = ms
+        return doc
+
+    def close(self):
+        if self._h:
+            _cons_lib().ks_cons_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,117 @@
+"""GPU parity for consolidation: the batched simulations + on-GPU computeConsolidation decisions,
+replayed by the host selection, must equal the oracle's restatement of pkg/controllers/disruption
+(oracle/consolidation.inc) exactly: candidate order and disruption costs, every simulation outcome
+(allNonPendingScheduled, #NewNodeClaims, NewNodeClaims[0] options and requirements) and the chosen
+multi-node and single-node commands (action, candidates, replacement options and requirements)."""
+import json
+import os
+import sys
+
+import pytest
+
+from karpenter_amd import Consolidator, synth
+from oracle import bridge
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import make_consolidation_fixtures as mcf  # noqa: E402
+
+FIXTURES = json.load(open(os.path.join(HERE, "golden", "consolidation_scenarios.json")))
+SCENARIOS = {s["name"]: s for s in mcf.scenarios()}
+
+
+def _both(snap, all_sims):
+    s = json.dumps(snap)
+    want, _ = bridge.consolidate(s, all_sims=all_sims)
+    got = Consolidator(s).consolidate(all_sims=all_sims)
+    got.pop("kernel_ms")
+    return want, got
+
+
+def _explain(a, b, path=""):
+    """Pinpoint the first difference between two JSON values."""
+    if type(a) != type(b):
+        return "%s: %r vs %r" % (path, a, b)
+    if isinstance(a, dict):
+        for k in sorted(set(a) | set(b)):
+            if a.get(k) != b.get(k):
+                return _explain(a.get(k), b.get(k), path + "." + k)
+    elif isinstance(a, list):
+        if len(a) != len(b):
+            sa, sb = set(map(json.dumps, a)), set(map(json.dumps, b))
+            return "%s: len %d vs %d; only want %s; only got %s" % (path, len(a), len(b), sorted(sa - sb)[:5],
+                                                                   sorted(sb - sa)[:5])
+        for i, (x, y) in enumerate(zip(a, b)):
+            if x != y:
+                return _explain(x, y, "%s[%d]" % (path, i))
+    return "%s: %r vs %r" % (path, a, b)
+
+
+def _first_diff(want, got):
+    if want == got:
+        return None
+    return _explain(want, got)
+
+
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
+def test_reference_consolidation_scenarios_gpu(fx):
+    """consolidation_test.go known answers (tests/golden), GPU path vs oracle and vs the expectation."""
+    scn = SCENARIOS[fx["name"]]
+    for all_sims in (False, True):
+        want, got = _both(scn["snapshot"], all_sims)
+        d = _first_diff(want, got)
+        assert d is None, d
+    m = got["multi"]["command"]
+    cmd = m if m["action"] != "no-op" else got["single"]["command"]
+    assert cmd["action"] == fx["expect"]["action"]
+    assert sorted(cmd["candidates"]) == sorted(fx["expect"]["candidates"])
+
+
+CASES = [
+    dict(n_nodes=12, pods_per_node=6, n_its=40, it_range=(8, 24), seed=1),
+    dict(n_nodes=24, pods_per_node=10, n_its=60, it_range=(6, 30), seed=2, spot_frac=0.6),
+    dict(n_nodes=30, pods_per_node=12, n_its=80, it_range=(10, 40), seed=3, n_pending=5),
+    dict(n_nodes=20, pods_per_node=8, n_its=50, it_range=(5, 20), seed=4, uninitialized_frac=0.2, not_ready_frac=0.2),
+    dict(n_nodes=25, pods_per_node=10, n_its=60, it_range=(8, 30), seed=5, pod_selectors=True),
+    dict(n_nodes=16, pods_per_node=15, n_its=40, it_range=(2, 10), seed=6, expire_after="48h"),
+    dict(n_nodes=40, pods_per_node=5, n_its=100, it_range=(20, 60), seed=7, spot_frac=1.0),
+    dict(n_nodes=18, pods_per_node=9, n_its=40, it_range=(4, 16), seed=8, limits={"cpu": "300"}),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=["c%d" % c["seed"] for c in CASES])
+def test_random_cluster_parity(case):
+    snap = synth.cluster_snapshot(**case)
+    for all_sims in (True, False):
+        want, got = _both(snap, all_sims)
+        d = _first_diff(want, got)
+        assert d is None, d
+
+
+def test_sharded_runs_gather_to_the_same_decision():
+    """Ranks r of world W run simulations s % W == r; the [rank][slot] gather decides identically."""
+    snap = json.dumps(synth.cluster_snapshot(30, 8, n_its=60, it_range=(6, 30), seed=11, spot_frac=0.5))
+    c = Consolidator(snap)
+    one = c.decide(c.run(0, 1)[0], 1, all_sims=True)
+    for world in (2, 3, 8):
+        recs = b"".join(c.run(r, world)[0] for r in range(world))
+        assert c.decide(recs, world, all_sims=True) == one
+
+
+def test_c5_shape_at_scale_properties():
+    """1000-node slice of the C5 cluster: every single-node simulation is evaluated; a delete must
+    leave every rescheduled pod placed (size-independent properties; the oracle checks the small
+    cases exactly)."""
+    snap = synth.cluster_snapshot(1000, 20, 400, seed=4205)
+    c = Consolidator(json.dumps(snap))
+    assert c.num_candidates == 1000 and c.num_sims == 1000 + 100
+    doc = c.consolidate(all_sims=True)
+    assert len(doc["single"]["sims"]) == 1000
+    for s in doc["single"]["sims"]:
+        assert s["allNonPendingScheduled"] or s["newNodeClaims"] >= 0
+    costs = [x["disruptionCost"] for x in doc["candidates"]]
+    assert costs == sorted(costs)
+    # determinism
+    assert c.consolidate(all_sims=True)["single"] == doc["single"]
