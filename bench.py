@@ -25,6 +25,90 @@ sys.path.insert(0, os.path.join(ROOT, "karpenter-sigs_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+def consolidation_bench(args, rank, world, local, dist, barrier_sync):
+    """C5 (BASELINE.json configs[4]): one consolidation pass = every candidate-deletion simulation of
+    a 5k-node / 100k-pod cluster (5000 single-node + 100 multi-node prefix sims), sharded over the
+    ranks by simulation index (s % world == rank), records all-gathered over RCCL, then the
+    reference's sequential selection on rank 0.  value = simulations completed per second."""
+    import torch
+
+    from karpenter_amd import Consolidator, synth
+
+    snap = json.dumps(synth.config5(args.cons_nodes))
+    c = Consolidator(snap)
+    per, rb = c.records_per_rank(world), c.record_bytes
+    dev = "cuda:%d" % local
+    out = gathered = None
+    if world > 1:
+        out = torch.empty(per * rb, dtype=torch.uint8, device=dev)
+        gathered = torch.empty(world * per * rb, dtype=torch.uint8, device=dev)
+
+    def one_pass():
+        if world == 1:
+            recs, ms = c.run(0, 1, device=local)
+        else:
+            _, ms = c.run(rank, world, device=local, out_ptr=out.data_ptr())
+            dist.all_gather_into_tensor(gathered, out)
+            recs = gathered.cpu().numpy().tobytes() if rank == 0 else None
+        doc = c.decide(recs, world) if rank == 0 else None
+        return ms, recs, doc
+
+    for _ in range(args.warmup):
+        one_pass()
+    barrier_sync()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.cons_steps):
+        ms, recs, doc = one_pass()
+        kms.append(ms)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed, max(kms)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kmax = float(t[0]), float(t[1])
+    else:
+        kmax = max(kms)
+    if rank != 0:
+        return None
+    k_ms = sum(kms) / len(kms)
+    algb = c.alg_bytes(recs, world)
+    achieved = algb / (k_ms / 1000.0) / 1e9 / world  # per GPU: each rank scans its own shard
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        from oracle import bridge
+
+        n, secs = bridge.time_cons_sims(snap, args.cpu_sims, args.cpu_threads)
+        cpu = {"value": round(n / secs, 2), "unit": "cands/s", "cores": args.cpu_threads, "kind": "port",
+               "sample": "first %d single-node simulations of C5 (simulateScheduling + computeConsolidation, "
+                         "oracle/cpu_ref.cpp, %d host threads, %.1f s)" % (n, args.cpu_threads, secs)}
+    return {
+        "metric": "consolidation cands/sec (C5: %d nodes x 20 pods, 400 instance types)" % args.cons_nodes,
+        "value": round(c.num_sims * args.cons_steps / elapsed, 1),
+        "unit": "cands/s",
+        "n_gpus": world,
+        "steps": args.cons_steps,
+        "ms_per_pass": round(elapsed * 1000.0 / args.cons_steps, 3),
+        "scaling": "strong",
+        "simulations_per_pass": c.num_sims,
+        "candidates": c.num_candidates,
+        "decision": {"multi": [doc["multi"]["command"]["action"], len(doc["multi"]["command"]["candidates"])],
+                     "single": [doc["single"]["command"]["action"], doc["single"]["command"]["candidates"]]},
+        "roofline": {"bound": "hbm", "kernel": "k_solve<SIM>", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("cons_c5"),
+                     "algorithmic_bytes_per_pass": algb, "kernel_ms": round(k_ms, 3), "kernel_ms_max_rank": round(kmax, 3)},
+        "cpu_baseline": cpu,
+    }
+
+
+def _traffic(tag):
+    tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % tag)
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -34,6 +118,12 @@ def main():
     ap.add_argument("--its", type=int, default=400)
     ap.add_argument("--cpu-pods", type=int, default=50000, help="oracle sample size (same workload shape)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--only-consolidation", action="store_true", help="profiling: skip the Solve section")
+    ap.add_argument("--cons-nodes", type=int, default=5000, help="C5 cluster size (20 pods per node)")
+    ap.add_argument("--cons-steps", type=int, default=20)
+    ap.add_argument("--cpu-sims", type=int, default=2400, help="oracle consolidation sample (simulations)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -49,6 +139,21 @@ def main():
 
     from karpenter_amd import Scheduler, synth
 
+    def barrier_sync():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    if args.only_consolidation:
+        cons = consolidation_bench(args, rank, world, local, dist, barrier_sync)
+        if rank == 0:
+            print(json.dumps({"consolidation": cons}))
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
     snap = synth.config2(args.pods) if args.its == 400 else synth.benchmark_snapshot(args.pods, args.its, 42, False)
     snap_json = json.dumps(snap)
     sch = Scheduler(snap_json)
@@ -58,13 +163,6 @@ def main():
     placed = sum(len(c["pods"]) for c in check.new_nodeclaims)
     assert placed + len(check.pod_errors) == args.pods, "solve lost pods"
     nclaims = len(check.new_nodeclaims)
-
-    def barrier_sync():
-        if dist is not None:
-            import torch
-
-            dist.barrier()
-            torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         sch.solve(device=local, timing_only=True)
@@ -84,19 +182,12 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    if rank != 0:
-        dist.destroy_process_group()
-        return
     ms_per_step = elapsed * 1000.0 / args.steps
     value = args.pods * world * args.steps / elapsed
     k_ms = sum(solve_ms) / len(solve_ms)
     bytes_per_launch = sum(algb) / len(algb)
     achieved = bytes_per_launch / (k_ms / 1000.0) / 1e9
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_c2.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    traffic = _traffic("c2")
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         from oracle import bridge
@@ -106,6 +197,10 @@ def main():
         cpu = {"value": round(args.cpu_pods / secs, 1), "unit": "pods/s", "cores": 1, "kind": "port",
                "sample": "1 Solve of C2 with %d pods x %d instance types (oracle/cpu_ref.cpp, single thread, "
                          "%.1f s)" % (args.cpu_pods, args.its, secs)}
+    cons = None if args.no_consolidation else consolidation_bench(args, rank, world, local, dist, barrier_sync)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
     out = {
         "metric": "pods/sec in Scheduler.Solve @50k pods x 400 types",
         "value": round(value, 1),
@@ -128,6 +223,7 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch, "kernel_ms": round(k_ms, 3),
                      "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3)},
         "cpu_baseline": cpu,
+        "consolidation": cons,
     }
     print(json.dumps(out))
     if dist is not None:

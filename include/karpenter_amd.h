@@ -92,6 +92,8 @@ double ks_results_algorithmic_bytes(const ks_results* r);
  * 42-88); each ends in the computeConsolidation decision (consolidation.go:113-194) on the GPU. */
 typedef struct ks_cons ks_cons;
 int ks_cons_create(const char* snapshot_json, size_t len, ks_cons** out);
+/* Host-only (no device): JSON {candidates:[{name, disruptionCost, pods}], sims, multiPrefixes, recordBytes}. */
+int ks_cons_inspect(const char* snapshot_json, size_t len, char** out_json);
 void ks_cons_free(ks_cons* c);
 int ks_cons_num_candidates(const ks_cons* c);
 int ks_cons_num_sims(const ks_cons* c);
@@ -107,6 +109,8 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
  * JSON {"candidates":[{name, disruptionCost}], "multi":{"command", "sims"}, "single":{"command", "sims"}}.
  * all_sims: report every simulation (otherwise only those the reference would have run). */
 int ks_cons_decide(const ks_cons* c, const void* records, int world, int all_sims, char** json_out);
+/* Algorithmic bytes the gathered simulations scanned, summed from their records. */
+double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world);
 
 void ks_free(void* p);
 const char* ks_last_error(void);

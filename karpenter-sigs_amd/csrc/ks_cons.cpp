@@ -392,7 +392,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     o.c_rs = a.add(4 * K * d.RSW);
     o.c_rem = a.add(4 * K * d.TW);
     o.order = a.add(4 * K);
-    o.n_req = a.add(8 * P * R);
+    o.n_req = a.add(8 * (size_t)N * R);  // indexed by node; written only where a pod lands
     o.n_rs = a.add(4 * P * d.RSW);
     o.n_slot = a.add(4 * (size_t)N);
     o.queue = a.add(4 * P);
@@ -722,6 +722,30 @@ int ks_cons_create(const char* json, size_t len, ks_cons** out) {
   API_CATCH
 }
 
+// Host-only: candidates (NewCandidate + disruption-cost order) and the simulation plan, no device.
+int ks_cons_inspect(const char* json, size_t len, char** out) {
+  API_TRY
+  if (!json || !out) throw KsError(KS_ERR_ARG, "null argument");
+  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  ks_cons c;
+  build_cons(c, root);
+  std::string o = "{\"candidates\":[";
+  for (size_t i = 0; i < c.cands.size(); i++) {
+    if (i) o += ",";
+    o += "{\"name\":";
+    ksjson::quote(o, c.cands[i].name);
+    char buf[96];
+    snprintf(buf, sizeof buf, ",\"disruptionCost\":%.17g,\"pods\":%zu}", c.cands[i].cost, c.cands[i].pods.size());
+    o += buf;
+  }
+  o += "],\"sims\":" + std::to_string(c.sims.size()) + ",\"multiPrefixes\":" + std::to_string(c.multiHi) +
+       ",\"recordBytes\":" + std::to_string(4 * c.recWords) + ",\"pods\":" + std::to_string(c.pb->host.dims.P) +
+       ",\"nodes\":" + std::to_string(c.pb->host.dims.N) + "}";
+  *out = strdup(o.c_str());
+  return KS_OK;
+  API_CATCH
+}
+
 void ks_cons_free(ks_cons* c) { delete c; }
 
 int ks_cons_num_candidates(const ks_cons* c) { return c ? (int)c->cands.size() : 0; }
@@ -770,6 +794,17 @@ int ks_cons_decide(const ks_cons* c, const void* records, int world, int all_sim
   *json_out = strdup(decide_json(*c, (const int32_t*)records, world, all_sims != 0).c_str());
   return KS_OK;
   API_CATCH
+}
+
+double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world) {
+  if (!c || !records || world < 1) return 0;
+  const int32_t* r = (const int32_t*)records;
+  double sum = 0;
+  for (size_t i = 0; i < (size_t)c->per_rank(world) * world; i++) {
+    const int32_t* x = r + i * c->recWords;
+    sum += (double)(((uint64_t)(uint32_t)x[RF_ALGB_HI] << 32) | (uint32_t)x[RF_ALGB_LO]);
+  }
+  return sum;
 }
 
 }  // extern "C"

@@ -133,6 +133,8 @@ enum RecField {
   RF_NPRICE,        // options left by filterByPrice
   RF_NSAME,         // options left by filterOutSameType (multi-node only)
   RF_ERROR,         // KernelError of the simulation's Solve
+  RF_ALGB_LO,       // algorithmic bytes the simulation scanned, low / high word
+  RF_ALGB_HI,
   RF_HDR = 16,      // then: [TW] options, [TW] after filterByPrice, [TW] after filterOutSameType, [RSW] requirements
 };
 enum RecBit { RB_ALL_SCHEDULED = 1, RB_NARROWED = 2, RB_HAS_SPOT = 4, RB_HAS_OD = 8 };
@@ -172,7 +174,7 @@ struct KsWork {
   const int64_t KS_G* pool0;    // [NPOOL][R] remaining limits with the candidates' capacity not subtracted
   const double KS_G* st_price;  // [T] filterOutSameType price per instance type, NaN: not a candidate type
   int32_t KS_G* rec;            // [rec_words] output record
-  int32_t KS_G* n_slot;         // [N] compact state slot of a touched node (valid where s_tch is set)
+  int32_t KS_G* n_slot;         // [N] W.n_rs slot of a node whose requirements changed (valid where s_tchr is set)
   double price;                 // getCandidatePrices (consolidation.go:197-207), summed in candidate order
   int32_t cflags;               // ConsFlag
 };

@@ -111,7 +111,7 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 // One queue entry per lane (the 64-pod window), read wave-uniformly with readlane.
 template <int RT>
 struct Window {
-  int p, g, uid, s, flags, toltpl;
+  int p, g, uid, s, flags, toltpl, pf;
   uint64_t ll, tol0, tol1;
   int64_t req[RT > 0 ? RT : kMaxR];
 };
@@ -146,7 +146,8 @@ struct Solver {
   LU32 s_rem;           // [TW+2] candidate options
   LU32 s_cand;          // [TW+2] limit-filtered template options
   LU32 s_rmv;           // SIM: [ceil(N/32)] nodes removed by the simulation (the candidates)
-  LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose mutable state lives in W.n_req / W.n_rs
+  LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose requests live in a W.n_req slot
+  LU32 s_tchr;          // SIM: [ceil(N/32)] nodes whose requirements live in a W.n_rs slot
   int64_t algbytes = 0;
 
   __device__ Solver(const KsDev& D_, const KsWork& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
@@ -235,45 +236,92 @@ struct Solver {
   // --- existing nodes (ExistingNode.Add, existingnode.go:64-124) -------------------------------
   // Lane (n & 63) is the only lane that ever reads or writes node n's mutable state.
   __device__ __forceinline__ bool tbit(LU32 m, int n) const { return (m[n >> 5] >> (n & 31)) & 1u; }
-  __device__ __forceinline__ bool node_ok(int n, int s, int sflags, const int64_t* pod, uint64_t tol0,
-                                          uint64_t tol1) const {
-    if (SIM && tbit(s_rmv, n)) return false;
-    const bool own = !SIM || tbit(s_tch, n);
-    const uint64_t KS_G* nt = D.n_taint + 2 * n;
-    if (((nt[0] & ~tol0) | (nt[1] & ~tol1)) != 0) return false;
-    const int64_t KS_G* av = D.n_avail + (int64_t)n * R();
-    const int slot = SIM && own ? W.n_slot[n] : n;
-    const int64_t KS_G* rq = own ? W.n_req + (int64_t)slot * R() : D.n_req0 + (int64_t)n * R();
-    bool ok = true;
+  // Existing-node check for two nodes per lane (positions n and n + 64 of the first-fit order):
+  // every load of both is issued before any test, so a 128-node step of the scan costs one memory
+  // round trip.  Out-of-range positions are clamped for the loads and masked.  nf: NodeFlag bits.
+  __device__ __forceinline__ void node_ok2(int n0, int s, int sflags, const int64_t* pod, uint64_t tol0,
+                                           uint64_t tol1, bool& ok0, bool& ok1, int& nf0, int& nf1) const {
+    const int n1 = n0 + kWave;
+    const int c0 = n0 < d.N ? n0 : d.N - 1, c1 = n1 < d.N ? n1 : d.N - 1;
+    const bool own0 = !SIM || tbit(s_tch, c0), own1 = !SIM || tbit(s_tch, c1);
+    const uint64_t KS_G* t0p = D.n_taint + 2 * c0;
+    const uint64_t KS_G* t1p = D.n_taint + 2 * c1;
+    const int64_t KS_G* a0p = D.n_avail + (int64_t)c0 * R();
+    const int64_t KS_G* a1p = D.n_avail + (int64_t)c1 * R();
+    const int64_t KS_G* q0p = (own0 ? W.n_req : D.n_req0) + (int64_t)c0 * R();
+    const int64_t KS_G* q1p = (own1 ? W.n_req : D.n_req0) + (int64_t)c1 * R();
+    const uint64_t x0 = t0p[0], y0 = t0p[1], x1 = t1p[0], y1 = t1p[1];
+    int64_t a0[RM], a1[RM], q0[RM], q1[RM];
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
-      const int64_t a = av[r];
-      ok &= (a >= 0) & (rq[r] + pod[r] <= a);
+      a0[r] = a0p[r];
+      a1[r] = a1p[r];
+      q0[r] = q0p[r];
+      q1[r] = q1p[r];
     }
-    if (ok && (sflags & SF_HAS_KEYS))  // strict Compatible: no AllowUndefinedWellKnownLabels
-      ok = rs_compatible(L, own ? W.n_rs + (int64_t)slot * d.RSW : D.n_rs0 + (int64_t)n * d.RSW,
-                         D.st_rs + (int64_t)s * d.RSW, 0);
-    return ok;
+    nf0 = SIM ? D.n_flags[c0] : 0;
+    nf1 = SIM ? D.n_flags[c1] : 0;
+    ok0 = (n0 < d.N) & (((x0 & ~tol0) | (y0 & ~tol1)) == 0);  // Taints.Tolerates
+    ok1 = (n1 < d.N) & (((x1 & ~tol0) | (y1 & ~tol1)) == 0);
+    if (SIM) {  // the simulation removed these candidates
+      ok0 &= !tbit(s_rmv, c0);
+      ok1 &= !tbit(s_rmv, c1);
+    }
+#pragma unroll
+    for (int r = 0; r < RM; r++) {  // Fits(requests + pod, Available())
+      if (RT == 0 && r >= d.R) break;
+      ok0 &= (a0[r] >= 0) & (q0[r] + pod[r] <= a0[r]);
+      ok1 &= (a1[r] >= 0) & (q1[r] + pod[r] <= a1[r]);
+    }
+    if (sflags & SF_HAS_KEYS) {  // strict Compatible: no AllowUndefinedWellKnownLabels
+      if (ok0) ok0 = rs_compatible(L, node_rs(c0), D.st_rs + (int64_t)s * d.RSW, 0);
+      if (ok1) ok1 = rs_compatible(L, node_rs(c1), D.st_rs + (int64_t)s * d.RSW, 0);
+    }
   }
-  // commit of a pod to node j, by j's owner lane.  SIM: copy-on-write — the first pod to land on a
-  // node moves its state into the next compact slot (`fresh`, wave-uniform), so a simulation's
-  // node workspace is proportional to its pods, not to the cluster.
-  __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod, int fresh) {
-    int slot = j;
-    if constexpr (SIM) {
-      if (!tbit(s_tch, j)) {
-        slot = fresh;
-        W.n_slot[j] = slot;
-        for (int r = 0; r < R(); r++) W.n_req[(int64_t)slot * R() + r] = D.n_req0[(int64_t)j * R() + r];
-        for (int i = 0; i < d.RSW; i++) W.n_rs[(int64_t)slot * d.RSW + i] = D.n_rs0[(int64_t)j * d.RSW + i];
-        s_tch[j >> 5] |= 1u << (j & 31);
-      } else {
-        slot = W.n_slot[j];
-      }
+  __device__ __forceinline__ const uint32_t KS_G* node_rs(int n) const {
+    if (!SIM) return W.n_rs + (int64_t)n * d.RSW;
+    return tbit(s_tchr, n) ? W.n_rs + (int64_t)W.n_slot[n] * d.RSW : D.n_rs0 + (int64_t)n * d.RSW;
+  }
+  // Solve: commit of a pod to node j by its owner lane.
+  __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod) {
+    for (int r = 0; r < R(); r++) W.n_req[(int64_t)j * R() + r] += pod[r];
+    if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+  }
+  // SIM: copy-on-write commit (wave-uniform).  W.n_req is indexed by node but only the nodes a pod
+  // landed on are ever written (s_tch marks them), so a fresh simulation needs no initialisation.
+  // Requirements are copied only when a pod with label requirements lands, into the next compact
+  // slot of W.n_rs (wave-cooperatively, through LDS).
+  __device__ __forceinline__ void sim_node_commit(int j, int s, int sflags, const int64_t* pod, int& nrs) {
+    const int owner = j & (kWave - 1);
+    const bool fresh = !tbit(s_tch, j);
+    wsync();
+    if (lane() == owner) {
+      int64_t KS_G* q = W.n_req + (int64_t)j * R();
+      for (int r = 0; r < R(); r++) q[r] = (fresh ? D.n_req0[(int64_t)j * R() + r] : q[r]) + pod[r];
+      if (fresh) s_tch[j >> 5] |= 1u << (j & 31);
     }
-    for (int r = 0; r < R(); r++) W.n_req[(int64_t)slot * R() + r] += pod[r];
-    if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)slot * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+    if (sflags & SF_HAS_KEYS) {
+      const bool rsfresh = !tbit(s_tchr, j);
+      int slot;
+      if (rsfresh) {
+        slot = nrs++;
+        copy_words(s_rs, D.n_rs0 + (int64_t)j * d.RSW, d.RSW);
+      } else {
+        int v = 0;
+        if (lane() == owner) v = W.n_slot[j];
+        slot = rdl(v, owner);
+        copy_words(s_rs, W.n_rs + (int64_t)slot * d.RSW, d.RSW);
+      }
+      wsync();
+      if (lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
+      wsync();
+      copy_words(W.n_rs + (int64_t)slot * d.RSW, s_rs, d.RSW);
+      if (lane() == owner && rsfresh) W.n_slot[j] = slot;
+      if (lane() == 0) s_tchr[j >> 5] |= 1u << (j & 31);
+      hbm_release();
+    }
+    wsync();
   }
 
   // --- NodeClaim quick reject at sorted position j: necessary conditions of NodeClaim.Add ------
@@ -718,6 +766,8 @@ struct Solver {
       rec[RF_NPRICE] = nprice;
       rec[RF_NSAME] = nsame;
       rec[RF_ERROR] = err;
+      rec[RF_ALGB_LO] = (int32_t)(uint32_t)(uint64_t)algbytes;
+      rec[RF_ALGB_HI] = (int32_t)(uint32_t)((uint64_t)algbytes >> 32);
     }
   }
 
@@ -734,6 +784,7 @@ struct Solver {
       w.s = ld_sc1(W.pod_state + w.p);
       w.ll = ld_sc1(W.last_len + w.uid);
       w.flags = D.st_flags[w.s];
+      w.pf = SIM ? D.pod_flags[w.g] : 0;
       w.toltpl = D.st_toltpl[w.s];
       w.tol0 = D.st_tol[2 * w.s];
       w.tol1 = D.st_tol[2 * w.s + 1];
@@ -779,6 +830,7 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   const int NWN = (d.N + 31) >> 5;
   S.s_rmv = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tch = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
+  S.s_tchr = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.gc.tpl = W.c_tpl;
   S.gc.req = W.c_req;
   S.gc.max = W.c_max;
@@ -796,6 +848,7 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     for (int i = lane(); i < NWN; i += kWave) {
       S.s_rmv[i] = 0;
       S.s_tch[i] = 0;
+      S.s_tchr[i] = 0;
     }
     for (int i = lane(); i < P; i += kWave) {
       W.queue[i] = i;
@@ -833,7 +886,7 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
 
   int nclaims = 0, nlog = 0, hostCtr = SIM ? 0 : d.hostnameSeed;
   bool allSched = true;  // SIM: AllNonPendingPodsScheduled so far (pods placed on unusable nodes)
-  int ntouched = 0;      // SIM: compact node-state slots in use
+  int nrs = 0;           // SIM: compact node-requirement slots in use
   bool srt = true;      // s.newNodeClaims non-decreasing in len(Pods)
   bool pushed = false;  // a failed pod was pushed back since the last window refill
   uint32_t epoch = 1;
@@ -890,24 +943,25 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     bool placed = false;
     // 1) existing nodes in order
     PH_BEGIN(t1);
-    for (int base = 0; base < d.N && !placed; base += kWave) {
-      const int n = base + lane();
-      const bool ok = n < d.N && S.node_ok(n, s, sflags, pod, tol0, tol1);
-      const uint64_t m = wballot(ok);
-      S.algbytes += (int64_t)min(kWave, d.N - base) * (16 * R + 16);
-      if (m) {
-        const int j = base + ctz64(m);
+    for (int base = 0; base < d.N && !placed; base += 2 * kWave) {
+      bool ok0, ok1;
+      int nf0, nf1;
+      S.node_ok2(base + lane(), s, sflags, pod, tol0, tol1, ok0, ok1, nf0, nf1);
+      const uint64_t m0 = wballot(ok0), m1 = wballot(ok1);
+      if (m0 | m1) {
+        const int j = m0 ? base + ctz64(m0) : base + kWave + ctz64(m1);
+        S.algbytes += (int64_t)(j - base + 1) * (16 * R + 16);
         if constexpr (SIM) {
-          const bool fresh = !S.tbit(S.s_tch, j);
-          wsync();
-          if (lane() == (j & (kWave - 1))) S.node_commit(j, s, sflags, pod, ntouched);  // j's owner lane
-          ntouched += fresh ? 1 : 0;
-        } else {
-          if (lane() == (j & (kWave - 1))) S.node_commit(j, s, sflags, pod, 0);
+          S.sim_node_commit(j, s, sflags, pod, nrs);
+          const int nf = rdl(m0 ? nf0 : nf1, j & (kWave - 1));
+          if ((nf & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
+        } else if (lane() == (j & (kWave - 1))) {
+          S.node_commit(j, s, sflags, pod);  // the owner lane of node j
         }
-        if (SIM && (D.n_flags[j] & NF_UNUSABLE) && !(D.pod_flags[g] & PF_PROVISIONABLE)) allSched = false;
         S.log_commit(p, -(j + 1), nlog);
         placed = true;
+      } else {
+        S.algbytes += (int64_t)min(2 * kWave, d.N - base) * (16 * R + 16);
       }
     }
     PH_END(t1, 1);
@@ -1023,7 +1077,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim) {
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
                        r16(4 * (size_t)d.RSW) + 2 * r16(4 * TW + 8) + 16 * 16 +
-                       (sim ? 2 * r16(4 * (size_t)((d.N + 31) / 32)) : 0);
+                       (sim ? 3 * r16(4 * (size_t)((d.N + 31) / 32)) : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)
   const size_t clmB = 16 + 16 * R + 4 * TW + 4 * R;      // tpl, cnt, req, max, rem, thr (+ rounding)
   const size_t slack = 10 * 16;                          // per-array 16-byte rounding

@@ -153,14 +153,30 @@ def _cons_lib():
         vp = ctypes.c_void_p
         l.ks_cons_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
         l.ks_cons_free.argtypes = [vp]
+        l.ks_cons_inspect.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
         for f in ("ks_cons_num_candidates", "ks_cons_num_sims", "ks_cons_record_bytes"):
             getattr(l, f).argtypes = [vp]
         l.ks_cons_records_per_rank.argtypes = [vp, ctypes.c_int]
         l.ks_cons_run.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_Opts), vp, ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_double)]
         l.ks_cons_decide.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        l.ks_cons_records_alg_bytes.argtypes = [vp, vp, ctypes.c_int]
+        l.ks_cons_records_alg_bytes.restype = ctypes.c_double
         l._cons_ready = True
     return l
+
+
+def inspect_consolidation(snapshot):
+    """Host-only: the ordered candidates and the simulation plan of a cluster snapshot."""
+    b = _encode(snapshot)
+    out = ctypes.c_void_p()
+    _check(_cons_lib().ks_cons_inspect(b, len(b), ctypes.byref(out)))
+    return json.loads(_take_str(out))
+
+
+def shard_slot(sim, world):
+    """Where simulation `sim` lands in the [rank][slot] gather (ks_cons_run / ks_cons_decide)."""
+    return sim % world, sim // world
 
 
 class Consolidator:
@@ -207,6 +223,10 @@ class Consolidator:
         _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, 1 if all_sims else 0,
                                 ctypes.byref(js)))
         return json.loads(_take_str(js))
+
+    def alg_bytes(self, records, world=1):
+        buf = ctypes.create_string_buffer(bytes(records), len(records))
+        return _cons_lib().ks_cons_records_alg_bytes(self._h, ctypes.cast(buf, ctypes.c_void_p), world)
 
     def consolidate(self, all_sims=False, device=-1):
         recs, ms = self.run(0, 1, device)

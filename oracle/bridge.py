@@ -28,6 +28,8 @@ def lib():
         l.oref_consolidate_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_double)]
         l.oref_consolidate_json.restype = ctypes.c_int
+        l.oref_time_cons_sims.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        l.oref_time_cons_sims.restype = ctypes.c_int
         l.oref_last_error.restype = ctypes.c_char_p
         l.oref_free.argtypes = [ctypes.c_void_p]
         _lib = l
@@ -71,6 +73,18 @@ def consolidate(snapshot, all_sims=False):
     if l.oref_consolidate_json(s.encode(), 1 if all_sims else 0, ctypes.byref(out), ctypes.byref(secs)) != 0:
         raise RuntimeError("oracle: " + l.oref_last_error().decode())
     return json.loads(_take(out)), secs.value
+
+
+def time_cons_sims(snapshot, count, threads=1):
+    """Time the oracle's first `count` single-node consolidation simulations over `threads` host
+    threads; returns (n, seconds)."""
+    l = lib()
+    s = snapshot if isinstance(snapshot, str) else json.dumps(snapshot)
+    secs = ctypes.c_double()
+    n = l.oref_time_cons_sims(s.encode(), count, threads, ctypes.byref(secs))
+    if n < 0:
+        raise RuntimeError("oracle: " + l.oref_last_error().decode())
+    return n, secs.value
 
 
 def eval_ops(ops, well_known=None):

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cctype>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <limits>
 #include <memory>
@@ -1442,6 +1443,31 @@ int oref_consolidate_json(const char* snapshot, int all_sims, char** out, double
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (out) *out = dupstr(r);
     return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// CPU baseline sample: the first `count` single-node consolidation simulations (simulateScheduling +
+// computeConsolidation per candidate, as SingleNodeConsolidation runs them), timed after parsing.
+// `threads` > 1 splits the (independent) simulations over that many host threads.
+int oref_time_cons_sims(const char* snapshot, int count, int threads, double* seconds) {
+  try {
+    ojson::Value root = ojson::parse(snapshot);
+    oref::ConsProblem cp = oref::parseConsProblem(root);
+    const int n = std::min<int>(count, (int)cp.candidates.size());
+    const int nt = std::max(1, std::min(threads, n));
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; t++)
+      pool.emplace_back([&cp, n, nt, t] {
+        int64_t counter = cp.base.hostnameSeed;
+        for (int i = t; i < n; i += nt) oref::computeConsolidation(cp, {i}, counter);
+      });
+    for (auto& th : pool) th.join();
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return n;
   } catch (const std::exception& e) {
     g_err = e.what();
     return -1;

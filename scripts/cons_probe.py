@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Probe: C5 consolidation on one GPU (create time, run time per pass, outcome summary)."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "karpenter-sigs_amd"))
+from karpenter_amd import Consolidator, synth  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
+t = time.time()
+snap = json.dumps(synth.config5(n))
+t1 = time.time()
+c = Consolidator(snap)
+t2 = time.time()
+print("snapshot %.2fs (%d MB) create %.2fs sims %d" % (t1 - t, len(snap) >> 20, t2 - t1, c.num_sims), flush=True)
+for i in range(4):
+    t = time.time()
+    recs, ms = c.run()
+    print("run %d: kernel %.3f ms wall %.3f ms" % (i, ms, (time.time() - t) * 1e3), flush=True)
+doc = c.decide(recs, 1, all_sims=True)
+acts = {}
+for s in doc["single"]["sims"]:
+    k = (s["allNonPendingScheduled"], s["newNodeClaims"])
+    acts[k] = acts.get(k, 0) + 1
+print("single outcomes", acts)
+print("multi", doc["multi"]["command"]["action"], len(doc["multi"]["command"]["candidates"]))
+print("single", doc["single"]["command"]["action"], doc["single"]["command"]["candidates"])

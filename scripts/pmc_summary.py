@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Summarise a scripts/profile.sh run: per-launch kernel stats + PMC counters for one kernel.
 
-Usage: scripts/pmc_summary.py <tag> [kernel_substring]   (reads gpurun_out/prof_<tag>_*)
-Writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.txt and profiles/traffic_c2.json.
+Usage: scripts/pmc_summary.py <tag> [kernel_substring] [traffic_name]   (reads gpurun_out/prof_<tag>_*)
+Writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.txt and profiles/traffic_<traffic_name>.json.
 HBM bytes follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB; on gfx950
 FETCH_SIZE reports half the bytes of a coalesced read, so it is doubled.
 """
@@ -19,6 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     tag = sys.argv[1]
     kname = sys.argv[2] if len(sys.argv) > 2 else "k_solve"
+    tname = sys.argv[3] if len(sys.argv) > 3 else "c2"
     out = os.path.join(ROOT, "gpurun_out")
     prof = os.path.join(ROOT, "profiles")
     shutil.copy(os.path.join(out, "prof_%s_trace" % tag, "run_kernel_stats.csv"),
@@ -40,7 +41,7 @@ def main():
         rd = 2 * vals["FETCH_SIZE"] * 1024
         wr = vals["WRITE_SIZE"] * 1024
         lines.append("HBM bytes per launch: read %.0f (FETCH_SIZE x2 KiB) + write %.0f = %.0f" % (rd, wr, rd + wr))
-        with open(os.path.join(prof, "traffic_c2.json"), "w") as f:
+        with open(os.path.join(prof, "traffic_%s.json" % tname), "w") as f:
             json.dump({"tag": tag, "kernel": kname, "hbm_read_bytes_per_launch": rd,
                        "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr}, f, indent=1)
     if "SQ_WAVE_CYCLES" in vals and "SQ_BUSY_CYCLES" in vals:
