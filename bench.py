@@ -49,8 +49,23 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync):
         else:
             _, ms = c.run(rank, world, device=local, out_ptr=out.data_ptr())
             dist.all_gather_into_tensor(gathered, out)
-            recs = gathered.cpu().numpy().tobytes() if rank == 0 else None
-        doc = c.decide(recs, world) if rank == 0 else None
+            recs = gathered.cpu().numpy().tobytes()
+        if world == 1:
+            doc = c.decide(recs, 1, candidates=False)
+        else:
+            # every rank holds the gathered records, so every rank knows which simulations' NodeClaim
+            # requirements the decision needs; each is broadcast by the rank that ran it
+            need = c.needed_sims(recs, world)
+            rsw = c.requirement_words
+            table = {}
+            for s in need:
+                owner = s % world
+                t = torch.zeros(rsw, dtype=torch.int32, device=dev)
+                if rank == owner:
+                    t.copy_(torch.frombuffer(bytearray(c.claim_requirements(s)), dtype=torch.int32))
+                dist.broadcast(t, src=owner)
+                table[s] = t.cpu().numpy().tobytes()
+            doc = c.decide(recs, world, fetch=table.__getitem__, candidates=False) if rank == 0 else None
         return ms, recs, doc
 
     for _ in range(args.warmup):

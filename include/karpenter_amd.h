@@ -107,8 +107,21 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
                 double* kernel_ms);
 /* Replay the reference's sequential choice over the gathered records ([rank][slot] layout):
  * JSON {"candidates":[{name, disruptionCost}], "multi":{"command", "sims"}, "single":{"command", "sims"}}.
- * all_sims: report every simulation (otherwise only those the reference would have run). */
-int ks_cons_decide(const ks_cons* c, const void* records, int world, int all_sims, char** json_out);
+ * flags: KS_CONS_ALL_SIMS reports every simulation (otherwise only those the reference would have
+ * run); KS_CONS_CANDIDATES includes the candidate list (otherwise "candidates" is empty).
+ * Requirement records (NewNodeClaims[0].Requirements) stay on the GPU that ran a simulation:
+ * ks_cons_needed_sims lists (returns the count; writes up to cap) the simulations the output needs,
+ * their owners (rank = sim % world) read them with ks_cons_claim_requirements (requirement_words
+ * uint32 each), and rs_table passes them to ks_cons_decide in that order. */
+#define KS_CONS_ALL_SIMS 1   /* flags: report every simulation */
+#define KS_CONS_CANDIDATES 2 /* flags: include the ordered candidate list */
+int ks_cons_requirement_words(const ks_cons* c);
+int ks_cons_needed_sims(const ks_cons* c, const void* records, int world, int flags, int32_t* out, int cap);
+int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out);
+int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
+                   char** json_out);
+/* Diagnostics: the 24 solve counters of simulation `sim` in the last ks_cons_run of this handle. */
+int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out24);
 /* Algorithmic bytes the gathered simulations scanned, summed from their records. */
 double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world);
 

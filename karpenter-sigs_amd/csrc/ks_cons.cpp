@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstring>
 #include <ctime>
+#include <functional>
 #include <limits>
 #include <map>
 #include <memory>
@@ -149,6 +150,7 @@ struct ks_cons {
   size_t ltempBytes = 0;
   int lnent = 0, lrbits = 0, lsbits = 0;
   Plan lplan{};
+  std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
   int32_t* rank = nullptr;  // global NewQueue rank of every pod
 
   int sim_of_multi(int mid) const { return multiHi - mid; }  // mid in [1, multiHi]
@@ -330,7 +332,7 @@ void build_cons(ks_cons& c, const Value& root) {
     s.cands.push_back(i);
     c.sims.push_back(s);
   }
-  c.recWords = rec_words(h.dims.TW, h.dims.RSW);
+  c.recWords = rec_words(h.dims.TW);
 }
 
 // Offerings.Get(capacityType, zone) (all offerings, available or not): first match
@@ -525,6 +527,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   }
   HIPCHK(hipMemcpy(c.lbuf, stage.data(), a.total, hipMemcpyHostToDevice));
   if (ns) HIPCHK(hipMemcpy(c.lworks, works.data(), sizeof(KsWork) * ns, hipMemcpyHostToDevice));
+  c.lhost = works;
   // LDS plan: a small budget per simulation so several simulations share a CU
   KsDims dd = d;
   dd.Kcap = std::max(1, std::min(maxP, 16384));
@@ -553,7 +556,11 @@ std::vector<int> bits_to_its(const Host& h, int tpl, const int32_t* bits) {
 }
 
 // The reference's sequential selection over the simulation records.
-std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool allSims) {
+// rsOf(sim): NewNodeClaims[0]'s requirement record of simulation `sim` (kept in the workspace of the
+// GPU that ran it; ks_cons_needed_sims lists the simulations whose record the output needs).
+using RsFn = std::function<const uint32_t*(int)>;
+std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool allSims, const RsFn& rsOf,
+                        bool withCandidates = true) {
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
   const int per = c.per_rank(world);
@@ -590,7 +597,7 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
       ksjson::quote(o, h.tpls[(size_t)r[RF_TPL]].pool);
       o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR));
       o += ",\"requirementsString\":";
-      ksjson::quote(o, h.reqsString((const uint32_t*)(r + RF_HDR + 3 * d.TW), before.at(sim) + r[RF_HOST]));
+      ksjson::quote(o, h.reqsString(rsOf(sim), before.at(sim) + r[RF_HOST]));
       o += "}";
     }
     return o + "}";
@@ -604,7 +611,8 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
                     (r[RF_ACTION] == CA_NOOP || r[RF_ACTION] == CA_ERROR ? std::string("[]") : candNames(c.sims[(size_t)sim].cands));
     if (r[RF_ACTION] == CA_REPLACE) {
       const bool multi = c.sims[(size_t)sim].multi;
-      std::vector<uint32_t> rs((const uint32_t*)(r + RF_HDR + 3 * d.TW), (const uint32_t*)(r + RF_HDR + 3 * d.TW) + d.RSW);
+      const uint32_t* r0 = rsOf(sim);
+      std::vector<uint32_t> rs(r0, r0 + d.RSW);
       if (r[RF_FLAGS] & RB_NARROWED) {
         std::vector<uint32_t> spot = h.emptyRec();
         h.addNSR(spot, kCTKey, "In", {"spot"});
@@ -629,14 +637,15 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
   };
 
   std::string o = "{\"candidates\":[";
-  for (int i = 0; i < n; i++) {
-    if (i) o += ",";
-    o += "{\"name\":";
-    ksjson::quote(o, c.cands[(size_t)i].name);
-    char buf[64];
-    snprintf(buf, sizeof buf, ",\"disruptionCost\":%.17g}", c.cands[(size_t)i].cost);
-    o += buf;
-  }
+  if (withCandidates)
+    for (int i = 0; i < n; i++) {
+      if (i) o += ",";
+      o += "{\"name\":";
+      ksjson::quote(o, c.cands[(size_t)i].name);
+      char buf[64];
+      snprintf(buf, sizeof buf, ",\"disruptionCost\":%.17g}", c.cands[(size_t)i].cost);
+      o += buf;
+    }
   // MultiNodeConsolidation.firstNConsolidationOption: binary search over the prefix length
   int multiSim = -1;
   bool multiErr = false;
@@ -788,11 +797,79 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
   API_CATCH
 }
 
-int ks_cons_decide(const ks_cons* c, const void* records, int world, int all_sims, char** json_out) {
+// The simulations whose NewNodeClaims[0] requirement record the decision output needs, in the order
+// ks_cons_decide consumes them (a dry run of the replay that records every lookup).
+static std::vector<int> needed_sims(const ks_cons& c, const int32_t* recs, int world, bool allSims) {
+  std::vector<int> need;
+  std::set<int> seen;
+  std::vector<uint32_t> zero(std::max(c.pb->host.dims.RSW, 1), 0);
+  decide_json(
+      c, recs, world, allSims,
+      [&](int sim) -> const uint32_t* {
+        if (seen.insert(sim).second) need.push_back(sim);
+        return zero.data();
+      },
+      false);
+  return need;
+}
+
+int ks_cons_requirement_words(const ks_cons* c) { return c ? c->pb->host.dims.RSW : 0; }
+
+int ks_cons_needed_sims(const ks_cons* c, const void* records, int world, int flags, int32_t* out, int cap) {
+  API_TRY
+  if (!c || !records || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
+  std::vector<int> need = needed_sims(*c, (const int32_t*)records, world, (flags & KS_CONS_ALL_SIMS) != 0);
+  for (int i = 0; i < (int)need.size() && i < cap; i++) out[i] = need[(size_t)i];
+  return (int)need.size();
+  API_CATCH
+}
+
+// NewNodeClaims[0]'s requirement record of simulation `sim` from this handle's last run (the rank
+// that ran it).
+int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out) {
+  API_TRY
+  if (!c || !out) throw KsError(KS_ERR_ARG, "bad argument");
+  const int RSW = c->pb->host.dims.RSW;
+  for (size_t k = 0; k < c->lsims.size(); k++)
+    if (c->lsims[k] == sim) {
+      int32_t claim = -1;
+      HIPCHK(hipMemcpy(&claim, c->lrec + k * c->recWords + RF_CLAIM, 4, hipMemcpyDeviceToHost));
+      if (claim < 0) throw KsError(KS_ERR_ARG, "simulation has no NodeClaim");
+      HIPCHK(hipMemcpy(out, c->lhost[k].c_rs + (size_t)claim * RSW, 4 * (size_t)RSW, hipMemcpyDeviceToHost));
+      return KS_OK;
+    }
+  throw KsError(KS_ERR_ARG, "simulation not in this rank's launch");
+  API_CATCH
+}
+
+int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
+                   char** json_out) {
   API_TRY
   if (!c || !records || !json_out || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
-  *json_out = strdup(decide_json(*c, (const int32_t*)records, world, all_sims != 0).c_str());
+  const int32_t* recs = (const int32_t*)records;
+  const bool all_sims = (flags & KS_CONS_ALL_SIMS) != 0;
+  std::vector<int> need = needed_sims(*c, recs, world, all_sims);
+  if (!need.empty() && !rs_table) throw KsError(KS_ERR_ARG, "requirement records of the needed simulations missing");
+  std::map<int, const uint32_t*> table;
+  for (size_t i = 0; i < need.size(); i++) table[need[i]] = rs_table + i * c->pb->host.dims.RSW;
+  *json_out = strdup(decide_json(*c, recs, world, all_sims, [&](int sim) { return table.at(sim); },
+                                 (flags & KS_CONS_CANDIDATES) != 0)
+                         .c_str());
   return KS_OK;
+  API_CATCH
+}
+
+// Diagnostics: the solve counters (ks_problem.h Counter) of the last run's simulation `sim` (this
+// rank's launch; with the KS_PHASE_STATS build they include per-phase cycles).
+int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out) {
+  API_TRY
+  if (!c || !out) throw KsError(KS_ERR_ARG, "bad argument");
+  for (size_t k = 0; k < c->lsims.size(); k++)
+    if (c->lsims[k] == sim) {
+      HIPCHK(hipMemcpy(out, c->lhost[k].counters, 8 * CT_NCOUNTERS, hipMemcpyDeviceToHost));
+      return KS_OK;
+    }
+  throw KsError(KS_ERR_ARG, "simulation not in this rank's launch");
   API_CATCH
 }
 

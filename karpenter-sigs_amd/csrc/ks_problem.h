@@ -135,10 +135,11 @@ enum RecField {
   RF_ERROR,         // KernelError of the simulation's Solve
   RF_ALGB_LO,       // algorithmic bytes the simulation scanned, low / high word
   RF_ALGB_HI,
-  RF_HDR = 16,      // then: [TW] options, [TW] after filterByPrice, [TW] after filterOutSameType, [RSW] requirements
+  RF_CLAIM,         // claim id of NewNodeClaims[0] in the simulation's workspace (its requirements stay there)
+  RF_HDR = 16,      // then: [TW] options, [TW] after filterByPrice, [TW] after filterOutSameType
 };
 enum RecBit { RB_ALL_SCHEDULED = 1, RB_NARROWED = 2, RB_HAS_SPOT = 4, RB_HAS_OD = 8 };
-KS_HD int rec_words(int TW, int RSW) { return RF_HDR + 3 * TW + RSW; }
+KS_HD int rec_words(int TW) { return RF_HDR + 3 * TW; }
 
 // Per-solve workspace (one slice per replica / simulation).
 struct KsWork {
@@ -184,6 +185,7 @@ enum Counter {
   CT_CLAIM_FULL, CT_CLAIM_QUICK_FAIL, CT_WINDOWS,
   // diagnostic build (-DKS_PHASE_STATS): s_memtime cycles per phase
   CT_CYC_POP, CT_CYC_NODES, CT_CYC_SORT, CT_CYC_QUICK, CT_CYC_FULL, CT_CYC_COMMIT, CT_CYC_TPL, CT_CYC_TOTAL,
+  CT_CYC_NCOMMIT,  // existing-node commit (inside CT_CYC_NODES)
   CT_NCOUNTERS = 24
 };
 enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3 };

@@ -111,7 +111,7 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 // One queue entry per lane (the 64-pod window), read wave-uniformly with readlane.
 template <int RT>
 struct Window {
-  int p, g, uid, s, flags, toltpl, pf;
+  int p, g, uid, s, flags, toltpl, pf, st;
   uint64_t ll, tol0, tol1;
   int64_t req[RT > 0 ? RT : kMaxR];
 };
@@ -126,10 +126,12 @@ struct Window {
 template <int RT, bool TL, bool SIM>
 struct Solver {
   static constexpr int RM = RT > 0 ? RT : kMaxR;
-  const KsDev& D;
-  const KsDims& d;
-  const KsWork& W;
-  const Plan& pl;
+  // By value: a reference to a byval kernel argument forces a scratch copy of the whole struct
+  // (every field access then becomes a scratch load); values scalarise into SGPRs.
+  const KsDev D;
+  const KsDims d;
+  const KsWork W;
+  const Plan pl;
   DevLayout L;
   ClaimView<true> lc;   // claims [0, KL)
   ClaimView<false> gc;  // claims [KL, KO)
@@ -217,16 +219,16 @@ struct Solver {
     return false;
   }
   template <class PD, class PS>
-  __device__ void copy_words(PD dst, PS src, int n) const {
+  __device__ __forceinline__ void copy_words(PD dst, PS src, int n) const {
     for (int i = lane(); i < n; i += kWave) dst[i] = src[i];
   }
-  __device__ void store_bits(LU32 dst, int base, uint64_t m) const {
+  __device__ __forceinline__ void store_bits(LU32 dst, int base, uint64_t m) const {
     if (lane() == 0) {
       dst[base >> 5] = (uint32_t)m;
       if ((base >> 5) + 1 < d.TW) dst[(base >> 5) + 1] = (uint32_t)(m >> 32);
     }
   }
-  __device__ int popc_words(LU32 w, int n) const {
+  __device__ __forceinline__ int popc_words(LU32 w, int n) const {
     int c = 0;
     for (int i = lane(); i < n; i += kWave) c += __popc(w[i]);
     for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
@@ -240,7 +242,8 @@ struct Solver {
   // every load of both is issued before any test, so a 128-node step of the scan costs one memory
   // round trip.  Out-of-range positions are clamped for the loads and masked.  nf: NodeFlag bits.
   __device__ __forceinline__ void node_ok2(int n0, int s, int sflags, const int64_t* pod, uint64_t tol0,
-                                           uint64_t tol1, bool& ok0, bool& ok1, int& nf0, int& nf1) const {
+                                           uint64_t tol1, bool& ok0, bool& ok1, int& nf0, int& nf1,
+                                           int64_t* q0, int64_t* q1) const {
     const int n1 = n0 + kWave;
     const int c0 = n0 < d.N ? n0 : d.N - 1, c1 = n1 < d.N ? n1 : d.N - 1;
     const bool own0 = !SIM || tbit(s_tch, c0), own1 = !SIM || tbit(s_tch, c1);
@@ -251,7 +254,7 @@ struct Solver {
     const int64_t KS_G* q0p = (own0 ? W.n_req : D.n_req0) + (int64_t)c0 * R();
     const int64_t KS_G* q1p = (own1 ? W.n_req : D.n_req0) + (int64_t)c1 * R();
     const uint64_t x0 = t0p[0], y0 = t0p[1], x1 = t1p[0], y1 = t1p[1];
-    int64_t a0[RM], a1[RM], q0[RM], q1[RM];
+    int64_t a0[RM], a1[RM];
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
@@ -292,13 +295,19 @@ struct Solver {
   // landed on are ever written (s_tch marks them), so a fresh simulation needs no initialisation.
   // Requirements are copied only when a pod with label requirements lands, into the next compact
   // slot of W.n_rs (wave-cooperatively, through LDS).
-  __device__ __forceinline__ void sim_node_commit(int j, int s, int sflags, const int64_t* pod, int& nrs) {
+  // `q`: the owner lane's requests of node j as node_ok2 loaded them (no reload before the store).
+  // regReq: node j sits in the register window (its requests are updated there, not in HBM).
+  __device__ __forceinline__ void sim_node_commit(int j, int s, int sflags, const int64_t* pod, const int64_t* q,
+                                                  int& nrs, bool regReq) {
     const int owner = j & (kWave - 1);
     const bool fresh = !tbit(s_tch, j);
     wsync();
-    if (lane() == owner) {
-      int64_t KS_G* q = W.n_req + (int64_t)j * R();
-      for (int r = 0; r < R(); r++) q[r] = (fresh ? D.n_req0[(int64_t)j * R() + r] : q[r]) + pod[r];
+    if (!regReq && lane() == owner) {
+#pragma unroll
+      for (int r = 0; r < RM; r++) {
+        if (RT == 0 && r >= d.R) break;
+        W.n_req[(int64_t)j * R() + r] = q[r] + pod[r];
+      }
       if (fresh) s_tch[j >> 5] |= 1u << (j & 31);
     }
     if (sflags & SF_HAS_KEYS) {
@@ -688,7 +697,7 @@ struct Solver {
   }
   // simulateScheduling's post-check (helpers.go:115-124) + computeConsolidation (consolidation.go:
   // 113-194) + filterOutSameType (multinodeconsolidation.go:155-188), into the record W.rec
-  __device__ void sim_record(int P, int nclaims, int hostCtr, bool allSched, int err) {
+  __device__ __forceinline__ void sim_record(int P, int nclaims, int hostCtr, bool allSched, int err) {
     hbm_release();  // pod statuses written by lane 0
     bool bad = false;
     for (int i = lane(); i < P; i += kWave)
@@ -699,7 +708,6 @@ struct Solver {
     int32_t KS_G* o_opt = rec + RF_HDR;
     int32_t KS_G* o_price = o_opt + TW;
     int32_t KS_G* o_same = o_price + TW;
-    int32_t KS_G* o_rs = o_same + TW;
     for (int i = lane(); i < 3 * TW; i += kWave) o_opt[i] = 0;
     int flags = allSched ? RB_ALL_SCHEDULED : 0, tpl = -1, host = -1, nopt = 0, nprice = 0, nsame = 0;
     int action = CA_NOOP;
@@ -711,7 +719,7 @@ struct Solver {
       const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
       wsync();
       for (int i = lane(); i < TW; i += kWave) o_opt[i] = inl ? lc.rem[(int64_t)c * TW + i] : gc.rem[(int64_t)c * TW + i];
-      for (int i = lane(); i < d.RSW; i += kWave) o_rs[i] = crs[i];
+      if (lane() == 0) rec[RF_CLAIM] = c;
       {
         int cc = 0;
         for (int i = lane(); i < TW; i += kWave) cc += __popc(inl ? lc.rem[(int64_t)c * TW + i] : gc.rem[(int64_t)c * TW + i]);
@@ -785,6 +793,7 @@ struct Solver {
       w.ll = ld_sc1(W.last_len + w.uid);
       w.flags = D.st_flags[w.s];
       w.pf = SIM ? D.pod_flags[w.g] : 0;
+      w.st = SIM ? ld_sc1(W.pod_status + w.p) : 0;
       w.toltpl = D.st_toltpl[w.s];
       w.tol0 = D.st_tol[2 * w.s];
       w.tol1 = D.st_tol[2 * w.s + 1];
@@ -798,12 +807,12 @@ struct Solver {
 };
 
 template <int RT, bool TL, bool SIM>
-__global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan pl) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_solve(KsDev D, const KsWork* works, Plan pl) {
   constexpr int RM = Solver<RT, TL, SIM>::RM;
   extern __shared__ __attribute__((aligned(16))) char smem_generic[];
   char KS_L* smem = (char KS_L*)smem_generic;
   const KsWork W = works[blockIdx.x];
-  const KsDims& d = D.d;
+  const KsDims d = D.d;
   Solver<RT, TL, SIM> S(D, W, pl);
   const int R = S.R();
   char KS_L* sp = smem;
@@ -884,6 +893,30 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
   S.L.vInt = D.vInt;
   wsync();
 
+  // Register window: the first NW*64 nodes of the first-fit order (where every scan starts) stay in
+  // VGPRs for the whole Solve — lane l holds nodes l, l+64, ...: taints, Available, requests and
+  // flags.  A pod that fits there costs no memory round trip; commits update the owner's registers.
+  constexpr int NW = RT > 0 ? 4 : 0;
+  constexpr int NWA = NW > 0 ? NW : 1;
+  uint64_t wtx[NWA], wty[NWA];
+  int64_t wav[NWA][RM], wrq[NWA][RM];
+  int wnf[NWA];
+  if constexpr (NW > 0) {
+    if (d.N > 0) {
+#pragma unroll
+      for (int k = 0; k < NW; k++) {
+        const int n = k * kWave + lane(), c = n < d.N ? n : d.N - 1;
+        wtx[k] = D.n_taint[2 * c];
+        wty[k] = D.n_taint[2 * c + 1];
+#pragma unroll
+        for (int r = 0; r < RM; r++) {
+          wav[k][r] = D.n_avail[(int64_t)c * RM + r];
+          wrq[k][r] = D.n_req0[(int64_t)c * RM + r];
+        }
+        wnf[k] = SIM ? D.n_flags[c] : 0;
+      }
+    }
+  }
   int nclaims = 0, nlog = 0, hostCtr = SIM ? 0 : d.hostnameSeed;
   bool allSched = true;  // SIM: AllNonPendingPodsScheduled so far (pods placed on unusable nodes)
   int nrs = 0;           // SIM: compact node-requirement slots in use
@@ -943,22 +976,78 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
     bool placed = false;
     // 1) existing nodes in order
     PH_BEGIN(t1);
-    for (int base = 0; base < d.N && !placed; base += 2 * kWave) {
+    int scanFrom = 0;
+    if constexpr (NW > 0) {
+      if (d.N > 0) {
+        int kj = -1;
+        uint64_t mj = 0;
+        asm volatile("; KS_MARK window_begin");
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+          const int n = k * kWave + lane();
+          bool ok = (n < d.N) & (((wtx[k] & ~tol0) | (wty[k] & ~tol1)) == 0);
+          if (SIM) ok &= !S.tbit(S.s_rmv, n < d.N ? n : 0);
+#pragma unroll
+          for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
+          if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), D.st_rs + (int64_t)s * d.RSW, 0);
+          const uint64_t m = wballot(ok);
+          if (m) {
+            kj = k;
+            mj = m;
+            break;
+          }
+        }
+        asm volatile("; KS_MARK window_end");
+        if (kj >= 0) {
+          const int j = kj * kWave + ctz64(mj), owner = j & (kWave - 1);
+          int nfv = 0;
+#pragma unroll
+          for (int k = 0; k < NW; k++)
+            if (k == kj) {
+              nfv = wnf[k];
+              if (lane() == owner)
+#pragma unroll
+                for (int r = 0; r < RM; r++) wrq[k][r] += pod[r];
+            }
+          PH_BEGIN(t7);
+          if constexpr (SIM) {
+            if (sflags & SF_HAS_KEYS) S.sim_node_commit(j, s, sflags, pod, pod, nrs, true);
+            if ((rdl(nfv, owner) & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
+          } else if ((sflags & SF_HAS_KEYS) && lane() == owner) {
+            rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+          }
+          S.log_commit(p, -(j + 1), nlog);
+          PH_END(t7, 7);
+          S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
+          placed = true;
+        } else {
+          S.algbytes += (int64_t)min(NW * kWave, d.N) * (16 * R + 16);
+        }
+        scanFrom = NW * kWave;
+      }
+    }
+    for (int base = scanFrom; base < d.N && !placed; base += 2 * kWave) {
       bool ok0, ok1;
       int nf0, nf1;
-      S.node_ok2(base + lane(), s, sflags, pod, tol0, tol1, ok0, ok1, nf0, nf1);
+      int64_t q0[RM], q1[RM];
+      S.node_ok2(base + lane(), s, sflags, pod, tol0, tol1, ok0, ok1, nf0, nf1, q0, q1);
       const uint64_t m0 = wballot(ok0), m1 = wballot(ok1);
       if (m0 | m1) {
         const int j = m0 ? base + ctz64(m0) : base + kWave + ctz64(m1);
         S.algbytes += (int64_t)(j - base + 1) * (16 * R + 16);
+        PH_BEGIN(t7);
         if constexpr (SIM) {
-          S.sim_node_commit(j, s, sflags, pod, nrs);
+          int64_t qs[RM];
+#pragma unroll
+          for (int r = 0; r < RM; r++) qs[r] = m0 ? q0[r] : q1[r];
+          S.sim_node_commit(j, s, sflags, pod, qs, nrs, false);
           const int nf = rdl(m0 ? nf0 : nf1, j & (kWave - 1));
           if ((nf & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
         } else if (lane() == (j & (kWave - 1))) {
           S.node_commit(j, s, sflags, pod);  // the owner lane of node j
         }
         S.log_commit(p, -(j + 1), nlog);
+        PH_END(t7, 7);
         placed = true;
       } else {
         S.algbytes += (int64_t)min(2 * kWave, d.N - base) * (16 * R + 16);
@@ -1022,7 +1111,8 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
       }
     }
     if (placed) {
-      if (SIM && lane() == 0) W.pod_status[p] = ST_SCHEDULED;
+      // SIM: the epilogue reads the final status; only a pod that failed before needs a store
+      if (SIM && rdl(w.st, wi - 1) == ST_FAILED && lane() == 0) W.pod_status[p] = ST_SCHEDULED;
       continue;
     }
     // failure: Preferences.Relax (preferences.go:38) + Queue.Push (queue.go:64-71)
@@ -1062,6 +1152,7 @@ __global__ __launch_bounds__(64) void k_solve(KsDev D, const KsWork* works, Plan
 #ifdef KS_PHASE_STATS
     for (int i = 0; i < 7; i++) W.counters[CT_CYC_POP + i] = (int64_t)cyc[i];
     W.counters[CT_CYC_TOTAL] = (int64_t)(__builtin_amdgcn_s_memtime() - tstart);
+    W.counters[CT_CYC_NCOMMIT] = (int64_t)cyc[7];
 #endif
   }
   if constexpr (SIM) S.sim_record(P, nclaims, hostCtr, allSched, err);

@@ -159,7 +159,11 @@ def _cons_lib():
         l.ks_cons_records_per_rank.argtypes = [vp, ctypes.c_int]
         l.ks_cons_run.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_Opts), vp, ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_double)]
-        l.ks_cons_decide.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        l.ks_cons_decide.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+        l.ks_cons_requirement_words.argtypes = [vp]
+        l.ks_cons_needed_sims.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
+        l.ks_cons_claim_requirements.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+        l.ks_cons_sim_counters.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
         l.ks_cons_records_alg_bytes.argtypes = [vp, vp, ctypes.c_int]
         l.ks_cons_records_alg_bytes.restype = ctypes.c_double
         l._cons_ready = True
@@ -196,6 +200,7 @@ class Consolidator:
         self.num_candidates = l.ks_cons_num_candidates(h)
         self.num_sims = l.ks_cons_num_sims(h)
         self.record_bytes = l.ks_cons_record_bytes(h)
+        self.requirement_words = l.ks_cons_requirement_words(h)
 
     def records_per_rank(self, world=1):
         return _cons_lib().ks_cons_records_per_rank(self._h, world)
@@ -215,14 +220,48 @@ class Consolidator:
         _check(l.ks_cons_run(self._h, rank, world, ctypes.byref(o), ctypes.c_void_p(out_ptr), 1, ctypes.byref(ms)))
         return None, ms.value
 
-    def decide(self, records, world=1, all_sims=False):
-        """Sequential selection over the gathered records ([rank][slot] layout, bytes)."""
+    def needed_sims(self, records, world=1, all_sims=False):  # noqa: D401
+        """Simulations whose NewNodeClaims[0] requirements the decision output needs (in order)."""
         l = _cons_lib()
         buf = ctypes.create_string_buffer(bytes(records), len(records))
+        cap = 64
+        while True:
+            out = (ctypes.c_int32 * cap)()
+            n = l.ks_cons_needed_sims(self._h, ctypes.cast(buf, ctypes.c_void_p), world, 1 if all_sims else 0, out, cap)
+            if n < 0:
+                _check(n)
+            if n <= cap:
+                return list(out[:n])
+            cap = n
+
+    def claim_requirements(self, sim):
+        """NewNodeClaims[0]'s requirement record of `sim` (this rank must have run it)."""
+        l = _cons_lib()
+        out = (ctypes.c_uint32 * max(l.ks_cons_requirement_words(self._h), 1))()
+        _check(l.ks_cons_claim_requirements(self._h, sim, out))
+        return bytes(out)
+
+    def decide(self, records, world=1, all_sims=False, fetch=None, candidates=True):
+        """Sequential selection over the gathered records ([rank][slot] layout, bytes).  fetch(sim)
+        returns the requirement record bytes of a needed simulation (default: this handle's run);
+        candidates=False leaves out the ordered candidate list (the commands are unchanged)."""
+        l = _cons_lib()
+        need = self.needed_sims(records, world, all_sims)
+        fetch = fetch or self.claim_requirements
+        table = b"".join(fetch(s) for s in need)
+        tbuf = ctypes.create_string_buffer(table, max(len(table), 4))
+        buf = ctypes.create_string_buffer(bytes(records), len(records))
         js = ctypes.c_void_p()
-        _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, 1 if all_sims else 0,
-                                ctypes.byref(js)))
+        flags = (1 if all_sims else 0) | (2 if candidates else 0)
+        _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, flags,
+                                ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(js)))
         return json.loads(_take_str(js))
+
+    def sim_counters(self, sim):
+        """Solve counters of simulation `sim` from the last run (ks_problem.h Counter order)."""
+        out = (ctypes.c_int64 * 24)()
+        _check(_cons_lib().ks_cons_sim_counters(self._h, sim, out))
+        return list(out)
 
     def alg_bytes(self, records, world=1):
         buf = ctypes.create_string_buffer(bytes(records), len(records))

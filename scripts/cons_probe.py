@@ -28,3 +28,16 @@ for s in doc["single"]["sims"]:
 print("single outcomes", acts)
 print("multi", doc["multi"]["command"]["action"], len(doc["multi"]["command"]["candidates"]))
 print("single", doc["single"]["command"]["action"], doc["single"]["command"]["candidates"])
+if os.environ.get("KS_LIB_VARIANT") == "stats":
+    names = ["nclaims", "ncommits", "hostCtr", "error", "pops", "algBytes", "sorts", "sortSlow", "claimFull",
+             "quickFail", "windows", "cycPop", "cycNodes", "cycSort", "cycQuick", "cycFull", "cycCommit", "cycTpl",
+             "cycTotal", "cycNodeCommit"]
+    for sim in (0, 50, 99, 100, 2000):
+        if sim >= c.num_sims:
+            continue
+        ct = c.sim_counters(sim)
+        d = dict(zip(names, ct))
+        pops = max(d["pops"], 1)
+        print("sim %d: pops %d total %.0f cyc/pod | pop %.0f nodes %.0f (commit %.0f) claims %.0f tpl %.0f" % (
+            sim, d["pops"], d["cycTotal"] / pops, d["cycPop"] / pops, d["cycNodes"] / pops, d["cycNodeCommit"] / pops,
+            (d["cycQuick"] + d["cycFull"] + d["cycCommit"] + d["cycSort"]) / pops, d["cycTpl"] / pops))

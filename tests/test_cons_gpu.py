@@ -96,8 +96,10 @@ def test_sharded_runs_gather_to_the_same_decision():
     c = Consolidator(snap)
     one = c.decide(c.run(0, 1)[0], 1, all_sims=True)
     for world in (2, 3, 8):
-        recs = b"".join(c.run(r, world)[0] for r in range(world))
-        assert c.decide(recs, world, all_sims=True) == one
+        ranks = [Consolidator(snap) for _ in range(world)]  # one handle per "GPU"
+        recs = b"".join(ranks[r].run(r, world)[0] for r in range(world))
+        got = c.decide(recs, world, all_sims=True, fetch=lambda s: ranks[s % world].claim_requirements(s))
+        assert got == one
 
 
 def test_c5_shape_at_scale_properties():
