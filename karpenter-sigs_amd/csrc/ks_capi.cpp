@@ -23,7 +23,7 @@ namespace {
 
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
-      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, total;
+      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, total;
 };
 
 WorkLayout work_layout(const KsDims& d) {
@@ -53,6 +53,8 @@ WorkLayout work_layout(const KsDims& d) {
   w.fail_host = a.add(4 * P * std::max(d.NTPL, 1));
   w.pool_rem = a.add(8 * (size_t)std::max(d.NPOOL, 1) * d.R);
   w.counters = a.add(8 * CT_NCOUNTERS);
+  w.n_hp = a.add(8 * N);
+  w.c_hp = a.add(8 * K);
   w.total = a.total;
   return w;
 }
@@ -82,6 +84,8 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.fail_host = (int32_t*)(base + w.fail_host);
   k.pool_rem = (int64_t*)(base + w.pool_rem);
   k.counters = (int64_t*)(base + w.counters);
+  k.n_hp = (uint64_t*)(base + w.n_hp);
+  k.c_hp = (uint64_t*)(base + w.c_hp);
   return k;
 }
 
@@ -159,6 +163,9 @@ void ks_upload(ks_problem* pb) {
   size_t o_nf = put(t.n_flags.data(), t.n_flags.size() * 4);
   size_t o_pf = put(t.pod_flags.data(), t.pod_flags.size() * 4);
   size_t o_op = put(t.off_price.data(), t.off_price.size() * 8);
+  size_t o_phc = put(t.pod_hpc.data(), t.pod_hpc.size() * 8);
+  size_t o_phu = put(t.pod_hpu.data(), t.pod_hpu.size() * 8);
+  size_t o_nhp = put(t.n_hp0.data(), t.n_hp0.size() * 8);
   HIPCHK(hipMalloc(&pb->dbuf, a.total));
   std::vector<char> staging(a.total, 0);
   for (auto& it : items)
@@ -203,6 +210,9 @@ void ks_upload(ks_problem* pb) {
   D.n_flags = (const int32_t*)(b + o_nf);
   D.pod_flags = (const int32_t*)(b + o_pf);
   D.off_price = (const double*)(b + o_op);
+  D.pod_hpc = (const uint64_t*)(b + o_phc);
+  D.pod_hpu = (const uint64_t*)(b + o_phu);
+  D.n_hp0 = (const uint64_t*)(b + o_nhp);
 }
 
 // Rebuild Results from the replica-0 workspace.

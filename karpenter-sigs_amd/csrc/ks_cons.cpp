@@ -365,7 +365,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   Arena a;
   struct Off {
     size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
-        last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price;
+        last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price, n_hp,
+        c_hp;
   };
   std::vector<Off> offs(ns);
   std::vector<int> simP(ns), entBeg(ns + 1, 0);
@@ -407,6 +408,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     o.fail_code = a.add(4 * P * NT);
     o.fail_host = a.add(4 * P * NT);
     o.counters = a.add(8 * CT_NCOUNTERS);
+    o.n_hp = a.add(d.hpAny ? 8 * (size_t)N : 8);
+    o.c_hp = a.add(8 * K);
     o.rm = a.add(4 * std::max<size_t>(sm.cands.size(), 1));
     o.pool0 = a.add(8 * (size_t)NP * R);
     o.st_price = sm.multi ? a.add(8 * (size_t)std::max(d.T, 1)) : 0;
@@ -515,6 +518,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     w.fail_host = (int32_t*)(base + o.fail_host);
     w.pool_rem = nullptr;
     w.counters = (int64_t*)(base + o.counters);
+    w.n_hp = (uint64_t*)(base + o.n_hp);
+    w.c_hp = (uint64_t*)(base + o.c_hp);
     w.pod_map = c.lpodmap + entBeg[k];
     w.P = simP[k];
     w.nrm = (int32_t)rm.size();

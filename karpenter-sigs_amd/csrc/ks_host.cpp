@@ -12,6 +12,9 @@
 //   Taints.Tolerates / ToleratesTaint pkg/scheduling/taints.go:38-50 (k8s.io/api v0.28.4)
 #include "ks_host.h"
 
+#include <arpa/inet.h>
+#include <cstring>
+
 #include <algorithm>
 #include <cstring>
 
@@ -137,6 +140,40 @@ static void mergeInto(QList& dst, const QList& src) {
 }
 
 // Ceiling(pod).Requests + pods (resources.go:27-35,99-115,124-147)
+bool HostPortH::unspecified() const {
+  if (!ipValid) return false;
+  for (int i = 0; i < 16; i++) {
+    // IPv4 unspecified is ::ffff:0.0.0.0 in the 16-byte form
+    if (i == 10 || i == 11) continue;
+    if (ip16[i]) return false;
+  }
+  return (ip16[10] == 0 && ip16[11] == 0) || (ip16[10] == 0xff && ip16[11] == 0xff);
+}
+
+bool HostPortH::matches(const HostPortH& o) const {
+  if (proto != o.proto || port != o.port) return false;
+  const bool equal = ipValid && o.ipValid ? ip16 == o.ip16 : (!ipValid && !o.ipValid);  // net.IP.Equal
+  return equal || unspecified() || o.unspecified();
+}
+
+HostPortH make_host_port(const std::string& ip, int32_t port, const std::string& proto) {
+  HostPortH h;
+  h.ip = ip;
+  h.port = port;
+  h.proto = proto;
+  in6_addr a6;
+  in_addr a4;
+  if (inet_pton(AF_INET, ip.c_str(), &a4) == 1) {  // net.ParseIP: IPv4 -> v4-in-v6 form
+    h.ip16[10] = h.ip16[11] = 0xff;
+    memcpy(&h.ip16[12], &a4, 4);
+    h.ipValid = true;
+  } else if (inet_pton(AF_INET6, ip.c_str(), &a6) == 1) {
+    memcpy(h.ip16.data(), &a6, 16);
+    h.ipValid = true;
+  }
+  return h;
+}
+
 static QList podRequests(const Value& pod, bool& hostPorts, bool& volumes) {
   QList req;
   const Value* sp = pod.get("spec");
@@ -245,6 +282,17 @@ PodH parse_pod(const Value& v) {
       for (auto& t : ts->arr()) p.tscWhen.push_back(jstr(&t, "whenUnsatisfiable"));
   }
   p.requests = podRequests(v, p.hostPorts, p.volumes);
+  if (sp)
+    if (auto* cs = sp->get("containers"))
+      for (auto& c : cs->arr())
+        if (auto* ps = c.get("ports"))
+          for (auto& x : ps->arr()) {
+            const int64_t hp = x.get("hostPort") ? x.get("hostPort")->i64() : 0;
+            if (hp == 0) continue;
+            std::string ip = jstr(&x, "hostIP");
+            if (ip.empty()) ip = "0.0.0.0";  // GetHostPorts defaults the IP, keeps the protocol as given
+            p.ports.push_back(make_host_port(ip, (int32_t)hp, jstr(&x, "protocol")));
+          }
   p.provisionable = nodeName.empty() && nominated.empty() && failedToSchedule && !p.ownedByDaemonSet && !p.ownedByNode;
   return p;
 }
@@ -457,6 +505,12 @@ void Host::build(const Value& root) {
       n.dsRequests = jqlist(e.get("daemonSetRequests"));
       n.initialized = e.get("initialized") ? e.get("initialized")->boolean(true) : true;
       n.ready = e.get("ready") ? e.get("ready")->boolean(true) : true;
+      if (auto* hu = e.get("hostPortUsage"))  // StateNode.HostPortUsage(): pod key -> ports
+        for (auto& kv : hu->obj())
+          for (auto& x : kv.second.arr())
+            n.hostPorts.push_back({kv.first, make_host_port(x.get("ip") ? x.get("ip")->str() : "0.0.0.0",
+                                                            (int32_t)(x.get("port") ? x.get("port")->i64() : 0),
+                                                            x.get("protocol") ? x.get("protocol")->str() : "TCP")});
       n.origIndex = (int)nodes.size();
       nodes.push_back(std::move(n));
     }
@@ -466,10 +520,8 @@ void Host::build(const Value& root) {
   });
   if (auto* v = root.get("daemonSetPods")) for (auto& e : v->arr()) daemons.push_back(parse_pod(e));
   if (auto* v = root.get("pods")) for (auto& e : v->arr()) pods.push_back(parse_pod(e));
-  for (auto& p : pods) {
-    if (p.hostPorts) throw KsError(-2, "pod " + p.ns + "/" + p.name + " uses hostPorts (not encoded by this build)");
+  for (auto& p : pods)
     if (p.volumes) throw KsError(-2, "pod " + p.ns + "/" + p.name + " mounts PVC volumes (not encoded by this build)");
-  }
 
   // --- universe of keys and values
   internKey(kHostname);
@@ -725,9 +777,37 @@ void Host::build(const Value& root) {
   tab.n_rs0.assign((size_t)std::max(N, 1) * dims.RSW, 0);
   tab.n_taint.assign((size_t)std::max(N, 1) * 2, 0);
   tab.n_flags.assign(std::max(N, 1), 0);
+  tab.n_hp0.assign(std::max(N, 1), 0);
+  // --- host ports: masks over the distinct (IP, port, protocol) triples.  A node's reserved set and a
+  // pod's ports conflict iff some pair Matches (hostportusage.go:74-85); the pod-key exception of
+  // Conflicts never applies because no pod being scheduled is in a node's initial usage (checked).
+  std::set<std::string> podKeys;
+  for (auto& p : pods) podKeys.insert(p.ns + "/" + p.name);
+  auto internHP = [&](const HostPortH& h) {
+    for (size_t i = 0; i < hostPortUniverse.size(); i++)
+      if (hostPortUniverse[i].ip == h.ip && hostPortUniverse[i].port == h.port && hostPortUniverse[i].proto == h.proto)
+        return (int)i;
+    hostPortUniverse.push_back(h);
+    return (int)hostPortUniverse.size() - 1;
+  };
+  for (auto& p : pods) for (auto& h : p.ports) internHP(h);
+  for (auto& n : nodes)
+    for (auto& e : n.hostPorts) {
+      if (podKeys.count(e.first))
+        throw KsError(-2, "pod " + e.first + " is scheduled while it holds host ports on node " + n.name);
+      internHP(e.second);
+    }
+  if (hostPortUniverse.size() > 64) throw KsError(-3, "more than 64 distinct host ports");
+  auto hpMask = [&](const std::vector<std::pair<std::string, HostPortH>>& v) {
+    uint64_t m = 0;
+    for (auto& e : v) m |= 1ull << internHP(e.second);
+    return m;
+  };
+  dims.hpAny = hostPortUniverse.empty() ? 0 : 1;
   for (int i = 0; i < N; i++) {
     Node& n = nodes[i];
     tab.n_flags[i] = (!n.initialized || !n.ready) ? NF_UNUSABLE : 0;
+    tab.n_hp0[i] = hpMask(n.hostPorts);
     std::vector<uint32_t> lab = emptyRec();
     addLabels(lab, n.labels);
     QList dreq;
@@ -795,7 +875,18 @@ void Host::build(const Value& root) {
   tab.pod_nstate.assign(std::max(P, 1), 0);
   tab.pod_uid.assign(std::max(P, 1), 0);
   tab.pod_flags.assign(std::max(P, 1), 0);
-  for (int i = 0; i < P; i++) tab.pod_flags[i] = pods[i].provisionable ? PF_PROVISIONABLE : 0;
+  tab.pod_hpc.assign(std::max(P, 1), 0);
+  tab.pod_hpu.assign(std::max(P, 1), 0);
+  for (int i = 0; i < P; i++) {
+    tab.pod_flags[i] = pods[i].provisionable ? PF_PROVISIONABLE : 0;
+    for (auto& h : pods[i].ports) {
+      for (size_t u = 0; u < hostPortUniverse.size(); u++) {
+        if (hostPortUniverse[u].ip == h.ip && hostPortUniverse[u].port == h.port && hostPortUniverse[u].proto == h.proto)
+          tab.pod_hpu[i] |= 1ull << u;
+        if (h.matches(hostPortUniverse[u])) tab.pod_hpc[i] |= 1ull << u;
+      }
+    }
+  }
   std::map<std::string, int> uids;
   for (auto& p : pods) uids[p.uid] = 0;
   int u = 0;

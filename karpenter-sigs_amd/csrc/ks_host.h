@@ -25,6 +25,16 @@ struct NSR { std::string key, op; std::vector<std::string> values; };
 struct TaintH { std::string key, value, effect; };
 struct TolH { std::string key, op, value, effect; };
 struct PrefTerm { int32_t weight; std::vector<NSR> exprs; };
+// HostPort (hostportusage.go:38-43): IP (net.ParseIP, 16-byte form), port, protocol
+struct HostPortH {
+  std::string ip, proto;
+  int32_t port = 0;
+  std::array<uint8_t, 16> ip16{};
+  bool ipValid = false;
+  bool unspecified() const;
+  bool matches(const HostPortH& o) const;  // HostPort.Matches (hostportusage.go:49-61)
+};
+HostPortH make_host_port(const std::string& ip, int32_t port, const std::string& proto);
 
 // The pod fields the Solve path reads (pod spec subset; pkg/utils/pod, requirements.go:64-100,
 // preferences.go, resources.go Ceiling).
@@ -41,6 +51,7 @@ struct PodH {
   std::vector<TolH> tols;
   QList requests;  // RequestsForPods(pod) incl. pods=1
   bool hostPorts = false, volumes = false;
+  std::vector<HostPortH> ports;  // GetHostPorts (hostportusage.go:92-114)
   bool provisionable = true;  // IsProvisionable (pkg/utils/pod/scheduling.go:28-34)
   // fields the disruption path reads (node.go:32-53 GetNodePods, helpers.go:137-159, scheduling.go:85-92)
   bool ownedByNode = false, ownedByDaemonSet = false, terminal = false, deleting = false;
@@ -75,6 +86,7 @@ struct Host {
   std::vector<int> resShift;  // device value = nano / 10^shift
   // taints
   std::vector<TaintH> taints;
+  std::vector<HostPortH> hostPortUniverse;  // distinct (IP, port, protocol), bit i of the host-port masks
   // instance types
   struct Offer { std::string zone, ct; double price = 0; bool available = true; };
   struct IT { std::string name; std::vector<NSR> reqs; QList capacity, alloc; std::vector<std::pair<std::string, std::string>> offers;
@@ -97,7 +109,8 @@ struct Host {
   bool toleratePreferNoSchedule = false;
   // existing nodes (sorted)
   struct Node { std::string name, hostName; std::map<std::string, std::string> labels; std::vector<TaintH> taints;
-                QList available, capacity, dsRequests, req0; bool initialized = true, ready = true; int origIndex = 0; };
+                QList available, capacity, dsRequests, req0; bool initialized = true, ready = true; int origIndex = 0;
+                std::vector<std::pair<std::string, HostPortH>> hostPorts; };  // HostPortUsage: (pod key, port)
   std::vector<Node> nodes;
   std::vector<PodH> daemons;
   std::vector<PodH> pods;
@@ -110,6 +123,7 @@ struct Host {
     std::vector<int64_t> tsort_alloc, it_alloc, it_cap, tpl_daemon, pool_rem0, pod_req, pod_sortkey, n_avail, n_req0;
     std::vector<double> off_price;
     std::vector<int32_t> n_flags, pod_flags;
+    std::vector<uint64_t> pod_hpc, pod_hpu, n_hp0;
     std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask, st_toltpl;
     std::vector<uint64_t> tpl_taint, st_tol, n_taint;
     std::vector<int32_t> tsort_pos, it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,

@@ -57,6 +57,7 @@ struct KsDims {
   int32_t totalTplIts; // sum of template instance-type list lengths
   int32_t negReq;      // 1 if any pod or daemon request is negative (disables the threshold filter)
   int32_t spotBit, odBit;  // capacity-type value bits of "spot" / "on-demand" (always interned)
+  int32_t hpAny;           // some pod or node uses host ports
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
@@ -113,6 +114,9 @@ struct KsDev {
   const int32_t KS_G* n_flags;     // [N] NF_UNUSABLE: not initialized or not Ready (helpers.go:118-124)
   const int32_t KS_G* pod_flags;   // [P] PF_PROVISIONABLE (pkg/utils/pod/scheduling.go IsProvisionable)
   const double KS_G* off_price;    // available offerings' prices (worstLaunchPrice, helpers.go:235-258)
+  const uint64_t KS_G* pod_hpc;    // [P] host-port triples a pod's ports Match (conflict mask)
+  const uint64_t KS_G* pod_hpu;    // [P] host-port triples a pod reserves
+  const uint64_t KS_G* n_hp0;      // [N] host-port triples reserved on an existing node
 };
 
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };
@@ -166,6 +170,8 @@ struct KsWork {
   int32_t KS_G* fail_host;  // [P][NTPL]
   int64_t KS_G* pool_rem;   // [NPOOL][R]
   int64_t KS_G* counters;   // [16]
+  uint64_t KS_G* n_hp;      // [N] host ports reserved per existing node (SIM: valid where s_tch is set)
+  uint64_t KS_G* c_hp;      // [Kcap] host ports reserved per NodeClaim
   // consolidation simulations only (k_solve<.., SIM=true>): this simulation's view of the shared
   // cluster problem (helpers.go:73-127 — candidates removed, their pods added to the pending ones)
   const int32_t KS_G* pod_map;  // [P] local -> global pod, in NewQueue order (k_sim_keys + sort)

@@ -90,6 +90,7 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
     const KsWork W = works[r];
     for (int64_t i = gtid; i < (int64_t)d.N * d.R; i += gsz) W.n_req[i] = D.n_req0[i];
     for (int64_t i = gtid; i < (int64_t)d.N * d.RSW; i += gsz) W.n_rs[i] = D.n_rs0[i];
+    for (int64_t i = gtid; i < d.N; i += gsz) W.n_hp[i] = D.n_hp0[i];
     for (int64_t i = gtid; i < d.P; i += gsz) {
       W.queue[i] = qorder[i];
       W.pod_state[i] = D.pod_state0[i];
@@ -112,7 +113,7 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 template <int RT>
 struct Window {
   int p, g, uid, s, flags, toltpl, pf, st;
-  uint64_t ll, tol0, tol1;
+  uint64_t ll, tol0, tol1, hpc, hpu;
   int64_t req[RT > 0 ? RT : kMaxR];
 };
 
@@ -151,6 +152,7 @@ struct Solver {
   LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose requests live in a W.n_req slot
   LU32 s_tchr;          // SIM: [ceil(N/32)] nodes whose requirements live in a W.n_rs slot
   int64_t algbytes = 0;
+  uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
 
   __device__ Solver(const KsDev& D_, const KsWork& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
   __device__ __forceinline__ int R() const { return RT > 0 ? RT : d.R; }
@@ -265,8 +267,13 @@ struct Solver {
     }
     nf0 = SIM ? D.n_flags[c0] : 0;
     nf1 = SIM ? D.n_flags[c1] : 0;
-    ok0 = (n0 < d.N) & (((x0 & ~tol0) | (y0 & ~tol1)) == 0);  // Taints.Tolerates
-    ok1 = (n1 < d.N) & (((x1 & ~tol0) | (y1 & ~tol1)) == 0);
+    uint64_t h0 = 0, h1 = 0;
+    if (d.hpAny) {  // HostPortUsage.Conflicts (hostportusage.go:74-85)
+      h0 = own0 ? W.n_hp[c0] : D.n_hp0[c0];
+      h1 = own1 ? W.n_hp[c1] : D.n_hp0[c1];
+    }
+    ok0 = (n0 < d.N) & (((x0 & ~tol0) | (y0 & ~tol1)) == 0) & ((h0 & cur_hpc) == 0);  // Taints.Tolerates
+    ok1 = (n1 < d.N) & (((x1 & ~tol0) | (y1 & ~tol1)) == 0) & ((h1 & cur_hpc) == 0);
     if (SIM) {  // the simulation removed these candidates
       ok0 &= !tbit(s_rmv, c0);
       ok1 &= !tbit(s_rmv, c1);
@@ -289,6 +296,7 @@ struct Solver {
   // Solve: commit of a pod to node j by its owner lane.
   __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod) {
     for (int r = 0; r < R(); r++) W.n_req[(int64_t)j * R() + r] += pod[r];
+    if (d.hpAny) W.n_hp[j] |= cur_hpu;
     if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
   }
   // SIM: copy-on-write commit (wave-uniform).  W.n_req is indexed by node but only the nodes a pod
@@ -308,6 +316,7 @@ struct Solver {
         if (RT == 0 && r >= d.R) break;
         W.n_req[(int64_t)j * R() + r] = q[r] + pod[r];
       }
+      if (d.hpAny) W.n_hp[j] = (fresh ? D.n_hp0[j] : W.n_hp[j]) | cur_hpu;
       if (fresh) s_tch[j >> 5] |= 1u << (j & 31);
     }
     if (sflags & SF_HAS_KEYS) {
@@ -336,6 +345,7 @@ struct Solver {
   // --- NodeClaim quick reject at sorted position j: necessary conditions of NodeClaim.Add ------
   __device__ __forceinline__ bool claim_quick(int j, int s, int sflags, uint32_t toltpl, const int64_t* pod) const {
     if (!((toltpl >> s_ptpl[j]) & 1u)) return false;  // Taints.Tolerates (nodeclaim.go:68-71)
+    if (d.hpAny && (W.c_hp[s_order[j]] & cur_hpc)) return false;  // host port conflicts (:72-75)
     bool ok = true;
 #pragma unroll
     for (int r = 0; r < RM; r++) {
@@ -473,13 +483,14 @@ struct Solver {
       }
       v.cnt[c] = ncnt;
       s_okey[pos] = okNew;
+      if (d.hpAny) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
     }
     if (sflags & SF_HAS_KEYS) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
     copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     log_commit(p, c, nlog);
     // The max bound stays valid as the options only shrink; it is tightened lazily when a full check
     // fails.  HBM-resident claim state is re-read by other lanes: drain the stores first.
-    if ((sflags & SF_HAS_KEYS) || !INL) hbm_release();
+    if ((sflags & SF_HAS_KEYS) || !INL || d.hpAny) hbm_release();
     wsync();
     algbytes += 24 * R() + 4 * d.TW + 8;
     return srt;
@@ -591,6 +602,7 @@ struct Solver {
                   gc.cnt[c] = cnt;
                 }
                 W.c_tpl[c] = t;
+                W.c_hp[c] = cur_hpu;
                 W.c_host[c] = hostid;
                 s_order[c] = c;
                 s_okey[c] = 1;
@@ -797,6 +809,8 @@ struct Solver {
       w.toltpl = D.st_toltpl[w.s];
       w.tol0 = D.st_tol[2 * w.s];
       w.tol1 = D.st_tol[2 * w.s + 1];
+      w.hpc = D.pod_hpc[w.g];
+      w.hpu = D.pod_hpu[w.g];
 #pragma unroll
       for (int r = 0; r < RM; r++) {
         if (RT == 0 && r >= d.R) break;
@@ -898,7 +912,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // flags.  A pod that fits there costs no memory round trip; commits update the owner's registers.
   constexpr int NW = RT > 0 ? 4 : 0;
   constexpr int NWA = NW > 0 ? NW : 1;
-  uint64_t wtx[NWA], wty[NWA];
+  uint64_t wtx[NWA], wty[NWA], whp[NWA];
   int64_t wav[NWA][RM], wrq[NWA][RM];
   int wnf[NWA];
   if constexpr (NW > 0) {
@@ -914,6 +928,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           wrq[k][r] = D.n_req0[(int64_t)c * RM + r];
         }
         wnf[k] = SIM ? D.n_flags[c] : 0;
+        whp[k] = D.n_hp0[c];
       }
     }
   }
@@ -966,6 +981,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const int sflags = rdl(w.flags, wi);
     const uint32_t toltpl = (uint32_t)rdl((int)w.toltpl, wi);
     const uint64_t tol0 = (uint64_t)rdl64((int64_t)w.tol0, wi), tol1 = (uint64_t)rdl64((int64_t)w.tol1, wi);
+    if (d.hpAny) {
+      S.cur_hpc = (uint64_t)rdl64((int64_t)w.hpc, wi);
+      S.cur_hpu = (uint64_t)rdl64((int64_t)w.hpu, wi);
+    }
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= R) break;
@@ -989,6 +1008,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           if (SIM) ok &= !S.tbit(S.s_rmv, n < d.N ? n : 0);
 #pragma unroll
           for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
+          ok &= (whp[k] & S.cur_hpc) == 0;
           if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), D.st_rs + (int64_t)s * d.RSW, 0);
           const uint64_t m = wballot(ok);
           if (m) {
@@ -1005,9 +1025,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           for (int k = 0; k < NW; k++)
             if (k == kj) {
               nfv = wnf[k];
-              if (lane() == owner)
+              if (lane() == owner) {
 #pragma unroll
                 for (int r = 0; r < RM; r++) wrq[k][r] += pod[r];
+                whp[k] |= S.cur_hpu;
+              }
             }
           PH_BEGIN(t7);
           if constexpr (SIM) {

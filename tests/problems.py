@@ -105,7 +105,24 @@ def random_pod(rng, i):
     return p
 
 
-def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None):
+HOST_PORTS = [("", 80, "TCP"), ("", 443, "TCP"), ("10.0.0.1", 8080, "TCP"), ("0.0.0.0", 8080, "TCP"),
+              ("10.0.0.2", 8080, "TCP"), ("", 53, "UDP"), ("::", 9090, "TCP"), ("fd00::1", 9090, "TCP")]
+
+
+def add_host_ports(rng, pod):
+    """hostPort container ports (hostportusage.go:92-114): IP / port / protocol combinations that do
+    and do not Match each other (unspecified IPs match everything on the same port + protocol)."""
+    ports = []
+    for _ in range(int(rng.integers(1, 3))):
+        ip, port, proto = HOST_PORTS[int(rng.integers(len(HOST_PORTS)))]
+        e = {"containerPort": port, "hostPort": port, "protocol": proto}
+        if ip:
+            e["hostIP"] = ip
+        ports.append(e)
+    pod["spec"]["containers"][0]["ports"] = ports
+
+
+def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False):
     rng = np.random.default_rng(seed)
     its = random_its(rng, n_its)
     n_templates = int(rng.integers(1, 4)) if n_templates is None else n_templates
@@ -149,6 +166,10 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None):
             "daemonSetRequests": {"cpu": "100m"} if rng.random() < 0.5 else {},
             "initialized": bool(rng.random() < 0.8),
         })
+        if host_ports and rng.random() < 0.5:
+            ip, port, proto = HOST_PORTS[int(rng.integers(len(HOST_PORTS)))]
+            nodes[-1]["hostPortUsage"] = {"default/bound-%d" % i: [{"ip": ip or "0.0.0.0", "port": port,
+                                                                   "protocol": proto}]}
     daemons = []
     for i in range(int(rng.integers(0, 3))):
         d = synth.pod(100000 + i, cpu=_pick(rng, ["50m", "100m", "200m"]), mem=_pick(rng, ["64Mi", "128Mi"]))
@@ -158,6 +179,10 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None):
             d["spec"]["nodeSelector"] = {synth.ARCH: _pick(rng, ARCHS)}
         daemons.append(d)
     pods = [random_pod(rng, i) for i in range(n_pods)]
+    if host_ports:
+        for p in pods:
+            if rng.random() < 0.4:
+                add_host_ports(rng, p)
     return {
         "wellKnownLabels": synth.FAKE_WELL_KNOWN,
         "instanceTypes": its,

@@ -54,9 +54,20 @@ def test_unsupported_topology_is_loud():
     assert e.value.code == -2
 
 
-def test_unsupported_host_ports_is_loud():
+def test_host_ports_are_encoded():
     snap = synth.config2(10)
     snap["pods"][0]["spec"]["containers"][0]["ports"] = [{"hostPort": 80, "containerPort": 80}]
+    snap["stateNodes"] = []
+    assert inspect(snap)["pods"] == 10
+
+
+def test_scheduled_pod_holding_host_ports_is_loud():
+    """Conflicts' same-pod exception (hostportusage.go:78) is not encoded: a pod being scheduled that
+    already holds ports on an existing node is refused."""
+    snap = problems.random_problem(3, n_nodes=2)
+    snap["pods"][0]["spec"]["containers"][0]["ports"] = [{"hostPort": 80, "containerPort": 80}]
+    p0 = snap["pods"][0]["metadata"]
+    snap["stateNodes"][0]["hostPortUsage"] = {"%s/%s" % (p0["namespace"], p0["name"]): [{"port": 80}]}
     with pytest.raises(KsError) as e:
         inspect(snap)
     assert e.value.code == -2

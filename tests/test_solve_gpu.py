@@ -45,6 +45,14 @@ def test_random_problem_parity(seed):
     assert d is None, d
 
 
+@pytest.mark.parametrize("seed", list(range(200, 216)))
+def test_host_ports_parity(seed):
+    """HostPortUsage on existing nodes and in-flight NodeClaims (hostportusage.go:74-85)."""
+    want, got = _solve_both(problems.random_problem(seed, n_pods=150, n_nodes=int(seed % 3) * 6, host_ports=True))
+    d = _diff(want, got)
+    assert d is None, d
+
+
 @pytest.mark.parametrize("seed", [100, 101, 102, 103])
 def test_random_problem_parity_larger(seed):
     want, got = _solve_both(problems.random_problem(seed, n_pods=800, n_its=120, n_nodes=30))
