@@ -116,6 +116,27 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync):
     }
 
 
+def c3_bench(args, local):
+    """C3 (BASELINE.json configs[2]): requirement-heavy Solve, 1 GPU, reported beside the C2 line."""
+    from karpenter_amd import Scheduler, synth
+
+    sch = Scheduler(json.dumps(synth.config3(args.c3_pods)))
+    r = sch.solve(device=local)
+    placed = sum(len(c["pods"]) for c in r.new_nodeclaims)
+    for _ in range(max(args.warmup - 1, 0)):
+        sch.solve(device=local, timing_only=True)
+    t0 = time.perf_counter()
+    ks = []
+    for _ in range(2):
+        ks.append(sch.solve(device=local, timing_only=True).solve_kernel_ms)
+    el = (time.perf_counter() - t0) / 2
+    return {"metric": "pods/sec in Scheduler.Solve (C3: %d pods, 800 instance types x 8 offerings, 3 tainted "
+                      "NodePools, selectors/affinity/tolerations)" % args.c3_pods,
+            "value": round(args.c3_pods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1000, 3),
+            "kernel_ms": round(sum(ks) / len(ks), 3), "new_nodeclaims": len(r.new_nodeclaims),
+            "pods_placed": placed, "pod_errors": len(r.pod_errors)}
+
+
 def _traffic(tag):
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % tag)
     if os.path.exists(tpath):
@@ -134,6 +155,8 @@ def main():
     ap.add_argument("--cpu-pods", type=int, default=50000, help="oracle sample size (same workload shape)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--no-c3", action="store_true")
+    ap.add_argument("--c3-pods", type=int, default=20000)
     ap.add_argument("--only-consolidation", action="store_true", help="profiling: skip the Solve section")
     ap.add_argument("--cons-nodes", type=int, default=5000, help="C5 cluster size (20 pods per node)")
     ap.add_argument("--cons-steps", type=int, default=20)
@@ -212,6 +235,7 @@ def main():
         cpu = {"value": round(args.cpu_pods / secs, 1), "unit": "pods/s", "cores": 1, "kind": "port",
                "sample": "1 Solve of C2 with %d pods x %d instance types (oracle/cpu_ref.cpp, single thread, "
                          "%.1f s)" % (args.cpu_pods, args.its, secs)}
+    c3 = None if args.no_c3 or world > 1 else c3_bench(args, local)
     cons = None if args.no_consolidation else consolidation_bench(args, rank, world, local, dist, barrier_sync)
     if rank != 0:
         dist.destroy_process_group()
@@ -238,6 +262,7 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_launch, "kernel_ms": round(k_ms, 3),
                      "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3)},
         "cpu_baseline": cpu,
+        "solve_c3": c3,
         "consolidation": cons,
     }
     print(json.dumps(out))

@@ -471,7 +471,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   size_t budget = 160 * 1024 - 256;
   if (reps > 256) budget = std::max<size_t>(24 * 1024, budget * 256 / reps);
   if (opts && opts->lds_budget > 0) budget = std::min<size_t>(budget, (size_t)opts->lds_budget);
-  Plan pl = make_plan(d, budget);
+  Plan pl = make_plan(d, budget, false, pb->wideKO);
   if (pl.lds > 160 * 1024 || pl.KO < 1)
     throw KsError(KS_ERR_CAPACITY, "solve state does not fit the LDS budget");
   pb->lastKO = pl.KO;
@@ -495,14 +495,25 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&em));
   HIPCHK(hipEventCreate(&e1));
-  HIPCHK(hipEventRecord(e0, pb->stream));
-  HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp, pb->stempBytes,
-                      pb->stream, em));
-  HIPCHK(hipEventRecord(e1, pb->stream));
-  HIPCHK(hipEventSynchronize(e1));
   float ms = 0, setup = 0;
-  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-  HIPCHK(hipEventElapsedTime(&setup, e0, em));
+  for (int attempt = 0; attempt < 2; attempt++) {
+    HIPCHK(hipEventRecord(e0, pb->stream));
+    HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp,
+                        pb->stempBytes, pb->stream, em));
+    HIPCHK(hipEventRecord(e1, pb->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    HIPCHK(hipEventElapsedTime(&setup, e0, em));
+    int64_t err = 0;
+    HIPCHK(hipMemcpy(&err, w0.counters + CT_ERROR, 8, hipMemcpyDeviceToHost));
+    if (err != KE_CLAIM_CAP || pb->wideKO) break;
+    // more NodeClaims than the default plan holds: re-plan with claim positions filling the LDS
+    // (remembered for later Solves of this problem) and solve again
+    pb->wideKO = true;
+    pl = make_plan(d, budget, false, true);
+    if (pl.lds > 160 * 1024 || pl.KO < 1) break;
+    pb->lastKO = pl.KO;
+  }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(em);
   (void)hipEventDestroy(e1);

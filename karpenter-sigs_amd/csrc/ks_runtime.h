@@ -14,7 +14,7 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
                         hipEvent_t mid);
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st);
-Plan make_plan(const KsDims& d, size_t budget, bool sim = false);
+Plan make_plan(const KsDims& d, size_t budget, bool sim = false, bool wideKO = false);
 size_t queue_sort_temp_bytes(int n);
 hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
                       hipStream_t st);
@@ -54,6 +54,7 @@ struct ks_problem {
   hipStream_t stream = nullptr;
   int device = -1;
   int lastKO = 0;  // claim capacity of the last launch plan
+  bool wideKO = false;  // a Solve of this problem outgrew the default plan's NodeClaim capacity
   // NewQueue radix-sort workspace
   uint64_t* skeys = nullptr;
   int32_t* svals = nullptr;

@@ -1184,7 +1184,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 // per Solve (KO); claims [0, KL) also keep their template/requests/max/options/thresholds in LDS,
 // the rest in HBM.  The instance-type tables go to LDS first when they leave room for 64 claims.
 // One-Solve launches use the whole 160 KiB of a CU; batched simulations pass a smaller budget.
-Plan make_plan(const KsDims& d, size_t budget, bool sim) {
+// wideKO: a Solve that created more NodeClaims than the default plan holds is re-planned with the
+// instance-type tables in HBM and almost all LDS given to claim positions.
+Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   Plan pl{};
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
@@ -1199,13 +1201,16 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim) {
   size_t avail = budget > fixed + slack ? budget - fixed - slack : 0;
   // The threshold filter needs the sorted lists only without negative requests.
   const size_t tablesB = tallocB + (d.negReq ? 0 : tsortB);
-  pl.talloc = (tablesB + 64 * (posB + clmB) <= avail) ? 1 : 0;
+  pl.talloc = (!wideKO && tablesB + 64 * (posB + clmB) <= avail) ? 1 : 0;
   pl.tsort = pl.talloc && !d.negReq;
   if (pl.talloc) avail -= tablesB;
   const size_t kAll = avail / (posB + clmB);
   size_t ko, kl;
   if (kAll >= (size_t)d.Kcap) {
     ko = kl = d.Kcap;
+  } else if (wideKO) {  // 64 LDS-resident claims, the rest to positions
+    kl = std::min<size_t>(64, kAll);
+    ko = std::min((size_t)d.Kcap, (avail - kl * clmB) / posB);
   } else {  // half the LDS to positions, half to claim state
     ko = std::min((size_t)d.Kcap, std::max(kAll, avail / 2 / posB));
     kl = std::min(ko, (avail - ko * posB) / clmB);

@@ -274,3 +274,87 @@ def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, 
 def config5(n_nodes=5000, pods_per_node=20, seed=4205):
     """C5: multi-node + single-node consolidation over a 5k-node / 100k-pod cluster."""
     return cluster_snapshot(n_nodes, pods_per_node, 400, seed)
+
+
+C3_ZONES = ["test-zone-1", "test-zone-2", "test-zone-3", "test-zone-4"]
+
+
+def config3(n_pods=20000, seed=4203):
+    """C3 (BASELINE.json configs[2]): pods with nodeSelector / required + preferred node affinity and
+    tolerations over 800 instance types (100 cpu x memory shapes x 2 arch x 4 families), each offered
+    in 4 zones x {spot, on-demand} (spot = 0.3 x the fake price), and 3 weighted NodePools with
+    NoSchedule taints and zone / capacity-type requirements.  40 % of pods carry a nodeSelector
+    (zone / arch / capacity-type), 30 % required node affinity (In / NotIn / Gt / Lt on `integer`),
+    20 % preferred node affinity, 30 % tolerations."""
+    rng = np.random.default_rng(seed)
+    its = []
+    shapes = [(c, m) for c in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128) for m in (1, 2, 4, 6, 8, 12, 16, 24, 32, 48)][:100]
+    for fam in ("c", "m", "r", "t"):
+        for arch in ("amd64", "arm64"):
+            for cpu, ratio in shapes:
+                mem = cpu * ratio
+                price = price_from_resources(cpu, mem * GI) * {"c": 1.0, "m": 1.1, "r": 1.3, "t": 0.9}[fam]
+                offers = [{"capacityType": ct, "zone": z, "price": price * (0.3 if ct == "spot" else 1.0),
+                           "available": bool(rng.random() < 0.95)}
+                          for z in C3_ZONES for ct in ("spot", "on-demand")]
+                name = "%s%d-%s-%dc-%dg" % (fam, len(its) % 7, arch, cpu, mem)
+                its.append(fake_instance_type(name, cpu, mem, pods=min(250, 10 * cpu + 8), arch=arch,
+                                              oses=("linux",), offerings=offers))
+    pools = [
+        node_pool("general", weight=10, requirements=[{"key": CT, "operator": "In", "values": ["on-demand", "spot"]}]),
+        node_pool("spot-batch", weight=50, requirements=[{"key": CT, "operator": "In", "values": ["spot"]},
+                                                          {"key": ZONE, "operator": "NotIn", "values": ["test-zone-4"]}],
+                  taints=[{"key": "batch", "value": "true", "effect": "NoSchedule"}]),
+        node_pool("gpu-team", weight=90, requirements=[{"key": ZONE, "operator": "In", "values": C3_ZONES[:2]}],
+                  taints=[{"key": "team", "value": "ml", "effect": "NoSchedule"}], labels={"team": "ml"},
+                  limits={"cpu": "20000"}),
+    ]
+    by_pool = {"general": list(range(len(its))), "spot-batch": [i for i in range(len(its)) if i % 2 == 0],
+               "gpu-team": [i for i in range(len(its)) if its[i]["capacity"]["cpu"] not in ("1", "2")]}
+    cpus, mems = CPU_CHOICES + ["2", "4"], MEM_CHOICES + ["8Gi"]
+    pods = []
+    for i in range(n_pods):
+        p = pod(i, cpu=cpus[int(rng.integers(len(cpus)))], mem=mems[int(rng.integers(len(mems)))],
+                labels={"my-label": LABEL_VALUES[int(rng.integers(7))]})
+        spec = p["spec"]
+        u = rng.random()
+        if u < 0.4:
+            k = int(rng.integers(3))
+            spec["nodeSelector"] = [{ZONE: C3_ZONES[int(rng.integers(4))]},
+                                    {ARCH: ("amd64", "arm64")[int(rng.integers(2))]},
+                                    {CT: ("spot", "on-demand")[int(rng.integers(2))]}][k]
+        elif u < 0.7:
+            exprs = []
+            v = int(rng.integers(4))
+            if v == 0:
+                exprs.append({"key": ZONE, "operator": "In", "values": sorted(set(
+                    C3_ZONES[int(j)] for j in rng.integers(0, 4, size=2)))})
+            elif v == 1:
+                exprs.append({"key": ZONE, "operator": "NotIn", "values": [C3_ZONES[int(rng.integers(4))]]})
+            elif v == 2:
+                exprs.append({"key": "integer", "operator": "Gt", "values": [str(int(rng.choice([2, 4, 8, 16])))]})
+            else:
+                exprs.append({"key": "integer", "operator": "Lt", "values": [str(int(rng.choice([16, 32, 64])))]})
+            terms = [{"matchExpressions": exprs}]
+            if rng.random() < 0.3:
+                terms.append({"matchExpressions": [{"key": ARCH, "operator": "In", "values": ["arm64"]}]})
+            spec["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": terms}}}
+        elif u < 0.9:
+            spec["affinity"] = {"nodeAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+                {"weight": int(rng.integers(1, 100)),
+                 "preference": {"matchExpressions": [{"key": CT, "operator": "In", "values": ["spot"]}]}}]}}
+        if rng.random() < 0.3:
+            spec["tolerations"] = [[{"key": "batch", "operator": "Equal", "value": "true", "effect": "NoSchedule"}],
+                                   [{"key": "team", "operator": "Exists"}],
+                                   [{"operator": "Exists"}]][int(rng.integers(3))]
+        pods.append(p)
+    return {
+        "wellKnownLabels": FAKE_WELL_KNOWN,
+        "instanceTypes": its,
+        "instanceTypesByNodePool": by_pool,
+        "nodeClaimTemplates": sorted(pools, key=lambda x: -x["spec"]["weight"]),
+        "nodePools": pools,
+        "stateNodes": [],
+        "daemonSetPods": [],
+        "pods": pods,
+    }

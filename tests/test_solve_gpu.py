@@ -60,6 +60,14 @@ def test_random_problem_parity_larger(seed):
     assert d is None, d
 
 
+def test_config3_selectors_affinity_taints():
+    """C3 shape (BASELINE.json configs[2]) at 1500 pods: 800 instance types x 8 offerings, 3 tainted
+    weighted NodePools, selectors / required + preferred affinity / tolerations."""
+    want, got = _solve_both(synth.config3(1500))
+    d = _diff(want, got)
+    assert d is None, d
+
+
 def test_config1_benchmark_scheduling_2000():
     """BenchmarkScheduling2000 (scheduling_benchmark_test.go:72-74,116-182)."""
     want, got = _solve_both(synth.config1())
