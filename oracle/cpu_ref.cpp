@@ -367,6 +367,25 @@ static bool HostPortMatches(const HostPort& p, const HostPort& q) {  // hostport
 struct PreferredTerm { int32_t weight = 0; vector<NSR> exprs; };
 struct Container { ResourceList requests, limits; vector<HostPort> ports; };
 
+struct LabelSelectorReq { string key, op; vector<string> values; };
+struct LabelSelector {
+  bool present = false;           // nil selector: selects() matches nothing, TopologyListOptions lists everything
+  vector<LabelSelectorReq> reqs;  // matchLabels (op "In", one value) then matchExpressions
+};
+struct PodAffinityTermS {
+  LabelSelector selector;
+  vector<string> namespaces;
+  bool hasNamespaceSelector = false;
+  string topologyKey;
+};
+struct TSCS {
+  string key, when;
+  int32_t maxSkew = 0;
+  bool hasMinDomains = false;
+  int32_t minDomains = 0;
+  LabelSelector selector;
+};
+
 struct Pod {
   string name, ns, uid;
   map<string, string> labels;
@@ -378,14 +397,13 @@ struct Pod {
   vector<vector<NSR>> requiredTerms;
   vector<PreferredTerm> preferred;
   bool hasPodAffinity = false, hasPodAnti = false;
-  int podAffinityRequired = 0, podAffinityPreferred = 0;  // counts (weights kept for Relax ordering)
-  vector<int32_t> podAffinityPreferredWeights, podAntiPreferredWeights;
-  int podAntiRequired = 0;
+  vector<PodAffinityTermS> affRequired, antiRequired;
+  vector<std::pair<int32_t, PodAffinityTermS>> affPreferred, antiPreferred;
   vector<Toleration> tolerations;
   vector<Container> containers, initContainers;
   bool hasOverhead = false;
   ResourceList overhead;
-  vector<string> tscWhen;  // topologySpreadConstraints whenUnsatisfiable (inert with an empty Topology)
+  vector<TSCS> tsc;  // topologySpreadConstraints
   map<string, string> annotations;
   bool hasPriority = false;
   int32_t priority = 0;
@@ -560,6 +578,8 @@ struct InstanceType {
 struct NodeClaimTemplate {  // nodeclaimtemplate.go:35-53
   string nodePoolName;
   Requirements reqs;
+  vector<NSR> poolRequirements;       // NodePool spec.template.spec.requirements (topology domains)
+  map<string, string> poolLabels;     // NodePool spec.template.metadata.labels (without karpenter.sh/nodepool)
   vector<Taint> taints;
   vector<int> instanceTypes;  // indices into Problem::its (the pool's GetInstanceTypes list)
 };
@@ -581,6 +601,9 @@ struct Problem {
   vector<Pod> daemonSetPods;
   vector<Pod> pods;
   int64_t hostnameSeed = 0;
+  // cluster state the Topology counts (topology.go:190-291): bound pods and node labels by node name
+  vector<Pod> clusterPods;
+  map<string, map<string, string>> nodeLabels;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -648,6 +671,31 @@ static Container parseContainer(const ojson::Value& c) {
     }
   return k;
 }
+static LabelSelector parseLabelSelector(const ojson::Value* v) {  // metav1.LabelSelector
+  LabelSelector s;
+  if (!v || v->is_null()) return s;
+  s.present = true;
+  for (auto& kv : strMap(v->get("matchLabels"))) s.reqs.push_back({kv.first, "In", {kv.second}});
+  if (auto* es = v->get("matchExpressions"))
+    for (auto& e : es->arr()) {
+      LabelSelectorReq r;
+      r.key = e.get("key") ? e.get("key")->str() : "";
+      r.op = e.get("operator") ? e.get("operator")->str() : "";
+      if (auto* vs = e.get("values")) for (auto& x : vs->arr()) r.values.push_back(x.str());
+      s.reqs.push_back(r);
+    }
+  return s;
+}
+
+static PodAffinityTermS parseAffinityTerm(const ojson::Value& t) {
+  PodAffinityTermS a;
+  a.selector = parseLabelSelector(t.get("labelSelector"));
+  if (auto* ns = t.get("namespaces")) for (auto& x : ns->arr()) a.namespaces.push_back(x.str());
+  if (auto* nss = t.get("namespaceSelector"); nss && !nss->is_null()) a.hasNamespaceSelector = true;
+  a.topologyKey = t.get("topologyKey") ? t.get("topologyKey")->str() : "";
+  return a;
+}
+
 static Pod parsePod(const ojson::Value& v) {
   Pod p;
   const ojson::Value* md = v.get("metadata");
@@ -689,17 +737,17 @@ static Pod parsePod(const ojson::Value& v) {
             p.preferred.push_back(pt);
           }
       }
-      if (auto* pa = af->get("podAffinity"); pa && !pa->is_null()) {
-        p.hasPodAffinity = true;
-        if (auto* r = pa->get("requiredDuringSchedulingIgnoredDuringExecution")) p.podAffinityRequired = (int)r->arr().size();
+      for (int anti = 0; anti < 2; anti++) {
+        auto* pa = af->get(anti ? "podAntiAffinity" : "podAffinity");
+        if (!pa || pa->is_null()) continue;
+        (anti ? p.hasPodAnti : p.hasPodAffinity) = true;
+        if (auto* r = pa->get("requiredDuringSchedulingIgnoredDuringExecution"))
+          for (auto& t : r->arr()) (anti ? p.antiRequired : p.affRequired).push_back(parseAffinityTerm(t));
         if (auto* r = pa->get("preferredDuringSchedulingIgnoredDuringExecution"))
-          for (auto& t : r->arr()) p.podAffinityPreferredWeights.push_back(t.get("weight") ? (int32_t)t.get("weight")->i64() : 0);
-      }
-      if (auto* pa = af->get("podAntiAffinity"); pa && !pa->is_null()) {
-        p.hasPodAnti = true;
-        if (auto* r = pa->get("requiredDuringSchedulingIgnoredDuringExecution")) p.podAntiRequired = (int)r->arr().size();
-        if (auto* r = pa->get("preferredDuringSchedulingIgnoredDuringExecution"))
-          for (auto& t : r->arr()) p.podAntiPreferredWeights.push_back(t.get("weight") ? (int32_t)t.get("weight")->i64() : 0);
+          for (auto& t : r->arr())
+            (anti ? p.antiPreferred : p.affPreferred)
+                .push_back({t.get("weight") ? (int32_t)t.get("weight")->i64() : 0,
+                            t.get("podAffinityTerm") ? parseAffinityTerm(*t.get("podAffinityTerm")) : PodAffinityTermS{}});
       }
     }
     if (auto* ts = sp->get("tolerations"))
@@ -715,7 +763,18 @@ static Pod parsePod(const ojson::Value& v) {
     if (auto* cs = sp->get("initContainers")) for (auto& c : cs->arr()) p.initContainers.push_back(parseContainer(c));
     if (auto* oh = sp->get("overhead"); oh && !oh->is_null()) { p.hasOverhead = true; p.overhead = resList(oh); }
     if (auto* ts = sp->get("topologySpreadConstraints"))
-      for (auto& t : ts->arr()) p.tscWhen.push_back(t.get("whenUnsatisfiable") ? t.get("whenUnsatisfiable")->str() : "");
+      for (auto& t : ts->arr()) {
+        TSCS c;
+        c.key = t.get("topologyKey") ? t.get("topologyKey")->str() : "";
+        c.when = t.get("whenUnsatisfiable") ? t.get("whenUnsatisfiable")->str() : "";
+        c.maxSkew = t.get("maxSkew") ? (int32_t)t.get("maxSkew")->i64() : 0;
+        if (auto* md = t.get("minDomains"); md && !md->is_null()) {
+          c.hasMinDomains = true;
+          c.minDomains = (int32_t)md->i64();
+        }
+        c.selector = parseLabelSelector(t.get("labelSelector"));
+        p.tsc.push_back(c);
+      }
   }
   if (auto* st = v.get("status")) {
     if (auto* x = st->get("phase")) p.phase = x->str();
@@ -744,6 +803,8 @@ static NodeClaimTemplate templateFromNodePool(const ojson::Value& np) {
       t.taints = taintList(ts->get("taints"));
     }
   }
+  t.poolRequirements = reqs;
+  t.poolLabels = labels;
   labels[kNodePool] = t.nodePoolName;
   t.reqs = NewNodeSelectorRequirements(reqs);
   t.reqs.AddAll(NewLabelRequirements(labels));
@@ -834,9 +895,15 @@ static Problem parseProblem(const ojson::Value& root) {
   if (auto* ds = root.get("daemonSetPods")) for (auto& v : ds->arr()) pb.daemonSetPods.push_back(parsePod(v));
   if (auto* ps = root.get("pods")) for (auto& v : ps->arr()) pb.pods.push_back(parsePod(v));
   if (auto* hs = root.get("hostnameSeed")) pb.hostnameSeed = hs->i64();
+  if (auto* cps = root.get("clusterPods")) for (auto& v : cps->arr()) pb.clusterPods.push_back(parsePod(v));
+  for (auto& n : pb.nodes) pb.nodeLabels[n.name] = n.labels;
+  if (auto* cns = root.get("clusterNodes"))
+    for (auto& v : cns->arr()) pb.nodeLabels[v.get("name") ? v.get("name")->str() : ""] = strMap(v.get("labels"));
   (void)itIndex;
   return pb;
 }
+
+#include "topology.inc"
 
 // ---------------------------------------------------------------------------------------------
 // Scheduler (scheduler.go, nodeclaim.go, existingnode.go, queue.go, preferences.go)
@@ -899,6 +966,7 @@ class Scheduler {
  public:
   explicit Scheduler(Problem& pb) : pb_(pb) {
     nodeID_ = pb.hostnameSeed;
+    buildTopology();
     // NewScheduler (scheduler.go:49-83)
     for (auto& np : pb.nodePools) if (np.preferNoSchedule) toleratePreferNoSchedule_ = true;
     for (size_t t = 0; t < pb.templates.size(); t++) {  // getDaemonOverhead :324-341
@@ -931,6 +999,7 @@ class Scheduler {
       en.reqs = NewLabelRequirements(n.labels);
       en.reqs.Add(NewRequirement(kHostname, "In", {n.hostName}));
       en.hostPorts = n.hostPorts;
+      topo_.Register(kHostname, n.hostName);  // NewExistingNode (existingnode.go:60)
       existing_.push_back(std::move(en));
       auto lp = n.labels.find(kNodePool);
       string pool = lp == n.labels.end() ? "" : lp->second;
@@ -970,7 +1039,7 @@ class Scheduler {
       if (errors_[p].ok) continue;
       bool relaxed = Relax(pb_.pods[p]);
       Push(p, relaxed);
-      // relaxed -> topology.Update(pod): the empty topology tracks nothing
+      if (relaxed) topo_.Update(pb_.pods[p]);
     }
     for (auto& nc : claims_) nc.reqs.m.erase(kHostname);  // FinalizeScheduling nodeclaim.go:123-128
   }
@@ -988,6 +1057,24 @@ class Scheduler {
 
  private:
   Problem& pb_;
+  Topology topo_;
+
+  // Provisioner.NewScheduler -> NewTopology (provisioner.go:229-287, topology.go:61-85)
+  void buildTopology() {
+    topo_.domains = topologyDomains(pb_);
+    topo_.clusterPods = &pb_.clusterPods;
+    topo_.nodes = &pb_.nodeLabels;
+    for (auto& p : pb_.pods) topo_.excluded.insert(p.uid);
+    for (auto& cp : pb_.clusterPods) {  // updateInverseAffinities via ForPodsWithAntiAffinity
+      if (!(cp.hasAffinity && cp.hasPodAnti && !cp.antiRequired.empty())) continue;
+      if (cp.nodeName.empty()) continue;
+      auto n = pb_.nodeLabels.find(cp.nodeName);
+      if (n == pb_.nodeLabels.end()) continue;
+      if (topo_.excluded.count(cp.uid)) continue;
+      topo_.inverseAnti(cp, &n->second);
+    }
+    for (auto& p : pb_.pods) topo_.Update(p);
+  }
   int64_t nodeID_ = 0;
   bool toleratePreferNoSchedule_ = false;
   vector<ResourceList> daemonOverhead_;
@@ -1046,16 +1133,17 @@ class Scheduler {
       return true;
     }
     // removePreferredPodAffinityTerm (SliceStable by weight desc, drop first)
-    if (pod.hasAffinity && pod.hasPodAffinity && !pod.podAffinityPreferredWeights.empty()) {
-      auto& w = pod.podAffinityPreferredWeights;
-      std::stable_sort(w.begin(), w.end(), [](int32_t a, int32_t b) { return a > b; });
-      w.erase(w.begin());
+    auto byWeight = [](const std::pair<int32_t, PodAffinityTermS>& a, const std::pair<int32_t, PodAffinityTermS>& b) {
+      return a.first > b.first;
+    };
+    if (pod.hasAffinity && pod.hasPodAffinity && !pod.affPreferred.empty()) {
+      std::stable_sort(pod.affPreferred.begin(), pod.affPreferred.end(), byWeight);
+      pod.affPreferred.erase(pod.affPreferred.begin());
       return true;
     }
-    if (pod.hasAffinity && pod.hasPodAnti && !pod.podAntiPreferredWeights.empty()) {
-      auto& w = pod.podAntiPreferredWeights;
-      std::stable_sort(w.begin(), w.end(), [](int32_t a, int32_t b) { return a > b; });
-      w.erase(w.begin());
+    if (pod.hasAffinity && pod.hasPodAnti && !pod.antiPreferred.empty()) {
+      std::stable_sort(pod.antiPreferred.begin(), pod.antiPreferred.end(), byWeight);
+      pod.antiPreferred.erase(pod.antiPreferred.begin());
       return true;
     }
     // removePreferredNodeAffinityTerm
@@ -1066,10 +1154,10 @@ class Scheduler {
       return true;
     }
     // removeTopologySpreadScheduleAnyway: swap-with-last then truncate
-    for (size_t i = 0; i < pod.tscWhen.size(); i++) {
-      if (pod.tscWhen[i] == "ScheduleAnyway") {
-        pod.tscWhen[i] = pod.tscWhen.back();
-        pod.tscWhen.pop_back();
+    for (size_t i = 0; i < pod.tsc.size(); i++) {
+      if (pod.tsc[i].when == "ScheduleAnyway") {
+        pod.tsc[i] = pod.tsc.back();
+        pod.tsc.pop_back();
         return true;
       }
     }
@@ -1097,10 +1185,16 @@ class Scheduler {
     Requirements podReqs = NewPodRequirements(pod);
     if (!Compatible(nodeReqs, podReqs, nullptr).empty()) return false;
     nodeReqs.AddAll(podReqs);
-    // topology.AddRequirements with an empty Topology returns the node requirements unchanged.
+    Requirements strict = HasPreferredNodeAffinity(pod) ? NewStrictPodRequirements(pod) : podReqs;
+    Requirements topoReqs;
+    string terr;
+    if (!topo_.AddRequirements(strict, nodeReqs, pod, nullptr, topoReqs, terr)) return false;
+    if (!Compatible(nodeReqs, topoReqs, nullptr).empty()) return false;
+    nodeReqs.AddAll(topoReqs);
     n.pods.push_back(p);
     n.requests = requests;
     n.reqs = nodeReqs;
+    topo_.Record(pod, nodeReqs, nullptr);
     n.hostPorts.Add(key, hp);
     return true;
   }
@@ -1152,7 +1246,17 @@ class Scheduler {
     Errs ce = Compatible(ncReqs, podReqs, &pb_.wellKnown);
     if (!ce.empty()) { res.ok = false; res.errs = {"incompatible requirements, " + joinErrs(ce)}; return res; }
     ncReqs.AddAll(podReqs);
-    // empty Topology: AddRequirements returns ncReqs, Compatible(ncReqs, ncReqs) holds.
+    Requirements strict = HasPreferredNodeAffinity(pod) ? NewStrictPodRequirements(pod) : podReqs;
+    Requirements topoReqs;
+    string terr;
+    if (!topo_.AddRequirements(strict, ncReqs, pod, &pb_.wellKnown, topoReqs, terr)) {
+      res.ok = false;
+      res.errs = {terr};
+      return res;
+    }
+    Errs te2 = Compatible(ncReqs, topoReqs, &pb_.wellKnown);
+    if (!te2.empty()) { res.ok = false; res.errs = te2; return res; }
+    ncReqs.AddAll(topoReqs);
     ResourceList podReq = RequestsForPods({&pod});
     ResourceList requests = Merge({&n.requests, &podReq});
     FilterResults f = filterInstanceTypes(n.itOptions, ncReqs, requests);
@@ -1167,6 +1271,7 @@ class Scheduler {
     n.itOptions = f.remaining;
     n.requests = requests;
     n.reqs = ncReqs;
+    topo_.Record(pod, ncReqs, &pb_.wellKnown);
     n.hostPorts.Add(key, hp);
     return res;
   }
@@ -1213,6 +1318,7 @@ class Scheduler {
       char hb[64];
       snprintf(hb, sizeof hb, "hostname-placeholder-%04lld", (long long)(++nodeID_));
       nc.hostname = hb;
+      topo_.Register(kHostname, nc.hostname);
       nc.reqs = tpl.reqs;
       nc.reqs.Add(NewRequirement(kHostname, "In", {nc.hostname}));
       nc.itOptions = its;
