@@ -23,7 +23,8 @@ namespace {
 
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
-      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, total;
+      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, tg_cnt, tg_reg,
+      tg_ccnt, fail_rs, total;
 };
 
 WorkLayout work_layout(const KsDims& d) {
@@ -55,6 +56,10 @@ WorkLayout work_layout(const KsDims& d) {
   w.counters = a.add(8 * CT_NCOUNTERS);
   w.n_hp = a.add(8 * N);
   w.c_hp = a.add(8 * K);
+  w.tg_cnt = a.add(4 * std::max<size_t>(d.G ? (size_t)d.tgCntWords : 1, 1));
+  w.tg_reg = a.add(4 * std::max<size_t>(d.G ? (size_t)d.tgRegWords : 1, 1));
+  w.tg_ccnt = a.add(4 * (size_t)std::max(d.G, 1) * (d.G ? K + 1 : 1));
+  w.fail_rs = a.add(d.G ? 4 * (size_t)P * std::max(d.NTPL, 1) * d.FSW : 4);
   w.total = a.total;
   return w;
 }
@@ -86,6 +91,10 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.counters = (int64_t*)(base + w.counters);
   k.n_hp = (uint64_t*)(base + w.n_hp);
   k.c_hp = (uint64_t*)(base + w.c_hp);
+  k.tg_cnt = (int32_t*)(base + w.tg_cnt);
+  k.tg_reg = (uint32_t*)(base + w.tg_reg);
+  k.tg_ccnt = (int32_t*)(base + w.tg_ccnt);
+  k.fail_rs = (uint32_t*)(base + w.fail_rs);
   return k;
 }
 
@@ -166,6 +175,15 @@ void ks_upload(ks_problem* pb) {
   size_t o_phc = put(t.pod_hpc.data(), t.pod_hpc.size() * 8);
   size_t o_phu = put(t.pod_hpu.data(), t.pod_hpu.size() * 8);
   size_t o_nhp = put(t.n_hp0.data(), t.n_hp0.size() * 8);
+  size_t o_tgm = put(t.tg_meta.data(), t.tg_meta.size() * 4);
+  size_t o_tgc = put(t.tg_cnt0.data(), t.tg_cnt0.size() * 4);
+  size_t o_tgr = put(t.tg_reg0.data(), t.tg_reg0.size() * 4);
+  size_t o_tgf = put(t.tg_frs.data(), t.tg_frs.size() * 4);
+  size_t o_sgo = put(t.st_gown.data(), t.st_gown.size() * 8);
+  size_t o_pgs = put(t.pod_gsel.data(), t.pod_gsel.size() * 8);
+  size_t o_pgi = put(t.pod_ginv.data(), t.pod_ginv.size() * 8);
+  size_t o_srs = put(t.st_rss.data(), t.st_rss.size() * 4);
+  size_t o_ntd = put(t.n_tdom.data(), t.n_tdom.size() * 4);
   HIPCHK(hipMalloc(&pb->dbuf, a.total));
   std::vector<char> staging(a.total, 0);
   for (auto& it : items)
@@ -213,6 +231,15 @@ void ks_upload(ks_problem* pb) {
   D.pod_hpc = (const uint64_t*)(b + o_phc);
   D.pod_hpu = (const uint64_t*)(b + o_phu);
   D.n_hp0 = (const uint64_t*)(b + o_nhp);
+  D.tg_meta = (const int32_t*)(b + o_tgm);
+  D.tg_cnt0 = (const int32_t*)(b + o_tgc);
+  D.tg_reg0 = (const uint32_t*)(b + o_tgr);
+  D.tg_frs = (const uint32_t*)(b + o_tgf);
+  D.st_gown = (const uint64_t*)(b + o_sgo);
+  D.pod_gsel = (const uint64_t*)(b + o_pgs);
+  D.pod_ginv = (const uint64_t*)(b + o_pgi);
+  D.st_rss = (const uint32_t*)(b + o_srs);
+  D.n_tdom = (const int32_t*)(b + o_ntd);
 }
 
 // Rebuild Results from the replica-0 workspace.
@@ -246,6 +273,21 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
   dl(fcode, W.fail_code, (size_t)d.P * std::max(d.NTPL, 1), st);
   dl(fhost, W.fail_host, (size_t)d.P * std::max(d.NTPL, 1), st);
   HIPCHK(hipStreamSynchronize(st));
+  std::vector<uint32_t> frs;  // topology failure snapshots, only when some pod failed on one
+  if (d.G) {
+    bool need = false;
+    for (int p = 0; p < d.P && !need; p++) {
+      if (status[p] != ST_FAILED) continue;
+      for (int t = 0; t < d.NTPL; t++) {
+        const uint32_t c = fcode[(size_t)p * d.NTPL + t] & 0xff;
+        need = need || c == FC_TOPO || c == FC_TOPO_COMPAT || (fcode[(size_t)p * d.NTPL + t] & FC_RS_SNAP);
+      }
+    }
+    if (need) {
+      dl(frs, W.fail_rs, (size_t)d.P * d.NTPL * d.FSW, st);
+      HIPCHK(hipStreamSynchronize(st));
+    }
+  }
 
   auto* res = new ks_results();
   res->counters = ctr;
@@ -354,9 +396,14 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
           break;
         }
         case FC_NO_IT: {
-          uint32_t f = code >> 8;
+          uint32_t f = (code >> 8) & 0x3f;
           std::vector<uint32_t> r(h.tab.tpl_rs.begin() + (size_t)t * d.RSW, h.tab.tpl_rs.begin() + (size_t)(t + 1) * d.RSW);
-          rs_add(h.L, r.data(), ps.rsAll.data());
+          if (code & FC_RS_SNAP) {
+            const uint32_t* snap = &frs[((size_t)p * d.NTPL + t) * d.FSW];
+            r.assign(snap, snap + d.RSW);
+          } else {
+            rs_add(h.L, r.data(), ps.rsAll.data());
+          }
           QList cum = tp.daemon;
           for (auto& kv : h.pods[p].requests) cum[kv.first].add(kv.second);
           bool rq = f & FF_REQ, fi = f & FF_FITS, of = f & FF_OFF;
@@ -377,6 +424,41 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
           else why = "no instance type met the requirements/resources/offering tuple";
           segs.push_back(pre + "no instance type satisfied resources " + qlist_json(cum) + " and requirements " +
                          h.reqsString(r.data(), host) + " (" + why + ")");
+          break;
+        }
+        case FC_TOPO: {  // Topology.AddRequirements (topology.go:160-165)
+          const int g = (int)(code >> 16) & 0xff;
+          const int32_t* gm = &h.tab.tg_meta[(size_t)g * TGM_WORDS];
+          const int k = gm[TGM_KEY], nv = gm[TGM_NV];
+          const uint32_t* fr = &frs[((size_t)p * d.NTPL + t) * d.FSW];
+          std::string counts = "map[";
+          if (!gm[TGM_HOST]) {  // registered domains in name order with their counts at the failure
+            bool first = true;
+            for (int v = 0; v < nv; v++)
+              if ((fr[nv + (v >> 5)] >> (v & 31)) & 1u) {
+                counts += (first ? "" : " ") + h.values[(size_t)k][(size_t)v] + ":" + std::to_string((int32_t)fr[v]);
+                first = false;
+              }
+          }
+          counts += "]";  // hostname groups: the per-placeholder counts are not snapshotted
+          std::vector<uint32_t> nr(h.tab.tpl_rs.begin() + (size_t)t * d.RSW, h.tab.tpl_rs.begin() + (size_t)(t + 1) * d.RSW);
+          rs_add(h.L, nr.data(), ps.rsAll.data());
+          auto dom = [&](const uint32_t* rec) {
+            return bit(rs_present(rec), k) ? h.reqString(rec, k, false, host) : h.keyNames[(size_t)k] + " Exists";
+          };
+          segs.push_back(pre + "unsatisfiable topology constraint for " +
+                         (gm[TGM_TYPE] == TG_SPREAD ? "topology spread" : "pod anti-affinity") + ", key=" +
+                         h.keyNames[(size_t)k] + " (counts = " + counts + ", podDomains = " + dom(ps.rsStrict.data()) +
+                         ", nodeDomains = " + dom(nr.data()) + ")");
+          break;
+        }
+        case FC_TOPO_COMPAT: {  // Compatible(nodeRequirements, topologyRequirements) (nodeclaim.go:96-98)
+          std::vector<uint32_t> nr(h.tab.tpl_rs.begin() + (size_t)t * d.RSW, h.tab.tpl_rs.begin() + (size_t)(t + 1) * d.RSW);
+          rs_add(h.L, nr.data(), ps.rsAll.data());
+          auto errs = h.compatErrors(nr.data(), &frs[((size_t)p * d.NTPL + t) * d.FSW], true, host);
+          std::string m;
+          for (size_t i = 0; i < errs.size(); i++) m += (i ? "; " : "") + errs[i];
+          segs.push_back(pre + m);
           break;
         }
         default:
@@ -437,7 +519,7 @@ int ks_problem_inspect(const char* json, size_t len, char** out) {
   auto kv = [&](const char* k, long long v) { o += std::string(o.size() > 1 ? "," : "") + "\"" + k + "\":" + std::to_string(v); };
   kv("R", d.R); kv("keys", d.NK); kv("W", d.W); kv("NB", d.NB); kv("RSW", d.RSW); kv("T", d.T); kv("templates", d.NTPL);
   kv("pools", d.NPOOL); kv("nodes", d.N); kv("pods", d.P); kv("states", d.S); kv("uids", d.NU); kv("TW", d.TW);
-  kv("Kcap", d.Kcap); kv("taints", (long long)h.taints.size());
+  kv("Kcap", d.Kcap); kv("taints", (long long)h.taints.size()); kv("G", d.G); kv("G1", d.G1);
   // LDS plans (ks_solve.hip make_plan) at the default and a few reduced budgets
   o += ",\"plans\":{";
   const size_t budgets[] = {160 * 1024 - 256, 6000, 9000, 14000, 24000, 40000};

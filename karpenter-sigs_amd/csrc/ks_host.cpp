@@ -216,6 +216,30 @@ static QList podRequests(const Value& pod, bool& hostPorts, bool& volumes) {
   return req;
 }
 
+static LabelSel jsel(const Value* v) {  // metav1.LabelSelector
+  LabelSel s;
+  if (!v || v->is_null()) return s;
+  s.present = true;
+  for (auto& kv : jmap(v->get("matchLabels"))) s.reqs.push_back({kv.first, "In", {kv.second}});
+  if (auto* es = v->get("matchExpressions"))
+    for (auto& e : es->arr()) {
+      SelReq r{jstr(&e, "key"), jstr(&e, "operator"), {}};
+      if (auto* vs = e.get("values")) for (auto& x : vs->arr()) r.values.push_back(x.str());
+      s.reqs.push_back(r);
+    }
+  return s;
+}
+
+static AffTerm jaffterm(const Value* t) {  // v1.PodAffinityTerm
+  AffTerm a;
+  if (!t) return a;
+  a.sel = jsel(t->get("labelSelector"));
+  if (auto* ns = t->get("namespaces")) for (auto& x : ns->arr()) a.namespaces.push_back(x.str());
+  if (auto* nss = t->get("namespaceSelector"); nss && !nss->is_null()) a.nsSelector = true;
+  a.key = jstr(t, "topologyKey");
+  return a;
+}
+
 PodH parse_pod(const Value& v) {
   PodH p;
   const Value* md = v.get("metadata");
@@ -240,6 +264,7 @@ PodH parse_pod(const Value& v) {
     const std::string ph = jstr(st, "phase");
     p.terminal = ph == "Failed" || ph == "Succeeded";
     nominated = jstr(st, "nominatedNodeName");
+    p.phase = ph;
     if (auto* cs = st->get("conditions"))
       for (auto& c : cs->arr())
         if (jstr(&c, "type") == "PodScheduled" && jstr(&c, "reason") == "Unschedulable") failedToSchedule = true;
@@ -247,6 +272,7 @@ PodH parse_pod(const Value& v) {
   const Value* sp = v.get("spec");
   if (sp) {
     nodeName = jstr(sp, "nodeName");
+    p.nodeName = nodeName;
     if (auto* x = sp->get("priority"); x && !x->is_null()) {
       p.hasPriority = true;
       p.priority = (int32_t)x->i64();
@@ -271,15 +297,26 @@ PodH parse_pod(const Value& v) {
         auto* pa = af->get(anti ? "podAntiAffinity" : "podAffinity");
         if (!pa || pa->is_null()) continue;
         (anti ? p.hasPodAnti : p.hasPodAffinity) = true;
+        if (auto* r = pa->get("requiredDuringSchedulingIgnoredDuringExecution"))
+          for (auto& t : r->arr()) (anti ? p.antiRequired : p.affRequired).push_back(jaffterm(&t));
         if (auto* r = pa->get("preferredDuringSchedulingIgnoredDuringExecution"))
           for (auto& t : r->arr())
-            (anti ? p.podAntiPrefW : p.podAffPrefW).push_back((int32_t)(t.get("weight") ? t.get("weight")->i64() : 0));
+            (anti ? p.antiPreferred : p.affPreferred)
+                .push_back({(int32_t)(t.get("weight") ? t.get("weight")->i64() : 0), jaffterm(t.get("podAffinityTerm"))});
       }
     }
     if (auto* ts = sp->get("tolerations"))
       for (auto& t : ts->arr()) p.tols.push_back(TolH{jstr(&t, "key"), jstr(&t, "operator"), jstr(&t, "value"), jstr(&t, "effect")});
     if (auto* ts = sp->get("topologySpreadConstraints"))
-      for (auto& t : ts->arr()) p.tscWhen.push_back(jstr(&t, "whenUnsatisfiable"));
+      for (auto& t : ts->arr()) {
+        SpreadC c;
+        c.key = jstr(&t, "topologyKey");
+        c.when = jstr(&t, "whenUnsatisfiable");
+        c.maxSkew = t.get("maxSkew") ? (int32_t)t.get("maxSkew")->i64() : 0;
+        if (auto* md = t.get("minDomains"); md && !md->is_null()) c.minDomains = (int32_t)md->i64();
+        c.sel = jsel(t.get("labelSelector"));
+        p.tsc.push_back(c);
+      }
   }
   p.requests = podRequests(v, p.hostPorts, p.volumes);
   if (sp)
@@ -415,13 +452,17 @@ std::string Host::placeholder(int64_t id) const {
 // ---------------------------------------------------------------------------------------------
 void Host::build(const Value& root) {
   if (auto* t = root.get("topology"); t && !t->is_null())
-    throw KsError(-2, "topology groups (spread / pod affinity) are not encoded by this build; "
-                      "pass an empty topology like BenchmarkScheduling does");
+    throw KsError(-2, "explicit topology groups are not accepted: pass the pods' topology spread / pod "
+                      "(anti-)affinity terms and the cluster's bound pods (clusterPods, clusterNodes)");
+  if (auto* cps = root.get("clusterPods")) for (auto& v : cps->arr()) clusterPods.push_back(parse_pod(v));
+  if (auto* cns = root.get("clusterNodes"))
+    for (auto& v : cns->arr()) nodeLabelsByName[jstr(&v, "name")] = jmap(v.get("labels"));
   if (auto* wk = root.get("wellKnownLabels")) for (auto& x : wk->arr()) wellKnown.insert(x.str());
   else
     wellKnown = {kNodePoolKey, kZone, "topology.kubernetes.io/region", "node.kubernetes.io/instance-type",
                  "kubernetes.io/arch", "kubernetes.io/os", kCT, "node.kubernetes.io/windows-build"};
   if (auto* hs = root.get("hostnameSeed")) hostnameSeed = hs->i64();
+  if (auto* et = root.get("emptyTopology")) emptyTopology = et->boolean();
 
   // --- instance types
   if (auto* v = root.get("instanceTypes"))
@@ -470,6 +511,7 @@ void Host::build(const Value& root) {
           t.taints = jtaints(ts->get("taints"));
         }
       }
+      t.poolLabels = t.labels;
       t.labels[kNodePoolKey] = t.pool;
       if (byPool && byPool->get(t.pool))
         for (auto& x : byPool->get(t.pool)->arr()) {
@@ -554,6 +596,28 @@ void Host::build(const Value& root) {
   for (auto& n : nodes) { visitLabels(n.labels); intern(kHostname, n.hostName); }
   for (auto& p : pods) visitPod(p);
   for (auto& p : daemons) visitPod(p);
+  // topology keys and the domains the cluster's nodes contribute (countDomains, updateInverseAffinities)
+  {
+    std::set<std::string> tkeys;
+    auto visitTopo = [&](const PodH& p) {
+      for (auto& c : p.tsc) tkeys.insert(c.key);
+      for (auto& t : p.antiRequired) tkeys.insert(t.key);
+      for (auto& t : p.antiPreferred) tkeys.insert(t.second.key);
+      for (auto& t : p.affRequired) tkeys.insert(t.key);
+      for (auto& t : p.affPreferred) tkeys.insert(t.second.key);
+    };
+    for (auto& p : pods) visitTopo(p);
+    for (auto& p : clusterPods) visitTopo(p);
+    for (auto& n : nodes) nodeLabelsByName[n.name] = n.labels;
+    for (auto& k : tkeys) {
+      internKey(k);  // topology keys are matched verbatim (not normalised) by the reference
+      for (auto& kv : nodeLabelsByName) {
+        auto l = kv.second.find(k);
+        if (l != kv.second.end()) intern(k, l->second);
+        else if (k == kHostname) intern(k, kv.first);
+      }
+    }
+  }
   for (auto& kv : valueSet_[kHostname])
     if (kv.rfind("hostname-placeholder-", 0) == 0)
       throw KsError(-2, "input names a hostname-placeholder value (reserved for new NodeClaims)");
@@ -916,19 +980,24 @@ void Host::build(const Value& root) {
       st.rsStrict = podRequirements(cur, false);
       st.hasPreferred = cur.hasAffinity && cur.hasNodeAffinity && !cur.preferred.empty();
       st.tols = cur.tols;
+      if (!cur.tsc.empty() || !cur.antiRequired.empty() || !cur.antiPreferred.empty() || !cur.affRequired.empty() ||
+          !cur.affPreferred.empty())
+        st.spec = std::make_shared<PodH>(cur);
       chain.push_back(std::move(st));
       // Preferences.Relax (preferences.go:38-58)
       bool relaxed = false;
       if (cur.hasAffinity && cur.hasNodeAffinity && cur.hasRequired && cur.requiredTerms.size() > 1) {
         cur.requiredTerms.erase(cur.requiredTerms.begin());
         relaxed = true;
-      } else if (cur.hasAffinity && cur.hasPodAffinity && !cur.podAffPrefW.empty()) {
-        std::stable_sort(cur.podAffPrefW.begin(), cur.podAffPrefW.end(), std::greater<int32_t>());
-        cur.podAffPrefW.erase(cur.podAffPrefW.begin());
+      } else if (cur.hasAffinity && cur.hasPodAffinity && !cur.affPreferred.empty()) {
+        std::stable_sort(cur.affPreferred.begin(), cur.affPreferred.end(),
+                         [](const std::pair<int32_t, AffTerm>& a, const std::pair<int32_t, AffTerm>& b) { return a.first > b.first; });
+        cur.affPreferred.erase(cur.affPreferred.begin());
         relaxed = true;
-      } else if (cur.hasAffinity && cur.hasPodAnti && !cur.podAntiPrefW.empty()) {
-        std::stable_sort(cur.podAntiPrefW.begin(), cur.podAntiPrefW.end(), std::greater<int32_t>());
-        cur.podAntiPrefW.erase(cur.podAntiPrefW.begin());
+      } else if (cur.hasAffinity && cur.hasPodAnti && !cur.antiPreferred.empty()) {
+        std::stable_sort(cur.antiPreferred.begin(), cur.antiPreferred.end(),
+                         [](const std::pair<int32_t, AffTerm>& a, const std::pair<int32_t, AffTerm>& b) { return a.first > b.first; });
+        cur.antiPreferred.erase(cur.antiPreferred.begin());
         relaxed = true;
       } else if (cur.hasAffinity && cur.hasNodeAffinity && !cur.preferred.empty()) {
         std::stable_sort(cur.preferred.begin(), cur.preferred.end(),
@@ -936,10 +1005,10 @@ void Host::build(const Value& root) {
         cur.preferred.erase(cur.preferred.begin());
         relaxed = true;
       } else {
-        for (size_t j = 0; j < cur.tscWhen.size(); j++)
-          if (cur.tscWhen[j] == "ScheduleAnyway") {
-            cur.tscWhen[j] = cur.tscWhen.back();
-            cur.tscWhen.pop_back();
+        for (size_t j = 0; j < cur.tsc.size(); j++)
+          if (cur.tsc[j].when == "ScheduleAnyway") {
+            cur.tsc[j] = cur.tsc.back();
+            cur.tsc.pop_back();
             relaxed = true;
             break;
           }
@@ -987,10 +1056,13 @@ void Host::build(const Value& root) {
                               " tie on (cpu, memory, creationTimestamp, uid); queue order would depend on sort.Slice tie order");
   }
   dims.S = std::max(S, 1);
+  buildTopology();
   tab.st_rs.assign((size_t)dims.S * dims.RSW, 0);
   tab.st_tol.assign((size_t)dims.S * 2, 0);
   tab.st_flags.assign(dims.S, 0);
   tab.st_toltpl.assign(dims.S, 0);
+  tab.st_gown.assign(dims.S, 0);
+  tab.st_rss.assign(groups.empty() ? 1 : (size_t)dims.S * dims.RSW, 0);
   int s = 0;
   for (auto& chain : states)
     for (auto& st : chain) {
@@ -1004,6 +1076,10 @@ void Host::build(const Value& root) {
       for (int t = 0; t < dims.NTPL; t++)
         if (((tab.tpl_taint[(size_t)t * 2] & ~m[0]) | (tab.tpl_taint[(size_t)t * 2 + 1] & ~m[1])) == 0) tt |= 1u << t;
       tab.st_toltpl[s] = tt;
+      if (!groups.empty()) {
+        tab.st_gown[s] = st.gown;
+        std::copy(st.rsStrict.begin(), st.rsStrict.end(), tab.st_rss.begin() + (size_t)s * dims.RSW);
+      }
       tab.st_flags[s] = (st.hasPreferred ? SF_HAS_PREFERRED : 0) | ((pres & itKeys) ? SF_TOUCHES_IT_KEYS : 0) |
                         (pres ? SF_HAS_KEYS : 0);
       s++;

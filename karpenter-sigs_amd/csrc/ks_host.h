@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <functional>
 #include <map>
+#include <memory>
 #include <set>
 #include <string>
 #include <vector>
@@ -25,6 +26,11 @@ struct NSR { std::string key, op; std::vector<std::string> values; };
 struct TaintH { std::string key, value, effect; };
 struct TolH { std::string key, op, value, effect; };
 struct PrefTerm { int32_t weight; std::vector<NSR> exprs; };
+// metav1.LabelSelector: matchLabels (as In with one value) then matchExpressions; nil = !present
+struct SelReq { std::string key, op; std::vector<std::string> values; };
+struct LabelSel { bool present = false; std::vector<SelReq> reqs; };
+struct AffTerm { LabelSel sel; std::vector<std::string> namespaces; bool nsSelector = false; std::string key; };
+struct SpreadC { std::string key, when; int32_t maxSkew = 0; int32_t minDomains = -1; LabelSel sel; };
 // HostPort (hostportusage.go:38-43): IP (net.ParseIP, 16-byte form), port, protocol
 struct HostPortH {
   std::string ip, proto;
@@ -46,8 +52,10 @@ struct PodH {
   std::vector<std::vector<NSR>> requiredTerms;
   std::vector<PrefTerm> preferred;
   bool hasPodAffinity = false, hasPodAnti = false;
-  std::vector<int32_t> podAffPrefW, podAntiPrefW;
-  std::vector<std::string> tscWhen;
+  std::vector<AffTerm> affRequired, antiRequired;
+  std::vector<std::pair<int32_t, AffTerm>> affPreferred, antiPreferred;
+  std::vector<SpreadC> tsc;  // topologySpreadConstraints
+  std::string nodeName, phase;  // cluster pods (topology counting)
   std::vector<TolH> tols;
   QList requests;  // RequestsForPods(pod) incl. pods=1
   bool hostPorts = false, volumes = false;
@@ -65,6 +73,22 @@ struct PodState {  // one point of the relaxation chain
   std::vector<uint32_t> rsAll, rsStrict;
   bool hasPreferred = false;
   std::vector<TolH> tols;
+  uint64_t gown = 0;  // topology groups the pod owns in this state (Topology.Update, topology.go:91-122)
+  std::shared_ptr<PodH> spec;  // the (relaxed) pod spec of this state, kept for topology pods only
+};
+
+// One topology group (topologygroup.go:56-68) as the device sees it.  Groups [0, G1) are
+// t.topologies (creation order), [G1, G) t.inverseTopologies.
+struct TopoGroup {
+  int type = 0;  // TG_SPREAD / TG_ANTI
+  std::string key, hash;
+  int keyId = -1;
+  int32_t maxSkew = 0, minDomains = -1;
+  std::set<std::string> namespaces;
+  LabelSel sel;
+  bool filterNil = true;
+  std::vector<std::vector<uint32_t>> filter;  // OR of requirement records (TopologyNodeFilter)
+  std::map<std::string, int32_t> domains;    // registered domain -> count (initial state)
 };
 
 struct Host {
@@ -97,6 +121,7 @@ struct Host {
     std::string pool;
     std::vector<NSR> reqs;
     std::map<std::string, std::string> labels;
+    std::map<std::string, std::string> poolLabels;  // spec.template.metadata.labels (no karpenter.sh/nodepool)
     std::vector<TaintH> taints;
     std::vector<int> its;
     QList daemon;
@@ -115,7 +140,14 @@ struct Host {
   std::vector<PodH> daemons;
   std::vector<PodH> pods;
   std::vector<std::vector<PodState>> states;  // per pod relaxation chain
+  // topology (topology.go): groups, the cluster's bound pods and node labels it counts
+  std::vector<TopoGroup> groups;
+  int groupsOwned = 0;  // G1
+  std::vector<PodH> clusterPods;
+  std::map<std::string, std::map<std::string, std::string>> nodeLabelsByName;
+  std::vector<uint64_t> podGsel, podGinv;  // per pod: groups that select it / inverse groups it owns
   int64_t hostnameSeed = 0;
+  bool emptyTopology = false;  // the benchmark's &scheduling.Topology{}: no groups (scheduling_benchmark_test.go:124)
   KsDims dims{};
 
   // host images of the device tables
@@ -124,6 +156,14 @@ struct Host {
     std::vector<double> off_price;
     std::vector<int32_t> n_flags, pod_flags;
     std::vector<uint64_t> pod_hpc, pod_hpu, n_hp0;
+    // topology groups (ks_topo.cpp)
+    std::vector<int32_t> tg_meta;   // [G][TGM_WORDS]
+    std::vector<int32_t> tg_cnt0;   // counts per (group, value) at NewScheduler time
+    std::vector<uint32_t> tg_reg0;  // registered-domain bitsets per group
+    std::vector<uint32_t> tg_frs;   // node-filter requirement records
+    std::vector<uint64_t> st_gown, pod_gsel, pod_ginv;
+    std::vector<uint32_t> st_rss;   // [S][RSW] strict pod requirements (NewStrictPodRequirements)
+    std::vector<int32_t> n_tdom;    // [N][G] value index of the node's label for the group's key (-1: none)
     std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask, st_toltpl;
     std::vector<uint64_t> tpl_taint, st_tol, n_taint;
     std::vector<int32_t> tsort_pos, it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,
@@ -131,6 +171,7 @@ struct Host {
   } tab;
 
   void build(const ksjson::Value& root);
+  void buildTopology();  // ks_topo.cpp: after the pods' relaxation chains
 
   // encoded algebra helpers
   std::vector<uint32_t> emptyRec() const { return std::vector<uint32_t>(dims.RSW, 0); }

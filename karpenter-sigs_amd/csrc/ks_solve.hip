@@ -91,6 +91,11 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
     for (int64_t i = gtid; i < (int64_t)d.N * d.R; i += gsz) W.n_req[i] = D.n_req0[i];
     for (int64_t i = gtid; i < (int64_t)d.N * d.RSW; i += gsz) W.n_rs[i] = D.n_rs0[i];
     for (int64_t i = gtid; i < d.N; i += gsz) W.n_hp[i] = D.n_hp0[i];
+    if (d.G) {
+      for (int64_t i = gtid; i < d.tgCntWords; i += gsz) W.tg_cnt[i] = D.tg_cnt0[i];
+      for (int64_t i = gtid; i < d.tgRegWords; i += gsz) W.tg_reg[i] = D.tg_reg0[i];
+      for (int64_t i = gtid; i < (int64_t)d.G * (d.Kcap + 1); i += gsz) W.tg_ccnt[i] = 0;
+    }
     for (int64_t i = gtid; i < d.P; i += gsz) {
       W.queue[i] = qorder[i];
       W.pod_state[i] = D.pod_state0[i];
@@ -151,6 +156,14 @@ struct Solver {
   LU32 s_rmv;           // SIM: [ceil(N/32)] nodes removed by the simulation (the candidates)
   LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose requests live in a W.n_req slot
   LU32 s_tchr;          // SIM: [ceil(N/32)] nodes whose requirements live in a W.n_rs slot
+  LI32 s_tgm;           // [G][TGM_WORDS] topology group metadata
+  LI32 s_tmin;          // [G] domainMinCount of the popped pod, per spread group
+  LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
+  LU32 s_trs1;          // [RSW] one group's domains as a single-key record
+  uint64_t t_mask = 0;  // groups matching the popped pod (owned in its state | inverse groups selecting it)
+  uint64_t t_sel = 0;   // groups whose selector selects the popped pod
+  uint64_t t_inv = 0;   // inverse groups the popped pod owns
+  int t_s = 0;          // the popped pod's relaxation state
   int64_t algbytes = 0;
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
 
@@ -288,6 +301,10 @@ struct Solver {
       if (ok0) ok0 = rs_compatible(L, node_rs(c0), D.st_rs + (int64_t)s * d.RSW, 0);
       if (ok1) ok1 = rs_compatible(L, node_rs(c1), D.st_rs + (int64_t)s * d.RSW, 0);
     }
+    if (t_mask) {  // topology (existingnode.go:106-114)
+      if (ok0) ok0 = topo_node_ok(c0);
+      if (ok1) ok1 = topo_node_ok(c1);
+    }
   }
   __device__ __forceinline__ const uint32_t KS_G* node_rs(int n) const {
     if (!SIM) return W.n_rs + (int64_t)n * d.RSW;
@@ -342,6 +359,180 @@ struct Solver {
     wsync();
   }
 
+  // --- Topology (topology.go, topologygroup.go) ------------------------------------------------
+  // Counts and registered bits are written by one lane and read by others: loads bypass the L1.
+  __device__ __forceinline__ int tg(int g, int f) const { return s_tgm[g * TGM_WORDS + f]; }
+  __device__ __forceinline__ bool treg(int g, int v) const {
+    return (ld_sc1(W.tg_reg + tg(g, TGM_REG) + (v >> 5)) >> (v & 31)) & 1u;
+  }
+  __device__ __forceinline__ int tcnt(int g, int v) const { return ld_sc1(W.tg_cnt + tg(g, TGM_CNT) + v); }
+  __device__ __forceinline__ int tccnt(int g, int claim) const { return ld_sc1(W.tg_ccnt + (int64_t)g * (d.Kcap + 1) + claim); }  // claim <= Kcap (a fresh claim at the cap)
+  __device__ __forceinline__ bool tpod_has(int g, int v) const {  // podDomains.Has (strict pod requirements)
+    return rs_member(L, D.st_rss + (int64_t)t_s * d.RSW, tg(g, TGM_KEY), v);
+  }
+  // Per pop: the matching groups (getMatchingTopologies, topology.go:366-379: owned groups, then
+  // inverse groups whose selector selects the pod) and domainMinCount per spread group (:192-213).
+  __device__ __forceinline__ void topo_pop(int s, int gpod) {
+    t_s = s;
+    t_sel = D.pod_gsel[gpod];
+    t_inv = D.pod_ginv[gpod];
+    const uint64_t all = d.G >= 64 ? ~0ull : ((1ull << d.G) - 1);
+    const uint64_t owned = d.G1 >= 64 ? ~0ull : ((1ull << d.G1) - 1);
+    t_mask = D.st_gown[s] | (t_sel & all & ~owned);
+    for (uint64_t m = t_mask; m; m &= m - 1) {
+      const int g = ctz64(m);
+      if (tg(g, TGM_TYPE) != TG_SPREAD) continue;
+      int mn = 0x7fffffff, num = 0;
+      if (!tg(g, TGM_HOST)) {  // hostname groups always have a min of 0
+        const int nv = tg(g, TGM_NV);
+        for (int v = lane(); v < nv; v += kWave)
+          if (treg(g, v) && tpod_has(g, v)) {
+            num++;
+            const int c = tcnt(g, v);
+            mn = c < mn ? c : mn;
+          }
+        for (int off = 32; off >= 1; off >>= 1) {
+          const int o = __shfl_xor(mn, off);
+          mn = o < mn ? o : mn;
+          num += __shfl_xor(num, off);
+        }
+        if (tg(g, TGM_MIND) >= 0 && num < tg(g, TGM_MIND)) mn = 0;
+      } else {
+        mn = 0;
+      }
+      if (lane() == 0) s_tmin[g] = mn;
+    }
+    wsync();
+  }
+  // ExistingNode.Add's topology step for node n (one lane): the node's single domain of each
+  // matching group must be the one TopologyGroup.Get returns (existingnode.go:106-114).
+  __device__ __forceinline__ bool topo_node_ok(int n) const {
+    for (uint64_t m = t_mask; m; m &= m - 1) {
+      const int g = ctz64(m);
+      const int v = D.n_tdom[(int64_t)n * d.G + g];
+      if (v < 0 || !treg(g, v)) return false;
+      const int c = tcnt(g, v);
+      if (tg(g, TGM_TYPE) == TG_SPREAD) {
+        const int self = (int)((t_sel >> g) & 1ull);
+        if ((int64_t)c + self - s_tmin[g] > tg(g, TGM_SKEW)) return false;
+      } else if (c != 0 || !tpod_has(g, v)) {
+        return false;
+      }
+    }
+    return true;
+  }
+  // Topology.AddRequirements + Compatible on a NodeClaim's candidate record `rs` (LDS), wave-wide.
+  // Returns 0, FC_TOPO | group << 16, or FC_TOPO_COMPAT; on success rs holds the final requirements.
+  __device__ __forceinline__ uint32_t topo_apply(LU32 rs, int claim) {
+    copy_words(s_trs0, rs, d.RSW);
+    wsync();
+    for (uint64_t m = t_mask; m; m &= m - 1) {
+      const int g = ctz64(m);
+      const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
+      const bool host = tg(g, TGM_HOST) != 0;
+      const KeyMeta km = L.keys[k];
+      const int nslot = nv + (host ? 1 : 0);  // + the claim's own hostname-placeholder (private bit)
+      for (int i = lane(); i < d.RSW; i += kWave) s_trs1[i] = 0;
+      wsync();
+      if (tg(g, TGM_TYPE) == TG_SPREAD) {  // nextDomainTopologySpread: smallest count, then smallest name
+        const int self = (int)((t_sel >> g) & 1ull), mn = s_tmin[g], skew = tg(g, TGM_SKEW);
+        uint64_t best = ~0ull;
+        for (int v = lane(); v < nslot; v += kWave) {
+          const bool nodeHas = rs_member(L, s_trs0, k, v);
+          bool cand = nodeHas && (v >= nv || treg(g, v));
+          int c = 0;
+          if (cand) c = (v < nv ? tcnt(g, v) : tccnt(g, claim)) + self;
+          if (cand && (int64_t)c - mn <= skew) {
+            const uint64_t key = ((uint64_t)(uint32_t)c << 32) | (uint32_t)v;
+            best = key < best ? key : best;
+          }
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+          const uint64_t o = __shfl_xor(best, off);
+          best = o < best ? o : best;
+        }
+        if (best == ~0ull) return FC_TOPO | ((uint32_t)g << 16);
+        const int bv = (int)(uint32_t)best;
+        if (lane() == 0) s_trs1[L.HDR + km.off + (bv >> 5)] = 1u << (bv & 31);
+      } else {  // nextDomainAntiAffinity: registered zero-count domains the pod's domains allow
+        bool any = false;
+        for (int v = lane(); v < nslot; v += kWave) {
+          bool in;
+          if (v < nv) {
+            in = treg(g, v) && tcnt(g, v) == 0 && tpod_has(g, v);
+          } else {
+            const bool has = tpod_has(g, v);
+            any = any || has;  // some registered placeholder has a zero count (the fresh claim's, at least)
+            in = has && tccnt(g, claim) == 0;
+          }
+          if (in) {
+            __hip_atomic_fetch_or(s_trs1 + L.HDR + km.off + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+            any = true;
+          }
+        }
+        if (wballot(any) == 0) return FC_TOPO | ((uint32_t)g << 16);
+      }
+      wsync();
+      if (lane() == 0) {  // requirements.Add(domains)
+        wr64(s_trs1, 0, 1ull << k);
+        rs_add(L, rs, s_trs1);
+      }
+      wsync();
+    }
+    // Compatible(nodeRequirements, topologyRequirements, AllowUndefinedWellKnownLabels)
+    int ok = 1;
+    if (lane() == 0) ok = rs_compatible(L, s_trs0, rs, d.allowWK) ? 1 : 0;
+    ok = rdl(ok, 0);
+    return ok ? 0u : (uint32_t)FC_TOPO_COMPAT;
+  }
+  // Topology.Record (topology.go:125-148) for the pod's final requirements F on NodeClaim `claim`
+  // (-1: an existing node), wave-wide.
+  template <class PR>
+  __device__ __forceinline__ void topo_record(PR F, int claim, uint64_t allow) {
+    hbm_release();
+    const uint64_t pres = rs_present(F), compl_ = rs_compl(F);
+    for (int g = 0; g < d.G; g++) {
+      const bool ownedGroup = g < d.G1;
+      if (ownedGroup) {
+        if (!((t_sel >> g) & 1ull)) continue;  // Counts: selects(pod) ...
+        if (tg(g, TGM_TYPE) == TG_SPREAD && tg(g, TGM_FEND) > tg(g, TGM_FBEG)) {  // ... && nodeFilter matches
+          int match = 0;
+          if (lane() == 0)
+            for (int f = tg(g, TGM_FBEG); f < tg(g, TGM_FEND) && !match; f++)
+              match = rs_compatible(L, F, D.tg_frs + (int64_t)f * d.RSW, allow) ? 1 : 0;
+          if (!rdl(match, 0)) continue;
+        }
+      } else if (!((t_inv >> g) & 1ull)) {
+        continue;  // inverse groups record where their owner lands
+      }
+      const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
+      if (!bit(pres, k)) continue;  // Get() of a missing key is Exists: no values
+      const KeyMeta km = L.keys[k];
+      if (ownedGroup && tg(g, TGM_TYPE) == TG_SPREAD) {  // spread / affinity: only a collapsed domain
+        int tot = 0;
+        for (int w = lane(); w < km.nw; w += kWave) tot += __popc(F[L.HDR + km.off + w]);
+        for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off);
+        if (bit(compl_, k) || tot != 1) continue;
+      }
+      for (int w = lane(); w < km.nw; w += kWave) {  // anti-affinity: every domain of the requirement
+        uint32_t x = F[L.HDR + km.off + w];
+        while (x) {
+          const int v = w * 32 + __builtin_ctz(x);
+          x &= x - 1;
+          if (v >= nv) {
+            if (claim >= 0) W.tg_ccnt[(int64_t)g * (d.Kcap + 1) + claim] += 1;
+          } else {
+            W.tg_cnt[tg(g, TGM_CNT) + v] += 1;
+            W.tg_reg[tg(g, TGM_REG) + (v >> 5)] |= 1u << (v & 31);
+          }
+        }
+      }
+    }
+    hbm_release();
+    wsync();
+  }
+
   // --- NodeClaim quick reject at sorted position j: necessary conditions of NodeClaim.Add ------
   __device__ __forceinline__ bool claim_quick(int j, int s, int sflags, uint32_t toltpl, const int64_t* pod) const {
     if (!((toltpl >> s_ptpl[j]) & 1u)) return false;  // Taints.Tolerates (nodeclaim.go:68-71)
@@ -364,13 +555,18 @@ struct Solver {
                                              int& ncnt) {
     const ClaimView<INL>& v = cv<INL>();
     bool changed = false;
-    if (sflags & SF_HAS_KEYS) {
+    if ((sflags & SF_HAS_KEYS) || t_mask) {
       const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
       copy_words(s_rs, crs, d.RSW);
       wsync();
-      if (lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
+      if ((sflags & SF_HAS_KEYS) && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
       wsync();
-      changed = (sflags & SF_TOUCHES_IT_KEYS) && !rs_equal_keys(L, s_rs, crs, d.itKeys);
+      if (t_mask && topo_apply(s_rs, c) != 0) {  // topology requirements (nodeclaim.go:92-100)
+        ncnt = 0;
+        return false;
+      }
+      changed = (((sflags & SF_HAS_KEYS) && (sflags & SF_TOUCHES_IT_KEYS)) || t_mask) &&
+                !rs_equal_keys(L, s_rs, crs, d.itKeys);
       algbytes += 8 * d.RSW;
     }
     const int t = uni(v.tpl[c]);
@@ -485,13 +681,17 @@ struct Solver {
       s_okey[pos] = okNew;
       if (d.hpAny) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
     }
-    if (sflags & SF_HAS_KEYS) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
+    if ((sflags & SF_HAS_KEYS) || t_mask) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
     copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     log_commit(p, c, nlog);
     // The max bound stays valid as the options only shrink; it is tightened lazily when a full check
     // fails.  HBM-resident claim state is re-read by other lanes: drain the stores first.
     if ((sflags & SF_HAS_KEYS) || !INL || d.hpAny) hbm_release();
     wsync();
+    if (d.G && (t_sel | t_inv)) {  // Topology.Record on the claim's final requirements (nodeclaim.go:121)
+      if ((sflags & SF_HAS_KEYS) || t_mask) topo_record(s_rs, c, d.allowWK);
+      else topo_record(W.c_rs + (int64_t)c * d.RSW, c, d.allowWK);
+    }
     algbytes += 24 * R() + 4 * d.TW + 8;
     return srt;
   }
@@ -537,8 +737,25 @@ struct Solver {
             if (ok && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
             wsync();
           }
+          if (ok && t_mask) {  // topology requirements of the fresh NodeClaim (nodeclaim.go:92-100)
+            const uint32_t tc = topo_apply(s_rs, nclaims);
+            if (tc) {
+              ok = false;
+              code = tc;
+              const int64_t slot = ((int64_t)p * d.NTPL + t) * d.FSW;
+              if (tc == FC_TOPO_COMPAT) {
+                copy_words(W.fail_rs + slot, s_rs, d.RSW);  // the topology requirements, for the message
+              } else {
+                const int g = (int)(tc >> 16) & 0xff, nv = tg(g, TGM_NV), rw = (nv + 31) >> 5;
+                if (!tg(g, TGM_HOST)) {  // counts + registered domains, for the message (FSW fits them)
+                  for (int v = lane(); v < nv; v += kWave) W.fail_rs[slot + v] = (uint32_t)tcnt(g, v);
+                  for (int i = lane(); i < rw; i += kWave) W.fail_rs[slot + nv + i] = ld_sc1(W.tg_reg + tg(g, TGM_REG) + i);
+                }
+              }
+            }
+          }
           if (!ok) {
-            code = FC_COMPAT;
+            if (code == FC_NONE) code = FC_COMPAT;
           } else {
             int64_t req[RM];
             for (int r = 0; r < R(); r++) req[r] = D.tpl_daemon[(int64_t)t * R() + r] + pod[r];
@@ -568,6 +785,10 @@ struct Solver {
             wsync();
             if (any == 0) {
               code = FC_NO_IT | (flags << 8);
+              if (t_mask) {  // the message prints the requirements the topology narrowed
+                copy_words(W.fail_rs + ((int64_t)p * d.NTPL + t) * d.FSW, s_rs, d.RSW);
+                code |= FC_RS_SNAP;
+              }
             } else {
               if (nclaims >= pl.KO) return -1;
               const int c = nclaims++;
@@ -612,6 +833,7 @@ struct Solver {
               log_commit(p, c, nlog);
               hbm_release();  // c_rs / c_tpl / overflow state are read by other lanes later
               wsync();
+              if (d.G && (t_sel | t_inv)) topo_record(s_rs, c, d.allowWK);
               if (inl) recompute_max<true>(c, s_rem, t, c);
               else recompute_max<false>(c, s_rem, t, c);
               if (pool >= 0) {  // subtractMax (scheduler.go:347-362)
@@ -854,6 +1076,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   S.s_rmv = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tch = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tchr = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
+  S.s_tgm = (LI32)take(4 * (size_t)d.G * TGM_WORDS);
+  S.s_tmin = (LI32)take(4 * (size_t)d.G);
+  S.s_trs0 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
+  S.s_trs1 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
+  for (int i = lane(); i < d.G * TGM_WORDS; i += kWave) S.s_tgm[i] = D.tg_meta[i];
   S.gc.tpl = W.c_tpl;
   S.gc.req = W.c_req;
   S.gc.max = W.c_max;
@@ -985,6 +1212,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       S.cur_hpc = (uint64_t)rdl64((int64_t)w.hpc, wi);
       S.cur_hpu = (uint64_t)rdl64((int64_t)w.hpu, wi);
     }
+    if (d.G) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= R) break;
@@ -1010,6 +1238,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
           ok &= (whp[k] & S.cur_hpc) == 0;
           if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), D.st_rs + (int64_t)s * d.RSW, 0);
+          if (S.t_mask && ok) ok = S.topo_node_ok(n);
           const uint64_t m = wballot(ok);
           if (m) {
             kj = k;
@@ -1038,6 +1267,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           } else if ((sflags & SF_HAS_KEYS) && lane() == owner) {
             rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
           }
+          if (!SIM && d.G && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, 0);  // existingnode.go:121
           S.log_commit(p, -(j + 1), nlog);
           PH_END(t7, 7);
           S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
@@ -1068,6 +1298,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         } else if (lane() == (j & (kWave - 1))) {
           S.node_commit(j, s, sflags, pod);  // the owner lane of node j
         }
+        if (!SIM && d.G && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, 0);  // existingnode.go:121
         S.log_commit(p, -(j + 1), nlog);
         PH_END(t7, 7);
         placed = true;
@@ -1192,7 +1423,8 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
                        r16(4 * (size_t)d.RSW) + 2 * r16(4 * TW + 8) + 16 * 16 +
-                       (sim ? 3 * r16(4 * (size_t)((d.N + 31) / 32)) : 0);
+                       (sim ? 3 * r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
+                       (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)
   const size_t clmB = 16 + 16 * R + 4 * TW + 4 * R;      // tpl, cnt, req, max, rem, thr (+ rounding)
   const size_t slack = 10 * 16;                          // per-array 16-byte rounding

@@ -1,0 +1,371 @@
+// ks_topo.cpp — host half of the Topology (pkg/controllers/provisioning/scheduling/topology.go):
+// the NewTopology construction the reference runs inside Provisioner.NewScheduler, encoded for the
+// device.
+//
+//   domain universe     provisioner.go:229-283 (pool requirements + labels + instance types)
+//   inverse groups      updateInverseAffinities / updateInverseAntiAffinity (topology.go:190-232)
+//   owned groups        Update -> newForTopologies / newForAffinities, deduplicated by Hash
+//                       (topology.go:91-122,293-337, topologygroup.go:70-91,142-158)
+//   initial counts      countDomains over the cluster's bound pods (topology.go:238-291)
+//   registration        NewExistingNode registers every node's hostname (existingnode.go:60)
+//
+// Device view: groups [0, G1) are t.topologies in creation order, [G1, G) t.inverseTopologies; the
+// kernels iterate them in that order.  Every relaxation state of a pod must own a subset of the
+// groups the initial Update pass created: a group created later (a relaxed required node-affinity
+// term changes a spread group's node filter) would start counting mid-Solve, which is refused.
+// Pod (positive) affinity and namespaceSelector terms are refused (KS_ERR_UNSUPPORTED).
+#include <algorithm>
+#include <climits>
+
+#include "ks_host.h"
+
+namespace ks {
+
+namespace {
+
+const char* kHostnameKey = "kubernetes.io/hostname";
+
+bool sel_req_matches(const SelReq& r, const std::map<std::string, std::string>& labels) {
+  auto it = labels.find(r.key);
+  const bool has = it != labels.end();
+  if (r.op == "In") return has && std::find(r.values.begin(), r.values.end(), it->second) != r.values.end();
+  if (r.op == "NotIn") return !has || std::find(r.values.begin(), r.values.end(), it->second) == r.values.end();
+  if (r.op == "Exists") return has;
+  if (r.op == "DoesNotExist") return !has;
+  return false;
+}
+bool sel_valid(const LabelSel& s) {  // LabelSelectorAsSelector: an invalid requirement -> error
+  for (auto& r : s.reqs) {
+    if ((r.op == "In" || r.op == "NotIn") && r.values.empty()) return false;
+    if ((r.op == "Exists" || r.op == "DoesNotExist") && !r.values.empty()) return false;
+    if (r.op != "In" && r.op != "NotIn" && r.op != "Exists" && r.op != "DoesNotExist") return false;
+  }
+  return true;
+}
+// TopologyGroup.selects (topologygroup.go:259-265): nil or invalid selector -> labels.Nothing()
+bool sel_selects(const LabelSel& s, const std::map<std::string, std::string>& labels) {
+  if (!s.present || !sel_valid(s)) return false;
+  for (auto& r : s.reqs) if (!sel_req_matches(r, labels)) return false;
+  return true;
+}
+// TopologyListOptions (topology.go:381-401): nil -> labels.Everything()
+bool sel_lists(const LabelSel& s, const std::map<std::string, std::string>& labels) {
+  if (!s.present) return true;
+  if (!sel_valid(s)) return false;
+  for (auto& r : s.reqs) if (!sel_req_matches(r, labels)) return false;
+  return true;
+}
+std::string sel_key(const LabelSel& s) {  // Hash identity (hashstructure with SlicesAsSets)
+  if (!s.present) return "nil";
+  std::vector<std::string> parts;
+  for (auto& r : s.reqs) {
+    std::vector<std::string> v = r.values;
+    std::sort(v.begin(), v.end());
+    std::string x = r.key + "|" + r.op + "|";
+    for (auto& y : v) x += y + ",";
+    parts.push_back(x);
+  }
+  std::sort(parts.begin(), parts.end());
+  std::string o;
+  for (auto& p : parts) o += p + ";";
+  return o;
+}
+
+}  // namespace
+
+void Host::buildTopology() {
+  bool any = false;
+  for (auto& chain : states)
+    for (auto& st : chain) any = any || st.spec != nullptr;
+  for (auto& cp : clusterPods) any = any || !cp.antiRequired.empty();
+  if (emptyTopology) any = false;  // AddRequirements / Record see no groups; pod affinity terms are inert
+  const int P = (int)pods.size(), N = (int)nodes.size(), S = dims.S;
+  tab.pod_gsel.assign(std::max(P, 1), 0);
+  tab.pod_ginv.assign(std::max(P, 1), 0);
+  if (!any) {
+    dims.G = dims.G1 = 0;
+    dims.tgCntWords = dims.tgRegWords = 1;
+    dims.FSW = dims.RSW;
+    tab.tg_meta.assign(TGM_WORDS, 0);
+    tab.tg_cnt0.assign(1, 0);
+    tab.tg_reg0.assign(1, 0);
+    tab.tg_frs.assign(dims.RSW, 0);
+    tab.n_tdom.assign(1, -1);
+    return;
+  }
+  for (auto& p : pods) {
+    if (!p.affRequired.empty() || !p.affPreferred.empty())
+      throw KsError(-2, "pod " + p.ns + "/" + p.name + " has pod affinity terms (not encoded by this build)");
+    for (auto& t : p.antiRequired)
+      if (t.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
+    for (auto& t : p.antiPreferred)
+      if (t.second.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
+  }
+  for (auto& p : clusterPods)
+    for (auto& t : p.antiRequired)
+      if (t.nsSelector) throw KsError(-2, "cluster pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
+
+  // --- domain universe (provisioner.go:229-283)
+  std::map<std::string, std::set<std::string>> dom;
+  auto valuesOf = [&](const std::vector<uint32_t>& rec, int k) {  // Requirement.Values(): the raw set
+    std::vector<std::string> out;
+    const KeyMeta& km = keys[(size_t)k];
+    for (int b = 0; b < (int)values[(size_t)k].size(); b++)
+      if ((rec[(size_t)(L.HDR + km.off + (b >> 5))] >> (b & 31)) & 1u) out.push_back(values[(size_t)k][(size_t)b]);
+    return out;
+  };
+  for (auto& t : tpls) {
+    if (t.its.empty()) continue;
+    std::vector<uint32_t> base = emptyRec();
+    for (auto& n : t.reqs) addNSR(base, n.key, n.op, n.values);
+    addLabels(base, t.poolLabels);
+    for (int i : t.its) {
+      std::vector<uint32_t> r = base;
+      rs_add(L, r.data(), &tab.it_rs[(size_t)i * dims.RSW]);
+      const uint64_t pr = rs_present(r.data());
+      for (int k = 0; k < dims.NK; k++)
+        if (bit(pr, k)) for (auto& v : valuesOf(r, k)) dom[keyNames[(size_t)k]].insert(v);
+    }
+    const uint64_t pr = rs_present(base.data());
+    for (int k = 0; k < dims.NK; k++)
+      if (bit(pr, k) && rs_op(L, base.data(), k) == OP_IN) for (auto& v : valuesOf(base, k)) dom[keyNames[(size_t)k]].insert(v);
+  }
+
+  // --- groups
+  std::set<std::string> excluded;
+  for (auto& p : pods) excluded.insert(p.uid);
+  std::vector<TopoGroup> own, inv;
+  std::map<std::string, int> ownByHash, invByHash;
+  auto nodeRec = [&](const std::map<std::string, std::string>& labels) {
+    std::vector<uint32_t> r = emptyRec();
+    addLabels(r, labels);
+    return r;
+  };
+  auto filterMatches = [&](const TopoGroup& g, const std::vector<uint32_t>& rec, uint64_t allow) {
+    if (g.filterNil || g.filter.empty()) return true;
+    for (auto& f : g.filter)
+      if (rs_compatible(L, rec.data(), f.data(), allow)) return true;
+    return false;
+  };
+  auto makeGroup = [&](int type, const std::string& key, const PodH& p, const std::set<std::string>& ns,
+                       const LabelSel& sel, int32_t maxSkew, int32_t minDomains) {
+    TopoGroup g;  // NewTopologyGroup (topologygroup.go:70-91)
+    g.type = type;
+    g.key = key;
+    g.keyId = keyId.at(key);
+    g.namespaces = ns;
+    g.sel = sel;
+    g.maxSkew = maxSkew;
+    g.minDomains = minDomains;
+    auto d = dom.find(key);
+    if (d != dom.end()) for (auto& v : d->second) g.domains[v] = 0;
+    g.filterNil = type != TG_SPREAD;
+    if (type == TG_SPREAD) {  // MakeTopologyNodeFilter (topologynodefilter.go:33-51)
+      std::vector<uint32_t> sel0 = emptyRec();
+      addLabels(sel0, p.nodeSelector);
+      if (p.hasAffinity && p.hasNodeAffinity && p.hasRequired) {
+        for (auto& term : p.requiredTerms) {
+          std::vector<uint32_t> r = sel0;
+          for (auto& n : term) addNSR(r, n.key, n.op, n.values);
+          g.filter.push_back(r);
+        }
+      } else {
+        g.filter.push_back(sel0);
+      }
+    }
+    g.hash = key + "#" + std::to_string(type) + "#";
+    for (auto& n : ns) g.hash += n + ",";
+    g.hash += "#" + sel_key(sel) + "#" + std::to_string(maxSkew) + "#";
+    if (g.filterNil) g.hash += "nil";
+    for (auto& f : g.filter) {
+      for (uint32_t w : f) g.hash += std::to_string(w) + ".";
+      g.hash += "|";
+    }
+    return g;
+  };
+  auto termNs = [](const PodH& p, const AffTerm& t) {  // buildNamespaceList (topology.go:341-362)
+    return t.namespaces.empty() ? std::set<std::string>{p.ns} : std::set<std::string>(t.namespaces.begin(), t.namespaces.end());
+  };
+  auto countDomains = [&](TopoGroup& g) {  // topology.go:238-291
+    for (auto& cp : clusterPods) {
+      if (!g.namespaces.count(cp.ns) || !sel_lists(g.sel, cp.labels)) continue;
+      if (cp.nodeName.empty() || cp.phase == "Failed" || cp.phase == "Succeeded" || cp.deleting) continue;
+      if (excluded.count(cp.uid)) continue;
+      auto n = nodeLabelsByName.find(cp.nodeName);
+      if (n == nodeLabelsByName.end()) continue;
+      auto l = n->second.find(g.key);
+      std::string d;
+      if (l != n->second.end()) d = l->second;
+      else if (g.key == kHostnameKey) d = n->first;
+      else continue;
+      if (!filterMatches(g, nodeRec(n->second), 0)) continue;
+      g.domains[d]++;
+    }
+  };
+  auto inverseAnti = [&](const PodH& p, const std::map<std::string, std::string>* labels) {
+    uint64_t owned = 0;  // updateInverseAntiAffinity (topology.go:207-232)
+    for (auto& t : p.antiRequired) {
+      TopoGroup g = makeGroup(TG_ANTI, t.key, p, termNs(p, t), t.sel, INT32_MAX, -1);
+      auto it = invByHash.find(g.hash);
+      int idx;
+      if (it == invByHash.end()) {
+        idx = (int)inv.size();
+        invByHash[g.hash] = idx;
+        inv.push_back(g);
+      } else {
+        idx = it->second;
+      }
+      if (labels) {
+        auto d = labels->find(inv[(size_t)idx].key);
+        if (d != labels->end()) inv[(size_t)idx].domains[d->second]++;
+      }
+      owned |= 1ull << idx;
+    }
+    return owned;
+  };
+  auto ownedSpecGroups = [&](const PodH& sp) {  // newForTopologies + newForAffinities
+    std::vector<TopoGroup> fresh;
+    for (auto& c : sp.tsc) fresh.push_back(makeGroup(TG_SPREAD, c.key, sp, {sp.ns}, c.sel, c.maxSkew, c.minDomains));
+    if (sp.hasAffinity && sp.hasPodAnti) {
+      for (auto& t : sp.antiRequired) fresh.push_back(makeGroup(TG_ANTI, t.key, sp, termNs(sp, t), t.sel, INT32_MAX, -1));
+      for (auto& t : sp.antiPreferred)
+        fresh.push_back(makeGroup(TG_ANTI, t.second.key, sp, termNs(sp, t.second), t.second.sel, INT32_MAX, -1));
+    }
+    return fresh;
+  };
+  for (auto& cp : clusterPods) {  // ForPodsWithAntiAffinity: bound pods with required anti-affinity
+    if (cp.antiRequired.empty() || cp.nodeName.empty() || excluded.count(cp.uid)) continue;
+    auto n = nodeLabelsByName.find(cp.nodeName);
+    if (n == nodeLabelsByName.end()) continue;
+    inverseAnti(cp, &n->second);
+  }
+  std::vector<uint64_t> invOwned(P, 0);
+  for (int p = 0; p < P; p++) {  // NewTopology: Update(pod) for every pod, in order
+    const std::shared_ptr<PodH>& sp = states[(size_t)p][0].spec;
+    if (!sp) continue;
+    if (sp->hasAffinity && sp->hasPodAnti && (!sp->antiRequired.empty() || !sp->antiPreferred.empty()))
+      invOwned[(size_t)p] = inverseAnti(*sp, nullptr);
+    uint64_t gown = 0;
+    for (auto& g : ownedSpecGroups(*sp)) {
+      auto it = ownByHash.find(g.hash);
+      int idx;
+      if (it == ownByHash.end()) {
+        countDomains(g);
+        idx = (int)own.size();
+        ownByHash[g.hash] = idx;
+        own.push_back(g);
+      } else {
+        idx = it->second;
+      }
+      if (idx >= 64) throw KsError(-3, "more than 64 topology groups");
+      gown |= 1ull << idx;
+    }
+    states[(size_t)p][0].gown = gown;
+  }
+  if (own.size() + inv.size() > 64) throw KsError(-3, "more than 64 topology groups");
+  const int G1 = (int)own.size(), G = G1 + (int)inv.size();
+  for (int p = 0; p < P; p++)
+    for (size_t k = 1; k < states[(size_t)p].size(); k++) {
+      PodState& st = states[(size_t)p][k];
+      if (!st.spec) continue;
+      uint64_t gown = 0;
+      for (auto& g : ownedSpecGroups(*st.spec)) {
+        auto it = ownByHash.find(g.hash);
+        if (it == ownByHash.end())
+          throw KsError(-2, "pod " + pods[(size_t)p].ns + "/" + pods[(size_t)p].name +
+                                ": a relaxed state creates a new topology group mid-Solve (not encoded by this build)");
+        gown |= 1ull << it->second;
+      }
+      st.gown = gown;
+    }
+  groups = own;
+  groups.insert(groups.end(), inv.begin(), inv.end());
+  groupsOwned = G1;
+  for (auto& g : groups)  // NewExistingNode registers every node's hostname (existingnode.go:60)
+    if (g.key == kHostnameKey)
+      for (auto& n : nodes) g.domains.emplace(n.hostName, 0);
+  for (int p = 0; p < P; p++) {
+    tab.pod_ginv[(size_t)p] = invOwned[(size_t)p] << G1;
+    for (int g = 0; g < G; g++)
+      if (groups[(size_t)g].namespaces.count(pods[(size_t)p].ns) && sel_selects(groups[(size_t)g].sel, pods[(size_t)p].labels))
+        tab.pod_gsel[(size_t)p] |= 1ull << g;
+  }
+
+  // --- device tables
+  tab.tg_meta.assign((size_t)G * TGM_WORDS, 0);
+  tab.tg_cnt0.clear();
+  tab.tg_reg0.clear();
+  tab.tg_frs.clear();
+  int maxNv = 0;
+  for (int g = 0; g < G; g++) {
+    TopoGroup& tg = groups[(size_t)g];
+    int32_t* m = &tab.tg_meta[(size_t)g * TGM_WORDS];
+    const int nv = (int)values[(size_t)tg.keyId].size();  // universe values (the hostname private bit excluded)
+    maxNv = std::max(maxNv, nv);
+    m[TGM_TYPE] = tg.type;
+    m[TGM_KEY] = tg.keyId;
+    m[TGM_SKEW] = tg.maxSkew;
+    m[TGM_MIND] = tg.minDomains;
+    m[TGM_CNT] = (int32_t)tab.tg_cnt0.size();
+    m[TGM_NV] = nv;
+    m[TGM_REG] = (int32_t)tab.tg_reg0.size();
+    m[TGM_FBEG] = (int32_t)(tab.tg_frs.size() / dims.RSW);
+    m[TGM_HOST] = tg.key == kHostnameKey ? 1 : 0;
+    std::vector<int32_t> cnt(std::max(nv, 1), 0);
+    std::vector<uint32_t> reg((size_t)std::max(1, (nv + 31) / 32), 0);
+    for (auto& kv : tg.domains) {
+      auto vi = valueId[(size_t)tg.keyId].find(kv.first);
+      if (vi == valueId[(size_t)tg.keyId].end())
+        throw KsError(-5, "topology domain " + kv.first + " outside the value universe of " + tg.key);
+      cnt[(size_t)vi->second] = kv.second;
+      reg[(size_t)vi->second >> 5] |= 1u << (vi->second & 31);
+    }
+    tab.tg_cnt0.insert(tab.tg_cnt0.end(), cnt.begin(), cnt.end());
+    tab.tg_reg0.insert(tab.tg_reg0.end(), reg.begin(), reg.end());
+    for (auto& f : tg.filter) tab.tg_frs.insert(tab.tg_frs.end(), f.begin(), f.end());
+    m[TGM_FEND] = (int32_t)(tab.tg_frs.size() / dims.RSW);
+  }
+  if (tab.tg_frs.empty()) tab.tg_frs.assign(dims.RSW, 0);
+  tab.n_tdom.assign((size_t)std::max(N, 1) * G, -1);
+  for (int n = 0; n < N; n++)
+    for (int g = 0; g < G; g++) {
+      const TopoGroup& tg = groups[(size_t)g];
+      std::string d;
+      if (tg.key == kHostnameKey) {
+        d = nodes[(size_t)n].hostName;
+      } else {
+        auto l = nodes[(size_t)n].labels.find(tg.key);
+        if (l == nodes[(size_t)n].labels.end()) continue;
+        d = l->second;
+      }
+      tab.n_tdom[(size_t)n * G + g] = valueId[(size_t)tg.keyId].at(d);
+    }
+  // A node without a group's label takes that key only from a pod's NotIn requirement
+  // (existingnode.go:97-115: the strict Compatible admits nothing else), after which the topology
+  // domain would be chosen like a NodeClaim's.  The kernel treats an unlabelled node as failing the
+  // group; refuse the one input where that differs.
+  for (int g = 0; g < G; g++) {
+    const int k = groups[(size_t)g].keyId;
+    bool unlabelled = false;
+    for (int n = 0; n < N && !unlabelled; n++) unlabelled = tab.n_tdom[(size_t)n * G + g] < 0;
+    if (!unlabelled) continue;
+    for (auto& chain : states)
+      for (auto& st : chain)
+        if (bit(rs_present(st.rsAll.data()), k) && bit(rs_compl(st.rsAll.data()), k))
+          throw KsError(-2, "topology key " + groups[(size_t)g].key +
+                                                " is missing on an existing node while a pod constrains it with NotIn");
+  }
+  dims.G = G;
+  dims.G1 = G1;
+  dims.tgMaxNv = maxNv;
+  dims.FSW = dims.RSW;
+  for (auto& g : groups)
+    if (g.key != kHostnameKey) {
+      const int nv = (int)values[(size_t)g.keyId].size();
+      dims.FSW = std::max(dims.FSW, nv + (nv + 31) / 32);
+    }
+  dims.tgCntWords = (int32_t)tab.tg_cnt0.size();
+  dims.tgRegWords = (int32_t)tab.tg_reg0.size();
+}
+
+}  // namespace ks

@@ -174,6 +174,7 @@ def benchmark_snapshot(n_pods, n_its=400, seed=42, diverse=True):
         "stateNodes": [],
         "daemonSetPods": [],
         "pods": pods,
+        "emptyTopology": True,  # &scheduling.Topology{} (scheduling_benchmark_test.go:124)
     }
 
 

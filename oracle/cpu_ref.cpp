@@ -601,6 +601,7 @@ struct Problem {
   vector<Pod> daemonSetPods;
   vector<Pod> pods;
   int64_t hostnameSeed = 0;
+  bool emptyTopology = false;  // the benchmark's &scheduling.Topology{} (scheduling_benchmark_test.go:124)
   // cluster state the Topology counts (topology.go:190-291): bound pods and node labels by node name
   vector<Pod> clusterPods;
   map<string, map<string, string>> nodeLabels;
@@ -895,6 +896,7 @@ static Problem parseProblem(const ojson::Value& root) {
   if (auto* ds = root.get("daemonSetPods")) for (auto& v : ds->arr()) pb.daemonSetPods.push_back(parsePod(v));
   if (auto* ps = root.get("pods")) for (auto& v : ps->arr()) pb.pods.push_back(parsePod(v));
   if (auto* hs = root.get("hostnameSeed")) pb.hostnameSeed = hs->i64();
+  if (auto* et = root.get("emptyTopology")) pb.emptyTopology = et->boolean();
   if (auto* cps = root.get("clusterPods")) for (auto& v : cps->arr()) pb.clusterPods.push_back(parsePod(v));
   for (auto& n : pb.nodes) pb.nodeLabels[n.name] = n.labels;
   if (auto* cns = root.get("clusterNodes"))
@@ -1039,7 +1041,7 @@ class Scheduler {
       if (errors_[p].ok) continue;
       bool relaxed = Relax(pb_.pods[p]);
       Push(p, relaxed);
-      if (relaxed) topo_.Update(pb_.pods[p]);
+      if (relaxed && !pb_.emptyTopology) topo_.Update(pb_.pods[p]);
     }
     for (auto& nc : claims_) nc.reqs.m.erase(kHostname);  // FinalizeScheduling nodeclaim.go:123-128
   }
@@ -1061,6 +1063,7 @@ class Scheduler {
 
   // Provisioner.NewScheduler -> NewTopology (provisioner.go:229-287, topology.go:61-85)
   void buildTopology() {
+    if (pb_.emptyTopology) return;  // no groups: AddRequirements / Record are no-ops
     topo_.domains = topologyDomains(pb_);
     topo_.clusterPods = &pb_.clusterPods;
     topo_.nodes = &pb_.nodeLabels;

@@ -122,7 +122,92 @@ def add_host_ports(rng, pod):
     pod["spec"]["containers"][0]["ports"] = ports
 
 
-def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False):
+TOPO_KEYS = [synth.ZONE, synth.HOSTNAME, synth.CT]
+
+
+def _app_selector(rng, app):
+    if rng.random() < 0.8:
+        return {"matchLabels": {"app": app}}
+    return {"matchExpressions": [{"key": "app", "operator": _pick(rng, ["In", "NotIn"]),
+                                  "values": sorted({app, "a%d" % int(rng.integers(5))})}]}
+
+
+def _anti_term(rng, app):
+    return {"labelSelector": _app_selector(rng, app), "topologyKey": _pick(rng, [synth.HOSTNAME, synth.HOSTNAME, synth.ZONE])}
+
+
+def add_topology(rng, pods, nodes):
+    """Topology spread (zone / hostname / capacity-type, maxSkew 1-3, minDomains, DoNotSchedule and
+    ScheduleAnyway), required + preferred pod anti-affinity (topology.go, topologygroup.go) per app,
+    plus bound cluster pods on the existing nodes that seed the counts (countDomains) and inverse
+    anti-affinity groups.  Pods carrying a spread constraint keep one required node-affinity term:
+    relaxing OR'd terms would change the group's node filter mid-Solve (ks_topo.cpp refuses that)."""
+    apps = {}
+    for a in range(5):
+        app = "a%d" % a
+        spec = {}
+        if rng.random() < 0.7:
+            cs = []
+            for key in _pick(rng, TOPO_KEYS, int(rng.integers(1, 3))):
+                c = {"topologyKey": key, "maxSkew": int(rng.integers(1, 4)), "labelSelector": _app_selector(rng, app),
+                     "whenUnsatisfiable": "ScheduleAnyway" if rng.random() < 0.25 else "DoNotSchedule"}
+                if c["whenUnsatisfiable"] == "DoNotSchedule" and key != synth.HOSTNAME and rng.random() < 0.2:
+                    c["minDomains"] = int(rng.integers(2, 5))
+                cs.append(c)
+            spec["tsc"] = cs
+            f = rng.random()  # the app's node filter (nodeSelector / one required term), shared by its pods
+            if f < 0.2:
+                spec["sel"] = {synth.ZONE: _pick(rng, ZONES[:3])}
+            elif f < 0.35:
+                spec["sel"] = {synth.ARCH: _pick(rng, ARCHS)}
+            elif f < 0.5:
+                spec["req"] = [{"matchExpressions": [{"key": synth.ZONE, "operator": "In",
+                                                      "values": sorted(_pick(rng, ZONES, 2))}]}]
+        if rng.random() < 0.35:
+            spec["anti"] = [_anti_term(rng, app)]
+        if rng.random() < 0.25:
+            spec["antiPref"] = [{"weight": int(rng.integers(1, 100)), "podAffinityTerm": _anti_term(rng, app)}]
+        apps[app] = spec
+    for p in pods:
+        app = p["metadata"]["labels"]["app"]
+        spec = apps[app]
+        if rng.random() < 0.15:
+            continue  # some pods of the app carry no constraint (still counted by the selectors)
+        if "tsc" in spec:
+            p["spec"]["topologySpreadConstraints"] = spec["tsc"]
+            p["spec"].pop("nodeSelector", None)
+            if "sel" in spec:
+                p["spec"]["nodeSelector"] = dict(spec["sel"])
+            na = p["spec"].get("affinity", {}).get("nodeAffinity", {})
+            na.pop("requiredDuringSchedulingIgnoredDuringExecution", None)
+            if "req" in spec:
+                na = p["spec"].setdefault("affinity", {}).setdefault("nodeAffinity", {})
+                na["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": spec["req"]}
+            elif "affinity" in p["spec"] and p["spec"]["affinity"].get("nodeAffinity") == {}:
+                del p["spec"]["affinity"]["nodeAffinity"]
+        if "anti" in spec or "antiPref" in spec:
+            paa = {}
+            if "anti" in spec:
+                paa["requiredDuringSchedulingIgnoredDuringExecution"] = spec["anti"]
+            if "antiPref" in spec:
+                paa["preferredDuringSchedulingIgnoredDuringExecution"] = spec["antiPref"]
+            p["spec"].setdefault("affinity", {})["podAntiAffinity"] = paa
+    cluster = []
+    for i, n in enumerate(nodes):
+        for j in range(int(rng.integers(0, 4))):
+            app = "a%d" % int(rng.integers(5))
+            cp = synth.pod(500000 + i * 10 + j, cpu="100m", labels={"app": app})
+            cp["spec"]["nodeName"] = n["name"]
+            cp["status"] = {"phase": _pick(rng, ["Running", "Running", "Running", "Succeeded"])}
+            if rng.random() < 0.15:
+                cp["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                    {"labelSelector": {"matchLabels": {"app": "a%d" % int(rng.integers(5))}},
+                     "topologyKey": _pick(rng, [synth.HOSTNAME, synth.ZONE])}]}}
+            cluster.append(cp)
+    return cluster
+
+
+def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False, topology=False):
     rng = np.random.default_rng(seed)
     its = random_its(rng, n_its)
     n_templates = int(rng.integers(1, 4)) if n_templates is None else n_templates
@@ -183,6 +268,7 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
         for p in pods:
             if rng.random() < 0.4:
                 add_host_ports(rng, p)
+    cluster = add_topology(rng, pods, nodes) if topology else []
     return {
         "wellKnownLabels": synth.FAKE_WELL_KNOWN,
         "instanceTypes": its,
@@ -192,6 +278,7 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
         "stateNodes": nodes,
         "daemonSetPods": daemons,
         "pods": pods,
+        "clusterPods": cluster,
     }
 
 
