@@ -137,6 +137,37 @@ def c3_bench(args, local):
             "pods_placed": placed, "pod_errors": len(r.pod_errors)}
 
 
+def c4_bench(args, local):
+    """C4 (BASELINE.json configs[3]): topology Solve onto existing nodes, 1 GPU, beside the C2 line.
+    The oracle leg times a bounded sample of the same shape (fewer pods and nodes)."""
+    from karpenter_amd import Scheduler, synth
+
+    sch = Scheduler(json.dumps(synth.config4(args.c4_pods, args.c4_nodes)))
+    r = sch.solve(device=local)
+    on_nodes = sum(len(n["pods"]) for n in r.existing_nodes)
+    for _ in range(max(args.warmup - 1, 0)):
+        sch.solve(device=local, timing_only=True)
+    t0 = time.perf_counter()
+    ks = []
+    for _ in range(3):
+        ks.append(sch.solve(device=local, timing_only=True).solve_kernel_ms)
+    el = (time.perf_counter() - t0) / 3
+    out = {"metric": "pods/sec in Scheduler.Solve (C4: %d pods onto %d existing nodes, zonal + hostname spread, "
+                     "hostname anti-affinity, 20 apps)" % (args.c4_pods, args.c4_nodes),
+           "value": round(args.c4_pods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1000, 3),
+           "kernel_ms": round(sum(ks) / len(ks), 3), "new_nodeclaims": len(r.new_nodeclaims),
+           "pods_on_existing_nodes": on_nodes, "pod_errors": len(r.pod_errors), "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        from oracle import bridge
+
+        sp, sn = max(args.c4_pods // 4, 1), max(args.c4_nodes // 4, 1)
+        secs = bridge.time_solve(json.dumps(synth.config4(sp, sn)), 1)
+        out["cpu_baseline"] = {"value": round(sp / secs, 1), "unit": "pods/s", "cores": 1, "kind": "port",
+                               "sample": "1 Solve of C4 with %d pods onto %d nodes (oracle/cpu_ref.cpp, single "
+                                         "thread, %.1f s)" % (sp, sn, secs)}
+    return out
+
+
 def _traffic(tag):
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % tag)
     if os.path.exists(tpath):
@@ -157,6 +188,9 @@ def main():
     ap.add_argument("--no-consolidation", action="store_true")
     ap.add_argument("--no-c3", action="store_true")
     ap.add_argument("--c3-pods", type=int, default=20000)
+    ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--c4-pods", type=int, default=10000)
+    ap.add_argument("--c4-nodes", type=int, default=2000)
     ap.add_argument("--only-consolidation", action="store_true", help="profiling: skip the Solve section")
     ap.add_argument("--cons-nodes", type=int, default=5000, help="C5 cluster size (20 pods per node)")
     ap.add_argument("--cons-steps", type=int, default=20)
@@ -236,6 +270,7 @@ def main():
                "sample": "1 Solve of C2 with %d pods x %d instance types (oracle/cpu_ref.cpp, single thread, "
                          "%.1f s)" % (args.cpu_pods, args.its, secs)}
     c3 = None if args.no_c3 or world > 1 else c3_bench(args, local)
+    c4 = None if args.no_c4 or world > 1 else c4_bench(args, local)
     cons = None if args.no_consolidation else consolidation_bench(args, rank, world, local, dist, barrier_sync)
     if rank != 0:
         dist.destroy_process_group()
@@ -263,6 +298,7 @@ def main():
                      "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3)},
         "cpu_baseline": cpu,
         "solve_c3": c3,
+        "solve_c4": c4,
         "consolidation": cons,
     }
     print(json.dumps(out))

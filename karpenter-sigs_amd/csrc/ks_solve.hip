@@ -129,7 +129,7 @@ struct Window {
 // SIM: a consolidation simulation (helpers.go:73-127) over the shared cluster problem: pods are
 // the simulation's local subset (W.pod_map), the candidates' nodes are masked out, and existing
 // node state is copy-on-write (a node's HBM slot is initialised the first time a pod lands on it).
-template <int RT, bool TL, bool SIM>
+template <int RT, bool TL, bool SIM, bool TOPO>
 struct Solver {
   static constexpr int RM = RT > 0 ? RT : kMaxR;
   // By value: a reference to a byval kernel argument forces a scratch copy of the whole struct
@@ -301,7 +301,7 @@ struct Solver {
       if (ok0) ok0 = rs_compatible(L, node_rs(c0), D.st_rs + (int64_t)s * d.RSW, 0);
       if (ok1) ok1 = rs_compatible(L, node_rs(c1), D.st_rs + (int64_t)s * d.RSW, 0);
     }
-    if (t_mask) {  // topology (existingnode.go:106-114)
+    if (TOPO && t_mask) {  // topology (existingnode.go:106-114)
       if (ok0) ok0 = topo_node_ok(c0);
       if (ok1) ok1 = topo_node_ok(c1);
     }
@@ -555,17 +555,17 @@ struct Solver {
                                              int& ncnt) {
     const ClaimView<INL>& v = cv<INL>();
     bool changed = false;
-    if ((sflags & SF_HAS_KEYS) || t_mask) {
+    if ((sflags & SF_HAS_KEYS) || (TOPO && t_mask)) {
       const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
       copy_words(s_rs, crs, d.RSW);
       wsync();
       if ((sflags & SF_HAS_KEYS) && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
       wsync();
-      if (t_mask && topo_apply(s_rs, c) != 0) {  // topology requirements (nodeclaim.go:92-100)
+      if (TOPO && t_mask && topo_apply(s_rs, c) != 0) {  // topology requirements (nodeclaim.go:92-100)
         ncnt = 0;
         return false;
       }
-      changed = (((sflags & SF_HAS_KEYS) && (sflags & SF_TOUCHES_IT_KEYS)) || t_mask) &&
+      changed = (((sflags & SF_HAS_KEYS) && (sflags & SF_TOUCHES_IT_KEYS)) || (TOPO && t_mask)) &&
                 !rs_equal_keys(L, s_rs, crs, d.itKeys);
       algbytes += 8 * d.RSW;
     }
@@ -681,14 +681,14 @@ struct Solver {
       s_okey[pos] = okNew;
       if (d.hpAny) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
     }
-    if ((sflags & SF_HAS_KEYS) || t_mask) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
+    if ((sflags & SF_HAS_KEYS) || (TOPO && t_mask)) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
     copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     log_commit(p, c, nlog);
     // The max bound stays valid as the options only shrink; it is tightened lazily when a full check
     // fails.  HBM-resident claim state is re-read by other lanes: drain the stores first.
     if ((sflags & SF_HAS_KEYS) || !INL || d.hpAny) hbm_release();
     wsync();
-    if (d.G && (t_sel | t_inv)) {  // Topology.Record on the claim's final requirements (nodeclaim.go:121)
+    if (TOPO && (t_sel | t_inv)) {  // Topology.Record on the claim's final requirements (nodeclaim.go:121)
       if ((sflags & SF_HAS_KEYS) || t_mask) topo_record(s_rs, c, d.allowWK);
       else topo_record(W.c_rs + (int64_t)c * d.RSW, c, d.allowWK);
     }
@@ -737,7 +737,7 @@ struct Solver {
             if (ok && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
             wsync();
           }
-          if (ok && t_mask) {  // topology requirements of the fresh NodeClaim (nodeclaim.go:92-100)
+          if (TOPO && ok && t_mask) {  // topology requirements of the fresh NodeClaim (nodeclaim.go:92-100)
             const uint32_t tc = topo_apply(s_rs, nclaims);
             if (tc) {
               ok = false;
@@ -785,7 +785,7 @@ struct Solver {
             wsync();
             if (any == 0) {
               code = FC_NO_IT | (flags << 8);
-              if (t_mask) {  // the message prints the requirements the topology narrowed
+              if (TOPO && t_mask) {  // the message prints the requirements the topology narrowed
                 copy_words(W.fail_rs + ((int64_t)p * d.NTPL + t) * d.FSW, s_rs, d.RSW);
                 code |= FC_RS_SNAP;
               }
@@ -833,7 +833,7 @@ struct Solver {
               log_commit(p, c, nlog);
               hbm_release();  // c_rs / c_tpl / overflow state are read by other lanes later
               wsync();
-              if (d.G && (t_sel | t_inv)) topo_record(s_rs, c, d.allowWK);
+              if (TOPO && (t_sel | t_inv)) topo_record(s_rs, c, d.allowWK);
               if (inl) recompute_max<true>(c, s_rem, t, c);
               else recompute_max<false>(c, s_rem, t, c);
               if (pool >= 0) {  // subtractMax (scheduler.go:347-362)
@@ -1042,14 +1042,14 @@ struct Solver {
   }
 };
 
-template <int RT, bool TL, bool SIM>
+template <int RT, bool TL, bool SIM, bool TOPO>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_solve(KsDev D, const KsWork* works, Plan pl) {
-  constexpr int RM = Solver<RT, TL, SIM>::RM;
+  constexpr int RM = Solver<RT, TL, SIM, TOPO>::RM;
   extern __shared__ __attribute__((aligned(16))) char smem_generic[];
   char KS_L* smem = (char KS_L*)smem_generic;
   const KsWork W = works[blockIdx.x];
   const KsDims d = D.d;
-  Solver<RT, TL, SIM> S(D, W, pl);
+  Solver<RT, TL, SIM, TOPO> S(D, W, pl);
   const int R = S.R();
   char KS_L* sp = smem;
   auto take = [&](size_t bytes) { char KS_L* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       S.cur_hpc = (uint64_t)rdl64((int64_t)w.hpc, wi);
       S.cur_hpu = (uint64_t)rdl64((int64_t)w.hpu, wi);
     }
-    if (d.G) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
+    if (TOPO) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= R) break;
@@ -1238,7 +1238,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
           ok &= (whp[k] & S.cur_hpc) == 0;
           if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), D.st_rs + (int64_t)s * d.RSW, 0);
-          if (S.t_mask && ok) ok = S.topo_node_ok(n);
+          if (TOPO && S.t_mask && ok) ok = S.topo_node_ok(n);
           const uint64_t m = wballot(ok);
           if (m) {
             kj = k;
@@ -1267,7 +1267,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           } else if ((sflags & SF_HAS_KEYS) && lane() == owner) {
             rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
           }
-          if (!SIM && d.G && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, 0);  // existingnode.go:121
+          if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, 0);  // existingnode.go:121
           S.log_commit(p, -(j + 1), nlog);
           PH_END(t7, 7);
           S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
@@ -1298,7 +1298,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         } else if (lane() == (j & (kWave - 1))) {
           S.node_commit(j, s, sflags, pod);  // the owner lane of node j
         }
-        if (!SIM && d.G && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, 0);  // existingnode.go:121
+        if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, 0);  // existingnode.go:121
         S.log_commit(p, -(j + 1), nlog);
         PH_END(t7, 7);
         placed = true;
@@ -1466,12 +1466,18 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep, (const int32_t*)qorder);
   if (mid) (void)hipEventRecord(mid, st);
-#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, false>), dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl)
+  // Topology problems get their own instantiation: the group state would otherwise occupy SGPRs
+  // (and their spills) across the whole commit loop of every topology-free Solve.
+#define KS_LAUNCH(RT_, TL_)                                                                               \
+  {                                                                                                       \
+    if (D.d.G) hipLaunchKernelGGL((k_solve<RT_, TL_, false, true>), dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl); \
+    else hipLaunchKernelGGL((k_solve<RT_, TL_, false, false>), dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl);     \
+  }
   const bool tl = pl.talloc != 0;
   switch (D.d.R) {
-    case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;
-    case 4: if (tl) KS_LAUNCH(4, true); else KS_LAUNCH(4, false); break;
-    default: if (tl) KS_LAUNCH(0, true); else KS_LAUNCH(0, false); break;
+    case 3: if (tl) KS_LAUNCH(3, true) else KS_LAUNCH(3, false) break;
+    case 4: if (tl) KS_LAUNCH(4, true) else KS_LAUNCH(4, false) break;
+    default: if (tl) KS_LAUNCH(0, true) else KS_LAUNCH(0, false) break;
   }
 #undef KS_LAUNCH
   return hipGetLastError();
@@ -1482,7 +1488,7 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st) {
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
   if (nsims <= 0) return hipSuccess;
-#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, true>), dim3(nsims), dim3(kWave), pl.lds, st, D, works_dev, pl)
+#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, true, false>), dim3(nsims), dim3(kWave), pl.lds, st, D, works_dev, pl)
   const bool tl = pl.talloc != 0;
   switch (D.d.R) {
     case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;

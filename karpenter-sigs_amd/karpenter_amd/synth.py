@@ -280,6 +280,89 @@ def config5(n_nodes=5000, pods_per_node=20, seed=4205):
 C3_ZONES = ["test-zone-1", "test-zone-2", "test-zone-3", "test-zone-4"]
 
 
+def config4(n_pods=10000, n_nodes=2000, seed=4204, n_apps=20):
+    """C4 (BASELINE.json configs[3]): pending pods with zonal + hostname topology spread and pod
+    anti-affinity onto existing initialized nodes.  fake.InstanceTypes(400) offered in 4 zones x
+    {spot, on-demand}; `n_nodes` nodes (8-32 cpu, unique hostnames, zones round-robin) 50-80 %
+    utilised by bound cluster pods that carry the same app labels, so countDomains seeds every
+    group.  `n_apps` apps as label selectors: the first half zonal spread maxSkew 1, the next 30 %
+    hostname spread maxSkew 1, the rest required hostname anti-affinity."""
+    rng = np.random.default_rng(seed)
+    its = []
+    for i in range(400):
+        price = price_from_resources(i + 1, 2 * (i + 1) * GI)
+        offers = [{"capacityType": ct, "zone": z, "price": price * (0.5 if ct == "spot" else 1.0), "available": True}
+                  for z in C3_ZONES for ct in ("spot", "on-demand")]
+        its.append(fake_instance_type("fake-it-%d" % i, i + 1, 2 * (i + 1), pods=10 * (i + 1), offerings=offers))
+    pool = node_pool("default")
+    apps = ["app-%02d" % a for a in range(n_apps)]
+    n_zone, n_host = n_apps // 2, (n_apps * 3) // 10
+
+    def app_spec(a):
+        sel = {"matchLabels": {"app": apps[a]}}
+        if a < n_zone:
+            return {"topologySpreadConstraints": [{"maxSkew": 1, "topologyKey": ZONE, "whenUnsatisfiable": "DoNotSchedule",
+                                                   "labelSelector": sel}]}
+        if a < n_zone + n_host:
+            return {"topologySpreadConstraints": [{"maxSkew": 1, "topologyKey": HOSTNAME,
+                                                   "whenUnsatisfiable": "DoNotSchedule", "labelSelector": sel}]}
+        return {"affinity": {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"labelSelector": sel, "topologyKey": HOSTNAME}]}}}
+
+    cpu_m = [100, 250, 500, 1000, 1500]
+    mem_mi = [100, 256, 512, 1024, 2048, 4096]
+    nodes, cluster = [], []
+    pid = 1000000
+    for j in range(n_nodes):
+        i = int(rng.integers(7, 32))
+        alloc_cpu_m, alloc_mem, alloc_pods = (i + 1) * 1000 - 100, 2 * (i + 1) * GI - 10 * (1 << 20), 10 * (i + 1)
+        target = float(rng.uniform(0.5, 0.8))
+        used_cpu, used_mem, n_bound = 0, 0, 0
+        name = "node-%05d" % j
+        while used_cpu < target * alloc_cpu_m:
+            c, m = cpu_m[int(rng.integers(5))], mem_mi[int(rng.integers(6))] << 20
+            if used_cpu + c > alloc_cpu_m or used_mem + m > alloc_mem or n_bound + 1 >= alloc_pods:
+                break
+            a = int(rng.integers(n_apps))
+            if a >= n_zone + n_host and any(cp["metadata"]["labels"]["app"] == apps[a] and
+                                            cp["spec"]["nodeName"] == name for cp in cluster[-n_bound:] if n_bound):
+                a = int(rng.integers(n_zone))  # keep the running anti-affinity pods one per host
+            cp = pod(pid, cpu="%dm" % c, mem="%dMi" % (m >> 20), labels={"app": apps[a]})
+            cp["spec"]["nodeName"] = name
+            cp["status"] = {"phase": "Running"}
+            cluster.append(cp)
+            pid += 1
+            used_cpu, used_mem, n_bound = used_cpu + c, used_mem + m, n_bound + 1
+        zone = C3_ZONES[j % 4]
+        ct = "spot" if rng.random() < 0.3 else "on-demand"
+        labels = {NODEPOOL: "default", IT_LABEL: its[i]["name"], ZONE: zone, CT: ct, HOSTNAME: name, ARCH: "amd64",
+                  OS: "linux", "testing/cluster": "unspecified"}
+        nodes.append({
+            "name": name, "hostName": name, "labels": labels, "taints": [],
+            "capacity": dict(its[i]["capacity"]),
+            "available": {"cpu": "%dm" % (alloc_cpu_m - used_cpu), "memory": str(alloc_mem - used_mem),
+                          "pods": str(alloc_pods - n_bound)},
+            "daemonSetRequests": {}, "initialized": True,
+        })
+    pods = []
+    for i in range(n_pods):
+        a = int(rng.integers(n_apps))
+        p = pod(i, cpu=CPU_CHOICES[rng.integers(5)], mem=MEM_CHOICES[rng.integers(6)], labels={"app": apps[a]})
+        p["spec"].update(app_spec(a))
+        pods.append(p)
+    return {
+        "wellKnownLabels": FAKE_WELL_KNOWN,
+        "instanceTypes": its,
+        "instanceTypesByNodePool": {"default": list(range(400))},
+        "nodeClaimTemplates": [pool],
+        "nodePools": [],
+        "stateNodes": nodes,
+        "daemonSetPods": [],
+        "pods": pods,
+        "clusterPods": cluster,
+    }
+
+
 def config3(n_pods=20000, seed=4203):
     """C3 (BASELINE.json configs[2]): pods with nodeSelector / required + preferred node affinity and
     tolerations over 800 instance types (100 cpu x memory shapes x 2 arch x 4 families), each offered

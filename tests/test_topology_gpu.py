@@ -86,3 +86,48 @@ def test_topology_with_host_ports(seed):
     want, got = _solve_both(problems.random_problem(seed, n_pods=200, n_nodes=8, host_ports=True, topology=True))
     d = _diff(want, got)
     assert d is None, d
+
+
+def test_config4_topology_existing_nodes():
+    """C4 shape (BASELINE.json configs[3]) at 2000 pods onto 400 existing nodes with bound cluster
+    pods: zonal spread, hostname spread and hostname anti-affinity over 20 apps."""
+    from karpenter_amd import synth
+
+    want, got = _solve_both(synth.config4(2000, 400))
+    d = _diff(want, got)
+    assert d is None, d
+
+
+def test_config4_full_size_properties():
+    """Full C4 (10k pods, 2k nodes): no oracle run at this size; check the invariants the domain
+    gives: every pod placed exactly once or failed, and required hostname anti-affinity holds
+    against the bound cluster pods and this Solve's own placements."""
+    from karpenter_amd import Scheduler, synth
+
+    snap = synth.config4()
+    res = Scheduler(json.dumps(snap)).solve()
+    node_zone = {n["name"]: n["labels"][synth.ZONE] for n in snap["stateNodes"]}
+    seen = {}
+    for ni, n in enumerate(res.existing_nodes):
+        for p in n["pods"]:
+            assert p not in seen
+            seen[p] = n["name"]
+    for ci, c in enumerate(res.new_nodeclaims):
+        for p in c["pods"]:
+            assert p not in seen
+            seen[p] = "claim-%d" % ci
+    assert len(seen) + len(res.pod_errors) == len(snap["pods"])
+    host_apps = {}
+    for cp in snap["clusterPods"]:
+        host_apps.setdefault((cp["metadata"]["labels"]["app"], cp["spec"]["nodeName"]), 0)
+        host_apps[(cp["metadata"]["labels"]["app"], cp["spec"]["nodeName"])] += 1
+    for p, where in seen.items():
+        spec = snap["pods"][p]["spec"]
+        app = snap["pods"][p]["metadata"]["labels"]["app"]
+        if "affinity" in spec:  # hostname anti-affinity against cluster pods and this Solve's pods
+            host_apps[(app, where)] = host_apps.get((app, where), 0) + 1
+    for p, where in seen.items():
+        if "affinity" in snap["pods"][p]["spec"]:
+            app = snap["pods"][p]["metadata"]["labels"]["app"]
+            assert host_apps[(app, where)] == 1, (p, where)
+    assert all(w in node_zone or w.startswith("claim-") for w in seen.values())
