@@ -23,7 +23,7 @@ namespace {
 
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
-      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, tg_cnt, tg_reg,
+      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, tg_cnt,
       tg_ccnt, fail_rs, total;
 };
 
@@ -57,7 +57,6 @@ WorkLayout work_layout(const KsDims& d) {
   w.n_hp = a.add(8 * N);
   w.c_hp = a.add(8 * K);
   w.tg_cnt = a.add(4 * std::max<size_t>(d.G ? (size_t)d.tgCntWords : 1, 1));
-  w.tg_reg = a.add(4 * std::max<size_t>(d.G ? (size_t)d.tgRegWords : 1, 1));
   w.tg_ccnt = a.add(4 * (size_t)std::max(d.G, 1) * (d.G ? K + 1 : 1));
   w.fail_rs = a.add(d.G ? 4 * (size_t)P * std::max(d.NTPL, 1) * d.FSW : 4);
   w.total = a.total;
@@ -92,7 +91,6 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.n_hp = (uint64_t*)(base + w.n_hp);
   k.c_hp = (uint64_t*)(base + w.c_hp);
   k.tg_cnt = (int32_t*)(base + w.tg_cnt);
-  k.tg_reg = (uint32_t*)(base + w.tg_reg);
   k.tg_ccnt = (int32_t*)(base + w.tg_ccnt);
   k.fail_rs = (uint32_t*)(base + w.fail_rs);
   return k;
@@ -177,7 +175,6 @@ void ks_upload(ks_problem* pb) {
   size_t o_nhp = put(t.n_hp0.data(), t.n_hp0.size() * 8);
   size_t o_tgm = put(t.tg_meta.data(), t.tg_meta.size() * 4);
   size_t o_tgc = put(t.tg_cnt0.data(), t.tg_cnt0.size() * 4);
-  size_t o_tgr = put(t.tg_reg0.data(), t.tg_reg0.size() * 4);
   size_t o_tgf = put(t.tg_frs.data(), t.tg_frs.size() * 4);
   size_t o_sgo = put(t.st_gown.data(), t.st_gown.size() * 8);
   size_t o_pgs = put(t.pod_gsel.data(), t.pod_gsel.size() * 8);
@@ -233,7 +230,6 @@ void ks_upload(ks_problem* pb) {
   D.n_hp0 = (const uint64_t*)(b + o_nhp);
   D.tg_meta = (const int32_t*)(b + o_tgm);
   D.tg_cnt0 = (const int32_t*)(b + o_tgc);
-  D.tg_reg0 = (const uint32_t*)(b + o_tgr);
   D.tg_frs = (const uint32_t*)(b + o_tgf);
   D.st_gown = (const uint64_t*)(b + o_sgo);
   D.pod_gsel = (const uint64_t*)(b + o_pgs);
@@ -435,7 +431,7 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
           if (!gm[TGM_HOST]) {  // registered domains in name order with their counts at the failure
             bool first = true;
             for (int v = 0; v < nv; v++)
-              if ((fr[nv + (v >> 5)] >> (v & 31)) & 1u) {
+              if ((int32_t)fr[v] >= 0) {  // -1: not registered
                 counts += (first ? "" : " ") + h.values[(size_t)k][(size_t)v] + ":" + std::to_string((int32_t)fr[v]);
                 first = false;
               }
@@ -644,8 +640,8 @@ int ks_results_json(const ks_results* r, char** json_out) {
   static const char* names[] = {"nclaims", "ncommits", "hostnameCounter", "error", "pops", "algBytes",
                                 "sorts", "sortsWithDescent", "claimFull", "claimQuickFail", "windows",
                                 "cycPop", "cycNodes", "cycSort", "cycQuick", "cycFull", "cycCommit", "cycTemplates",
-                                "cycTotal"};
-  for (int i = 0; i < 19; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
+                                "cycTotal", "cycNodeCommit"};
+  for (int i = 0; i < 20; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
   o += "}}";
   *json_out = strdup(o.c_str());
   return KS_OK;

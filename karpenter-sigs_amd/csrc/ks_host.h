@@ -159,11 +159,10 @@ struct Host {
     // topology groups (ks_topo.cpp)
     std::vector<int32_t> tg_meta;   // [G][TGM_WORDS]
     std::vector<int32_t> tg_cnt0;   // counts per (group, value) at NewScheduler time
-    std::vector<uint32_t> tg_reg0;  // registered-domain bitsets per group
     std::vector<uint32_t> tg_frs;   // node-filter requirement records
     std::vector<uint64_t> st_gown, pod_gsel, pod_ginv;
     std::vector<uint32_t> st_rss;   // [S][RSW] strict pod requirements (NewStrictPodRequirements)
-    std::vector<int32_t> n_tdom;    // [N][G] value index of the node's label for the group's key (-1: none)
+    std::vector<int32_t> n_tdom;    // [G][N] value index of the node's label for the group's key (-1: none)
     std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask, st_toltpl;
     std::vector<uint64_t> tpl_taint, st_tol, n_taint;
     std::vector<int32_t> tsort_pos, it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,

@@ -63,7 +63,7 @@ struct KsDims {
   int32_t hpAny;           // some pod or node uses host ports
   int32_t G, G1;           // topology groups (ks_topo.cpp): [0, G1) t.topologies, [G1, G) inverse
   int32_t tgMaxNv;         // largest value universe of a topology key
-  int32_t tgCntWords, tgRegWords;  // sizes of the count / registered tables
+  int32_t tgCntWords;      // size of the count table
   int32_t FSW;             // fail_rs words per (pod, template): RSW, or counts + registered bits if larger
 };
 
@@ -126,20 +126,19 @@ struct KsDev {
   const uint64_t KS_G* n_hp0;      // [N] host-port triples reserved on an existing node
   // topology (topology.go; ks_topo.cpp)
   const int32_t KS_G* tg_meta;     // [G][TGM_WORDS]
-  const int32_t KS_G* tg_cnt0;     // per group: domain counts over its key's values (NewTopology state)
-  const uint32_t KS_G* tg_reg0;    // per group: registered-domain bitset
+  const int32_t KS_G* tg_cnt0;     // per group: domain counts over its key's values, -1 = not registered (NewTopology state)
   const uint32_t KS_G* tg_frs;     // node-filter requirement records (spread groups)
   const uint64_t KS_G* st_gown;    // [S] groups the pod owns in the state
   const uint64_t KS_G* pod_gsel;   // [P] groups whose selector selects the pod
   const uint64_t KS_G* pod_ginv;   // [P] inverse groups the pod owns
   const uint32_t KS_G* st_rss;     // [S][RSW] strict pod requirements (podDomains)
-  const int32_t KS_G* n_tdom;      // [N][G] value of the node's label for the group's key, -1 none
+  const int32_t KS_G* n_tdom;      // [G][N] value of the node's label for the group's key, -1 none
 };
 
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };
 enum TopoGroupType : int32_t { TG_SPREAD = 0, TG_ANTI = 2 };
 enum TgMeta : int32_t {  // per topology group, int32 words
-  TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_REG, TGM_FBEG, TGM_FEND, TGM_HOST, TGM_WORDS = 12
+  TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST, TGM_WORDS = 12
 };
 enum PodFlag : int32_t { PF_PROVISIONABLE = 1 };
 enum ConsFlag : int32_t { CF_PRICE_ERR = 1, CF_ALL_SPOT = 2, CF_MULTI = 4 };
@@ -194,7 +193,6 @@ struct KsWork {
   uint64_t KS_G* n_hp;      // [N] host ports reserved per existing node (SIM: valid where s_tch is set)
   uint64_t KS_G* c_hp;      // [Kcap] host ports reserved per NodeClaim
   int32_t KS_G* tg_cnt;     // topology domain counts (copy of tg_cnt0)
-  uint32_t KS_G* tg_reg;    // registered domains (copy of tg_reg0)
   int32_t KS_G* tg_ccnt;    // [G][Kcap] counts of the NodeClaims' hostname-placeholder domains
   uint32_t KS_G* fail_rs;   // [P][NTPL][FSW] FC_TOPO_COMPAT: requirements; FC_TOPO: the group's counts + registered bits
   // consolidation simulations only (k_solve<.., SIM=true>): this simulation's view of the shared

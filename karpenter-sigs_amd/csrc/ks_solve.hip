@@ -93,7 +93,6 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
     for (int64_t i = gtid; i < d.N; i += gsz) W.n_hp[i] = D.n_hp0[i];
     if (d.G) {
       for (int64_t i = gtid; i < d.tgCntWords; i += gsz) W.tg_cnt[i] = D.tg_cnt0[i];
-      for (int64_t i = gtid; i < d.tgRegWords; i += gsz) W.tg_reg[i] = D.tg_reg0[i];
       for (int64_t i = gtid; i < (int64_t)d.G * (d.Kcap + 1); i += gsz) W.tg_ccnt[i] = 0;
     }
     for (int64_t i = gtid; i < d.P; i += gsz) {
@@ -362,9 +361,7 @@ struct Solver {
   // --- Topology (topology.go, topologygroup.go) ------------------------------------------------
   // Counts and registered bits are written by one lane and read by others: loads bypass the L1.
   __device__ __forceinline__ int tg(int g, int f) const { return s_tgm[g * TGM_WORDS + f]; }
-  __device__ __forceinline__ bool treg(int g, int v) const {
-    return (ld_sc1(W.tg_reg + tg(g, TGM_REG) + (v >> 5)) >> (v & 31)) & 1u;
-  }
+  // count of domain v, -1 while the domain is not registered (absent from TopologyGroup.domains)
   __device__ __forceinline__ int tcnt(int g, int v) const { return ld_sc1(W.tg_cnt + tg(g, TGM_CNT) + v); }
   __device__ __forceinline__ int tccnt(int g, int claim) const { return ld_sc1(W.tg_ccnt + (int64_t)g * (d.Kcap + 1) + claim); }  // claim <= Kcap (a fresh claim at the cap)
   __device__ __forceinline__ bool tpod_has(int g, int v) const {  // podDomains.Has (strict pod requirements)
@@ -385,12 +382,13 @@ struct Solver {
       int mn = 0x7fffffff, num = 0;
       if (!tg(g, TGM_HOST)) {  // hostname groups always have a min of 0
         const int nv = tg(g, TGM_NV);
-        for (int v = lane(); v < nv; v += kWave)
-          if (treg(g, v) && tpod_has(g, v)) {
+        for (int v = lane(); v < nv; v += kWave) {
+          const int c = tcnt(g, v);
+          if (c >= 0 && tpod_has(g, v)) {
             num++;
-            const int c = tcnt(g, v);
             mn = c < mn ? c : mn;
           }
+        }
         for (int off = 32; off >= 1; off >>= 1) {
           const int o = __shfl_xor(mn, off);
           mn = o < mn ? o : mn;
@@ -409,9 +407,10 @@ struct Solver {
   __device__ __forceinline__ bool topo_node_ok(int n) const {
     for (uint64_t m = t_mask; m; m &= m - 1) {
       const int g = ctz64(m);
-      const int v = D.n_tdom[(int64_t)n * d.G + g];
-      if (v < 0 || !treg(g, v)) return false;
+      const int v = D.n_tdom[(int64_t)g * d.N + n];
+      if (v < 0) return false;
       const int c = tcnt(g, v);
+      if (c < 0) return false;  // unregistered: Get never returns it
       if (tg(g, TGM_TYPE) == TG_SPREAD) {
         const int self = (int)((t_sel >> g) & 1ull);
         if ((int64_t)c + self - s_tmin[g] > tg(g, TGM_SKEW)) return false;
@@ -439,9 +438,10 @@ struct Solver {
         uint64_t best = ~0ull;
         for (int v = lane(); v < nslot; v += kWave) {
           const bool nodeHas = rs_member(L, s_trs0, k, v);
-          bool cand = nodeHas && (v >= nv || treg(g, v));
-          int c = 0;
-          if (cand) c = (v < nv ? tcnt(g, v) : tccnt(g, claim)) + self;
+          int c = -1;
+          if (nodeHas) c = v < nv ? tcnt(g, v) : tccnt(g, claim);  // placeholders are always registered
+          const bool cand = c >= 0;
+          c += self;
           if (cand && (int64_t)c - mn <= skew) {
             const uint64_t key = ((uint64_t)(uint32_t)c << 32) | (uint32_t)v;
             best = key < best ? key : best;
@@ -459,7 +459,7 @@ struct Solver {
         for (int v = lane(); v < nslot; v += kWave) {
           bool in;
           if (v < nv) {
-            in = treg(g, v) && tcnt(g, v) == 0 && tpod_has(g, v);
+            in = tcnt(g, v) == 0 && tpod_has(g, v);
           } else {
             const bool has = tpod_has(g, v);
             any = any || has;  // some registered placeholder has a zero count (the fresh claim's, at least)
@@ -486,25 +486,36 @@ struct Solver {
     ok = rdl(ok, 0);
     return ok ? 0u : (uint32_t)FC_TOPO_COMPAT;
   }
-  // Topology.Record (topology.go:125-148) for the pod's final requirements F on NodeClaim `claim`
-  // (-1: an existing node), wave-wide.
+  // Topology.Record (topology.go:125-148) for the pod's final requirements F on NodeClaim `claim`,
+  // or on existing node `node` (claim -1), wave-wide.  Only groups that count the pod are visited:
+  // owned groups whose selector selects it, inverse groups it owns.  On an existing node F[key] is
+  // the node's own label value (the strict Compatible admitted nothing else; ks_topo.cpp refuses
+  // the one input where a pod's NotIn could stand in for a missing label), so the node's domain
+  // table replaces the scan over F's value words.
   template <class PR>
-  __device__ __forceinline__ void topo_record(PR F, int claim, uint64_t allow) {
+  __device__ __forceinline__ void topo_record(PR F, int claim, int node, uint64_t allow) {
     hbm_release();
+    const uint64_t owned = d.G1 >= 64 ? ~0ull : ((1ull << d.G1) - 1);
     const uint64_t pres = rs_present(F), compl_ = rs_compl(F);
-    for (int g = 0; g < d.G; g++) {
+    for (uint64_t m = (t_sel & owned) | t_inv; m; m &= m - 1) {
+      const int g = ctz64(m);
       const bool ownedGroup = g < d.G1;
-      if (ownedGroup) {
-        if (!((t_sel >> g) & 1ull)) continue;  // Counts: selects(pod) ...
-        if (tg(g, TGM_TYPE) == TG_SPREAD && tg(g, TGM_FEND) > tg(g, TGM_FBEG)) {  // ... && nodeFilter matches
-          int match = 0;
-          if (lane() == 0)
-            for (int f = tg(g, TGM_FBEG); f < tg(g, TGM_FEND) && !match; f++)
-              match = rs_compatible(L, F, D.tg_frs + (int64_t)f * d.RSW, allow) ? 1 : 0;
-          if (!rdl(match, 0)) continue;
+      if (ownedGroup && tg(g, TGM_TYPE) == TG_SPREAD && tg(g, TGM_FEND) > tg(g, TGM_FBEG)) {  // nodeFilter
+        int match = 0;
+        if (lane() == 0)
+          for (int f = tg(g, TGM_FBEG); f < tg(g, TGM_FEND) && !match; f++)
+            match = rs_compatible(L, F, D.tg_frs + (int64_t)f * d.RSW, allow) ? 1 : 0;
+        if (!rdl(match, 0)) continue;
+      }
+      if (node >= 0) {
+        if (lane() == 0) {
+          const int v = D.n_tdom[(int64_t)g * d.N + node];
+          if (v >= 0) {
+            const int c = W.tg_cnt[tg(g, TGM_CNT) + v];  // recording registers the domain
+            W.tg_cnt[tg(g, TGM_CNT) + v] = c < 0 ? 1 : c + 1;
+          }
         }
-      } else if (!((t_inv >> g) & 1ull)) {
-        continue;  // inverse groups record where their owner lands
+        continue;
       }
       const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
       if (!bit(pres, k)) continue;  // Get() of a missing key is Exists: no values
@@ -523,8 +534,8 @@ struct Solver {
           if (v >= nv) {
             if (claim >= 0) W.tg_ccnt[(int64_t)g * (d.Kcap + 1) + claim] += 1;
           } else {
-            W.tg_cnt[tg(g, TGM_CNT) + v] += 1;
-            W.tg_reg[tg(g, TGM_REG) + (v >> 5)] |= 1u << (v & 31);
+            const int c = W.tg_cnt[tg(g, TGM_CNT) + v];
+            W.tg_cnt[tg(g, TGM_CNT) + v] = c < 0 ? 1 : c + 1;
           }
         }
       }
@@ -689,8 +700,8 @@ struct Solver {
     if ((sflags & SF_HAS_KEYS) || !INL || d.hpAny) hbm_release();
     wsync();
     if (TOPO && (t_sel | t_inv)) {  // Topology.Record on the claim's final requirements (nodeclaim.go:121)
-      if ((sflags & SF_HAS_KEYS) || t_mask) topo_record(s_rs, c, d.allowWK);
-      else topo_record(W.c_rs + (int64_t)c * d.RSW, c, d.allowWK);
+      if ((sflags & SF_HAS_KEYS) || t_mask) topo_record(s_rs, c, -1, d.allowWK);
+      else topo_record(W.c_rs + (int64_t)c * d.RSW, c, -1, d.allowWK);
     }
     algbytes += 24 * R() + 4 * d.TW + 8;
     return srt;
@@ -746,11 +757,9 @@ struct Solver {
               if (tc == FC_TOPO_COMPAT) {
                 copy_words(W.fail_rs + slot, s_rs, d.RSW);  // the topology requirements, for the message
               } else {
-                const int g = (int)(tc >> 16) & 0xff, nv = tg(g, TGM_NV), rw = (nv + 31) >> 5;
-                if (!tg(g, TGM_HOST)) {  // counts + registered domains, for the message (FSW fits them)
+                const int g = (int)(tc >> 16) & 0xff, nv = tg(g, TGM_NV);
+                if (!tg(g, TGM_HOST))  // the counts (-1: unregistered), for the message (FSW fits them)
                   for (int v = lane(); v < nv; v += kWave) W.fail_rs[slot + v] = (uint32_t)tcnt(g, v);
-                  for (int i = lane(); i < rw; i += kWave) W.fail_rs[slot + nv + i] = ld_sc1(W.tg_reg + tg(g, TGM_REG) + i);
-                }
               }
             }
           }
@@ -833,7 +842,7 @@ struct Solver {
               log_commit(p, c, nlog);
               hbm_release();  // c_rs / c_tpl / overflow state are read by other lanes later
               wsync();
-              if (TOPO && (t_sel | t_inv)) topo_record(s_rs, c, d.allowWK);
+              if (TOPO && (t_sel | t_inv)) topo_record(s_rs, c, -1, d.allowWK);
               if (inl) recompute_max<true>(c, s_rem, t, c);
               else recompute_max<false>(c, s_rem, t, c);
               if (pool >= 0) {  // subtractMax (scheduler.go:347-362)
@@ -1267,7 +1276,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           } else if ((sflags & SF_HAS_KEYS) && lane() == owner) {
             rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
           }
-          if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, 0);  // existingnode.go:121
+          if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, j, 0);  // existingnode.go:121
           S.log_commit(p, -(j + 1), nlog);
           PH_END(t7, 7);
           S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
@@ -1298,7 +1307,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         } else if (lane() == (j & (kWave - 1))) {
           S.node_commit(j, s, sflags, pod);  // the owner lane of node j
         }
-        if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, 0);  // existingnode.go:121
+        if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, j, 0);  // existingnode.go:121
         S.log_commit(p, -(j + 1), nlog);
         PH_END(t7, 7);
         placed = true;

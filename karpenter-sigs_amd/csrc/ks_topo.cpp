@@ -84,11 +84,10 @@ void Host::buildTopology() {
   tab.pod_ginv.assign(std::max(P, 1), 0);
   if (!any) {
     dims.G = dims.G1 = 0;
-    dims.tgCntWords = dims.tgRegWords = 1;
+    dims.tgCntWords = 1;
     dims.FSW = dims.RSW;
     tab.tg_meta.assign(TGM_WORDS, 0);
     tab.tg_cnt0.assign(1, 0);
-    tab.tg_reg0.assign(1, 0);
     tab.tg_frs.assign(dims.RSW, 0);
     tab.n_tdom.assign(1, -1);
     return;
@@ -294,7 +293,6 @@ void Host::buildTopology() {
   // --- device tables
   tab.tg_meta.assign((size_t)G * TGM_WORDS, 0);
   tab.tg_cnt0.clear();
-  tab.tg_reg0.clear();
   tab.tg_frs.clear();
   int maxNv = 0;
   for (int g = 0; g < G; g++) {
@@ -308,25 +306,24 @@ void Host::buildTopology() {
     m[TGM_MIND] = tg.minDomains;
     m[TGM_CNT] = (int32_t)tab.tg_cnt0.size();
     m[TGM_NV] = nv;
-    m[TGM_REG] = (int32_t)tab.tg_reg0.size();
     m[TGM_FBEG] = (int32_t)(tab.tg_frs.size() / dims.RSW);
     m[TGM_HOST] = tg.key == kHostnameKey ? 1 : 0;
-    std::vector<int32_t> cnt(std::max(nv, 1), 0);
-    std::vector<uint32_t> reg((size_t)std::max(1, (nv + 31) / 32), 0);
+    std::vector<int32_t> cnt(std::max(nv, 1), -1);  // -1: domain not registered (absent from the map)
     for (auto& kv : tg.domains) {
       auto vi = valueId[(size_t)tg.keyId].find(kv.first);
       if (vi == valueId[(size_t)tg.keyId].end())
         throw KsError(-5, "topology domain " + kv.first + " outside the value universe of " + tg.key);
       cnt[(size_t)vi->second] = kv.second;
-      reg[(size_t)vi->second >> 5] |= 1u << (vi->second & 31);
     }
     tab.tg_cnt0.insert(tab.tg_cnt0.end(), cnt.begin(), cnt.end());
-    tab.tg_reg0.insert(tab.tg_reg0.end(), reg.begin(), reg.end());
-    for (auto& f : tg.filter) tab.tg_frs.insert(tab.tg_frs.end(), f.begin(), f.end());
+    bool trivial = false;  // an empty term is Compatible with everything: the filter always matches
+    for (auto& f : tg.filter) trivial = trivial || rs_present(f.data()) == 0;
+    if (!trivial)
+      for (auto& f : tg.filter) tab.tg_frs.insert(tab.tg_frs.end(), f.begin(), f.end());
     m[TGM_FEND] = (int32_t)(tab.tg_frs.size() / dims.RSW);
   }
   if (tab.tg_frs.empty()) tab.tg_frs.assign(dims.RSW, 0);
-  tab.n_tdom.assign((size_t)std::max(N, 1) * G, -1);
+  tab.n_tdom.assign((size_t)std::max(N, 1) * G, -1);  // [G][N]: a wave reads 64 nodes of one group
   for (int n = 0; n < N; n++)
     for (int g = 0; g < G; g++) {
       const TopoGroup& tg = groups[(size_t)g];
@@ -338,7 +335,7 @@ void Host::buildTopology() {
         if (l == nodes[(size_t)n].labels.end()) continue;
         d = l->second;
       }
-      tab.n_tdom[(size_t)n * G + g] = valueId[(size_t)tg.keyId].at(d);
+      tab.n_tdom[(size_t)g * N + n] = valueId[(size_t)tg.keyId].at(d);
     }
   // A node without a group's label takes that key only from a pod's NotIn requirement
   // (existingnode.go:97-115: the strict Compatible admits nothing else), after which the topology
@@ -347,7 +344,7 @@ void Host::buildTopology() {
   for (int g = 0; g < G; g++) {
     const int k = groups[(size_t)g].keyId;
     bool unlabelled = false;
-    for (int n = 0; n < N && !unlabelled; n++) unlabelled = tab.n_tdom[(size_t)n * G + g] < 0;
+    for (int n = 0; n < N && !unlabelled; n++) unlabelled = tab.n_tdom[(size_t)g * N + n] < 0;
     if (!unlabelled) continue;
     for (auto& chain : states)
       for (auto& st : chain)
@@ -362,10 +359,9 @@ void Host::buildTopology() {
   for (auto& g : groups)
     if (g.key != kHostnameKey) {
       const int nv = (int)values[(size_t)g.keyId].size();
-      dims.FSW = std::max(dims.FSW, nv + (nv + 31) / 32);
+      dims.FSW = std::max(dims.FSW, nv);
     }
   dims.tgCntWords = (int32_t)tab.tg_cnt0.size();
-  dims.tgRegWords = (int32_t)tab.tg_reg0.size();
 }
 
 }  // namespace ks
