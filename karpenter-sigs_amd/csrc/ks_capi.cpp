@@ -24,7 +24,7 @@ namespace {
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
       log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, tg_cnt,
-      tg_ccnt, fail_rs, total;
+      tg_ccnt, tg_cpos, fail_rs, total;
 };
 
 WorkLayout work_layout(const KsDims& d) {
@@ -58,6 +58,7 @@ WorkLayout work_layout(const KsDims& d) {
   w.c_hp = a.add(8 * K);
   w.tg_cnt = a.add(4 * std::max<size_t>(d.G ? (size_t)d.tgCntWords : 1, 1));
   w.tg_ccnt = a.add(4 * (size_t)std::max(d.G, 1) * (d.G ? K + 1 : 1));
+  w.tg_cpos = a.add(4 * (size_t)std::max(d.G, 1));
   w.fail_rs = a.add(d.G ? 4 * (size_t)P * std::max(d.NTPL, 1) * d.FSW : 4);
   w.total = a.total;
   return w;
@@ -92,6 +93,7 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.c_hp = (uint64_t*)(base + w.c_hp);
   k.tg_cnt = (int32_t*)(base + w.tg_cnt);
   k.tg_ccnt = (int32_t*)(base + w.tg_ccnt);
+  k.tg_cpos = (int32_t*)(base + w.tg_cpos);
   k.fail_rs = (uint32_t*)(base + w.fail_rs);
   return k;
 }
@@ -443,7 +445,7 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
             return bit(rs_present(rec), k) ? h.reqString(rec, k, false, host) : h.keyNames[(size_t)k] + " Exists";
           };
           segs.push_back(pre + "unsatisfiable topology constraint for " +
-                         (gm[TGM_TYPE] == TG_SPREAD ? "topology spread" : "pod anti-affinity") + ", key=" +
+                         (gm[TGM_TYPE] == TG_SPREAD ? "topology spread" : gm[TGM_TYPE] == TG_AFFINITY ? "pod affinity" : "pod anti-affinity") + ", key=" +
                          h.keyNames[(size_t)k] + " (counts = " + counts + ", podDomains = " + dom(ps.rsStrict.data()) +
                          ", nodeDomains = " + dom(nr.data()) + ")");
           break;

@@ -136,7 +136,7 @@ struct KsDev {
 };
 
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };
-enum TopoGroupType : int32_t { TG_SPREAD = 0, TG_ANTI = 2 };
+enum TopoGroupType : int32_t { TG_SPREAD = 0, TG_AFFINITY = 1, TG_ANTI = 2 };
 enum TgMeta : int32_t {  // per topology group, int32 words
   TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST, TGM_WORDS = 12
 };
@@ -193,6 +193,7 @@ struct KsWork {
   uint64_t KS_G* n_hp;      // [N] host ports reserved per existing node (SIM: valid where s_tch is set)
   uint64_t KS_G* c_hp;      // [Kcap] host ports reserved per NodeClaim
   int32_t KS_G* tg_cnt;     // topology domain counts (copy of tg_cnt0)
+  int32_t KS_G* tg_cpos;    // [G] NodeClaims whose placeholder domain has a positive count
   int32_t KS_G* tg_ccnt;    // [G][Kcap] counts of the NodeClaims' hostname-placeholder domains
   uint32_t KS_G* fail_rs;   // [P][NTPL][FSW] FC_TOPO_COMPAT: requirements; FC_TOPO: the group's counts + registered bits
   // consolidation simulations only (k_solve<.., SIM=true>): this simulation's view of the shared

@@ -94,6 +94,7 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
     if (d.G) {
       for (int64_t i = gtid; i < d.tgCntWords; i += gsz) W.tg_cnt[i] = D.tg_cnt0[i];
       for (int64_t i = gtid; i < (int64_t)d.G * (d.Kcap + 1); i += gsz) W.tg_ccnt[i] = 0;
+      for (int64_t i = gtid; i < d.G; i += gsz) W.tg_cpos[i] = 0;
     }
     for (int64_t i = gtid; i < d.P; i += gsz) {
       W.queue[i] = qorder[i];
@@ -368,7 +369,9 @@ struct Solver {
     return rs_member(L, D.st_rss + (int64_t)t_s * d.RSW, tg(g, TGM_KEY), v);
   }
   // Per pop: the matching groups (getMatchingTopologies, topology.go:366-379: owned groups, then
-  // inverse groups whose selector selects the pod) and domainMinCount per spread group (:192-213).
+  // inverse groups whose selector selects the pod), domainMinCount per spread group (:192-213) and,
+  // per affinity group, whether some domain the pod allows already holds a selected pod (:215-221;
+  // for hostname keys that includes NodeClaim placeholders, counted in tg_cpos).
   __device__ __forceinline__ void topo_pop(int s, int gpod) {
     t_s = s;
     t_sel = D.pod_gsel[gpod];
@@ -378,6 +381,15 @@ struct Solver {
     t_mask = D.st_gown[s] | (t_sel & all & ~owned);
     for (uint64_t m = t_mask; m; m &= m - 1) {
       const int g = ctz64(m);
+      if (tg(g, TGM_TYPE) == TG_AFFINITY) {
+        const int nv = tg(g, TGM_NV);
+        bool pos = false;
+        for (int v = lane(); v < nv && !pos; v += kWave) pos = tcnt(g, v) > 0 && tpod_has(g, v);
+        if (lane() == 0 && tg(g, TGM_HOST) && tpod_has(g, nv) && ld_sc1(W.tg_cpos + g) > 0) pos = true;
+        const bool any = wballot(pos) != 0;
+        if (lane() == 0) s_tmin[g] = any ? 1 : 0;
+        continue;
+      }
       if (tg(g, TGM_TYPE) != TG_SPREAD) continue;
       int mn = 0x7fffffff, num = 0;
       if (!tg(g, TGM_HOST)) {  // hostname groups always have a min of 0
@@ -411,9 +423,13 @@ struct Solver {
       if (v < 0) return false;
       const int c = tcnt(g, v);
       if (c < 0) return false;  // unregistered: Get never returns it
-      if (tg(g, TGM_TYPE) == TG_SPREAD) {
+      const int type = tg(g, TGM_TYPE);
+      if (type == TG_SPREAD) {
         const int self = (int)((t_sel >> g) & 1ull);
         if ((int64_t)c + self - s_tmin[g] > tg(g, TGM_SKEW)) return false;
+      } else if (type == TG_AFFINITY) {  // a selected pod's domain, or the bootstrap for a self-selecting pod
+        if (!tpod_has(g, v)) return false;
+        if (s_tmin[g] ? c == 0 : !((t_sel >> g) & 1ull)) return false;
       } else if (c != 0 || !tpod_has(g, v)) {
         return false;
       }
@@ -454,6 +470,39 @@ struct Solver {
         if (best == ~0ull) return FC_TOPO | ((uint32_t)g << 16);
         const int bv = (int)(uint32_t)best;
         if (lane() == 0) s_trs1[L.HDR + km.off + (bv >> 5)] = 1u << (bv & 31);
+      } else if (tg(g, TGM_TYPE) == TG_AFFINITY) {  // nextDomainAffinity
+        const bool self = (t_sel >> g) & 1ull;
+        if (s_tmin[g]) {  // the domains already holding a selected pod (other placeholders drop out in Add)
+          for (int v = lane(); v < nslot; v += kWave) {
+            const int c = v < nv ? tcnt(g, v) : tccnt(g, claim);
+            if (c > 0 && tpod_has(g, v))
+              __hip_atomic_fetch_or(s_trs1 + L.HDR + km.off + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
+          }
+        } else if (self) {  // bootstrap: first registered pod∩node domain, then first registered pod domain
+          // (canonical map order = sorted names = value order; for hostname keys the claim's own
+          // placeholder is its only node domain, and any other insert drops out in Add)
+          uint32_t z1 = ~0u, z2 = ~0u;
+          for (int v = lane(); v < nslot; v += kWave) {
+            const int c = v < nv ? tcnt(g, v) : 0;
+            if (c < 0 || !tpod_has(g, v)) continue;
+            if (v < nv) z2 = (uint32_t)v < z2 ? (uint32_t)v : z2;
+            if (rs_member(L, s_trs0, k, v)) z1 = (uint32_t)v < z1 ? (uint32_t)v : z1;
+            if (v >= nv) z2 = z2 == ~0u ? (uint32_t)v : z2;  // registered, so the options are not empty
+          }
+          for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t a = __shfl_xor(z1, off), b = __shfl_xor(z2, off);
+            z1 = a < z1 ? a : z1;
+            z2 = b < z2 ? b : z2;
+          }
+          if (z1 == ~0u && z2 == ~0u) return FC_TOPO | ((uint32_t)g << 16);
+          if (lane() == 0) {
+            if (z1 != ~0u) s_trs1[L.HDR + km.off + (z1 >> 5)] |= 1u << (z1 & 31);
+            if (z2 != ~0u) s_trs1[L.HDR + km.off + (z2 >> 5)] |= 1u << (z2 & 31);
+          }
+        } else {
+          return FC_TOPO | ((uint32_t)g << 16);
+        }
       } else {  // nextDomainAntiAffinity: registered zero-count domains the pod's domains allow
         bool any = false;
         for (int v = lane(); v < nslot; v += kWave) {
@@ -520,7 +569,7 @@ struct Solver {
       const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
       if (!bit(pres, k)) continue;  // Get() of a missing key is Exists: no values
       const KeyMeta km = L.keys[k];
-      if (ownedGroup && tg(g, TGM_TYPE) == TG_SPREAD) {  // spread / affinity: only a collapsed domain
+      if (ownedGroup && tg(g, TGM_TYPE) != TG_ANTI) {  // spread / affinity: only a collapsed domain
         int tot = 0;
         for (int w = lane(); w < km.nw; w += kWave) tot += __popc(F[L.HDR + km.off + w]);
         for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off);
@@ -532,7 +581,12 @@ struct Solver {
           const int v = w * 32 + __builtin_ctz(x);
           x &= x - 1;
           if (v >= nv) {
-            if (claim >= 0) W.tg_ccnt[(int64_t)g * (d.Kcap + 1) + claim] += 1;
+            if (claim >= 0) {
+              const int64_t at = (int64_t)g * (d.Kcap + 1) + claim;
+              const int cc = W.tg_ccnt[at];
+              W.tg_ccnt[at] = cc + 1;
+              if (cc == 0) W.tg_cpos[g] += 1;  // one more placeholder holding a counted pod
+            }
           } else {
             const int c = W.tg_cnt[tg(g, TGM_CNT) + v];
             W.tg_cnt[tg(g, TGM_CNT) + v] = c < 0 ? 1 : c + 1;

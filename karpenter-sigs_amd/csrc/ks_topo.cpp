@@ -13,7 +13,7 @@
 // kernels iterate them in that order.  Every relaxation state of a pod must own a subset of the
 // groups the initial Update pass created: a group created later (a relaxed required node-affinity
 // term changes a spread group's node filter) would start counting mid-Solve, which is refused.
-// Pod (positive) affinity and namespaceSelector terms are refused (KS_ERR_UNSUPPORTED).
+// namespaceSelector terms are refused (KS_ERR_UNSUPPORTED).
 #include <algorithm>
 #include <climits>
 
@@ -93,8 +93,10 @@ void Host::buildTopology() {
     return;
   }
   for (auto& p : pods) {
-    if (!p.affRequired.empty() || !p.affPreferred.empty())
-      throw KsError(-2, "pod " + p.ns + "/" + p.name + " has pod affinity terms (not encoded by this build)");
+    for (auto& t : p.affRequired)
+      if (t.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
+    for (auto& t : p.affPreferred)
+      if (t.second.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
     for (auto& t : p.antiRequired)
       if (t.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
     for (auto& t : p.antiPreferred)
@@ -225,6 +227,11 @@ void Host::buildTopology() {
   auto ownedSpecGroups = [&](const PodH& sp) {  // newForTopologies + newForAffinities
     std::vector<TopoGroup> fresh;
     for (auto& c : sp.tsc) fresh.push_back(makeGroup(TG_SPREAD, c.key, sp, {sp.ns}, c.sel, c.maxSkew, c.minDomains));
+    if (sp.hasAffinity && sp.hasPodAffinity) {  // the type map's affinity entry first (canonical order)
+      for (auto& t : sp.affRequired) fresh.push_back(makeGroup(TG_AFFINITY, t.key, sp, termNs(sp, t), t.sel, INT32_MAX, -1));
+      for (auto& t : sp.affPreferred)
+        fresh.push_back(makeGroup(TG_AFFINITY, t.second.key, sp, termNs(sp, t.second), t.second.sel, INT32_MAX, -1));
+    }
     if (sp.hasAffinity && sp.hasPodAnti) {
       for (auto& t : sp.antiRequired) fresh.push_back(makeGroup(TG_ANTI, t.key, sp, termNs(sp, t), t.sel, INT32_MAX, -1));
       for (auto& t : sp.antiPreferred)

@@ -50,10 +50,20 @@ class PodFactory:
         self.n = 0
 
     def __call__(self, count=1, labels=None, tscs=None, node_selector=None, cpu=None, anti_required=None,
-                 anti_preferred=None, node_preferences=None):
+                 anti_preferred=None, node_preferences=None, aff_required=None, aff_preferred=None, namespace="default",
+                 node_requirements=None):
         out = []
         for _ in range(count):
             aff = {}
+            if aff_required or aff_preferred:
+                aff["podAffinity"] = {}
+                if aff_required:
+                    aff["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"] = aff_required
+                if aff_preferred:
+                    aff["podAffinity"]["preferredDuringSchedulingIgnoredDuringExecution"] = aff_preferred
+            if node_requirements:
+                aff["nodeAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": {
+                    "nodeSelectorTerms": [{"matchExpressions": node_requirements}]}}
             if anti_required or anti_preferred:
                 aff["podAntiAffinity"] = {}
                 if anti_required:
@@ -61,9 +71,10 @@ class PodFactory:
                 if anti_preferred:
                     aff["podAntiAffinity"]["preferredDuringSchedulingIgnoredDuringExecution"] = anti_preferred
             if node_preferences:
-                aff["nodeAffinity"] = {"preferredDuringSchedulingIgnoredDuringExecution": [
-                    {"weight": 1, "preference": {"matchExpressions": node_preferences}}]}
-            p = synth.pod(self.n, cpu=cpu, labels=labels, node_selector=node_selector, affinity=aff or None)
+                aff.setdefault("nodeAffinity", {})["preferredDuringSchedulingIgnoredDuringExecution"] = [
+                    {"weight": 1, "preference": {"matchExpressions": node_preferences}}]
+            p = synth.pod(self.n, cpu=cpu, labels=labels, node_selector=node_selector, affinity=aff or None,
+                          namespace=namespace)
             p["metadata"]["labels"].pop("testing/cluster", None)  # test.Pod() sets no labels
             for k, v in (labels or {}).items():
                 p["metadata"]["labels"][k] = v
@@ -200,6 +211,63 @@ def scenarios():
         P(1, node_selector={zone: Z2}, cpu="2", anti_required=[term(zone)]) +
         P(1, node_selector={zone: Z3}, cpu="2", anti_required=[term(zone)]) + P(1, sec),
         {"scheduled": [0, 1, 2], "unscheduled": [3]})
+    # Pod affinity (topology_test.go "Pod Affinity/Anti-Affinity"); single-batch assertions only
+    arch, host = synth.ARCH, synth.HOSTNAME
+    P = PodFactory()
+    add("affinity-arch", "1426-1468",
+        P(1, sec, [tsc(host, selector={"matchLabels": dict(sec)})], cpu="2", node_selector={arch: "arm64"}) +
+        P(1, sec, [tsc(host, selector={"matchLabels": dict(sec)})], cpu="1", aff_required=[term(arch)]),
+        {"scheduled": [0, 1], "distinct": [[0, 1]], "same_label": [{"key": arch, "pods": [0, 1]}]})
+    P = PodFactory()
+    add("self-affinity-hostname", "1469-1492", P(3, sec, aff_required=[term(host)]),
+        {"scheduled": [0, 1, 2], "one_node": [0, 1, 2]})
+    P = PodFactory()
+    add("self-affinity-hostname-first-domain", "1493-1534", P(10, sec, aff_required=[term(host)]),
+        {"count_scheduled": 5, "nodes_used": 1})
+    P = PodFactory()
+    add("self-affinity-zone", "1579-1602", P(3, sec, aff_required=[term(zone)]),
+        {"scheduled": [0, 1, 2], "one_node": [0, 1, 2]})
+    P = PodFactory()
+    add("self-affinity-zone-constrained", "1603-1633",
+        P(3, sec, aff_required=[term(zone)], node_requirements=[{"key": zone, "operator": "In", "values": [Z3]}]),
+        {"scheduled": [0, 1, 2], "one_node": [0, 1, 2], "label_value": {"key": zone, "value": Z3, "pods": [0, 1, 2]}})
+    P = PodFactory()
+    add("affinity-preferred-violation", "1634-1666",
+        P(10, LABELS, [tsc(host)]) + P(1, aff_preferred=[{"weight": 50, "podAffinityTerm": term(host)}]),
+        {"scheduled": [10]})
+    P = PodFactory()
+    cons = tsc(host)
+    add("affinity-preference-vs-required-spread", "2034-2068",
+        P(3, LABELS, [cons], aff_preferred=[{"weight": 50, "podAffinityTerm": term(host)}]) + P(1, sec),
+        {"scheduled": [0, 1, 2, 3], "skew": {"key": host, "counts": [1, 1, 1]}})
+    P = PodFactory()
+    add("affinity-to-missing-pod", "2114-2130", P(10, aff_required=[term(zone)]),
+        {"unscheduled": list(range(10))})
+    P = PodFactory()
+    add("affinity-zone-unconstrained-target", "2131-2163", P(10, aff_required=[term(zone)]) + P(1, sec),
+        {"unscheduled": list(range(10)), "scheduled": [10], "skew": {"key": zone, "selector": None, "counts": [1]}})
+    P = PodFactory()
+    add("affinity-zone-constrained-target", "2164-2192",
+        P(10, aff_required=[term(zone)]) +
+        P(1, sec, node_requirements=[{"key": zone, "operator": "In", "values": [Z1]}]),
+        {"scheduled": list(range(11)), "skew": {"key": zone, "selector": None, "counts": [11]}})
+    P = PodFactory()
+    db, web, cache, ui = ({"type": t, "spread": "spread"} for t in ("db", "web", "cache", "ui"))
+    dep = lambda lab: [{"labelSelector": {"matchLabels": dict(lab)}, "topologyKey": host}]  # noqa: E731
+    add("multiple-dependent-affinities", "2193-2227",
+        P(1, db) + P(1, web, aff_required=dep(db)) + P(1, cache, aff_required=dep(web)) + P(1, ui, aff_required=dep(cache)),
+        {"scheduled": [0, 1, 2, 3]})
+    P = PodFactory()
+    add("unsatisfiable-dependencies", "2228-2243", P(1, db, aff_required=dep(web)), {"unscheduled": [0]})
+    P = PodFactory()
+    add("affinity-namespace-no-match", "2244-2281",
+        P(10, LABELS, [tsc(host)]) + P(1, sec, namespace="other-ns-no-match") + P(1, aff_required=[term(host)]),
+        {"scheduled": [10], "unscheduled": [11]})
+    P = PodFactory()
+    t_ns = {"labelSelector": {"matchLabels": dict(sec)}, "namespaces": ["other-ns-list"], "topologyKey": host}
+    add("affinity-namespace-list", "2282-2320",
+        P(10, LABELS, [tsc(host)]) + P(1, sec, namespace="other-ns-list") + P(1, aff_required=[t_ns]),
+        {"scheduled": [10, 11], "one_node": [10, 11]})
     return out
 
 
@@ -279,6 +347,19 @@ def check(scn, res):
     for a, b in exp.get("distinct", []):
         if where.get(a) == where.get(b):
             bad.append("pods %d and %d share a node" % (a, b))
+    if "count_scheduled" in exp and len(scheduled) != exp["count_scheduled"]:
+        bad.append("%d scheduled, want %d" % (len(scheduled), exp["count_scheduled"]))
+    if "nodes_used" in exp and len(res["newNodeClaims"]) != exp["nodes_used"]:
+        bad.append("%d nodes, want %d" % (len(res["newNodeClaims"]), exp["nodes_used"]))
+    for same in exp.get("same_label", []):
+        vals = {node_labels(res["newNodeClaims"][where[p]], snap).get(same["key"]) for p in same["pods"] if p in where}
+        if len(vals) != 1:
+            bad.append("pods %s on %s values %s" % (same["pods"], same["key"], sorted(map(str, vals))))
+    if "label_value" in exp:
+        lv = exp["label_value"]
+        for p in lv["pods"]:
+            if p in where and node_labels(res["newNodeClaims"][where[p]], snap).get(lv["key"]) != lv["value"]:
+                bad.append("pod %d not on %s=%s" % (p, lv["key"], lv["value"]))
     if "skew" in exp:
         sk = exp["skew"]
         sel = sk.get("selector", {"matchLabels": LABELS}) if "selector" in sk else {"matchLabels": LABELS}

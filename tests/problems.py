@@ -136,7 +136,7 @@ def _anti_term(rng, app):
     return {"labelSelector": _app_selector(rng, app), "topologyKey": _pick(rng, [synth.HOSTNAME, synth.HOSTNAME, synth.ZONE])}
 
 
-def add_topology(rng, pods, nodes):
+def add_topology(rng, pods, nodes, affinity=False):
     """Topology spread (zone / hostname / capacity-type, maxSkew 1-3, minDomains, DoNotSchedule and
     ScheduleAnyway), required + preferred pod anti-affinity (topology.go, topologygroup.go) per app,
     plus bound cluster pods on the existing nodes that seed the counts (countDomains) and inverse
@@ -167,6 +167,14 @@ def add_topology(rng, pods, nodes):
             spec["anti"] = [_anti_term(rng, app)]
         if rng.random() < 0.25:
             spec["antiPref"] = [{"weight": int(rng.integers(1, 100)), "podAffinityTerm": _anti_term(rng, app)}]
+        if affinity and rng.random() < 0.3:  # to itself or to another app, zone or hostname
+            other = app if rng.random() < 0.5 else "a%d" % int(rng.integers(5))
+            spec["aff"] = [{"labelSelector": {"matchLabels": {"app": other}},
+                            "topologyKey": _pick(rng, [synth.ZONE, synth.HOSTNAME, synth.CT])}]
+        if affinity and rng.random() < 0.2:
+            spec["affPref"] = [{"weight": int(rng.integers(1, 100)), "podAffinityTerm": {
+                "labelSelector": {"matchLabels": {"app": "a%d" % int(rng.integers(5))}},
+                "topologyKey": _pick(rng, [synth.ZONE, synth.HOSTNAME])}}]
         apps[app] = spec
     for p in pods:
         app = p["metadata"]["labels"]["app"]
@@ -192,6 +200,13 @@ def add_topology(rng, pods, nodes):
             if "antiPref" in spec:
                 paa["preferredDuringSchedulingIgnoredDuringExecution"] = spec["antiPref"]
             p["spec"].setdefault("affinity", {})["podAntiAffinity"] = paa
+        if "aff" in spec or "affPref" in spec:
+            pa = {}
+            if "aff" in spec:
+                pa["requiredDuringSchedulingIgnoredDuringExecution"] = spec["aff"]
+            if "affPref" in spec:
+                pa["preferredDuringSchedulingIgnoredDuringExecution"] = spec["affPref"]
+            p["spec"].setdefault("affinity", {})["podAffinity"] = pa
     cluster = []
     for i, n in enumerate(nodes):
         for j in range(int(rng.integers(0, 4))):
@@ -207,7 +222,8 @@ def add_topology(rng, pods, nodes):
     return cluster
 
 
-def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False, topology=False):
+def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False, topology=False,
+                   affinity=False):
     rng = np.random.default_rng(seed)
     its = random_its(rng, n_its)
     n_templates = int(rng.integers(1, 4)) if n_templates is None else n_templates
@@ -268,7 +284,7 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
         for p in pods:
             if rng.random() < 0.4:
                 add_host_ports(rng, p)
-    cluster = add_topology(rng, pods, nodes) if topology else []
+    cluster = add_topology(rng, pods, nodes, affinity) if topology else []
     return {
         "wellKnownLabels": synth.FAKE_WELL_KNOWN,
         "instanceTypes": its,

@@ -74,6 +74,15 @@ def test_random_topology_parity(seed):
     assert d is None, d
 
 
+@pytest.mark.parametrize("seed", list(range(360, 384)))
+def test_random_pod_affinity_parity(seed):
+    """Required / preferred pod affinity (zone, hostname, capacity-type; to itself or another app)
+    mixed with spread and anti-affinity."""
+    want, got = _solve_both(problems.random_problem(seed, n_pods=150, topology=True, affinity=True))
+    d = _diff(want, got)
+    assert d is None, d
+
+
 @pytest.mark.parametrize("seed", [340, 341, 342, 343])
 def test_random_topology_parity_larger(seed):
     want, got = _solve_both(problems.random_problem(seed, n_pods=800, n_its=120, n_nodes=30, topology=True))
