@@ -23,7 +23,7 @@ namespace {
 
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
-      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, tg_cnt,
+      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, n_vm, n_vc, tg_cnt,
       tg_ccnt, tg_cpos, fail_rs, total;
 };
 
@@ -56,6 +56,8 @@ WorkLayout work_layout(const KsDims& d) {
   w.counters = a.add(8 * CT_NCOUNTERS);
   w.n_hp = a.add(8 * N);
   w.c_hp = a.add(8 * K);
+  w.n_vm = a.add(d.volAny ? 8 * N : 8);
+  w.n_vc = a.add(d.volAny ? 4 * N * d.VD : 4);
   w.tg_cnt = a.add(4 * std::max<size_t>(d.G ? (size_t)d.tgCntWords : 1, 1));
   w.tg_ccnt = a.add(4 * (size_t)std::max(d.G, 1) * (d.G ? K + 1 : 1));
   w.tg_cpos = a.add(4 * (size_t)std::max(d.G, 1));
@@ -91,6 +93,8 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.counters = (int64_t*)(base + w.counters);
   k.n_hp = (uint64_t*)(base + w.n_hp);
   k.c_hp = (uint64_t*)(base + w.c_hp);
+  k.n_vm = (uint64_t*)(base + w.n_vm);
+  k.n_vc = (int32_t*)(base + w.n_vc);
   k.tg_cnt = (int32_t*)(base + w.tg_cnt);
   k.tg_ccnt = (int32_t*)(base + w.tg_ccnt);
   k.tg_cpos = (int32_t*)(base + w.tg_cpos);
@@ -175,6 +179,11 @@ void ks_upload(ks_problem* pb) {
   size_t o_phc = put(t.pod_hpc.data(), t.pod_hpc.size() * 8);
   size_t o_phu = put(t.pod_hpu.data(), t.pod_hpu.size() * 8);
   size_t o_nhp = put(t.n_hp0.data(), t.n_hp0.size() * 8);
+  size_t o_pvm = put(t.pod_vm.data(), t.pod_vm.size() * 8);
+  size_t o_vdm = put(t.vol_dm.data(), t.vol_dm.size() * 8);
+  size_t o_nvm = put(t.n_vm0.data(), t.n_vm0.size() * 8);
+  size_t o_nvc = put(t.n_vc0.data(), t.n_vc0.size() * 4);
+  size_t o_nvl = put(t.n_vlim.data(), t.n_vlim.size() * 4);
   size_t o_tgm = put(t.tg_meta.data(), t.tg_meta.size() * 4);
   size_t o_tgc = put(t.tg_cnt0.data(), t.tg_cnt0.size() * 4);
   size_t o_tgf = put(t.tg_frs.data(), t.tg_frs.size() * 4);
@@ -230,6 +239,11 @@ void ks_upload(ks_problem* pb) {
   D.pod_hpc = (const uint64_t*)(b + o_phc);
   D.pod_hpu = (const uint64_t*)(b + o_phu);
   D.n_hp0 = (const uint64_t*)(b + o_nhp);
+  D.pod_vm = (const uint64_t*)(b + o_pvm);
+  D.vol_dm = (const uint64_t*)(b + o_vdm);
+  D.n_vm0 = (const uint64_t*)(b + o_nvm);
+  D.n_vc0 = (const int32_t*)(b + o_nvc);
+  D.n_vlim = (const int32_t*)(b + o_nvl);
   D.tg_meta = (const int32_t*)(b + o_tgm);
   D.tg_cnt0 = (const int32_t*)(b + o_tgc);
   D.tg_frs = (const uint32_t*)(b + o_tgf);

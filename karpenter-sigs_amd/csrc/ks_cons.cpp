@@ -232,6 +232,8 @@ void build_cons(ks_cons& c, const Value& root) {
   h.build(solveRoot);
   if (h.dims.dupUids) throw KsError(KS_ERR_UNSUPPORTED, "consolidation snapshot has duplicate pod UIDs");
   if (h.dims.G) throw KsError(KS_ERR_UNSUPPORTED, "topology constraints in consolidation simulations are not encoded yet");
+  if (h.dims.volAny)
+    throw KsError(KS_ERR_UNSUPPORTED, "volume limits in consolidation simulations are not encoded yet");
   c.hostnameSeed = h.hostnameSeed;
   std::map<std::string, int> hostNode;  // node name -> host.nodes index (sorted order)
   for (size_t i = 0; i < h.nodes.size(); i++) hostNode[h.nodes[i].name] = (int)i;

@@ -320,6 +320,14 @@ PodH parse_pod(const Value& v) {
   }
   p.requests = podRequests(v, p.hostPorts, p.volumes);
   if (sp)
+    if (auto* vs = sp->get("volumes"))  // volume.GetPersistentVolumeClaim (utils/volume/volume.go:29-38)
+      for (auto& vol : vs->arr()) {
+        if (auto* pvc = vol.get("persistentVolumeClaim"); pvc && !pvc->is_null())
+          p.pvcNames.push_back(jstr(pvc, "claimName"));
+        else if (auto* eph = vol.get("ephemeral"); eph && !eph->is_null())
+          p.pvcNames.push_back(p.name + "-" + jstr(&vol, "name"));
+      }
+  if (sp)
     if (auto* cs = sp->get("containers"))
       for (auto& c : cs->arr())
         if (auto* ps = c.get("ports"))
@@ -553,6 +561,11 @@ void Host::build(const Value& root) {
             n.hostPorts.push_back({kv.first, make_host_port(x.get("ip") ? x.get("ip")->str() : "0.0.0.0",
                                                             (int32_t)(x.get("port") ? x.get("port")->i64() : 0),
                                                             x.get("protocol") ? x.get("protocol")->str() : "TCP")});
+      if (auto* vu = e.get("volumeUsage"))  // StateNode.VolumeUsage(): driver -> PVC keys
+        for (auto& kv : vu->obj())
+          for (auto& x : kv.second.arr()) n.volumes[kv.first].insert(x.str());
+      if (auto* vl = e.get("volumeLimits"))  // CSINode drivers' allocatable counts (cluster.go:468)
+        for (auto& kv : vl->obj()) n.volumeLimits[kv.first] = kv.second.i64();
       n.origIndex = (int)nodes.size();
       nodes.push_back(std::move(n));
     }
@@ -562,8 +575,8 @@ void Host::build(const Value& root) {
   });
   if (auto* v = root.get("daemonSetPods")) for (auto& e : v->arr()) daemons.push_back(parse_pod(e));
   if (auto* v = root.get("pods")) for (auto& e : v->arr()) pods.push_back(parse_pod(e));
-  for (auto& p : pods)
-    if (p.volumes) throw KsError(-2, "pod " + p.ns + "/" + p.name + " mounts PVC volumes (not encoded by this build)");
+  if (auto* v = root.get("volumeDrivers"))
+    for (auto& kv : v->obj()) volumeDrivers[kv.first] = kv.second.str();
 
   // --- universe of keys and values
   internKey(kHostname);
@@ -868,6 +881,74 @@ void Host::build(const Value& root) {
     return m;
   };
   dims.hpAny = hostPortUniverse.empty() ? 0 : 1;
+  // --- volume limits (ExistingNode.Add: GetVolumes + VolumeUsage.ExceedsLimits, existingnode.go:70-78).
+  // GetVolumes skips PVCs the snapshot does not resolve (NotFound) and empty drivers.  Only drivers some
+  // node limits can fail the check; their pending-pod PVCs form the universe.  Per node and driver:
+  // |usage ∪ pod| = count + |pod PVCs not yet mounted|.  A node already over a limit rejects every pod
+  // (the union always holds its own set), which the encoder folds into an unsatisfiable Available().
+  std::set<std::string> limited;
+  for (auto& n : nodes)
+    for (auto& kv : n.volumeLimits) {
+      if (kv.second < 0 || kv.second > INT32_MAX)
+        throw KsError(-2, "node " + n.name + ": volume limit out of range for driver " + kv.first);
+      limited.insert(kv.first);
+    }
+  auto podVolumes = [&](const PodH& p) {  // GetVolumes (volumeusage.go:82-113)
+    std::vector<std::pair<std::string, std::string>> out;  // (driver, pvc key)
+    for (auto& name : p.pvcNames) {
+      auto it = volumeDrivers.find(p.ns + "/" + name);
+      if (it == volumeDrivers.end() || it->second.empty()) continue;
+      out.push_back({it->second, p.ns + "/" + name});
+    }
+    return out;
+  };
+  std::map<std::string, int> volBit;
+  for (auto& p : pods)
+    for (auto& dv : podVolumes(p)) {
+      if (!limited.count(dv.first) || volBit.count(dv.second)) continue;
+      if (std::find(volDrivers.begin(), volDrivers.end(), dv.first) == volDrivers.end()) volDrivers.push_back(dv.first);
+      volBit[dv.second] = (int)volUniverse.size();
+      volUniverse.push_back(dv.second);
+    }
+  if (volUniverse.size() > 64) throw KsError(-3, "more than 64 distinct PVCs of limited drivers in the pending pods");
+  if (volDrivers.size() > (size_t)kMaxVD) throw KsError(-3, "more than 4 limited CSI drivers in the pending pods");
+  dims.volAny = volUniverse.empty() ? 0 : 1;
+  const int VD = (int)volDrivers.size();
+  dims.VD = VD;
+  tab.vol_dm.assign(std::max(VD, 1), 0);
+  for (int v = 0; v < VD; v++)
+    for (auto& p : pods)
+      for (auto& dv : podVolumes(p))
+        if (dv.first == volDrivers[v]) tab.vol_dm[v] |= 1ull << volBit[dv.second];
+  tab.n_vm0.assign(std::max(N, 1), 0);
+  tab.n_vc0.assign((size_t)std::max(N, 1) * std::max(VD, 1), 0);
+  tab.n_vlim.assign((size_t)std::max(N, 1) * std::max(VD, 1), INT32_MAX);
+  std::vector<char> volBlocked(std::max(N, 1), 0);
+  for (int i = 0; i < N; i++) {
+    Node& n = nodes[i];
+    for (auto& kv : n.volumeLimits) {
+      auto u = n.volumes.find(kv.first);
+      if (u != n.volumes.end() && (int64_t)u->second.size() > kv.second) volBlocked[i] = 1;
+    }
+    for (int v = 0; v < VD; v++) {
+      auto u = n.volumes.find(volDrivers[v]);
+      if (u != n.volumes.end()) {
+        tab.n_vc0[(size_t)i * VD + v] = (int32_t)u->second.size();
+        for (auto& key : u->second) {
+          auto b = volBit.find(key);
+          if (b != volBit.end()) tab.n_vm0[i] |= 1ull << b->second;
+        }
+      }
+      auto l = n.volumeLimits.find(volDrivers[v]);
+      if (l != n.volumeLimits.end()) tab.n_vlim[(size_t)i * VD + v] = (int32_t)l->second;
+    }
+  }
+  tab.pod_vm.assign(std::max((int)pods.size(), 1), 0);
+  for (size_t i = 0; i < pods.size(); i++)
+    for (auto& dv : podVolumes(pods[i])) {
+      auto b = volBit.find(dv.second);
+      if (b != volBit.end()) tab.pod_vm[i] |= 1ull << b->second;
+    }
   for (int i = 0; i < N; i++) {
     Node& n = nodes[i];
     tab.n_flags[i] = (!n.initialized || !n.ready) ? NF_UNUSABLE : 0;
@@ -898,6 +979,7 @@ void Host::build(const Value& root) {
       if (kv.second.n < 0) kv.second.n = 0;
     }
     vec(n.available, &tab.n_avail[(size_t)i * R]);
+    if (volBlocked[i]) tab.n_avail[(size_t)i * R] = -1;  // Fits fails on any negative total (resources.go:166-170)
     vec(n.req0, &tab.n_req0[(size_t)i * R]);
     addNSR(lab, kHostname, "In", {n.hostName});
     std::copy(lab.begin(), lab.end(), tab.n_rs0.begin() + (size_t)i * dims.RSW);

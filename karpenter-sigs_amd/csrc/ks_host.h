@@ -59,6 +59,7 @@ struct PodH {
   std::vector<TolH> tols;
   QList requests;  // RequestsForPods(pod) incl. pods=1
   bool hostPorts = false, volumes = false;
+  std::vector<std::string> pvcNames;  // volume.GetPersistentVolumeClaim names (claimName / <pod>-<volume>)
   std::vector<HostPortH> ports;  // GetHostPorts (hostportusage.go:92-114)
   bool provisionable = true;  // IsProvisionable (pkg/utils/pod/scheduling.go:28-34)
   // fields the disruption path reads (node.go:32-53 GetNodePods, helpers.go:137-159, scheduling.go:85-92)
@@ -111,6 +112,8 @@ struct Host {
   // taints
   std::vector<TaintH> taints;
   std::vector<HostPortH> hostPortUniverse;  // distinct (IP, port, protocol), bit i of the host-port masks
+  std::map<std::string, std::string> volumeDrivers;  // "ns/pvc" -> resolved CSI driver (resolveDriver, volumeusage.go:115-172)
+  std::vector<std::string> volDrivers, volUniverse;  // limited drivers; the pending pods' PVC keys (bit i)
   // instance types
   struct Offer { std::string zone, ct; double price = 0; bool available = true; };
   struct IT { std::string name; std::vector<NSR> reqs; QList capacity, alloc; std::vector<std::pair<std::string, std::string>> offers;
@@ -135,7 +138,9 @@ struct Host {
   // existing nodes (sorted)
   struct Node { std::string name, hostName; std::map<std::string, std::string> labels; std::vector<TaintH> taints;
                 QList available, capacity, dsRequests, req0; bool initialized = true, ready = true; int origIndex = 0;
-                std::vector<std::pair<std::string, HostPortH>> hostPorts; };  // HostPortUsage: (pod key, port)
+                std::vector<std::pair<std::string, HostPortH>> hostPorts;  // HostPortUsage: (pod key, port)
+                std::map<std::string, std::set<std::string>> volumes;      // VolumeUsage: driver -> PVC keys
+                std::map<std::string, int64_t> volumeLimits; };            // driver -> CSINode allocatable count
   std::vector<Node> nodes;
   std::vector<PodH> daemons;
   std::vector<PodH> pods;
@@ -156,6 +161,8 @@ struct Host {
     std::vector<double> off_price;
     std::vector<int32_t> n_flags, pod_flags;
     std::vector<uint64_t> pod_hpc, pod_hpu, n_hp0;
+    std::vector<uint64_t> pod_vm, vol_dm, n_vm0;  // volume limits (volumeusage.go:183-227)
+    std::vector<int32_t> n_vc0, n_vlim;
     // topology groups (ks_topo.cpp)
     std::vector<int32_t> tg_meta;   // [G][TGM_WORDS]
     std::vector<int32_t> tg_cnt0;   // counts per (group, value) at NewScheduler time

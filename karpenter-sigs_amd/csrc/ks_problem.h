@@ -26,6 +26,7 @@ namespace ks {
 constexpr int kMaxR = 16;         // resource names per problem
 constexpr int kMaxTpl = 32;       // NodeClaimTemplates (NodePools) per problem
 constexpr int kWave = 64;
+constexpr int kMaxVD = 4;        // CSI drivers with a volume limit that pending pods mount
 
 enum PodStatus : int32_t { ST_PENDING = 0, ST_SCHEDULED = 1, ST_FAILED = 2 };
 enum FailCode : uint32_t {
@@ -65,6 +66,8 @@ struct KsDims {
   int32_t tgMaxNv;         // largest value universe of a topology key
   int32_t tgCntWords;      // size of the count table
   int32_t FSW;             // fail_rs words per (pod, template): RSW, or counts + registered bits if larger
+  int32_t volAny;          // some pending pod mounts a PVC of a driver an existing node limits
+  int32_t VD;              // limited drivers (<= kMaxVD); vol_dm[VD] partitions the pods' PVC universe
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
@@ -124,6 +127,13 @@ struct KsDev {
   const uint64_t KS_G* pod_hpc;    // [P] host-port triples a pod's ports Match (conflict mask)
   const uint64_t KS_G* pod_hpu;    // [P] host-port triples a pod reserves
   const uint64_t KS_G* n_hp0;      // [N] host-port triples reserved on an existing node
+  // volume limits (volumeusage.go:183-227): the pending pods' PVCs of limited drivers are a <=64-bit
+  // universe; a node's usage per driver is a count (all its PVCs) plus the universe bits it mounts
+  const uint64_t KS_G* pod_vm;     // [P] universe PVCs the pod mounts (GetVolumes)
+  const uint64_t KS_G* vol_dm;     // [VD] universe PVCs resolved to driver v
+  const uint64_t KS_G* n_vm0;      // [N] universe PVCs mounted on the node
+  const int32_t KS_G* n_vc0;       // [N][VD] PVCs of driver v mounted on the node
+  const int32_t KS_G* n_vlim;      // [N][VD] the node's limit for driver v (INT32_MAX: none)
   // topology (topology.go; ks_topo.cpp)
   const int32_t KS_G* tg_meta;     // [G][TGM_WORDS]
   const int32_t KS_G* tg_cnt0;     // per group: domain counts over its key's values, -1 = not registered (NewTopology state)
@@ -192,6 +202,8 @@ struct KsWork {
   int64_t KS_G* counters;   // [16]
   uint64_t KS_G* n_hp;      // [N] host ports reserved per existing node (SIM: valid where s_tch is set)
   uint64_t KS_G* c_hp;      // [Kcap] host ports reserved per NodeClaim
+  uint64_t KS_G* n_vm;      // [N] volume usage per existing node (copies of n_vm0 / n_vc0)
+  int32_t KS_G* n_vc;       // [N][VD]
   int32_t KS_G* tg_cnt;     // topology domain counts (copy of tg_cnt0)
   int32_t KS_G* tg_cpos;    // [G] NodeClaims whose placeholder domain has a positive count
   int32_t KS_G* tg_ccnt;    // [G][Kcap] counts of the NodeClaims' hostname-placeholder domains

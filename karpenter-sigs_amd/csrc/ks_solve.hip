@@ -91,6 +91,10 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
     for (int64_t i = gtid; i < (int64_t)d.N * d.R; i += gsz) W.n_req[i] = D.n_req0[i];
     for (int64_t i = gtid; i < (int64_t)d.N * d.RSW; i += gsz) W.n_rs[i] = D.n_rs0[i];
     for (int64_t i = gtid; i < d.N; i += gsz) W.n_hp[i] = D.n_hp0[i];
+    if (d.volAny) {
+      for (int64_t i = gtid; i < d.N; i += gsz) W.n_vm[i] = D.n_vm0[i];
+      for (int64_t i = gtid; i < (int64_t)d.N * d.VD; i += gsz) W.n_vc[i] = D.n_vc0[i];
+    }
     if (d.G) {
       for (int64_t i = gtid; i < d.tgCntWords; i += gsz) W.tg_cnt[i] = D.tg_cnt0[i];
       for (int64_t i = gtid; i < (int64_t)d.G * (d.Kcap + 1); i += gsz) W.tg_ccnt[i] = 0;
@@ -118,7 +122,7 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 template <int RT>
 struct Window {
   int p, g, uid, s, flags, toltpl, pf, st;
-  uint64_t ll, tol0, tol1, hpc, hpu;
+  uint64_t ll, tol0, tol1, hpc, hpu, vm;
   int64_t req[RT > 0 ? RT : kMaxR];
 };
 
@@ -166,6 +170,7 @@ struct Solver {
   int t_s = 0;          // the popped pod's relaxation state
   int64_t algbytes = 0;
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
+  uint64_t cur_vm = 0;                // the popped pod's PVCs of limited drivers (Solve only; SIM refuses them)
 
   __device__ Solver(const KsDev& D_, const KsWork& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
   __device__ __forceinline__ int R() const { return RT > 0 ? RT : d.R; }
@@ -251,6 +256,22 @@ struct Solver {
   }
 
   // --- existing nodes (ExistingNode.Add, existingnode.go:64-124) -------------------------------
+  // VolumeUsage.ExceedsLimits (volumeusage.go:202-209) for the popped pod's PVCs: per limited driver,
+  // the node's count plus the pod's PVCs it does not mount yet.  Nodes over a limit before the Solve
+  // never fit (the encoder's Available()), so a pod without PVCs needs no check.
+  __device__ __forceinline__ bool vol_ok(int n) const {
+    const uint64_t add = cur_vm & ~W.n_vm[n];
+    bool ok = true;
+    for (int v = 0; v < d.VD; v++)
+      ok &= W.n_vc[(int64_t)n * d.VD + v] + __popcll(add & D.vol_dm[v]) <= D.n_vlim[(int64_t)n * d.VD + v];
+    return ok;
+  }
+  // VolumeUsage.Add (existingnode.go:122), by node n's owner lane.
+  __device__ __forceinline__ void vol_commit(int n) const {
+    const uint64_t add = cur_vm & ~W.n_vm[n];
+    for (int v = 0; v < d.VD; v++) W.n_vc[(int64_t)n * d.VD + v] += __popcll(add & D.vol_dm[v]);
+    W.n_vm[n] |= cur_vm;
+  }
   // Lane (n & 63) is the only lane that ever reads or writes node n's mutable state.
   __device__ __forceinline__ bool tbit(LU32 m, int n) const { return (m[n >> 5] >> (n & 31)) & 1u; }
   // Existing-node check for two nodes per lane (positions n and n + 64 of the first-fit order):
@@ -297,6 +318,10 @@ struct Solver {
       ok0 &= (a0[r] >= 0) & (q0[r] + pod[r] <= a0[r]);
       ok1 &= (a1[r] >= 0) & (q1[r] + pod[r] <= a1[r]);
     }
+    if (!SIM && d.volAny && cur_vm) {
+      if (ok0) ok0 = vol_ok(c0);
+      if (ok1) ok1 = vol_ok(c1);
+    }
     if (sflags & SF_HAS_KEYS) {  // strict Compatible: no AllowUndefinedWellKnownLabels
       if (ok0) ok0 = rs_compatible(L, node_rs(c0), D.st_rs + (int64_t)s * d.RSW, 0);
       if (ok1) ok1 = rs_compatible(L, node_rs(c1), D.st_rs + (int64_t)s * d.RSW, 0);
@@ -314,6 +339,7 @@ struct Solver {
   __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod) {
     for (int r = 0; r < R(); r++) W.n_req[(int64_t)j * R() + r] += pod[r];
     if (d.hpAny) W.n_hp[j] |= cur_hpu;
+    if (d.volAny && cur_vm) vol_commit(j);
     if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
   }
   // SIM: copy-on-write commit (wave-uniform).  W.n_req is indexed by node but only the nodes a pod
@@ -1096,6 +1122,7 @@ struct Solver {
       w.tol1 = D.st_tol[2 * w.s + 1];
       w.hpc = D.pod_hpc[w.g];
       w.hpu = D.pod_hpu[w.g];
+      w.vm = SIM ? 0 : D.pod_vm[w.g];
 #pragma unroll
       for (int r = 0; r < RM; r++) {
         if (RT == 0 && r >= d.R) break;
@@ -1275,6 +1302,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       S.cur_hpc = (uint64_t)rdl64((int64_t)w.hpc, wi);
       S.cur_hpu = (uint64_t)rdl64((int64_t)w.hpu, wi);
     }
+    if (!SIM && d.volAny) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
     if (TOPO) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
 #pragma unroll
     for (int r = 0; r < RM; r++) {
@@ -1300,6 +1328,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
           for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
           ok &= (whp[k] & S.cur_hpc) == 0;
+          if (!SIM && d.volAny && S.cur_vm && ok) ok = S.vol_ok(n);
           if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), D.st_rs + (int64_t)s * d.RSW, 0);
           if (TOPO && S.t_mask && ok) ok = S.topo_node_ok(n);
           const uint64_t m = wballot(ok);
@@ -1321,6 +1350,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                 for (int r = 0; r < RM; r++) wrq[k][r] += pod[r];
                 whp[k] |= S.cur_hpu;
+                if (!SIM && d.volAny && S.cur_vm) S.vol_commit(j);
               }
             }
           PH_BEGIN(t7);

@@ -407,6 +407,7 @@ struct Pod {
   map<string, string> annotations;
   bool hasPriority = false;
   int32_t priority = 0;
+  vector<string> pvcNames;  // spec.volumes: persistentVolumeClaim.claimName, or <pod>-<volume> for ephemeral
 };
 
 // pkg/utils/pod/scheduling.go:28-34
@@ -584,6 +585,32 @@ struct NodeClaimTemplate {  // nodeclaimtemplate.go:35-53
   vector<int> instanceTypes;  // indices into Problem::its (the pool's GetInstanceTypes list)
 };
 struct NodePoolLimits { string name; bool hasLimits = false; ResourceList limits; bool preferNoSchedule = false; };
+// VolumeUsage (volumeusage.go:183-227): driver -> unique PVC keys mounted, and per-driver limits
+// (CSINode allocatable counts, cluster.go:468).
+using Volumes = map<string, set<string>>;
+struct VolumeUsage {
+  Volumes volumes;
+  map<string, int> limits;
+  bool ExceedsLimits(const Volumes& add) const {  // volumeusage.go:202-209
+    for (auto& kv : add) {
+      auto l = limits.find(kv.first);
+      if (l == limits.end()) continue;
+      set<string> u = kv.second;
+      auto e = volumes.find(kv.first);
+      if (e != volumes.end()) u.insert(e->second.begin(), e->second.end());
+      if ((int)u.size() > l->second) return true;
+    }
+    for (auto& kv : volumes) {  // drivers only the node mounts: the union is the node's own set
+      if (add.count(kv.first)) continue;
+      auto l = limits.find(kv.first);
+      if (l != limits.end() && (int)kv.second.size() > l->second) return true;
+    }
+    return false;
+  }
+  void Add(const Volumes& v) {
+    for (auto& kv : v) volumes[kv.first].insert(kv.second.begin(), kv.second.end());
+  }
+};
 struct StateNodeSnap {
   string name, hostName;
   map<string, string> labels;
@@ -591,6 +618,7 @@ struct StateNodeSnap {
   ResourceList available, capacity, daemonSetRequests;
   bool initialized = true;
   HostPortUsage hostPorts;
+  VolumeUsage volumes;
 };
 struct Problem {
   set<string> wellKnown;
@@ -605,7 +633,20 @@ struct Problem {
   // cluster state the Topology counts (topology.go:190-291): bound pods and node labels by node name
   vector<Pod> clusterPods;
   map<string, map<string, string>> nodeLabels;
+  map<string, string> volumeDrivers;  // "ns/pvc" -> resolved CSI driver (resolveDriver, volumeusage.go:115-172)
 };
+
+// GetVolumes (volumeusage.go:82-113): PVCs the snapshot does not list are NotFound (skipped); an empty
+// driver (unbound PVC without a storage class) is skipped too.
+static Volumes GetVolumes(const Problem& pb, const Pod& p) {
+  Volumes v;
+  for (auto& name : p.pvcNames) {
+    auto d = pb.volumeDrivers.find(p.ns + "/" + name);
+    if (d == pb.volumeDrivers.end() || d->second.empty()) continue;
+    v[d->second].insert(p.ns + "/" + name);
+  }
+  return v;
+}
 
 // ---------------------------------------------------------------------------------------------
 // JSON -> model
@@ -751,6 +792,14 @@ static Pod parsePod(const ojson::Value& v) {
                             t.get("podAffinityTerm") ? parseAffinityTerm(*t.get("podAffinityTerm")) : PodAffinityTermS{}});
       }
     }
+    if (auto* vs = sp->get("volumes"))  // volume.GetPersistentVolumeClaim (utils/volume/volume.go:29-38)
+      for (auto& vol : vs->arr()) {
+        const string vname = vol.get("name") ? vol.get("name")->str() : "";
+        if (auto* pvc = vol.get("persistentVolumeClaim"); pvc && !pvc->is_null())
+          p.pvcNames.push_back(pvc->get("claimName") ? pvc->get("claimName")->str() : "");
+        else if (auto* eph = vol.get("ephemeral"); eph && !eph->is_null())
+          p.pvcNames.push_back(p.name + "-" + vname);
+      }
     if (auto* ts = sp->get("tolerations"))
       for (auto& t : ts->arr()) {
         Toleration tol;
@@ -879,6 +928,11 @@ static Problem parseProblem(const ojson::Value& root) {
       n.capacity = resList(v.get("capacity"));
       n.daemonSetRequests = resList(v.get("daemonSetRequests"));
       n.initialized = v.get("initialized") ? v.get("initialized")->boolean(true) : true;
+      if (auto* vu = v.get("volumeUsage"))
+        for (auto& kv : vu->obj())
+          for (auto& x : kv.second.arr()) n.volumes.volumes[kv.first].insert(x.str());
+      if (auto* vl = v.get("volumeLimits"))
+        for (auto& kv : vl->obj()) n.volumes.limits[kv.first] = (int)kv.second.i64();
       if (auto* hp = v.get("hostPortUsage"))
         for (auto& kv : hp->obj()) {
           vector<HostPort> ports;
@@ -897,6 +951,8 @@ static Problem parseProblem(const ojson::Value& root) {
   if (auto* ps = root.get("pods")) for (auto& v : ps->arr()) pb.pods.push_back(parsePod(v));
   if (auto* hs = root.get("hostnameSeed")) pb.hostnameSeed = hs->i64();
   if (auto* et = root.get("emptyTopology")) pb.emptyTopology = et->boolean();
+  if (auto* vd = root.get("volumeDrivers"))
+    for (auto& kv : vd->obj()) pb.volumeDrivers[kv.first] = kv.second.str();
   if (auto* cps = root.get("clusterPods")) for (auto& v : cps->arr()) pb.clusterPods.push_back(parsePod(v));
   for (auto& n : pb.nodes) pb.nodeLabels[n.name] = n.labels;
   if (auto* cns = root.get("clusterNodes"))
@@ -926,6 +982,7 @@ struct ExistingNode {
   ResourceList requests;
   Requirements reqs;
   HostPortUsage hostPorts;
+  VolumeUsage volumes;
 };
 
 struct FilterResults {  // nodeclaim.go:144-160
@@ -1001,6 +1058,7 @@ class Scheduler {
       en.reqs = NewLabelRequirements(n.labels);
       en.reqs.Add(NewRequirement(kHostname, "In", {n.hostName}));
       en.hostPorts = n.hostPorts;
+      en.volumes = n.volumes;
       topo_.Register(kHostname, n.hostName);  // NewExistingNode (existingnode.go:60)
       existing_.push_back(std::move(en));
       auto lp = n.labels.find(kNodePool);
@@ -1180,6 +1238,8 @@ class Scheduler {
     if (!Tolerates(sn.taints, pod).empty()) return false;
     vector<HostPort> hp = GetHostPorts(pod);
     string key = pod.ns + "/" + pod.name;
+    Volumes vols = GetVolumes(pb_, pod);
+    if (n.volumes.ExceedsLimits(vols)) return false;  // existingnode.go:76-78
     if (n.hostPorts.Conflicts(key, hp)) return false;
     ResourceList podReq = RequestsForPods({&pod});
     ResourceList requests = Merge({&n.requests, &podReq});
@@ -1199,6 +1259,7 @@ class Scheduler {
     n.reqs = nodeReqs;
     topo_.Record(pod, nodeReqs, nullptr);
     n.hostPorts.Add(key, hp);
+    n.volumes.Add(vols);  // existingnode.go:122
     return true;
   }
 

@@ -122,6 +122,48 @@ def add_host_ports(rng, pod):
     pod["spec"]["containers"][0]["ports"] = ports
 
 
+VOL_DRIVERS = ["ebs.csi.aws.com", "fake.csi.provider", "efs.csi.aws.com", "unlimited.csi"]
+
+
+def add_volumes(rng, pods, nodes):
+    """PVC volumes (volumeusage.go:82-227): pods mount 0-3 of a 40-claim pool (persistentVolumeClaim or
+    ephemeral <pod>-<volume>), claims resolve to one of 4 drivers, to "" (skipped) or not at all
+    (NotFound, skipped); nodes carry CSINode limits for some drivers (0-6) and an existing usage that
+    shares claims with the pods (sometimes already over its limit).  Returns the volumeDrivers map."""
+    claims = ["claim-%02d" % i for i in range(40)]
+    drivers = {}
+    for c in claims:
+        u = rng.random()
+        if u < 0.85:
+            drivers["default/" + c] = _pick(rng, VOL_DRIVERS)
+        elif u < 0.92:
+            drivers["default/" + c] = ""
+    for p in pods:
+        if rng.random() < 0.55:
+            vols = []
+            for k in range(int(rng.integers(1, 4))):
+                if rng.random() < 0.15:
+                    vols.append({"name": "eph%d" % k, "ephemeral": {"volumeClaimTemplate": {"spec": {}}}})
+                    drivers["default/%s-eph%d" % (p["metadata"]["name"], k)] = _pick(rng, VOL_DRIVERS[:2])
+                else:
+                    vols.append({"name": "v%d" % k, "persistentVolumeClaim": {"claimName": _pick(rng, claims)}})
+            p["spec"]["volumes"] = vols
+    for n in nodes:
+        lim = {}
+        for d in VOL_DRIVERS[:3]:
+            if rng.random() < 0.7:
+                lim[d] = int(rng.integers(0, 7))
+        usage = {}
+        for d in VOL_DRIVERS:
+            if rng.random() < 0.5:
+                mine = ["default/bound-%s-%d" % (n["name"], i) for i in range(int(rng.integers(0, 3)))]
+                shared = ["default/" + c for c in rng.choice(claims, size=int(rng.integers(0, 3)), replace=False)]
+                usage[d] = sorted(set(mine + [c for c in shared if drivers.get(c) == d]))
+        n["volumeLimits"] = lim
+        n["volumeUsage"] = usage
+    return drivers
+
+
 TOPO_KEYS = [synth.ZONE, synth.HOSTNAME, synth.CT]
 
 
@@ -223,7 +265,7 @@ def add_topology(rng, pods, nodes, affinity=False):
 
 
 def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False, topology=False,
-                   affinity=False):
+                   affinity=False, volumes=False):
     rng = np.random.default_rng(seed)
     its = random_its(rng, n_its)
     n_templates = int(rng.integers(1, 4)) if n_templates is None else n_templates
@@ -285,7 +327,9 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
             if rng.random() < 0.4:
                 add_host_ports(rng, p)
     cluster = add_topology(rng, pods, nodes, affinity) if topology else []
+    vdrivers = add_volumes(rng, pods, nodes) if volumes else {}
     return {
+        "volumeDrivers": vdrivers,
         "wellKnownLabels": synth.FAKE_WELL_KNOWN,
         "instanceTypes": its,
         "instanceTypesByNodePool": by_pool,

@@ -145,3 +145,31 @@ def test_small_lds_budget_config2_overflow():
     assert len(want["newNodeClaims"]) > 19
     got = Scheduler(s).solve(lds_budget=6000)
     assert _diff(problems.canonical(want), got) is None
+
+
+@pytest.mark.parametrize("seed", list(range(300, 316)))
+def test_volume_limits_parity(seed):
+    """VolumeUsage on existing nodes (volumeusage.go:82-227, existingnode.go:70-78,122): shared and
+    ephemeral claims, unresolved / driverless claims, nodes already over a limit."""
+    want, got = _solve_both(problems.random_problem(seed, n_pods=150, n_nodes=12 + seed % 5, volumes=True))
+    d = _diff(want, got)
+    assert d is None, d
+
+
+def _volume_scenarios():
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_volume_fixtures as mvf
+    return mvf
+
+
+@pytest.mark.parametrize("name", [s["name"] for s in _volume_scenarios().scenarios()])
+def test_volume_reference_scenarios_gpu(name):
+    """suite_test.go VolumeUsage scenarios on the GPU: the Go assertions and equality with the oracle."""
+    mvf = _volume_scenarios()
+    scn = {s["name"]: s for s in mvf.scenarios()}[name]
+    want, got = _solve_both(scn["snapshot"])
+    d = _diff(want, got)
+    assert d is None, d
+    assert not mvf.check(scn, want)
