@@ -25,12 +25,14 @@ struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
       log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, n_vm, n_vc, tg_cnt,
       tg_ccnt, tg_cpos, fail_rs, total;
+  int32_t ccs;  // tg_ccnt row stride
 };
 
 WorkLayout work_layout(const KsDims& d) {
   Arena a;
   WorkLayout w{};
   size_t K = d.Kcap, P = std::max(d.P, 1), N = std::max(d.N, 1);
+  w.ccs = d.Kcap + 1;
   w.c_tpl = a.add(4 * K);
   w.c_cnt = a.add(4 * K);
   w.c_thr = a.add(4 * K * d.R);
@@ -99,6 +101,7 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.tg_ccnt = (int32_t*)(base + w.tg_ccnt);
   k.tg_cpos = (int32_t*)(base + w.tg_cpos);
   k.fail_rs = (uint32_t*)(base + w.fail_rs);
+  k.ccs = w.ccs;
   return k;
 }
 

@@ -229,9 +229,16 @@ void build_cons(ks_cons& c, const Value& root) {
   (*solveRoot.o)["pods"] = a2;
   c.pb.reset(new ks_problem());
   Host& h = c.pb->host;
+  // NewTopology excludes the pods a simulation schedules (topology.go:72-75).  The pending and the
+  // deleting nodes' pods are in every simulation; the candidates' pods are taken out per simulation
+  // (prepare_launch), from the contributions the build records.
+  std::set<std::string> always;
+  for (int p : c.pending) always.insert(podMeta[(size_t)p].uid);
+  for (int p : c.deleting) always.insert(podMeta[(size_t)p].uid);
+  h.topoExcluded = &always;
   h.build(solveRoot);
+  h.topoExcluded = nullptr;
   if (h.dims.dupUids) throw KsError(KS_ERR_UNSUPPORTED, "consolidation snapshot has duplicate pod UIDs");
-  if (h.dims.G) throw KsError(KS_ERR_UNSUPPORTED, "topology constraints in consolidation simulations are not encoded yet");
   if (h.dims.volAny)
     throw KsError(KS_ERR_UNSUPPORTED, "volume limits in consolidation simulations are not encoded yet");
   c.hostnameSeed = h.hostnameSeed;
@@ -348,6 +355,58 @@ bool offering_price(const Host::IT& it, const std::string& ct, const std::string
   return false;
 }
 
+// One simulation's NewTopology (topology.go:61-85) relative to the shared counts: the candidates'
+// pods are excluded from countDomains and from the inverse anti-affinities (topology.go:190-203,
+// 262-265), and the candidates' hostnames are no longer registered by NewExistingNode
+// (existingnode.go:60).  Returns (tg_cnt offset, (pods removed << 1) | unregister-if-zero) pairs,
+// one per touched domain; `dead` gets the inverse groups none of whose owners is in the simulation.
+std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, const std::vector<int>& simPods,
+                                  uint64_t& dead) {
+  const Host& h = c.pb->host;
+  const KsDims& d = h.dims;
+  const int hostKey = h.keyId.count("kubernetes.io/hostname") ? h.keyId.at("kubernetes.io/hostname") : -1;
+  std::map<std::pair<int, int>, int> dec;  // (group, value) -> pods removed
+  std::vector<int> ownersGone((size_t)d.G, 0);
+  std::set<int> goneHosts;  // hostname value ids of the removed candidates
+  for (int ci : sm.cands) {
+    const ks_cons::Cand& k = c.cands[(size_t)ci];
+    for (int p : k.pods) {
+      const std::string& uid = h.pods[(size_t)p].uid;
+      auto ct = h.topoContrib.find(uid);
+      if (ct != h.topoContrib.end())
+        for (auto& gv : ct->second) dec[gv]++;
+      auto io = h.topoInvOwner.find(uid);
+      if (io != h.topoInvOwner.end())
+        for (uint64_t m = io->second; m; m &= m - 1) ownersGone[(size_t)__builtin_ctzll(m)]++;
+    }
+    auto hv = hostKey >= 0 ? h.valueId[(size_t)hostKey].find(h.nodes[(size_t)k.node].hostName)
+                           : h.valueId[0].end();
+    if (hostKey >= 0 && hv != h.valueId[(size_t)hostKey].end()) {
+      const int v = hv->second;
+      goneHosts.insert(v);
+      for (int g = 0; g < d.G; g++)
+        if (h.groups[(size_t)g].keyId == hostKey) dec[{g, v}] += 0;
+    }
+  }
+  std::vector<int32_t> out;
+  for (auto& e : dec) {
+    const int g = e.first.first, v = e.first.second;
+    const bool host = h.groups[(size_t)g].keyId == hostKey;
+    // still registered with no pod: a universe domain, or the hostname of a node the simulation keeps
+    const bool keep = h.topoUniverse[(size_t)g][(size_t)v] || (host && h.activeHost(v) && !goneHosts.count(v));
+    if (v < 0 || v >= h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_NV])
+      throw KsError(KS_ERR_CAPACITY, "topology domain outside its group's value range");
+    out.push_back(h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_CNT] + v);
+    out.push_back((e.second << 1) | (keep ? 0 : 1));
+  }
+  uint64_t simOwn = 0;  // inverse groups a simulation pod owns (Topology.Update, topology.go:91-122)
+  for (int p : simPods) simOwn |= h.tab.pod_ginv[(size_t)p];
+  dead = 0;
+  for (int g = d.G1; g < d.G; g++)
+    if (h.topoInvOwners[(size_t)g] - ownersGone[(size_t)g] <= 0 && !((simOwn >> g) & 1ull)) dead |= 1ull << g;
+  return out;
+}
+
 // Build and upload the launch of this rank's simulations (cached per (rank, world)).
 void prepare_launch(ks_cons& c, int rank, int world) {
   if (c.lrank == rank && c.lworld == world) return;
@@ -369,15 +428,19 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   struct Off {
     size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
         last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price, n_hp,
-        c_hp;
+        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel;
   };
   std::vector<Off> offs(ns);
   std::vector<int> simP(ns), entBeg(ns + 1, 0);
   std::vector<int32_t> entries, entrySim;
+  std::vector<std::vector<int32_t>> tdel(ns);
+  std::vector<uint64_t> tdead(ns, 0);
+  std::vector<std::vector<int>> simPods(ns);
   int maxP = 1;
   for (int k = 0; k < ns; k++) {
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
-    std::vector<int> pods = c.pending;
+    std::vector<int>& pods = simPods[k];
+    pods = c.pending;
     for (int ci : sm.cands) pods.insert(pods.end(), c.cands[(size_t)ci].pods.begin(), c.cands[(size_t)ci].pods.end());
     pods.insert(pods.end(), c.deleting.begin(), c.deleting.end());
     simP[k] = (int)pods.size();
@@ -416,6 +479,13 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     o.rm = a.add(4 * std::max<size_t>(sm.cands.size(), 1));
     o.pool0 = a.add(8 * (size_t)NP * R);
     o.st_price = sm.multi ? a.add(8 * (size_t)std::max(d.T, 1)) : 0;
+    if (d.G) {
+      o.tg_cnt = a.add(4 * (size_t)d.tgCntWords);
+      o.tg_ccnt = a.add(4 * (size_t)d.G * (P + 1));
+      o.tg_cpos = a.add(4 * (size_t)d.G);
+      tdel[k] = sim_topology(c, sm, simPods[k], tdead[k]);
+      o.tdel = a.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
+    }
   }
   c.lnent = (int)entries.size();
   HIPCHK(hipMalloc(&c.lbuf, std::max<size_t>(a.total, 256)));
@@ -531,6 +601,16 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     w.rec = c.lrec + (size_t)k * c.recWords;
     w.price = price;
     w.cflags = cflags;
+    w.ccs = simP[k] + 1;
+    if (d.G) {
+      w.tg_cnt = (int32_t*)(base + o.tg_cnt);
+      w.tg_ccnt = (int32_t*)(base + o.tg_ccnt);
+      w.tg_cpos = (int32_t*)(base + o.tg_cpos);
+      memcpy(stage.data() + o.tdel, tdel[k].data(), 4 * tdel[k].size());
+      w.tdel = (const int32_t*)(base + o.tdel);
+      w.ntdel = (int32_t)(tdel[k].size() / 2);
+      w.tdead = tdead[k];
+    }
     works[k] = w;
   }
   HIPCHK(hipMemcpy(c.lbuf, stage.data(), a.total, hipMemcpyHostToDevice));

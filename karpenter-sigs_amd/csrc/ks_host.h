@@ -151,6 +151,15 @@ struct Host {
   std::vector<PodH> clusterPods;
   std::map<std::string, std::map<std::string, std::string>> nodeLabelsByName;
   std::vector<uint64_t> podGsel, podGinv;  // per pod: groups that select it / inverse groups it owns
+  // Consolidation view (ks_cons.cpp): NewTopology excludes only these UIDs (the pods every simulation
+  // schedules); each simulation then subtracts its candidates' pods from the counts it records below.
+  const std::set<std::string>* topoExcluded = nullptr;
+  std::map<std::string, std::vector<std::pair<int, int>>> topoContrib;  // cluster pod UID -> (group, value) counted
+  std::map<std::string, uint64_t> topoInvOwner;                         // cluster pod UID -> inverse groups it owns
+  std::vector<int> topoInvOwners;                                       // per group: owning cluster pods
+  std::vector<std::vector<char>> topoUniverse;                          // per group, per value: in the domain universe
+  std::set<int> topoHostActive;                                         // hostname value ids of the nodes (Register)
+  bool activeHost(int v) const { return topoHostActive.count(v) != 0; }
   int64_t hostnameSeed = 0;
   bool emptyTopology = false;  // the benchmark's &scheduling.Topology{}: no groups (scheduling_benchmark_test.go:124)
   KsDims dims{};

@@ -220,6 +220,11 @@ struct KsWork {
   int32_t KS_G* n_slot;         // [N] W.n_rs slot of a node whose requirements changed (valid where s_tchr is set)
   double price;                 // getCandidatePrices (consolidation.go:197-207), summed in candidate order
   int32_t cflags;               // ConsFlag
+  int32_t ccs;                  // tg_ccnt row stride (NodeClaims + 1)
+  // SIM topology: NewTopology's counts with this simulation's pods excluded (topology.go:61-85)
+  const int32_t KS_G* tdel;     // [ntdel][2]: tg_cnt offset, (pods removed << 1) | unregister-if-zero
+  int32_t ntdel;
+  uint64_t tdead;               // inverse groups none of whose owners exist in this simulation
 };
 
 enum Counter {

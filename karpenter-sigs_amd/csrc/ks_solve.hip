@@ -390,7 +390,7 @@ struct Solver {
   __device__ __forceinline__ int tg(int g, int f) const { return s_tgm[g * TGM_WORDS + f]; }
   // count of domain v, -1 while the domain is not registered (absent from TopologyGroup.domains)
   __device__ __forceinline__ int tcnt(int g, int v) const { return ld_sc1(W.tg_cnt + tg(g, TGM_CNT) + v); }
-  __device__ __forceinline__ int tccnt(int g, int claim) const { return ld_sc1(W.tg_ccnt + (int64_t)g * (d.Kcap + 1) + claim); }  // claim <= Kcap (a fresh claim at the cap)
+  __device__ __forceinline__ int tccnt(int g, int claim) const { return ld_sc1(W.tg_ccnt + (int64_t)g * W.ccs + claim); }  // claim <= Kcap (a fresh claim at the cap)
   __device__ __forceinline__ bool tpod_has(int g, int v) const {  // podDomains.Has (strict pod requirements)
     return rs_member(L, D.st_rss + (int64_t)t_s * d.RSW, tg(g, TGM_KEY), v);
   }
@@ -405,6 +405,7 @@ struct Solver {
     const uint64_t all = d.G >= 64 ? ~0ull : ((1ull << d.G) - 1);
     const uint64_t owned = d.G1 >= 64 ? ~0ull : ((1ull << d.G1) - 1);
     t_mask = D.st_gown[s] | (t_sel & all & ~owned);
+    if (SIM) t_mask &= ~W.tdead;
     for (uint64_t m = t_mask; m; m &= m - 1) {
       const int g = ctz64(m);
       if (tg(g, TGM_TYPE) == TG_AFFINITY) {
@@ -608,7 +609,7 @@ struct Solver {
           x &= x - 1;
           if (v >= nv) {
             if (claim >= 0) {
-              const int64_t at = (int64_t)g * (d.Kcap + 1) + claim;
+              const int64_t at = (int64_t)g * W.ccs + claim;
               const int cc = W.tg_ccnt[at];
               W.tg_ccnt[at] = cc + 1;
               if (cc == 0) W.tg_cpos[g] += 1;  // one more placeholder holding a counted pod
@@ -834,7 +835,8 @@ struct Solver {
               ok = false;
               code = tc;
               const int64_t slot = ((int64_t)p * d.NTPL + t) * d.FSW;
-              if (tc == FC_TOPO_COMPAT) {
+              if (SIM) {  // simulations render no messages
+              } else if (tc == FC_TOPO_COMPAT) {
                 copy_words(W.fail_rs + slot, s_rs, d.RSW);  // the topology requirements, for the message
               } else {
                 const int g = (int)(tc >> 16) & 0xff, nv = tg(g, TGM_NV);
@@ -874,7 +876,7 @@ struct Solver {
             wsync();
             if (any == 0) {
               code = FC_NO_IT | (flags << 8);
-              if (TOPO && t_mask) {  // the message prints the requirements the topology narrowed
+              if (!SIM && TOPO && t_mask) {  // the message prints the requirements the topology narrowed
                 copy_words(W.fail_rs + ((int64_t)p * d.NTPL + t) * d.FSW, s_rs, d.RSW);
                 code |= FC_RS_SNAP;
               }
@@ -1196,6 +1198,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       W.pod_status[i] = ST_PENDING;
       W.pod_fstate[i] = -1;
       W.last_len[i] = 0;
+    }
+    if constexpr (TOPO) {
+      // NewTopology for this simulation: the shared counts minus the candidates' pods, which the
+      // simulation schedules and NewTopology therefore excludes (topology.go:72-75,262-265); a
+      // domain left with no pod and no other registration drops out of TopologyGroup.domains.
+      for (int i = lane(); i < d.tgCntWords; i += kWave) W.tg_cnt[i] = D.tg_cnt0[i];
+      for (int i = lane(); i < d.G * W.ccs; i += kWave) W.tg_ccnt[i] = 0;
+      for (int i = lane(); i < d.G; i += kWave) W.tg_cpos[i] = 0;
+      hbm_release();
+      wsync();
+      for (int i = lane(); i < W.ntdel; i += kWave) {  // offsets are distinct within one simulation
+        const int off = W.tdel[2 * i], x = W.tdel[2 * i + 1];
+        const int c = D.tg_cnt0[off] - (x >> 1);
+        W.tg_cnt[off] = (c == 0 && (x & 1)) ? -1 : c;
+      }
+      hbm_release();
     }
     wsync();
     if (lane() == 0)
@@ -1581,12 +1599,16 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st) {
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
   if (nsims <= 0) return hipSuccess;
-#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, true, false>), dim3(nsims), dim3(kWave), pl.lds, st, D, works_dev, pl)
+#define KS_LAUNCH(RT_, TL_)                                                                                  \
+  {                                                                                                          \
+    if (D.d.G) hipLaunchKernelGGL((k_solve<RT_, TL_, true, true>), dim3(nsims), dim3(kWave), pl.lds, st, D, works_dev, pl); \
+    else hipLaunchKernelGGL((k_solve<RT_, TL_, true, false>), dim3(nsims), dim3(kWave), pl.lds, st, D, works_dev, pl);     \
+  }
   const bool tl = pl.talloc != 0;
   switch (D.d.R) {
-    case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;
-    case 4: if (tl) KS_LAUNCH(4, true); else KS_LAUNCH(4, false); break;
-    default: if (tl) KS_LAUNCH(0, true); else KS_LAUNCH(0, false); break;
+    case 3: if (tl) KS_LAUNCH(3, true) else KS_LAUNCH(3, false) break;
+    case 4: if (tl) KS_LAUNCH(4, true) else KS_LAUNCH(4, false) break;
+    default: if (tl) KS_LAUNCH(0, true) else KS_LAUNCH(0, false) break;
   }
 #undef KS_LAUNCH
   return hipGetLastError();

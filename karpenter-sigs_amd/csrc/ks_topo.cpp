@@ -134,7 +134,12 @@ void Host::buildTopology() {
 
   // --- groups
   std::set<std::string> excluded;
-  for (auto& p : pods) excluded.insert(p.uid);
+  if (topoExcluded) excluded = *topoExcluded;
+  else for (auto& p : pods) excluded.insert(p.uid);
+  topoContrib.clear();
+  topoInvOwner.clear();
+  // (group index, domain) per counted cluster pod, resolved to value ids once the groups are final
+  std::map<std::string, std::vector<std::pair<int, std::string>>> contrib;
   std::vector<TopoGroup> own, inv;
   std::map<std::string, int> ownByHash, invByHash;
   auto nodeRec = [&](const std::map<std::string, std::string>& labels) {
@@ -187,7 +192,7 @@ void Host::buildTopology() {
   auto termNs = [](const PodH& p, const AffTerm& t) {  // buildNamespaceList (topology.go:341-362)
     return t.namespaces.empty() ? std::set<std::string>{p.ns} : std::set<std::string>(t.namespaces.begin(), t.namespaces.end());
   };
-  auto countDomains = [&](TopoGroup& g) {  // topology.go:238-291
+  auto countDomains = [&](TopoGroup& g, int gidx) {  // topology.go:238-291
     for (auto& cp : clusterPods) {
       if (!g.namespaces.count(cp.ns) || !sel_lists(g.sel, cp.labels)) continue;
       if (cp.nodeName.empty() || cp.phase == "Failed" || cp.phase == "Succeeded" || cp.deleting) continue;
@@ -201,9 +206,10 @@ void Host::buildTopology() {
       else continue;
       if (!filterMatches(g, nodeRec(n->second), 0)) continue;
       g.domains[d]++;
+      if (topoExcluded) contrib[cp.uid].push_back({gidx, d});
     }
   };
-  auto inverseAnti = [&](const PodH& p, const std::map<std::string, std::string>* labels) {
+  auto inverseAnti = [&](const PodH& p, const std::map<std::string, std::string>* labels, bool cluster) {
     uint64_t owned = 0;  // updateInverseAntiAffinity (topology.go:207-232)
     for (auto& t : p.antiRequired) {
       TopoGroup g = makeGroup(TG_ANTI, t.key, p, termNs(p, t), t.sel, INT32_MAX, -1);
@@ -218,8 +224,13 @@ void Host::buildTopology() {
       }
       if (labels) {
         auto d = labels->find(inv[(size_t)idx].key);
-        if (d != labels->end()) inv[(size_t)idx].domains[d->second]++;
+        if (d != labels->end()) {
+          inv[(size_t)idx].domains[d->second]++;
+          if (topoExcluded) contrib[p.uid].push_back({-1 - idx, d->second});
+        }
       }
+      if (idx >= 64) throw KsError(-3, "more than 64 topology groups");
+      if (cluster && topoExcluded) topoInvOwner[p.uid] |= 1ull << idx;
       owned |= 1ull << idx;
     }
     return owned;
@@ -243,21 +254,21 @@ void Host::buildTopology() {
     if (cp.antiRequired.empty() || cp.nodeName.empty() || excluded.count(cp.uid)) continue;
     auto n = nodeLabelsByName.find(cp.nodeName);
     if (n == nodeLabelsByName.end()) continue;
-    inverseAnti(cp, &n->second);
+    inverseAnti(cp, &n->second, true);
   }
   std::vector<uint64_t> invOwned(P, 0);
   for (int p = 0; p < P; p++) {  // NewTopology: Update(pod) for every pod, in order
     const std::shared_ptr<PodH>& sp = states[(size_t)p][0].spec;
     if (!sp) continue;
     if (sp->hasAffinity && sp->hasPodAnti && (!sp->antiRequired.empty() || !sp->antiPreferred.empty()))
-      invOwned[(size_t)p] = inverseAnti(*sp, nullptr);
+      invOwned[(size_t)p] = inverseAnti(*sp, nullptr, false);
     uint64_t gown = 0;
     for (auto& g : ownedSpecGroups(*sp)) {
       auto it = ownByHash.find(g.hash);
       int idx;
       if (it == ownByHash.end()) {
-        countDomains(g);
         idx = (int)own.size();
+        countDomains(g, idx);
         ownByHash[g.hash] = idx;
         own.push_back(g);
       } else {
@@ -358,6 +369,31 @@ void Host::buildTopology() {
         if (bit(rs_present(st.rsAll.data()), k) && bit(rs_compl(st.rsAll.data()), k))
           throw KsError(-2, "topology key " + groups[(size_t)g].key +
                                                 " is missing on an existing node while a pod constrains it with NotIn");
+  }
+  if (topoExcluded) {  // the consolidation view: what each simulation's exclusions take away
+    for (auto& kv : contrib)
+      for (auto& gd : kv.second) {
+        const int g = gd.first >= 0 ? gd.first : G1 + (-1 - gd.first);
+        topoContrib[kv.first].push_back({g, valueId[(size_t)groups[(size_t)g].keyId].at(gd.second)});
+      }
+    for (auto& kv : topoInvOwner) kv.second <<= G1;
+    topoInvOwners.assign((size_t)G, 0);
+    for (auto& kv : topoInvOwner)
+      for (uint64_t m = kv.second; m; m &= m - 1) topoInvOwners[(size_t)__builtin_ctzll(m)]++;
+    topoHostActive.clear();
+    if (keyId.count(kHostnameKey))
+      for (auto& n : nodes) {
+        auto v = valueId[(size_t)keyId.at(kHostnameKey)].find(n.hostName);
+        if (v != valueId[(size_t)keyId.at(kHostnameKey)].end()) topoHostActive.insert(v->second);
+      }
+    topoUniverse.assign((size_t)G, {});
+    for (int g = 0; g < G; g++) {
+      const TopoGroup& tg = groups[(size_t)g];
+      topoUniverse[(size_t)g].assign(values[(size_t)tg.keyId].size(), 0);
+      auto d = dom.find(tg.key);
+      if (d != dom.end())
+        for (auto& v : d->second) topoUniverse[(size_t)g][(size_t)valueId[(size_t)tg.keyId].at(v)] = 1;
+    }
   }
   dims.G = G;
   dims.G1 = G1;

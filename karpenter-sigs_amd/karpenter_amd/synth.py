@@ -198,20 +198,51 @@ NOW = 1760000000  # fixed "now" for lifetimeRemaining (types.go:136-145)
 
 def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, spot_frac=0.3, it_range=(15, 40),
                      uninitialized_frac=0.0, not_ready_frac=0.0, expire_after="720h", pod_selectors=False,
-                     limits=None):
+                     limits=None, topology=0):
     """A consolidation snapshot: an existing cluster of `n_nodes` nodes launched from one
     WhenUnderutilized NodePool over fake.InstanceTypes(n_its), each running `pods_per_node` bound pods
     (C1 cpu/memory distributions, distinct pod-deletion-cost annotations so candidate costs are
     distinct), plus `n_pending` pending pods.  Every node is listed as a candidate; the host applies
-    NewCandidate / filterCandidates / the disruption-cost sort.  Schema: INTEGRATION.md §5."""
+    NewCandidate / filterCandidates / the disruption-cost sort.  Schema: INTEGRATION.md §5.
+
+    topology=A > 0: the pods belong to A apps whose specs carry zonal / hostname spread (DoNotSchedule
+    or ScheduleAnyway, some with minDomains), required hostname or zonal anti-affinity, or required /
+    preferred zonal pod affinity; every bound pod is also listed in clusterPods (NewTopology's
+    countDomains and inverse anti-affinity source)."""
     rng = np.random.default_rng(seed)
     its = fake_instance_types(n_its)
     pool = node_pool("default", limits=limits)
     pool["spec"]["disruption"] = {"consolidationPolicy": "WhenUnderutilized", "expireAfter": expire_after}
     cpu_m = [100, 250, 500, 1000, 1500]
     mem_mi = [100, 256, 512, 1024, 2048, 4096]
-    nodes, cands = [], []
+    nodes, cands, cluster = [], [], []
     pid = 0
+    apps = ["app-%d" % a for a in range(topology)]
+
+    def app_spec(a):
+        sel = {"matchLabels": {"app": apps[a]}}
+        kind = a % 8
+        if kind in (0, 1):
+            c = {"maxSkew": 1 + a % 3, "topologyKey": ZONE, "labelSelector": sel,
+                 "whenUnsatisfiable": "DoNotSchedule" if kind == 0 else "ScheduleAnyway"}
+            if a % 5 == 0:
+                c["minDomains"] = 3
+            return {"topologySpreadConstraints": [c]}
+        if kind in (2, 3):
+            return {"topologySpreadConstraints": [{"maxSkew": 1 + a % 2, "topologyKey": HOSTNAME, "labelSelector": sel,
+                                                   "whenUnsatisfiable": "DoNotSchedule" if kind == 2 else "ScheduleAnyway"}]}
+        if kind == 4:
+            return {"affinity": {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": sel, "topologyKey": HOSTNAME}]}}}
+        if kind == 5:
+            return {"affinity": {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": sel, "topologyKey": ZONE}]}}}
+        if kind == 6:
+            return {"affinity": {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+                {"weight": 50, "podAffinityTerm": {"labelSelector": sel, "topologyKey": ZONE}}]}}}
+        return {"affinity": {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"labelSelector": {"matchLabels": {"app": apps[(a + 1) % len(apps)]}}, "topologyKey": ZONE}]}}}
+
     for j in range(n_nodes):
         i = int(rng.integers(it_range[0], it_range[1]))
         it = its[i]
@@ -230,13 +261,21 @@ def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, 
                 continue
             used_cpu += c
             used_mem += m
-            p = pod(pid, cpu="%dm" % c, mem="%dMi" % (m >> 20), labels={"my-label": LABEL_VALUES[rng.integers(7)]})
+            labels = {"my-label": LABEL_VALUES[rng.integers(7)]}
+            a = int(rng.integers(topology)) if topology else -1
+            if a >= 0:
+                labels["app"] = apps[a]
+            p = pod(pid, cpu="%dm" % c, mem="%dMi" % (m >> 20), labels=labels)
+            if a >= 0:
+                p["spec"].update(app_spec(a))
             if pod_selectors and rng.random() < 0.2:
                 p["spec"]["nodeSelector"] = {ARCH: "amd64"}
             p["metadata"]["annotations"] = {"controller.kubernetes.io/pod-deletion-cost": str(int(rng.integers(-1000, 1000000)))}
             p["spec"]["nodeName"] = "node-%05d" % j
             p["status"] = {"phase": "Running", "conditions": [{"type": "PodScheduled", "status": "True"}]}
             pods.append(p)
+            if topology:
+                cluster.append(p)
             pid += 1
         name = "node-%05d" % j
         labels = {NODEPOOL: "default", IT_LABEL: it["name"], ZONE: off["zone"], CT: off["capacityType"],
@@ -255,7 +294,12 @@ def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, 
         cands.append(name)
     pending = []
     for _ in range(n_pending):
-        pending.append(pod(pid, cpu=CPU_CHOICES[rng.integers(5)], mem=MEM_CHOICES[rng.integers(6)]))
+        p = pod(pid, cpu=CPU_CHOICES[rng.integers(5)], mem=MEM_CHOICES[rng.integers(6)])
+        if topology:
+            a = int(rng.integers(topology))
+            p["metadata"]["labels"]["app"] = apps[a]
+            p["spec"].update(app_spec(a))
+        pending.append(p)
         pid += 1
     return {
         "wellKnownLabels": FAKE_WELL_KNOWN,
@@ -269,6 +313,7 @@ def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, 
         "candidates": cands,
         "now": _fmt_time(NOW),
         "hostnameSeed": 0,
+        **({"clusterPods": cluster} if topology else {}),
     }
 
 

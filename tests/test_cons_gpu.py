@@ -90,6 +90,33 @@ def test_random_cluster_parity(case):
         assert d is None, d
 
 
+TOPO_CASES = [
+    dict(n_nodes=40, pods_per_node=5, n_its=60, seed=0, n_pending=3, topology=8),
+    dict(n_nodes=40, pods_per_node=8, n_its=60, seed=1, n_pending=3, topology=16),
+    dict(n_nodes=40, pods_per_node=10, n_its=60, seed=2, n_pending=3, topology=4),
+    dict(n_nodes=40, pods_per_node=3, n_its=60, seed=3, n_pending=3, topology=12),
+    dict(n_nodes=24, pods_per_node=10, n_its=60, it_range=(6, 30), seed=21, spot_frac=0.6, topology=6),
+    dict(n_nodes=30, pods_per_node=12, n_its=80, it_range=(10, 40), seed=22, n_pending=5, topology=24),
+    dict(n_nodes=20, pods_per_node=8, n_its=50, it_range=(5, 20), seed=23, uninitialized_frac=0.2,
+         not_ready_frac=0.2, topology=10),
+    dict(n_nodes=25, pods_per_node=10, n_its=60, it_range=(8, 30), seed=24, pod_selectors=True, topology=3),
+    dict(n_nodes=16, pods_per_node=15, n_its=40, it_range=(2, 10), seed=25, topology=2),
+    dict(n_nodes=60, pods_per_node=4, n_its=100, it_range=(20, 60), seed=26, topology=40),
+]
+
+
+@pytest.mark.parametrize("case", TOPO_CASES, ids=["t%d" % c["seed"] for c in TOPO_CASES])
+def test_topology_cluster_parity(case):
+    """Simulations whose pods carry spread / pod affinity / anti-affinity over a cluster whose bound pods
+    seed NewTopology: every simulation's counts exclude its own pods (topology.go:72-75) and its removed
+    nodes' hostnames are no longer registered."""
+    snap = synth.cluster_snapshot(**case)
+    for all_sims in (True, False):
+        want, got = _both(snap, all_sims)
+        d = _first_diff(want, got)
+        assert d is None, d
+
+
 def test_sharded_runs_gather_to_the_same_decision():
     """Ranks r of world W run simulations s % W == r; the [rank][slot] gather decides identically."""
     snap = json.dumps(synth.cluster_snapshot(30, 8, n_its=60, it_range=(6, 30), seed=11, spot_frac=0.5))

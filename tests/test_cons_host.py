@@ -18,7 +18,9 @@ import make_consolidation_fixtures as mcf  # noqa: E402
 SNAPS = [("scn-" + s["name"], s["snapshot"]) for s in mcf.scenarios()] + [
     ("rand-%d" % seed, synth.cluster_snapshot(n, 6, n_its=40, it_range=(4, 30), seed=seed, spot_frac=0.4,
                                                uninitialized_frac=0.1, n_pending=3, expire_after=exp))
-    for seed, n, exp in [(21, 10, "720h"), (22, 40, "24h"), (23, 130, "2h30m")]]
+    for seed, n, exp in [(21, 10, "720h"), (22, 40, "24h"), (23, 130, "2h30m")]] + [
+    ("topo-%d" % seed, synth.cluster_snapshot(30, 6, n_its=40, it_range=(4, 30), seed=seed, n_pending=3, topology=apps))
+    for seed, apps in [(31, 8), (32, 24)]]
 
 
 @pytest.mark.parametrize("name,snap", SNAPS, ids=[n for n, _ in SNAPS])
