@@ -239,8 +239,6 @@ void build_cons(ks_cons& c, const Value& root) {
   h.build(solveRoot);
   h.topoExcluded = nullptr;
   if (h.dims.dupUids) throw KsError(KS_ERR_UNSUPPORTED, "consolidation snapshot has duplicate pod UIDs");
-  if (h.dims.volAny)
-    throw KsError(KS_ERR_UNSUPPORTED, "volume limits in consolidation simulations are not encoded yet");
   c.hostnameSeed = h.hostnameSeed;
   std::map<std::string, int> hostNode;  // node name -> host.nodes index (sorted order)
   for (size_t i = 0; i < h.nodes.size(); i++) hostNode[h.nodes[i].name] = (int)i;
@@ -428,7 +426,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   struct Off {
     size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
         last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price, n_hp,
-        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel;
+        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, n_vm, n_vc;
   };
   std::vector<Off> offs(ns);
   std::vector<int> simP(ns), entBeg(ns + 1, 0);
@@ -479,6 +477,10 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     o.rm = a.add(4 * std::max<size_t>(sm.cands.size(), 1));
     o.pool0 = a.add(8 * (size_t)NP * R);
     o.st_price = sm.multi ? a.add(8 * (size_t)std::max(d.T, 1)) : 0;
+    if (d.volAny) {  // indexed by node, written only where a pod with PVCs lands (copy-on-write)
+      o.n_vm = a.add(8 * (size_t)N);
+      o.n_vc = a.add(4 * (size_t)N * std::max(d.VD, 1));
+    }
     if (d.G) {
       o.tg_cnt = a.add(4 * (size_t)d.tgCntWords);
       o.tg_ccnt = a.add(4 * (size_t)d.G * (P + 1));
@@ -602,6 +604,10 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     w.price = price;
     w.cflags = cflags;
     w.ccs = simP[k] + 1;
+    if (d.volAny) {
+      w.n_vm = (uint64_t*)(base + o.n_vm);
+      w.n_vc = (int32_t*)(base + o.n_vc);
+    }
     if (d.G) {
       w.tg_cnt = (int32_t*)(base + o.tg_cnt);
       w.tg_ccnt = (int32_t*)(base + o.tg_ccnt);

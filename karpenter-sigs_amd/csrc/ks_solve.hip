@@ -28,6 +28,10 @@
 // of thousands of them fills the 256 CUs.  Nothing here is a dense contraction: no MFMA.
 #include <hip/hip_runtime.h>
 
+#ifndef KS_TU
+#define KS_TU 0
+#endif
+
 #include "ks_gosort.h"
 #include "ks_problem.h"
 #include "ks_reqset.h"
@@ -82,6 +86,7 @@ __device__ __forceinline__ uint32_t lds_and(LU32 p, uint32_t v) {  // ds_and_rtn
 // ------------------------------------------------------------------------------------------------
 // Init: per-replica workspace state (copies of the resident initial state), one grid-stride pass.
 // ------------------------------------------------------------------------------------------------
+#if KS_TU == 0
 __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qorder) {
   const KsDims d = D.d;
   const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -110,6 +115,8 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
     for (int64_t i = gtid; i < CT_NCOUNTERS; i += gsz) W.counters[i] = 0;
   }
 }
+
+#endif  // KS_TU == 0
 
 // ------------------------------------------------------------------------------------------------
 // Solve
@@ -160,6 +167,7 @@ struct Solver {
   LU32 s_rmv;           // SIM: [ceil(N/32)] nodes removed by the simulation (the candidates)
   LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose requests live in a W.n_req slot
   LU32 s_tchr;          // SIM: [ceil(N/32)] nodes whose requirements live in a W.n_rs slot
+  LU32 s_tvol;          // SIM: [ceil(N/32)] nodes whose volume usage lives in W.n_vm / W.n_vc
   LI32 s_tgm;           // [G][TGM_WORDS] topology group metadata
   LI32 s_tmin;          // [G] domainMinCount of the popped pod, per spread group
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
@@ -259,15 +267,23 @@ struct Solver {
   // VolumeUsage.ExceedsLimits (volumeusage.go:202-209) for the popped pod's PVCs: per limited driver,
   // the node's count plus the pod's PVCs it does not mount yet.  Nodes over a limit before the Solve
   // never fit (the encoder's Available()), so a pod without PVCs needs no check.
+  // SIM: a node's usage lives in W only once a pod of this simulation mounted something there
+  // (s_tvol, copy-on-write from the shared n_vm0 / n_vc0).
   __device__ __forceinline__ bool vol_ok(int n) const {
-    const uint64_t add = cur_vm & ~W.n_vm[n];
+    const bool own = !SIM || tbit(s_tvol, n);
+    const uint64_t add = cur_vm & ~(own ? W.n_vm[n] : D.n_vm0[n]);
+    const int32_t KS_G* vc = (own ? W.n_vc : D.n_vc0) + (int64_t)n * d.VD;
     bool ok = true;
-    for (int v = 0; v < d.VD; v++)
-      ok &= W.n_vc[(int64_t)n * d.VD + v] + __popcll(add & D.vol_dm[v]) <= D.n_vlim[(int64_t)n * d.VD + v];
+    for (int v = 0; v < d.VD; v++) ok &= vc[v] + __popcll(add & D.vol_dm[v]) <= D.n_vlim[(int64_t)n * d.VD + v];
     return ok;
   }
   // VolumeUsage.Add (existingnode.go:122), by node n's owner lane.
   __device__ __forceinline__ void vol_commit(int n) const {
+    if (SIM && !tbit(s_tvol, n)) {
+      W.n_vm[n] = D.n_vm0[n];
+      for (int v = 0; v < d.VD; v++) W.n_vc[(int64_t)n * d.VD + v] = D.n_vc0[(int64_t)n * d.VD + v];
+      s_tvol[n >> 5] |= 1u << (n & 31);
+    }
     const uint64_t add = cur_vm & ~W.n_vm[n];
     for (int v = 0; v < d.VD; v++) W.n_vc[(int64_t)n * d.VD + v] += __popcll(add & D.vol_dm[v]);
     W.n_vm[n] |= cur_vm;
@@ -318,7 +334,7 @@ struct Solver {
       ok0 &= (a0[r] >= 0) & (q0[r] + pod[r] <= a0[r]);
       ok1 &= (a1[r] >= 0) & (q1[r] + pod[r] <= a1[r]);
     }
-    if (!SIM && d.volAny && cur_vm) {
+    if (d.volAny && cur_vm) {
       if (ok0) ok0 = vol_ok(c0);
       if (ok1) ok1 = vol_ok(c1);
     }
@@ -360,6 +376,7 @@ struct Solver {
         W.n_req[(int64_t)j * R() + r] = q[r] + pod[r];
       }
       if (d.hpAny) W.n_hp[j] = (fresh ? D.n_hp0[j] : W.n_hp[j]) | cur_hpu;
+      if (d.volAny && cur_vm) vol_commit(j);
       if (fresh) s_tch[j >> 5] |= 1u << (j & 31);
     }
     if (sflags & SF_HAS_KEYS) {
@@ -1124,7 +1141,7 @@ struct Solver {
       w.tol1 = D.st_tol[2 * w.s + 1];
       w.hpc = D.pod_hpc[w.g];
       w.hpu = D.pod_hpu[w.g];
-      w.vm = SIM ? 0 : D.pod_vm[w.g];
+      w.vm = D.pod_vm[w.g];
 #pragma unroll
       for (int r = 0; r < RM; r++) {
         if (RT == 0 && r >= d.R) break;
@@ -1168,6 +1185,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   S.s_rmv = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tch = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tchr = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
+  S.s_tvol = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tgm = (LI32)take(4 * (size_t)d.G * TGM_WORDS);
   S.s_tmin = (LI32)take(4 * (size_t)d.G);
   S.s_trs0 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
@@ -1191,6 +1209,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       S.s_rmv[i] = 0;
       S.s_tch[i] = 0;
       S.s_tchr[i] = 0;
+      S.s_tvol[i] = 0;
     }
     for (int i = lane(); i < P; i += kWave) {
       W.queue[i] = i;
@@ -1320,7 +1339,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       S.cur_hpc = (uint64_t)rdl64((int64_t)w.hpc, wi);
       S.cur_hpu = (uint64_t)rdl64((int64_t)w.hpu, wi);
     }
-    if (!SIM && d.volAny) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
+    if (d.volAny) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
     if (TOPO) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
 #pragma unroll
     for (int r = 0; r < RM; r++) {
@@ -1346,7 +1365,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
           for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
           ok &= (whp[k] & S.cur_hpc) == 0;
-          if (!SIM && d.volAny && S.cur_vm && ok) ok = S.vol_ok(n);
+          if (d.volAny && S.cur_vm && ok) ok = S.vol_ok(n);
           if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), D.st_rs + (int64_t)s * d.RSW, 0);
           if (TOPO && S.t_mask && ok) ok = S.topo_node_ok(n);
           const uint64_t m = wballot(ok);
@@ -1368,7 +1387,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                 for (int r = 0; r < RM; r++) wrq[k][r] += pod[r];
                 whp[k] |= S.cur_hpu;
-                if (!SIM && d.volAny && S.cur_vm) S.vol_commit(j);
+                if (d.volAny && S.cur_vm) S.vol_commit(j);
               }
             }
           PH_BEGIN(t7);
@@ -1522,6 +1541,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if constexpr (SIM) S.sim_record(P, nclaims, hostCtr, allSched, err);
 }
 
+// Every translation unit instantiates one k_solve family (KS_TU 0: Solve, 1: Solve + topology,
+// 2: simulations, 3: simulations + topology; ks_solve_topo.hip / ks_sim.hip / ks_sim_topo.hip
+// include this file), so the four compile in parallel.
+template <bool SIM, bool TOPO>
+hipError_t launch_family(const KsDev& D, const KsWork* works_dev, int n, const Plan& pl, hipStream_t st) {
+#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, SIM, TOPO>), dim3(n), dim3(kWave), pl.lds, st, D, works_dev, pl)
+  const bool tl = pl.talloc != 0;
+  switch (D.d.R) {
+    case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;
+    case 4: if (tl) KS_LAUNCH(4, true); else KS_LAUNCH(4, false); break;
+    default: if (tl) KS_LAUNCH(0, true); else KS_LAUNCH(0, false); break;
+  }
+#undef KS_LAUNCH
+  return hipGetLastError();
+}
+using FamilyFn = hipError_t (*)(const KsDev&, const KsWork*, int, const Plan&, hipStream_t);
+hipError_t launch_solve_plain(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
+hipError_t launch_solve_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
+hipError_t launch_sims_plain(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
+hipError_t launch_sims_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
+
+#if KS_TU == 1
+hipError_t launch_solve_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
+  return launch_family<false, true>(D, w, n, pl, st);
+}
+#elif KS_TU == 2
+hipError_t launch_sims_plain(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
+  return launch_family<true, false>(D, w, n, pl, st);
+}
+#elif KS_TU == 3
+hipError_t launch_sims_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
+  return launch_family<true, true>(D, w, n, pl, st);
+}
+#else
+hipError_t launch_solve_plain(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
+  return launch_family<false, false>(D, w, n, pl, st);
+}
+
 // LDS plan.  Position-indexed state (order, pod count, template, headroom) bounds the NodeClaims
 // per Solve (KO); claims [0, KL) also keep their template/requests/max/options/thresholds in LDS,
 // the rest in HBM.  The instance-type tables go to LDS first when they leave room for 64 claims.
@@ -1534,7 +1591,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
                        r16(4 * (size_t)d.RSW) + 2 * r16(4 * TW + 8) + 16 * 16 +
-                       (sim ? 3 * r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
+                       (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
                        (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)
   const size_t clmB = 16 + 16 * R + 4 * TW + 4 * R;      // tpl, cnt, req, max, rem, thr (+ rounding)
@@ -1569,6 +1626,8 @@ hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp,
                       hipStream_t st);
 
 // One ks_solve: queue sort -> workspace init -> [mid event] -> k_solve (all on one stream).
+// Topology problems get their own instantiation: the group state would otherwise occupy SGPRs (and
+// their spills) across the whole commit loop of every topology-free Solve.
 hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
                         hipEvent_t mid) {
@@ -1577,21 +1636,7 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep, (const int32_t*)qorder);
   if (mid) (void)hipEventRecord(mid, st);
-  // Topology problems get their own instantiation: the group state would otherwise occupy SGPRs
-  // (and their spills) across the whole commit loop of every topology-free Solve.
-#define KS_LAUNCH(RT_, TL_)                                                                               \
-  {                                                                                                       \
-    if (D.d.G) hipLaunchKernelGGL((k_solve<RT_, TL_, false, true>), dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl); \
-    else hipLaunchKernelGGL((k_solve<RT_, TL_, false, false>), dim3(nrep), dim3(kWave), pl.lds, st, D, works_dev, pl);     \
-  }
-  const bool tl = pl.talloc != 0;
-  switch (D.d.R) {
-    case 3: if (tl) KS_LAUNCH(3, true) else KS_LAUNCH(3, false) break;
-    case 4: if (tl) KS_LAUNCH(4, true) else KS_LAUNCH(4, false) break;
-    default: if (tl) KS_LAUNCH(0, true) else KS_LAUNCH(0, false) break;
-  }
-#undef KS_LAUNCH
-  return hipGetLastError();
+  return (D.d.G ? launch_solve_topo : launch_solve_plain)(D, works_dev, nrep, pl, st);
 }
 
 // A batch of consolidation simulations (one wavefront each); their pod_map lists must already be
@@ -1599,19 +1644,8 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st) {
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
   if (nsims <= 0) return hipSuccess;
-#define KS_LAUNCH(RT_, TL_)                                                                                  \
-  {                                                                                                          \
-    if (D.d.G) hipLaunchKernelGGL((k_solve<RT_, TL_, true, true>), dim3(nsims), dim3(kWave), pl.lds, st, D, works_dev, pl); \
-    else hipLaunchKernelGGL((k_solve<RT_, TL_, true, false>), dim3(nsims), dim3(kWave), pl.lds, st, D, works_dev, pl);     \
-  }
-  const bool tl = pl.talloc != 0;
-  switch (D.d.R) {
-    case 3: if (tl) KS_LAUNCH(3, true) else KS_LAUNCH(3, false) break;
-    case 4: if (tl) KS_LAUNCH(4, true) else KS_LAUNCH(4, false) break;
-    default: if (tl) KS_LAUNCH(0, true) else KS_LAUNCH(0, false) break;
-  }
-#undef KS_LAUNCH
-  return hipGetLastError();
+  return (D.d.G ? launch_sims_topo : launch_sims_plain)(D, works_dev, nsims, pl, st);
 }
+#endif
 
 }  // namespace ks

@@ -117,6 +117,30 @@ def test_topology_cluster_parity(case):
         assert d is None, d
 
 
+def _volume_cluster(seed, n_nodes, ppn, topology=0):
+    import numpy as np
+
+    import problems
+    snap = synth.cluster_snapshot(n_nodes, ppn, n_its=40, it_range=(4, 20), seed=seed, n_pending=2, topology=topology)
+    pods = snap["pendingPods"] + [p for n in snap["stateNodes"] for p in n["pods"]]
+    snap["volumeDrivers"] = problems.add_volumes(np.random.default_rng(seed), pods, snap["stateNodes"])
+    return snap
+
+
+VOL_CASES = [(41, 12, 5, 0), (42, 16, 4, 0), (43, 10, 6, 0), (44, 14, 4, 6), (45, 8, 8, 0), (46, 12, 3, 4)]
+
+
+@pytest.mark.parametrize("seed,n_nodes,ppn,topo", VOL_CASES, ids=["v%d" % c[0] for c in VOL_CASES])
+def test_volume_cluster_parity(seed, n_nodes, ppn, topo):
+    """Simulations whose pods mount PVCs of limited CSI drivers onto nodes with CSINode limits and an
+    existing usage (volumeusage.go:183-227): each simulation's usage is copy-on-write over the shared one."""
+    snap = _volume_cluster(seed, n_nodes, ppn, topo)
+    for all_sims in (True, False):
+        want, got = _both(snap, all_sims)
+        d = _first_diff(want, got)
+        assert d is None, d
+
+
 def test_sharded_runs_gather_to_the_same_decision():
     """Ranks r of world W run simulations s % W == r; the [rank][slot] gather decides identically."""
     snap = json.dumps(synth.cluster_snapshot(30, 8, n_its=60, it_range=(6, 30), seed=11, spot_frac=0.5))
