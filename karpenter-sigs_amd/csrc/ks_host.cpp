@@ -235,7 +235,10 @@ static AffTerm jaffterm(const Value* t) {  // v1.PodAffinityTerm
   if (!t) return a;
   a.sel = jsel(t->get("labelSelector"));
   if (auto* ns = t->get("namespaces")) for (auto& x : ns->arr()) a.namespaces.push_back(x.str());
-  if (auto* nss = t->get("namespaceSelector"); nss && !nss->is_null()) a.nsSelector = true;
+  if (auto* nss = t->get("namespaceSelector"); nss && !nss->is_null()) {
+    a.nsSelector = true;
+    a.nsSel = jsel(nss);
+  }
   a.key = jstr(t, "topologyKey");
   return a;
 }
@@ -463,6 +466,14 @@ void Host::build(const Value& root) {
     throw KsError(-2, "explicit topology groups are not accepted: pass the pods' topology spread / pod "
                       "(anti-)affinity terms and the cluster's bound pods (clusterPods, clusterNodes)");
   if (auto* cps = root.get("clusterPods")) for (auto& v : cps->arr()) clusterPods.push_back(parse_pod(v));
+  if (auto* nss = root.get("namespaces"))  // the cluster's Namespace list, for namespaceSelector terms
+    for (auto& v : nss->arr()) {
+      const Value* md = v.get("metadata") ? v.get("metadata") : &v;
+      std::map<std::string, std::string> labels;
+      if (const Value* l = md->get("labels"))
+        for (auto& kv : l->obj()) labels[kv.first] = kv.second.str();
+      namespaceList.push_back({jstr(md, "name"), labels});
+    }
   if (auto* cns = root.get("clusterNodes"))
     for (auto& v : cns->arr()) nodeLabelsByName[jstr(&v, "name")] = jmap(v.get("labels"));
   if (auto* wk = root.get("wellKnownLabels")) for (auto& x : wk->arr()) wellKnown.insert(x.str());

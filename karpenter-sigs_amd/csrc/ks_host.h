@@ -29,7 +29,7 @@ struct PrefTerm { int32_t weight; std::vector<NSR> exprs; };
 // metav1.LabelSelector: matchLabels (as In with one value) then matchExpressions; nil = !present
 struct SelReq { std::string key, op; std::vector<std::string> values; };
 struct LabelSel { bool present = false; std::vector<SelReq> reqs; };
-struct AffTerm { LabelSel sel; std::vector<std::string> namespaces; bool nsSelector = false; std::string key; };
+struct AffTerm { LabelSel sel; std::vector<std::string> namespaces; bool nsSelector = false; LabelSel nsSel; std::string key; };
 struct SpreadC { std::string key, when; int32_t maxSkew = 0; int32_t minDomains = -1; LabelSel sel; };
 // HostPort (hostportusage.go:38-43): IP (net.ParseIP, 16-byte form), port, protocol
 struct HostPortH {
@@ -150,6 +150,7 @@ struct Host {
   int groupsOwned = 0;  // G1
   std::vector<PodH> clusterPods;
   std::map<std::string, std::map<std::string, std::string>> nodeLabelsByName;
+  std::vector<std::pair<std::string, std::map<std::string, std::string>>> namespaceList;  // (name, labels)
   std::vector<uint64_t> podGsel, podGinv;  // per pod: groups that select it / inverse groups it owns
   // Consolidation view (ks_cons.cpp): NewTopology excludes only these UIDs (the pods every simulation
   // schedules); each simulation then subtracts its candidates' pods from the counts it records below.

@@ -13,7 +13,7 @@
 // kernels iterate them in that order.  Every relaxation state of a pod must own a subset of the
 // groups the initial Update pass created: a group created later (a relaxed required node-affinity
 // term changes a spread group's node filter) would start counting mid-Solve, which is refused.
-// namespaceSelector terms are refused (KS_ERR_UNSUPPORTED).
+// namespaceSelector terms resolve against the snapshot's namespace list ("namespaces").
 #include <algorithm>
 #include <climits>
 
@@ -92,20 +92,6 @@ void Host::buildTopology() {
     tab.n_tdom.assign(1, -1);
     return;
   }
-  for (auto& p : pods) {
-    for (auto& t : p.affRequired)
-      if (t.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
-    for (auto& t : p.affPreferred)
-      if (t.second.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
-    for (auto& t : p.antiRequired)
-      if (t.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
-    for (auto& t : p.antiPreferred)
-      if (t.second.nsSelector) throw KsError(-2, "pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
-  }
-  for (auto& p : clusterPods)
-    for (auto& t : p.antiRequired)
-      if (t.nsSelector) throw KsError(-2, "cluster pod " + p.ns + "/" + p.name + ": namespaceSelector is not encoded");
-
   // --- domain universe (provisioner.go:229-283)
   std::map<std::string, std::set<std::string>> dom;
   auto valuesOf = [&](const std::vector<uint32_t>& rec, int k) {  // Requirement.Values(): the raw set
@@ -189,8 +175,20 @@ void Host::buildTopology() {
     }
     return g;
   };
-  auto termNs = [](const PodH& p, const AffTerm& t) {  // buildNamespaceList (topology.go:341-362)
-    return t.namespaces.empty() ? std::set<std::string>{p.ns} : std::set<std::string>(t.namespaces.begin(), t.namespaces.end());
+  // buildNamespaceList (topology.go:339-362): the pod's namespace when neither is set, else the listed
+  // namespaces plus the namespaces whose labels the selector matches (empty selector: all of them)
+  auto termNs = [&](const PodH& p, const AffTerm& t) {
+    if (t.namespaces.empty() && !t.nsSelector) return std::set<std::string>{p.ns};
+    std::set<std::string> out(t.namespaces.begin(), t.namespaces.end());
+    if (!t.nsSelector) return out;
+    if (!sel_valid(t.nsSel))
+      throw KsError(-1, "pod " + p.ns + "/" + p.name + ": tracking topology counts, parsing selector: invalid namespaceSelector");
+    for (auto& ns : namespaceList) {
+      bool ok = true;
+      for (auto& r : t.nsSel.reqs) ok = ok && sel_req_matches(r, ns.second);
+      if (ok) out.insert(ns.first);
+    }
+    return out;
   };
   auto countDomains = [&](TopoGroup& g, int gidx) {  // topology.go:238-291
     for (auto& cp : clusterPods) {

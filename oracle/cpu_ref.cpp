@@ -376,6 +376,7 @@ struct PodAffinityTermS {
   LabelSelector selector;
   vector<string> namespaces;
   bool hasNamespaceSelector = false;
+  LabelSelector namespaceSelector;
   string topologyKey;
 };
 struct TSCS {
@@ -633,6 +634,7 @@ struct Problem {
   // cluster state the Topology counts (topology.go:190-291): bound pods and node labels by node name
   vector<Pod> clusterPods;
   map<string, map<string, string>> nodeLabels;
+  vector<std::pair<string, map<string, string>>> namespaces;  // the cluster's Namespace list (name, labels)
   map<string, string> volumeDrivers;  // "ns/pvc" -> resolved CSI driver (resolveDriver, volumeusage.go:115-172)
 };
 
@@ -733,7 +735,10 @@ static PodAffinityTermS parseAffinityTerm(const ojson::Value& t) {
   PodAffinityTermS a;
   a.selector = parseLabelSelector(t.get("labelSelector"));
   if (auto* ns = t.get("namespaces")) for (auto& x : ns->arr()) a.namespaces.push_back(x.str());
-  if (auto* nss = t.get("namespaceSelector"); nss && !nss->is_null()) a.hasNamespaceSelector = true;
+  if (auto* nss = t.get("namespaceSelector"); nss && !nss->is_null()) {
+    a.hasNamespaceSelector = true;
+    a.namespaceSelector = parseLabelSelector(nss);
+  }
   a.topologyKey = t.get("topologyKey") ? t.get("topologyKey")->str() : "";
   return a;
 }
@@ -954,6 +959,11 @@ static Problem parseProblem(const ojson::Value& root) {
   if (auto* vd = root.get("volumeDrivers"))
     for (auto& kv : vd->obj()) pb.volumeDrivers[kv.first] = kv.second.str();
   if (auto* cps = root.get("clusterPods")) for (auto& v : cps->arr()) pb.clusterPods.push_back(parsePod(v));
+  if (auto* nss = root.get("namespaces"))
+    for (auto& v : nss->arr()) {
+      const ojson::Value* md = v.get("metadata") ? v.get("metadata") : &v;
+      pb.namespaces.push_back({md->get("name") ? md->get("name")->str() : "", strMap(md->get("labels"))});
+    }
   for (auto& n : pb.nodes) pb.nodeLabels[n.name] = n.labels;
   if (auto* cns = root.get("clusterNodes"))
     for (auto& v : cns->arr()) pb.nodeLabels[v.get("name") ? v.get("name")->str() : ""] = strMap(v.get("labels"));
@@ -1125,6 +1135,7 @@ class Scheduler {
     topo_.domains = topologyDomains(pb_);
     topo_.clusterPods = &pb_.clusterPods;
     topo_.nodes = &pb_.nodeLabels;
+    topo_.namespaceList = &pb_.namespaces;
     for (auto& p : pb_.pods) topo_.excluded.insert(p.uid);
     for (auto& cp : pb_.clusterPods) {  // updateInverseAffinities via ForPodsWithAntiAffinity
       if (!(cp.hasAffinity && cp.hasPodAnti && !cp.antiRequired.empty())) continue;

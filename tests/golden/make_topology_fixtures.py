@@ -268,6 +268,31 @@ def scenarios():
     add("affinity-namespace-list", "2282-2320",
         P(10, LABELS, [tsc(host)]) + P(1, sec, namespace="other-ns-list") + P(1, aff_required=[t_ns]),
         {"scheduled": [10, 11], "one_node": [10, 11]})
+    # the envtest cluster's namespaces plus the one the test applies (topology_test.go:2331)
+    namespaces = [{"name": n} for n in ("default", "kube-system", "kube-public", "kube-node-lease")] + [
+        {"name": "empty-ns-selector", "labels": {"foo": "bar"}}]
+    P = PodFactory()
+    t_sel = {"labelSelector": {"matchLabels": dict(sec)}, "namespaceSelector": {"matchLabels": {}}, "topologyKey": host}
+    add("affinity-namespace-empty-selector", "2321-2361",
+        P(10, LABELS, [tsc(host)]) + P(1, sec, namespace="empty-ns-selector") + P(1, aff_required=[t_sel]),
+        {"scheduled": [10, 11], "one_node": [10, 11]})
+    out[-1]["snapshot"]["namespaces"] = namespaces
+    # the same test with a selector that picks the namespace by label, and one that matches nothing
+    P = PodFactory()
+    t_lab = {"labelSelector": {"matchLabels": dict(sec)}, "namespaceSelector": {"matchLabels": {"foo": "bar"}},
+             "topologyKey": host}
+    add("affinity-namespace-label-selector", "2321-2361",
+        P(10, LABELS, [tsc(host)]) + P(1, sec, namespace="empty-ns-selector") + P(1, aff_required=[t_lab]),
+        {"scheduled": [10, 11], "one_node": [10, 11]})
+    out[-1]["snapshot"]["namespaces"] = namespaces
+    P = PodFactory()
+    t_none = {"labelSelector": {"matchLabels": dict(sec)},
+              "namespaceSelector": {"matchExpressions": [{"key": "foo", "operator": "In", "values": ["baz"]}]},
+              "topologyKey": host}
+    add("affinity-namespace-selector-no-match", "2244-2281",
+        P(10, LABELS, [tsc(host)]) + P(1, sec, namespace="empty-ns-selector") + P(1, aff_required=[t_none]),
+        {"scheduled": [10], "unscheduled": [11]})
+    out[-1]["snapshot"]["namespaces"] = namespaces
     return out
 
 

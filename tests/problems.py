@@ -264,8 +264,43 @@ def add_topology(rng, pods, nodes, affinity=False):
     return cluster
 
 
+NAMESPACES = [("default", {"env": "prod"}), ("team-a", {"env": "prod", "team": "a"}), ("team-b", {"env": "dev"}),
+              ("kube-system", {})]
+
+
+def add_namespaces(rng, pods, cluster):
+    """Spread pods and cluster pods over four namespaces and give the (anti-)affinity terms a
+    namespace list or a namespaceSelector (buildNamespaceList, topology.go:339-362): empty (every
+    namespace), by label, or matching nothing.  Returns the snapshot's namespace list."""
+    terms = []
+    for p in pods + cluster:
+        p["metadata"]["namespace"] = _pick(rng, [n for n, _ in NAMESPACES[:3]])
+        aff = p["spec"].get("affinity", {})
+        for kind in ("podAffinity", "podAntiAffinity"):
+            for t in aff.get(kind, {}).get("requiredDuringSchedulingIgnoredDuringExecution", []):
+                terms.append(t)
+            for w in aff.get(kind, {}).get("preferredDuringSchedulingIgnoredDuringExecution", []):
+                terms.append(w["podAffinityTerm"])
+    seen = set()
+    for t in terms:  # app specs share term dicts: decide once per dict
+        if id(t) in seen:
+            continue
+        seen.add(id(t))
+        u = rng.random()
+        if u < 0.2:
+            t["namespaceSelector"] = {}
+        elif u < 0.4:
+            t["namespaceSelector"] = {"matchLabels": {"env": _pick(rng, ["prod", "dev"])}}
+        elif u < 0.5:
+            t["namespaceSelector"] = {"matchExpressions": [{"key": "team", "operator": "Exists"}]}
+            t["namespaces"] = ["team-b"]
+        elif u < 0.6:
+            t["namespaces"] = ["default", "team-a"]
+    return [{"name": n, "labels": lab} for n, lab in NAMESPACES]
+
+
 def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False, topology=False,
-                   affinity=False, volumes=False):
+                   affinity=False, volumes=False, namespaces=False):
     rng = np.random.default_rng(seed)
     its = random_its(rng, n_its)
     n_templates = int(rng.integers(1, 4)) if n_templates is None else n_templates
@@ -327,8 +362,10 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
             if rng.random() < 0.4:
                 add_host_ports(rng, p)
     cluster = add_topology(rng, pods, nodes, affinity) if topology else []
+    nss = add_namespaces(rng, pods, cluster) if namespaces else []
     vdrivers = add_volumes(rng, pods, nodes) if volumes else {}
     return {
+        **({"namespaces": nss} if namespaces else {}),
         "volumeDrivers": vdrivers,
         "wellKnownLabels": synth.FAKE_WELL_KNOWN,
         "instanceTypes": its,

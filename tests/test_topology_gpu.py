@@ -83,6 +83,15 @@ def test_random_pod_affinity_parity(seed):
     assert d is None, d
 
 
+@pytest.mark.parametrize("seed", list(range(390, 406)))
+def test_random_namespace_selector_parity(seed):
+    """Pods and cluster pods over four namespaces; (anti-)affinity terms with namespace lists and
+    namespaceSelectors (empty, by label, with a list) resolved against the snapshot's namespaces."""
+    want, got = _solve_both(problems.random_problem(seed, n_pods=150, topology=True, affinity=True, namespaces=True))
+    d = _diff(want, got)
+    assert d is None, d
+
+
 @pytest.mark.parametrize("seed", [340, 341, 342, 343])
 def test_random_topology_parity_larger(seed):
     want, got = _solve_both(problems.random_problem(seed, n_pods=800, n_its=120, n_nodes=30, topology=True))
