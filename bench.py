@@ -25,16 +25,19 @@ sys.path.insert(0, os.path.join(ROOT, "karpenter-sigs_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def consolidation_bench(args, rank, world, local, dist, barrier_sync):
+def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0):
     """C5 (BASELINE.json configs[4]): one consolidation pass = every candidate-deletion simulation of
     a 5k-node / 100k-pod cluster (5000 single-node + 100 multi-node prefix sims), sharded over the
     ranks by simulation index (s % world == rank), records all-gathered over RCCL, then the
-    reference's sequential selection on rank 0.  value = simulations completed per second."""
+    reference's sequential selection on rank 0.  value = simulations completed per second.
+    topology=A: the same cluster with its pods in A apps carrying zonal / hostname spread, pod
+    affinity and anti-affinity (synth.cluster_snapshot), every bound pod listed in clusterPods."""
     import torch
 
     from karpenter_amd import Consolidator, synth
 
-    snap = json.dumps(synth.config5(args.cons_nodes))
+    snap = json.dumps(synth.config5(args.cons_nodes) if not topology else
+                      synth.cluster_snapshot(args.cons_nodes, 20, 400, seed=4205, topology=topology))
     c = Consolidator(snap)
     per, rb = c.records_per_rank(world), c.record_bytes
     dev = "cuda:%d" % local
@@ -93,12 +96,13 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync):
     if not args.no_cpu_baseline and world == 1:
         from oracle import bridge
 
-        n, secs = bridge.time_cons_sims(snap, args.cpu_sims, args.cpu_threads)
+        n, secs = bridge.time_cons_sims(snap, args.cpu_sims if not topology else args.cpu_topo_sims, args.cpu_threads)
         cpu = {"value": round(n / secs, 2), "unit": "cands/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": "first %d single-node simulations of C5 (simulateScheduling + computeConsolidation, "
-                         "oracle/cpu_ref.cpp, %d host threads, %.1f s)" % (n, args.cpu_threads, secs)}
+               "sample": "first %d single-node simulations of the same cluster (simulateScheduling + "
+                         "computeConsolidation, oracle/cpu_ref.cpp, %d host threads, %.1f s)" % (n, args.cpu_threads, secs)}
+    name = "C5" if not topology else "C5 + topology (%d apps: spread, pod affinity, anti-affinity)" % topology
     return {
-        "metric": "consolidation cands/sec (C5: %d nodes x 20 pods, 400 instance types)" % args.cons_nodes,
+        "metric": "consolidation cands/sec (%s: %d nodes x 20 pods, 400 instance types)" % (name, args.cons_nodes),
         "value": round(c.num_sims * args.cons_steps / elapsed, 1),
         "unit": "cands/s",
         "n_gpus": world,
@@ -109,8 +113,9 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync):
         "candidates": c.num_candidates,
         "decision": {"multi": [doc["multi"]["command"]["action"], len(doc["multi"]["command"]["candidates"])],
                      "single": [doc["single"]["command"]["action"], doc["single"]["command"]["candidates"]]},
-        "roofline": {"bound": "hbm", "kernel": "k_solve<SIM>", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("cons_c5"),
+        "roofline": {"bound": "hbm", "kernel": "k_solve<SIM%s>" % (", TOPO" if topology else ""),
+                     "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("cons_c5" if not topology else "cons_c5t"),
                      "algorithmic_bytes_per_pass": algb, "kernel_ms": round(k_ms, 3), "kernel_ms_max_rank": round(kmax, 3)},
         "cpu_baseline": cpu,
     }
@@ -130,11 +135,20 @@ def c3_bench(args, local):
     for _ in range(2):
         ks.append(sch.solve(device=local, timing_only=True).solve_kernel_ms)
     el = (time.perf_counter() - t0) / 2
-    return {"metric": "pods/sec in Scheduler.Solve (C3: %d pods, 800 instance types x 8 offerings, 3 tainted "
-                      "NodePools, selectors/affinity/tolerations)" % args.c3_pods,
-            "value": round(args.c3_pods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1000, 3),
-            "kernel_ms": round(sum(ks) / len(ks), 3), "new_nodeclaims": len(r.new_nodeclaims),
-            "pods_placed": placed, "pod_errors": len(r.pod_errors)}
+    out = {"metric": "pods/sec in Scheduler.Solve (C3: %d pods, 800 instance types x 8 offerings, 3 tainted "
+                     "NodePools, selectors/affinity/tolerations)" % args.c3_pods,
+           "value": round(args.c3_pods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1000, 3),
+           "kernel_ms": round(sum(ks) / len(ks), 3), "new_nodeclaims": len(r.new_nodeclaims),
+           "pods_placed": placed, "pod_errors": len(r.pod_errors), "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        from oracle import bridge
+
+        sp = min(args.c3_cpu_pods, args.c3_pods)
+        secs = bridge.time_solve(json.dumps(synth.config3(sp)), 1)
+        out["cpu_baseline"] = {"value": round(sp / secs, 1), "unit": "pods/s", "cores": 1, "kind": "port",
+                               "sample": "1 Solve of C3 with %d pods (oracle/cpu_ref.cpp, single thread, %.1f s); "
+                                         "the oracle's per-pod cost grows with the pod count" % (sp, secs)}
+    return out
 
 
 def c4_bench(args, local):
@@ -196,6 +210,9 @@ def main():
     ap.add_argument("--cons-steps", type=int, default=20)
     ap.add_argument("--cpu-sims", type=int, default=2400, help="oracle consolidation sample (simulations)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--c3-cpu-pods", type=int, default=2000, help="oracle C3 sample (pods)")
+    ap.add_argument("--cons-topo-apps", type=int, default=20, help="topology consolidation line: apps (0: skip)")
+    ap.add_argument("--cpu-topo-sims", type=int, default=100, help="oracle sample for the topology consolidation line")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -220,8 +237,10 @@ def main():
 
     if args.only_consolidation:
         cons = consolidation_bench(args, rank, world, local, dist, barrier_sync)
+        ctopo = (consolidation_bench(args, rank, world, local, dist, barrier_sync, args.cons_topo_apps)
+                 if args.cons_topo_apps else None)
         if rank == 0:
-            print(json.dumps({"consolidation": cons}))
+            print(json.dumps({"consolidation": cons, "consolidation_topology": ctopo}))
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -272,6 +291,9 @@ def main():
     c3 = None if args.no_c3 or world > 1 else c3_bench(args, local)
     c4 = None if args.no_c4 or world > 1 else c4_bench(args, local)
     cons = None if args.no_consolidation else consolidation_bench(args, rank, world, local, dist, barrier_sync)
+    ctopo = None
+    if not args.no_consolidation and args.cons_topo_apps:
+        ctopo = consolidation_bench(args, rank, world, local, dist, barrier_sync, args.cons_topo_apps)
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -300,6 +322,7 @@ def main():
         "solve_c3": c3,
         "solve_c4": c4,
         "consolidation": cons,
+        "consolidation_topology": ctopo,
     }
     print(json.dumps(out))
     if dist is not None:

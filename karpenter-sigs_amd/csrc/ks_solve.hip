@@ -176,6 +176,7 @@ struct Solver {
   uint64_t t_sel = 0;   // groups whose selector selects the popped pod
   uint64_t t_inv = 0;   // inverse groups the popped pod owns
   int t_s = 0;          // the popped pod's relaxation state
+  bool t_nonode = false;  // some matching group admits no domain at all: no existing node can pass
   int64_t algbytes = 0;
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
   uint64_t cur_vm = 0;                // the popped pod's PVCs of limited drivers (Solve only; SIM refuses them)
@@ -423,34 +424,57 @@ struct Solver {
     const uint64_t owned = d.G1 >= 64 ? ~0ull : ((1ull << d.G1) - 1);
     t_mask = D.st_gown[s] | (t_sel & all & ~owned);
     if (SIM) t_mask &= ~W.tdead;
+    t_nonode = false;
     for (uint64_t m = t_mask; m; m &= m - 1) {
       const int g = ctz64(m);
       if (tg(g, TGM_TYPE) == TG_AFFINITY) {
         const int nv = tg(g, TGM_NV);
-        bool pos = false;
-        for (int v = lane(); v < nv && !pos; v += kWave) pos = tcnt(g, v) > 0 && tpod_has(g, v);
+        bool pos = false, reg = false;
+        for (int v = lane(); v < nv && !pos; v += kWave) {
+          const int c = tcnt(g, v);
+          const bool has = c >= 0 && tpod_has(g, v);
+          pos = has && c > 0;
+          reg = reg || has;
+        }
         if (lane() == 0 && tg(g, TGM_HOST) && tpod_has(g, nv) && ld_sc1(W.tg_cpos + g) > 0) pos = true;
         const bool any = wballot(pos) != 0;
         if (lane() == 0) s_tmin[g] = any ? 1 : 0;
+        // topo_node_ok's test for this group over every domain: with a selected pod somewhere the
+        // node's domain must hold one; otherwise only a self-selecting pod passes (a registered domain)
+        if (!tg(g, TGM_HOST) && !any && !(((t_sel >> g) & 1ull) && wballot(reg))) t_nonode = true;
+        continue;
+      }
+      if (tg(g, TGM_TYPE) == TG_ANTI) {  // topo_node_ok: the node's domain must hold no selected pod
+        if (!tg(g, TGM_HOST)) {
+          const int nv = tg(g, TGM_NV);
+          bool ok = false;
+          for (int v = lane(); v < nv && !ok; v += kWave) ok = tcnt(g, v) == 0 && tpod_has(g, v);
+          if (!wballot(ok)) t_nonode = true;
+        }
         continue;
       }
       if (tg(g, TGM_TYPE) != TG_SPREAD) continue;
       int mn = 0x7fffffff, num = 0;
       if (!tg(g, TGM_HOST)) {  // hostname groups always have a min of 0
         const int nv = tg(g, TGM_NV);
+        int lo = 0x7fffffff;  // smallest registered count (any domain): topo_node_ok's best case
         for (int v = lane(); v < nv; v += kWave) {
           const int c = tcnt(g, v);
+          if (c >= 0) lo = c < lo ? c : lo;
           if (c >= 0 && tpod_has(g, v)) {
             num++;
             mn = c < mn ? c : mn;
           }
         }
         for (int off = 32; off >= 1; off >>= 1) {
-          const int o = __shfl_xor(mn, off);
+          const int o = __shfl_xor(mn, off), l = __shfl_xor(lo, off);
           mn = o < mn ? o : mn;
+          lo = l < lo ? l : lo;
           num += __shfl_xor(num, off);
         }
         if (tg(g, TGM_MIND) >= 0 && num < tg(g, TGM_MIND)) mn = 0;
+        const int self = (int)((t_sel >> g) & 1ull);
+        if (lo == 0x7fffffff || (int64_t)lo + self - mn > tg(g, TGM_SKEW)) t_nonode = true;
       } else {
         mn = 0;
       }
@@ -1349,11 +1373,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     wi++;
     PH_END(t0, 0);
     bool placed = false;
-    // 1) existing nodes in order
+    // 1) existing nodes in order (none can pass when a matching group admits no domain)
     PH_BEGIN(t1);
+    const bool skipNodes = TOPO && S.t_nonode;
     int scanFrom = 0;
     if constexpr (NW > 0) {
-      if (d.N > 0) {
+      if (d.N > 0 && !skipNodes) {
         int kj = -1;
         uint64_t mj = 0;
         asm volatile("; KS_MARK window_begin");
@@ -1408,7 +1433,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         scanFrom = NW * kWave;
       }
     }
-    for (int base = scanFrom; base < d.N && !placed; base += 2 * kWave) {
+    for (int base = skipNodes ? d.N : scanFrom; base < d.N && !placed; base += 2 * kWave) {
       bool ok0, ok1;
       int nf0, nf1;
       int64_t q0[RM], q1[RM];

@@ -11,7 +11,8 @@ from karpenter_amd import Consolidator, synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
 t = time.time()
-snap = json.dumps(synth.config5(n))
+topo = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+snap = json.dumps(synth.config5(n) if not topo else synth.cluster_snapshot(n, 20, 400, seed=4205, topology=topo))
 t1 = time.time()
 c = Consolidator(snap)
 t2 = time.time()
