@@ -129,29 +129,38 @@ struct GoSortT {
 template <class P>
 struct GoSortExactT {
   GoSortT<P> s;
-  KS_HD void run(int n) {
+  // resumePivot >= 0: the top-level call already chose that pivot (increasing hint) and ran a
+  // partialInsertionSort that returned false (the kernels' wave-parallel one); continue from there.
+  KS_HD void run(int n, int resumePivot = -1) {
     struct Frame { int a, b, limit; bool wb, wp; };
     Frame stack[64];
     int sp = 0;
     stack[sp++] = Frame{0, n, GoSortT<P>::bitsLen((uint32_t)n), true, true};
+    bool resume = resumePivot >= 0;
     while (sp > 0) {
       Frame f = stack[--sp];
       int a = f.a, b = f.b, limit = f.limit;
       bool wasBalanced = f.wb, wasPartitioned = f.wp;
       for (;;) {
         int length = b - a;
-        if (length <= 12) { s.insertionSort(a, b); break; }
-        if (limit == 0) { s.heapSort(a, b); break; }
-        if (!wasBalanced) { s.breakPatterns(a, b); limit--; }
-        int hint;
-        int pivot = s.choosePivot(a, b, hint);
-        if (hint == 2) {
-          for (int i = a, j = b - 1; i < j; i++, j--) s.swap(i, j);
-          pivot = (b - 1) - (pivot - a);
-          hint = 1;
+        int pivot;
+        if (resume) {
+          resume = false;
+          pivot = resumePivot;
+        } else {
+          if (length <= 12) { s.insertionSort(a, b); break; }
+          if (limit == 0) { s.heapSort(a, b); break; }
+          if (!wasBalanced) { s.breakPatterns(a, b); limit--; }
+          int hint;
+          pivot = s.choosePivot(a, b, hint);
+          if (hint == 2) {
+            for (int i = a, j = b - 1; i < j; i++, j--) s.swap(i, j);
+            pivot = (b - 1) - (pivot - a);
+            hint = 1;
+          }
+          if (wasBalanced && wasPartitioned && hint == 1)
+            if (s.partialInsertionSort(a, b)) break;
         }
-        if (wasBalanced && wasPartitioned && hint == 1)
-          if (s.partialInsertionSort(a, b)) break;
         if (a > 0 && !s.less(a - 1, pivot)) {
           a = s.partitionEqual(a, b, pivot);
           continue;

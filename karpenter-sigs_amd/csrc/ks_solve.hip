@@ -1003,13 +1003,102 @@ struct Solver {
   // Called only when the array is not non-decreasing (a non-decreasing array is provably left
   // untouched by pdqsort).  Lane 0 replays Go's pdqsort_func; the position-indexed quick-reject
   // arrays are then regathered from the claims.
+  // Move the entry at position `from` to `to`, shifting the ones between by one (wave-parallel, in
+  // 64-entry chunks ordered so every chunk is read before it is overwritten).  Equals the adjacent
+  // swap chains of partialInsertionSort.
+  __device__ __forceinline__ void pis_move(int from, int to) {
+    if (from == to) return;
+    const int k0 = uni(s_okey[from]), v0 = uni(s_order[from]);
+    wsync();
+    if (to < from) {  // [to, from) shifts right, high chunk first
+      for (int hi = from; hi > to; hi -= kWave) {
+        const int lo = hi - kWave > to ? hi - kWave : to, j = lo + lane();
+        int k = 0, v = 0;
+        if (j < hi) { k = s_okey[j]; v = s_order[j]; }
+        wsync();
+        if (j < hi) { s_okey[j + 1] = k; s_order[j + 1] = v; }
+        wsync();
+      }
+    } else {  // (from, to] shifts left, low chunk first
+      for (int lo = from + 1; lo <= to; lo += kWave) {
+        const int hi = lo + kWave <= to + 1 ? lo + kWave : to + 1, j = lo + lane();
+        int k = 0, v = 0;
+        if (j < hi) { k = s_okey[j]; v = s_order[j]; }
+        wsync();
+        if (j < hi) { s_okey[j - 1] = k; s_order[j - 1] = v; }
+        wsync();
+      }
+    }
+    if (lane() == 0) { s_okey[to] = k0; s_order[to] = v0; }
+    wsync();
+  }
+  // First i in [from, n) with key[i] < key[i-1] (a descent), or n.
+  __device__ __forceinline__ int pis_descent(int from, int n) const {
+    for (int base = from; base < n; base += kWave) {
+      const int i = base + lane();
+      const uint64_t m = wballot(i < n && s_okey[i] < s_okey[i - 1]);
+      if (m) return base + ctz64(m);
+    }
+    return n;
+  }
+  // partialInsertionSort_func(data, 0, n) of Go 1.21 (zsortfunc.go), wave-parallel: each of its <= 5
+  // steps finds the next descent by ballot, swaps the pair, then moves the smaller entry left past
+  // every greater one and the greater entry right past every smaller one.  Returns its result and
+  // widens [tlo, thi] to the positions it moved.
+  __device__ __forceinline__ bool pis_wave(int n, int& tlo, int& thi) {
+    int i = 1;
+    for (int step = 0; step < 5; step++) {
+      i = pis_descent(i, n);
+      if (i == n) return true;
+      if (n < 50) return false;
+      const int x = uni(s_okey[i]), y = uni(s_okey[i - 1]);  // after the swap: x at i-1, y at i
+      int p = i - 1;  // x passes the entries q < i-1 with x < key[q]
+      for (int hi = i - 1; hi > 0; hi -= kWave) {
+        const int q = hi - 1 - lane();
+        const uint64_t m = wballot(q >= 0 && !(x < s_okey[q]));
+        if (m) { p = hi - ctz64(m); break; }
+        p = hi - kWave > 0 ? hi - kWave : 0;
+      }
+      int r = i;  // y passes the entries q > i with key[q] < y
+      for (int lo = i + 1; lo < n; lo += kWave) {
+        const int q = lo + lane();
+        const uint64_t m = wballot(q < n && !(s_okey[q] < y));
+        if (m) { r = lo + ctz64(m) - 1; break; }
+        r = lo + kWave - 1 < n - 1 ? lo + kWave - 1 : n - 1;
+      }
+      pis_move(i, p);  // x (at i before the swap) to p; y moves from i-1 to i with the shifted run
+      pis_move(i, r);  // y to r
+      tlo = p < tlo ? p : tlo;
+      thi = r > thi ? r : thi;
+    }
+    return false;
+  }
   __device__ __forceinline__ void sort_claims(int n) {
-    if (lane() == 0) {
-      GoSortExactT<LI32> g{GoSortT<LI32>{s_okey, s_order}};
-      g.run(n);
+    int tlo = n, thi = -1, pivot = -1;
+    bool done = false;
+    if (n > 12) {  // pdqsort_func's top-level frame: choosePivot (reads only), then partialInsertionSort
+      int hint = 0, pv = -1;
+      if (lane() == 0) {
+        GoSortT<LI32> g{s_okey, s_order};
+        pv = g.choosePivot(0, n, hint);
+      }
+      hint = rdl(hint, 0);
+      pv = rdl(pv, 0);
+      if (hint == 1) {
+        pivot = pv;
+        done = pis_wave(n, tlo, thi);
+      }
+    }
+    if (!done) {
+      if (lane() == 0) {
+        GoSortExactT<LI32> g{GoSortT<LI32>{s_okey, s_order}};
+        g.run(n, pivot);
+      }
+      tlo = 0;
+      thi = n - 1;
     }
     wsync();
-    for (int j = lane(); j < n; j += kWave) {
+    for (int j = tlo + lane(); j <= thi; j += kWave) {
       const int c = s_order[j];
       const bool inl = c < pl.KL;
       s_ptpl[j] = inl ? lc.tpl[c] : W.c_tpl[c];
@@ -1019,7 +1108,7 @@ struct Solver {
       }
     }
     wsync();
-    algbytes += (int64_t)n * (8 + 16 * R());
+    algbytes += (int64_t)(thi - tlo + 1) * (8 + 16 * R());
   }
 
   // --- consolidation decision for this simulation (SIM epilogue) -------------------------------

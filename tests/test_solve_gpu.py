@@ -68,6 +68,15 @@ def test_config3_selectors_affinity_taints():
     assert d is None, d
 
 
+def test_config3_long_claim_sorts():
+    """C3 at 4000 pods: ~200 NodeClaims, so the per-placement sort.Slice (scheduler.go:247) runs the
+    wave-parallel partialInsertionSort on long arrays, and falls back to the serial pdqsort resume."""
+    want, got = _solve_both(synth.config3(4000))
+    d = _diff(want, got)
+    assert d is None, d
+    assert got.stats["sortsWithDescent"] > 100
+
+
 def test_config1_benchmark_scheduling_2000():
     """BenchmarkScheduling2000 (scheduling_benchmark_test.go:72-74,116-182)."""
     want, got = _solve_both(synth.config1())
