@@ -362,7 +362,33 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     }
     j += "],\"requirementsString\":";
     ksjson::quote(j, h.reqsString(rec, cl.host));
-    j += "}";
+    // NodeClaimTemplate.ToNodeClaim's launch list (nodeclaimtemplate.go:55-60): the options ordered by
+    // (cheapest available offering the claim's zone / capacity-type requirements allow, name)
+    // (OrderByPrice, types.go:62-79; Offerings.Requirements / Cheapest :147-166), first 100.
+    auto allows = [&](int key, const std::string& v) {  // Requirements.Get(key).Has(v); missing key = Exists
+      if (key < 0 || !bit(rs_present(rec), key)) return true;
+      auto id = h.valueId[(size_t)key].find(v);
+      if (id != h.valueId[(size_t)key].end()) return rs_member(h.L, rec, key, id->second);
+      return bit(rs_compl(rec), key);  // a value outside the universe: only a complement set holds it
+    };
+    std::vector<std::pair<double, std::string>> launch;
+    for (int it : cl.its) {
+      double price = std::numeric_limits<double>::max();
+      bool any = false;
+      for (auto& of : h.its[(size_t)it].all) {
+        if (!of.available || !allows(h.zoneKey, of.zone) || !allows(h.ctKey, of.ct)) continue;
+        if (!any || of.price < price) price = of.price;
+        any = true;
+      }
+      launch.push_back({price, h.its[(size_t)it].name});
+    }
+    std::sort(launch.begin(), launch.end());
+    j += ",\"launchInstanceTypes\":[";
+    for (size_t i = 0; i < launch.size() && i < 100; i++) {
+      if (i) j += ",";
+      ksjson::quote(j, launch[i].second);
+    }
+    j += "]}";
     cl.json = j;
     res->claims.push_back(std::move(cl));
   }

@@ -1462,7 +1462,29 @@ string Scheduler::ResultsJSON() const {
     }
     o += "],\"requirementsString\":";
     ojson::quote(o, c.reqs.String());
-    o += "}";
+    // NodeClaimTemplate.ToNodeClaim (nodeclaimtemplate.go:55-60): the launch list is
+    // InstanceTypeOptions.OrderByPrice(Requirements) (types.go:62-79) cut to its first 100 entries;
+    // an option's price is its cheapest available offering the zone / capacity-type requirements
+    // allow (Offerings.Available().Requirements(reqs).Cheapest(), types.go:147-166), else MaxFloat64.
+    vector<std::pair<double, string>> launch;
+    const Requirement zone = c.reqs.Get(kZone), ct = c.reqs.Get(kCapacityType);
+    for (int it : c.itOptions) {
+      double price = std::numeric_limits<double>::max();
+      bool any = false;
+      for (auto& of : pb_.its[it].offerings) {
+        if (!of.available || !Has(zone, of.zone) || !Has(ct, of.capacityType)) continue;
+        if (!any || of.price < price) price = of.price;
+        any = true;
+      }
+      launch.push_back({price, pb_.its[it].name});
+    }
+    std::sort(launch.begin(), launch.end());  // price, then name (names are unique)
+    o += ",\"launchInstanceTypes\":[";
+    for (size_t i = 0; i < launch.size() && i < 100; i++) {
+      if (i) o += ",";
+      ojson::quote(o, launch[i].second);
+    }
+    o += "]}";
   }
   o += "],\"existingNodes\":[";
   for (size_t k = 0; k < existing_.size(); k++) {

@@ -3,7 +3,10 @@
 
 def launched_type(claim, snap):
     """fake CloudProvider.Create (fake/cloudprovider.go:96-141): the cheapest option by the price of its
-    available offerings (claim requirements restrict zone / capacity-type)."""
+    available offerings (claim requirements restrict zone / capacity-type).  With the launch list the
+    product renders (ToNodeClaim + OrderByPrice), that is its first entry; the fallback recomputes it."""
+    if claim.get("launchInstanceTypes"):
+        return claim["launchInstanceTypes"][0]
     its = {it["name"]: it for it in snap["instanceTypes"]}
     zone_ok, ct_ok = None, None
     for r in claim["requirements"]:
