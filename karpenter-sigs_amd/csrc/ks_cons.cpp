@@ -49,6 +49,67 @@ std::string jstr(const Value* v, const char* k, const std::string& d = "") {
   return x && x->is_str() ? x->str() : d;
 }
 
+// PDBLimits (pdblimits.go:36-110): the snapshot's PodDisruptionBudgets
+struct Pdb {
+  std::string ns;
+  bool present = false;  // LabelSelectorAsSelector(nil) = Nothing; {} = Everything
+  std::vector<std::pair<std::string, std::pair<std::string, std::vector<std::string>>>> reqs;  // key, (op, values)
+  int64_t allowed = 0;
+  bool unhealthyAlways = false;
+};
+std::vector<Pdb> parse_pdbs(const Value& root) {
+  std::vector<Pdb> out;
+  const Value* ps = root.get("podDisruptionBudgets");
+  if (!ps) return out;
+  for (auto& v : ps->arr()) {
+    Pdb b;
+    b.ns = jstr(v.get("metadata"), "namespace");
+    const Value* sp = v.get("spec");
+    const Value* sel = sp ? sp->get("selector") : nullptr;
+    if (sel && !sel->is_null()) {
+      b.present = true;
+      if (const Value* ml = sel->get("matchLabels"))
+        for (auto& kv : ml->obj()) b.reqs.push_back({kv.first, {"In", {kv.second.str()}}});
+      if (const Value* me = sel->get("matchExpressions"))
+        for (auto& e : me->arr()) {
+          std::vector<std::string> vals;
+          if (const Value* vs = e.get("values")) for (auto& x : vs->arr()) vals.push_back(x.str());
+          const std::string op = jstr(&e, "operator");
+          const bool setOp = op == "In" || op == "NotIn", exOp = op == "Exists" || op == "DoesNotExist";
+          if (!(setOp || exOp) || (setOp && vals.empty()) || (exOp && !vals.empty()))
+            throw KsError(KS_ERR_PARSE, "tracking PodDisruptionBudgets: invalid selector");
+          b.reqs.push_back({jstr(&e, "key"), {op, vals}});
+        }
+    }
+    b.unhealthyAlways = sp && jstr(sp, "unhealthyPodEvictionPolicy") == "AlwaysAllow";
+    const Value* st = v.get("status");
+    if (st && st->get("disruptionsAllowed")) b.allowed = st->get("disruptionsAllowed")->i64();
+    out.push_back(std::move(b));
+  }
+  return out;
+}
+// CanEvictPods (pdblimits.go:58-84)
+bool can_evict(const std::vector<Pdb>& pdbs, const PodH& p) {
+  for (auto& b : pdbs) {
+    if (b.ns != p.ns || !b.present) continue;
+    bool match = true;
+    for (auto& r : b.reqs) {
+      auto it = p.labels.find(r.first);
+      const bool has = it != p.labels.end();
+      const std::string& op = r.second.first;
+      const auto& vals = r.second.second;
+      const bool in = has && std::find(vals.begin(), vals.end(), it->second) != vals.end();
+      if (op == "In") match = match && in;
+      else if (op == "NotIn") match = match && !in;
+      else if (op == "Exists") match = match && has;
+      else match = match && !has;
+    }
+    if (!match) continue;
+    if (!(b.unhealthyAlways && p.notReady) && b.allowed == 0) return false;
+  }
+  return true;
+}
+
 int64_t parse_rfc3339(const std::string& s) {  // seconds; the snapshot uses "YYYY-MM-DDTHH:MM:SSZ"
   if (s.size() < 19) return 0;
   struct tm t{};
@@ -264,6 +325,7 @@ void build_cons(ks_cons& c, const Value& root) {
         poolTypes[kv.first][h.its[(size_t)i].name] = (int)i;
       }
   const int64_t nowNs = parse_rfc3339(jstr(&root, "now")) * 1000000000;
+  const std::vector<Pdb> pdbs = parse_pdbs(root);
 
   // NewCandidate for the listed nodes; nodes that would fail it are not candidates
   std::vector<ks_cons::Cand> cands;
@@ -302,8 +364,9 @@ void build_cons(ks_cons& c, const Value& root) {
         remaining = clampf(0.0, (total - age) / total, 1.0);
       }
       k.cost = cost * remaining;
+      // filterCandidates (helpers.go:47-71): a PDB allowing no eviction or a do-not-disrupt pod blocks it
       bool blocked = false;
-      for (int p : k.pods) blocked = blocked || do_not_disrupt(podMeta[(size_t)p]);
+      for (int p : k.pods) blocked = blocked || !can_evict(pdbs, podMeta[(size_t)p]) || do_not_disrupt(podMeta[(size_t)p]);
       if (!blocked) cands.push_back(std::move(k));
     }
   // sort.Slice(candidates, disruptionCost <): pdqsort only observes less(), so the costs' dense ranks

@@ -270,7 +270,10 @@ PodH parse_pod(const Value& v) {
     p.phase = ph;
     if (auto* cs = st->get("conditions"))
       for (auto& c : cs->arr())
+      {
         if (jstr(&c, "type") == "PodScheduled" && jstr(&c, "reason") == "Unschedulable") failedToSchedule = true;
+        if (jstr(&c, "type") == "Ready" && jstr(&c, "status") == "False") p.notReady = true;
+      }
   }
   const Value* sp = v.get("spec");
   if (sp) {

@@ -66,6 +66,7 @@ struct PodH {
   bool ownedByNode = false, ownedByDaemonSet = false, terminal = false, deleting = false;
   std::map<std::string, std::string> annotations;
   bool hasPriority = false;
+  bool notReady = false;  // a Ready condition with status False (PDBLimits.CanEvictPods, pdblimits.go:70-76)
   int32_t priority = 0;
 };
 PodH parse_pod(const ksjson::Value& v);

@@ -198,7 +198,7 @@ NOW = 1760000000  # fixed "now" for lifetimeRemaining (types.go:136-145)
 
 def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, spot_frac=0.3, it_range=(15, 40),
                      uninitialized_frac=0.0, not_ready_frac=0.0, expire_after="720h", pod_selectors=False,
-                     limits=None, topology=0):
+                     limits=None, topology=0, pdbs=False):
     """A consolidation snapshot: an existing cluster of `n_nodes` nodes launched from one
     WhenUnderutilized NodePool over fake.InstanceTypes(n_its), each running `pods_per_node` bound pods
     (C1 cpu/memory distributions, distinct pod-deletion-cost annotations so candidate costs are
@@ -208,7 +208,10 @@ def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, 
     topology=A > 0: the pods belong to A apps whose specs carry zonal / hostname spread (DoNotSchedule
     or ScheduleAnyway, some with minDomains), required hostname or zonal anti-affinity, or required /
     preferred zonal pod affinity; every bound pod is also listed in clusterPods (NewTopology's
-    countDomains and inverse anti-affinity source)."""
+    countDomains and inverse anti-affinity source).
+
+    pdbs=True: PodDisruptionBudgets over the my-label values (some with no disruptions left, some with
+    unhealthyPodEvictionPolicy AlwaysAllow) and some not-Ready pods (PDBLimits, pdblimits.go)."""
     rng = np.random.default_rng(seed)
     its = fake_instance_types(n_its)
     pool = node_pool("default", limits=limits)
@@ -273,6 +276,8 @@ def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, 
             p["metadata"]["annotations"] = {"controller.kubernetes.io/pod-deletion-cost": str(int(rng.integers(-1000, 1000000)))}
             p["spec"]["nodeName"] = "node-%05d" % j
             p["status"] = {"phase": "Running", "conditions": [{"type": "PodScheduled", "status": "True"}]}
+            if pdbs and rng.random() < 0.15:
+                p["status"]["conditions"].append({"type": "Ready", "status": "False"})
             pods.append(p)
             if topology:
                 cluster.append(p)
@@ -314,7 +319,26 @@ def cluster_snapshot(n_nodes, pods_per_node, n_its=400, seed=4205, n_pending=0, 
         "now": _fmt_time(NOW),
         "hostnameSeed": 0,
         **({"clusterPods": cluster} if topology else {}),
+        **({"podDisruptionBudgets": _pdbs(rng)} if pdbs else {}),
     }
+
+
+def _pdbs(rng):
+    """Budgets over my-label: a (none left), b (none left, unhealthy pods always evictable), c|d (one
+    left), e in another namespace (none left); f and g are unbudgeted."""
+    z = int(rng.integers(0, 2))
+    return [
+        {"metadata": {"name": "pdb-a", "namespace": "default"}, "spec": {"selector": {"matchLabels": {"my-label": "a"}}},
+         "status": {"disruptionsAllowed": 0}},
+        {"metadata": {"name": "pdb-b", "namespace": "default"},
+         "spec": {"selector": {"matchExpressions": [{"key": "my-label", "operator": "In", "values": ["b"]}]},
+                  "unhealthyPodEvictionPolicy": "AlwaysAllow"}, "status": {"disruptionsAllowed": z}},
+        {"metadata": {"name": "pdb-cd", "namespace": "default"},
+         "spec": {"selector": {"matchExpressions": [{"key": "my-label", "operator": "In", "values": ["c", "d"]}]}},
+         "status": {"disruptionsAllowed": 1}},
+        {"metadata": {"name": "pdb-e", "namespace": "other"}, "spec": {"selector": {"matchLabels": {"my-label": "e"}}},
+         "status": {"disruptionsAllowed": 0}},
+    ]
 
 
 def config5(n_nodes=5000, pods_per_node=20, seed=4205):

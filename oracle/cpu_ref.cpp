@@ -393,6 +393,7 @@ struct Pod {
   int64_t created = 0;
   string nodeName, phase, nominatedNodeName;
   bool failedToSchedule = false, ownedByDaemonSet = false, ownedByNode = false, deleting = false;
+  bool notReady = false;  // a PodReady condition with status False (pdblimits.go:70-76)
   map<string, string> nodeSelector;
   bool hasAffinity = false, hasNodeAffinity = false, hasRequired = false;
   vector<vector<NSR>> requiredTerms;
@@ -836,9 +837,13 @@ static Pod parsePod(const ojson::Value& v) {
     if (auto* x = st->get("nominatedNodeName")) p.nominatedNodeName = x->str();
     if (auto* cs = st->get("conditions"))
       for (auto& c : cs->arr())
+      {
         if (c.get("type") && c.get("type")->str() == "PodScheduled" && c.get("reason") &&
             c.get("reason")->str() == "Unschedulable")
           p.failedToSchedule = true;
+        if (c.get("type") && c.get("type")->str() == "Ready" && c.get("status") && c.get("status")->str() == "False")
+          p.notReady = true;
+      }
   }
   return p;
 }

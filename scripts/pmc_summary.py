@@ -26,17 +26,17 @@ def main():
                 os.path.join(prof, "%s_kernel_stats.csv" % tag))
     lines = ["PMC per launch of %s (averaged over the profiled launches)" % kname]
     vals = {}
-    for grp in ("fetch", "write", "sq"):
+    agg = collections.defaultdict(list)
+    for grp in ("fetch", "write", "sq", "cfetch", "cwrite"):
         path = os.path.join(out, "prof_%s_%s" % (tag, grp), "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
-        agg = collections.defaultdict(list)
         for r in csv.DictReader(open(path)):
             if kname in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-        for k, v in sorted(agg.items()):
-            vals[k] = sum(v) / len(v)
-            lines.append("  %-22s %16.1f   (%d launches)" % (k, vals[k], len(v)))
+    for k, v in sorted(agg.items()):
+        vals[k] = sum(v) / len(v)
+        lines.append("  %-22s %16.1f   (%d launches)" % (k, vals[k], len(v)))
     if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
         rd = 2 * vals["FETCH_SIZE"] * 1024
         wr = vals["WRITE_SIZE"] * 1024

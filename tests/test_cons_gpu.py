@@ -127,6 +127,16 @@ def _volume_cluster(seed, n_nodes, ppn, topology=0):
     return snap
 
 
+@pytest.mark.parametrize("seed", [61, 62, 63])
+def test_pdb_cluster_parity(seed):
+    """PodDisruptionBudgets filter the candidates (filterCandidates helpers.go:47-71) before any simulation."""
+    snap = synth.cluster_snapshot(30, 6, n_its=40, it_range=(4, 30), seed=seed, n_pending=2, pdbs=True)
+    for all_sims in (True, False):
+        want, got = _both(snap, all_sims)
+        d = _first_diff(want, got)
+        assert d is None, d
+
+
 VOL_CASES = [(41, 12, 5, 0), (42, 16, 4, 0), (43, 10, 6, 0), (44, 14, 4, 6), (45, 8, 8, 0), (46, 12, 3, 4)]
 
 

@@ -20,7 +20,21 @@ SNAPS = [("scn-" + s["name"], s["snapshot"]) for s in mcf.scenarios()] + [
                                                uninitialized_frac=0.1, n_pending=3, expire_after=exp))
     for seed, n, exp in [(21, 10, "720h"), (22, 40, "24h"), (23, 130, "2h30m")]] + [
     ("topo-%d" % seed, synth.cluster_snapshot(30, 6, n_its=40, it_range=(4, 30), seed=seed, n_pending=3, topology=apps))
-    for seed, apps in [(31, 8), (32, 24)]]
+    for seed, apps in [(31, 8), (32, 24)]] + [
+    ("pdb-%d" % seed, synth.cluster_snapshot(40, 6, n_its=40, it_range=(4, 30), seed=seed, n_pending=2, pdbs=True))
+    for seed in (51, 52, 53)]
+
+
+def test_pdbs_block_candidates():
+    """PDBLimits.CanEvictPods (pdblimits.go:58-84) inside filterCandidates (helpers.go:47-71): a budget with
+    no disruptions left removes every node running a selected pod, unless the budget always allows
+    evicting unhealthy pods and the pod is not Ready."""
+    snap = synth.cluster_snapshot(40, 6, n_its=40, it_range=(4, 30), seed=51, pdbs=True)
+    base = dict(snap)
+    base.pop("podDisruptionBudgets")
+    with_pdb = inspect_consolidation(json.dumps(snap))["candidates"]
+    without = inspect_consolidation(json.dumps(base))["candidates"]
+    assert 0 < len(with_pdb) < len(without)
 
 
 @pytest.mark.parametrize("name,snap", SNAPS, ids=[n for n, _ in SNAPS])
