@@ -120,6 +120,16 @@ int ks_cons_needed_sims(const ks_cons* c, const void* records, int world, int fl
 int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out);
 int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
                    char** json_out);
+/* Validation.IsValid after its wait + ValidateCommand (disruption/validation.go:68-180): the handle
+ * holds the current cluster snapshot (stateNodes may carry "nominated": Cluster.IsNodeNominated);
+ * command_json is a command as ks_cons_decide reports it ({"candidates": [names], "replacement":
+ * {"instanceTypeOptions": [...]}} or no "replacement"), computed on an earlier snapshot.  The command's
+ * candidates are re-filtered (NewCandidate, PDBs, do-not-disrupt), then re-simulated on the GPU.
+ * Writes JSON {"valid": bool, "reason": "" | "candidates-changed" | "candidate-nominated" |
+ * "no-candidates" | "pods-unschedulable" | "replacement-not-needed" | "multiple-nodeclaims" |
+ * "replacement-needed" | "instance-types-not-subset", "sim": null | {allNonPendingScheduled,
+ * newNodeClaims, claim0: {nodePoolName, instanceTypeOptions}}}.  Leaves the pass's plan unchanged. */
+int ks_cons_validate(ks_cons* c, const char* command_json, size_t len, const ks_solve_opts* opts, char** json_out);
 /* Diagnostics: the 24 solve counters of simulation `sim` in the last ks_cons_run of this handle. */
 int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out24);
 /* Algorithmic bytes the gathered simulations scanned, summed from their records. */

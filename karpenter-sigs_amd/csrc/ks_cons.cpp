@@ -193,6 +193,7 @@ struct ks_cons {
   std::vector<Sim> sims;  // multi-node prefixes first (largest first), then one per candidate
   int multiHi = 0;        // multi-node prefix lengths mid+1 for mid in [1, multiHi]
   std::vector<int> pending, deleting;
+  std::set<std::string> nominated;  // Cluster.IsNodeNominated (validation.go:99-103)
   int64_t hostnameSeed = 0;
   int recWords = 0;
 
@@ -263,6 +264,7 @@ void build_cons(ks_cons& c, const Value& root) {
     const bool del = nv.get("markedForDeletion") ? nv.get("markedForDeletion")->boolean(false) : false;
     nodeByName[name] = ni++;
     deletingNode.push_back(del);
+    if (nv.get("nominated") && nv.get("nominated")->boolean(false)) c.nominated.insert(name);
     if (!del) sub->push_back(nv);
     std::vector<int> mine;
     if (const Value* ps = nv.get("pods"))
@@ -855,6 +857,111 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
 
 }  // namespace
 
+namespace {
+
+// The queue sort + simulation kernel over this rank's simulations; records to host or device memory.
+// Returns the HIP-event time of both launches on the stream they ran on.
+double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
+  prepare_launch(c, rank, world);
+  ks_problem& pb = *c.pb;
+  const int ns = (int)c.lsims.size();
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, pb.stream));
+  HIPCHK(sim_queue_sort(c.rank, c.lentries, c.lentrySim, c.lnent, c.lrbits, c.lsbits, c.lkeys, c.lvals, c.ltemp,
+                        c.ltempBytes, c.lpodmap, pb.stream));
+  HIPCHK(launch_sims(pb.dev, c.lworks, ns, c.lplan, pb.stream));
+  HIPCHK(hipEventRecord(e1, pb.stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  const size_t bytes = 4 * (size_t)c.recWords * ns, all = 4 * (size_t)c.recWords * c.per_rank(world);
+  if (onDevice) {
+    HIPCHK(hipMemsetAsync(records, 0, all, pb.stream));
+    if (bytes) HIPCHK(hipMemcpyAsync(records, c.lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
+  } else {
+    memset(records, 0, all);
+    if (bytes) HIPCHK(hipMemcpyAsync(records, c.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
+  }
+  HIPCHK(hipStreamSynchronize(pb.stream));
+  return ms;
+}
+
+// Validation.IsValid after its wait (validation.go:68-107) + ValidateCommand (:120-180): the handle
+// holds the *current* cluster snapshot, `cmd` a command (ks_cons_decide's shape) computed on an
+// earlier one.  mapCandidates keeps GetCandidates order while c.cands is in disruption-cost order;
+// the simulation cannot observe the difference (its pods follow NewQueue's total order and prices are
+// not used).  The one re-simulation runs on the GPU through the same launch path as a pass.
+std::string validate_json(ks_cons& c, const Value& cmd) {
+  const Host& h = c.pb->host;
+  std::vector<std::string> names;
+  if (const Value* cs = cmd.get("candidates"))
+    for (auto& v : cs->arr()) names.push_back(v.str());
+  const std::set<std::string> proposed(names.begin(), names.end());
+  const Value* rv = cmd.get("replacement");
+  const bool hasReplacement = rv && rv->is_obj();
+  std::set<std::string> replacement;  // cmd.replacements[0].InstanceTypeOptions names
+  if (hasReplacement)
+    if (const Value* its = rv->get("instanceTypeOptions"))
+      for (auto& v : its->arr()) replacement.insert(v.str());
+  auto out = [](bool valid, const char* reason, const std::string& sim) {
+    std::string o = std::string("{\"valid\":") + (valid ? "true" : "false") + ",\"reason\":";
+    ksjson::quote(o, reason);
+    return o + ",\"sim\":" + (sim.empty() ? std::string("null") : sim) + "}";
+  };
+  std::vector<int> mapped;  // mapCandidates + filterCandidates (already applied to c.cands by build_cons)
+  for (int i = 0; i < (int)c.cands.size(); i++)
+    if (proposed.count(c.cands[(size_t)i].name)) mapped.push_back(i);
+  if (mapped.size() != names.size()) return out(false, "candidates-changed", "");
+  for (int i : mapped)
+    if (c.nominated.count(c.cands[(size_t)i].name)) return out(false, "candidate-nominated", "");
+  if (mapped.empty()) return out(false, "no-candidates", "");
+  // a plan holding only this simulation, then the pass's plan back
+  std::vector<ks_cons::Sim> saved(1);
+  saved[0].cands = mapped;
+  saved.swap(c.sims);
+  c.free_launch();
+  std::vector<int32_t> r((size_t)c.recWords, 0);
+  try {
+    (void)run_sims(c, 0, 1, r.data(), false);
+  } catch (...) {
+    c.sims.swap(saved);
+    c.free_launch();
+    throw;
+  }
+  c.sims.swap(saved);
+  c.free_launch();
+  if (r[RF_ERROR] != KE_OK)
+    throw KsError(r[RF_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
+                  "validation simulation reported kernel error " + std::to_string(r[RF_ERROR]));
+  const bool allSched = (r[RF_FLAGS] & RB_ALL_SCHEDULED) != 0;
+  const int nclaims = r[RF_NCLAIMS];
+  std::string sim = std::string("{\"allNonPendingScheduled\":") + (allSched ? "true" : "false") +
+                    ",\"newNodeClaims\":" + std::to_string(nclaims);
+  std::set<std::string> simTypes;
+  if (nclaims > 0) {
+    const std::vector<int> its = bits_to_its(h, r[RF_TPL], r.data() + RF_HDR);
+    sim += ",\"claim0\":{\"nodePoolName\":";
+    ksjson::quote(sim, h.tpls[(size_t)r[RF_TPL]].pool);
+    sim += ",\"instanceTypeOptions\":" + names_json(h, its) + "}";
+    for (int t : its) simTypes.insert(h.its[(size_t)t].name);
+  }
+  sim += "}";
+  if (!allSched) return out(false, "pods-unschedulable", sim);
+  if (nclaims == 0) return hasReplacement ? out(false, "replacement-not-needed", sim) : out(true, "", sim);
+  if (nclaims > 1) return out(false, "multiple-nodeclaims", sim);
+  if (!hasReplacement) return out(false, "replacement-needed", sim);
+  // instanceTypesAreSubset (validation.go:183-187) over name sets
+  for (auto& n : replacement)
+    if (!simTypes.count(n)) return out(false, "instance-types-not-subset", sim);
+  return out(true, "", sim);
+}
+
+}  // namespace
+
 extern "C" {
 
 int ks_cons_create(const char* json, size_t len, ks_cons** out) {
@@ -924,32 +1031,19 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
   API_TRY
   if (!c || !records || world < 1 || rank < 0 || rank >= world) throw KsError(KS_ERR_ARG, "bad argument");
   if (opts && opts->device >= 0) HIPCHK(hipSetDevice(opts->device));
-  prepare_launch(*c, rank, world);
-  ks_problem& pb = *c->pb;
-  const int ns = (int)c->lsims.size();
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
-  HIPCHK(hipEventRecord(e0, pb.stream));
-  HIPCHK(sim_queue_sort(c->rank, c->lentries, c->lentrySim, c->lnent, c->lrbits, c->lsbits, c->lkeys, c->lvals,
-                        c->ltemp, c->ltempBytes, c->lpodmap, pb.stream));
-  HIPCHK(launch_sims(pb.dev, c->lworks, ns, c->lplan, pb.stream));
-  HIPCHK(hipEventRecord(e1, pb.stream));
-  HIPCHK(hipEventSynchronize(e1));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  const size_t bytes = 4 * (size_t)c->recWords * ns, all = 4 * (size_t)c->recWords * c->per_rank(world);
-  if (records_on_device) {
-    HIPCHK(hipMemsetAsync(records, 0, all, pb.stream));
-    if (bytes) HIPCHK(hipMemcpyAsync(records, c->lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
-  } else {
-    memset(records, 0, all);
-    if (bytes) HIPCHK(hipMemcpyAsync(records, c->lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
-  }
-  HIPCHK(hipStreamSynchronize(pb.stream));
+  const double ms = run_sims(*c, rank, world, records, records_on_device != 0);
   if (kernel_ms) *kernel_ms = ms;
+  return KS_OK;
+  API_CATCH
+}
+
+int ks_cons_validate(ks_cons* c, const char* command_json, size_t len, const ks_solve_opts* opts, char** json_out) {
+  API_TRY
+  if (!c || !command_json || !json_out) throw KsError(KS_ERR_ARG, "null argument");
+  if (opts && opts->device >= 0) HIPCHK(hipSetDevice(opts->device));
+  ksjson::Value cmd = ksjson::Parser(command_json, len ? len : strlen(command_json)).parse();
+  if (!cmd.is_obj()) throw KsError(KS_ERR_PARSE, "command is not an object");
+  *json_out = strdup(validate_json(*c, cmd).c_str());
   return KS_OK;
   API_CATCH
 }

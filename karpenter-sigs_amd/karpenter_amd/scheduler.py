@@ -163,6 +163,7 @@ def _cons_lib():
         l.ks_cons_requirement_words.argtypes = [vp]
         l.ks_cons_needed_sims.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
         l.ks_cons_claim_requirements.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+        l.ks_cons_validate.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_Opts), ctypes.POINTER(vp)]
         l.ks_cons_sim_counters.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
         l.ks_cons_records_alg_bytes.argtypes = [vp, vp, ctypes.c_int]
         l.ks_cons_records_alg_bytes.restype = ctypes.c_double
@@ -255,6 +256,16 @@ class Consolidator:
         flags = (1 if all_sims else 0) | (2 if candidates else 0)
         _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, flags,
                                 ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(js)))
+        return json.loads(_take_str(js))
+
+    def validate(self, command, device=-1):
+        """Validation.IsValid after its wait + ValidateCommand (validation.go:68-180): `command` (a
+        decide() command, computed on an earlier snapshot) re-checked against this handle's snapshot,
+        its re-simulation run on the GPU.  Returns {"valid", "reason", "sim"}."""
+        b = (command if isinstance(command, str) else json.dumps(command)).encode()
+        js = ctypes.c_void_p()
+        o = _Opts(device, 1, 1, 0, 0)
+        _check(_cons_lib().ks_cons_validate(self._h, b, len(b), ctypes.byref(o), ctypes.byref(js)))
         return json.loads(_take_str(js))
 
     def sim_counters(self, sim):

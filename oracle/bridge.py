@@ -28,6 +28,8 @@ def lib():
         l.oref_consolidate_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_double)]
         l.oref_consolidate_json.restype = ctypes.c_int
+        l.oref_validate_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+        l.oref_validate_json.restype = ctypes.c_int
         l.oref_time_cons_sims.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         l.oref_time_cons_sims.restype = ctypes.c_int
         l.oref_last_error.restype = ctypes.c_char_p
@@ -73,6 +75,18 @@ def consolidate(snapshot, all_sims=False):
     if l.oref_consolidate_json(s.encode(), 1 if all_sims else 0, ctypes.byref(out), ctypes.byref(secs)) != 0:
         raise RuntimeError("oracle: " + l.oref_last_error().decode())
     return json.loads(_take(out)), secs.value
+
+
+def validate(snapshot, command):
+    """Oracle Validation.IsValid (after the wait) + ValidateCommand (validation.go:68-180): `command`
+    (consolidate()'s command shape) proposed earlier, checked against the current `snapshot`."""
+    l = lib()
+    s = snapshot if isinstance(snapshot, str) else json.dumps(snapshot)
+    c = command if isinstance(command, str) else json.dumps(command)
+    out = ctypes.c_void_p()
+    if l.oref_validate_json(s.encode(), c.encode(), ctypes.byref(out)) != 0:
+        raise RuntimeError("oracle: " + l.oref_last_error().decode())
+    return json.loads(_take(out))
 
 
 def time_cons_sims(snapshot, count, threads=1):

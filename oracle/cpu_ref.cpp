@@ -1657,6 +1657,21 @@ int oref_consolidate_json(const char* snapshot, int all_sims, char** out, double
   }
 }
 
+// Validation of a consolidation command against the current cluster snapshot (validation.go:68-180).
+int oref_validate_json(const char* snapshot, const char* command, char** out) {
+  try {
+    ojson::Value root = ojson::parse(snapshot);
+    ojson::Value cmd = ojson::parse(command);
+    oref::ConsProblem cp = oref::parseConsProblem(root);
+    std::string r = oref::validateJSON(cp, cmd);
+    if (out) *out = dupstr(r);
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
 // CPU baseline sample: the first `count` single-node consolidation simulations (simulateScheduling +
 // computeConsolidation per candidate, as SingleNodeConsolidation runs them), timed after parsing.
 // `threads` > 1 splits the (independent) simulations over that many host threads.

@@ -12,7 +12,11 @@ single-node consolidation; the first non-no-op wins):
   action      : "delete" | "replace" | "no-op"
   candidates  : node names removed by the command (set)
   replacement_excludes : an instance type the replacement must not offer
-Validation (the 15 s re-check) and PDBs are outside the restated path.
+
+validation_scenarios() transcribes the TTL-wait tests (consolidation_test.go:2212-2562): a command is
+computed on the snapshot `before`, the cluster changes during Validation's wait, and
+Validation.IsValid (validation.go:68-180) re-checks it against `after`.  `expect.valid` is the Go
+test's outcome (the node is kept when the command is invalid); `expect.reason` names the check.
 """
 import json
 import os
@@ -170,6 +174,78 @@ def scenarios():
     return S
 
 
+def blocking_pdb(app):
+    """test.PodDisruptionBudget(MaxUnavailable 0) over app=<app>: no disruptions allowed."""
+    return {"metadata": {"name": "pdb-" + app, "namespace": "default"},
+            "spec": {"selector": {"matchLabels": {"app": app}}}, "status": {"disruptionsAllowed": 0}}
+
+
+def validation_scenarios():
+    src = "pkg/controllers/disruption/consolidation_test.go"
+    its = assorted()
+    ods = od_sorted(its)
+    least, most = ods[0], ods[-1]
+    alloc = {"cpu": "32", "pods": "100"}
+    dnd = {"karpenter.sh/do-not-disrupt": "true"}
+    V = []
+
+    def blocker(i, bound_to, app="blocking"):
+        p = rs_pod(i, bound_to=bound_to)
+        p["metadata"]["labels"] = {"app": app}
+        return p
+
+    # "should not consolidate if the action becomes invalid during the node TTL wait" (:2212-2250):
+    # an empty node is deleted, then a do-not-disrupt pod binds to it
+    before = snapshot(its, [node("node-a", least, alloc, [])])
+    after = snapshot(its, [node("node-a", least, alloc, [rs_pod(0, bound_to="node-a", annotations=dnd)])])
+    V.append({"name": "empty-node-gets-do-not-disrupt-pod", "source": src + ":2212-2250", "before": before,
+              "after": after, "expect": {"command": "delete", "valid": False, "reason": "candidates-changed"}})
+    # "should not replace node if a pod schedules with a blocking PDB during the TTL wait" (:2351-2404)
+    before = snapshot(its, [node("node-a", most, {"cpu": "32"}, [rs_pod(0, bound_to="node-a")])])
+    after = snapshot(its, [node("node-a", most, {"cpu": "32"}, [rs_pod(0, bound_to="node-a"),
+                                                                blocker(1, "node-a")])])
+    after["podDisruptionBudgets"] = [blocking_pdb("blocking")]
+    V.append({"name": "replace-blocked-by-pdb-during-wait", "source": src + ":2351-2404", "before": before,
+              "after": after, "expect": {"command": "replace", "valid": False, "reason": "candidates-changed"}})
+    # "should not delete node if pods schedule with karpenter.sh/do-not-disrupt during the TTL wait"
+    # (:2455-2505) and "... with a blocking PDB during the TTL wait" (:2506-2562): two nodes, one deleted
+    two = lambda extra: [node("node-a", least, alloc, [rs_pod(0, bound_to="node-a")] + extra[0]),
+                         node("node-b", least, alloc, [rs_pod(1, bound_to="node-b")] + extra[1])]
+    before = snapshot(its, two(([], [])))
+    after = snapshot(its, two(([rs_pod(2, bound_to="node-a", annotations=dnd)],
+                               [rs_pod(3, bound_to="node-b", annotations=dnd)])))
+    V.append({"name": "delete-blocked-by-do-not-disrupt-during-wait", "source": src + ":2455-2505",
+              "before": before, "after": after,
+              "expect": {"command": "delete", "valid": False, "reason": "candidates-changed"}})
+    after = snapshot(its, two(([blocker(2, "node-a")], [blocker(3, "node-b")])))
+    after["podDisruptionBudgets"] = [blocking_pdb("blocking")]
+    V.append({"name": "delete-blocked-by-pdb-during-wait", "source": src + ":2506-2562",
+              "before": before, "after": after,
+              "expect": {"command": "delete", "valid": False, "reason": "candidates-changed"}})
+    # Unchanged clusters: every consolidation test above passes Validation (ValidateCommand :135-180)
+    for sc in scenarios():
+        if sc["name"] in ("can-replace-node", "can-delete-nodes", "merge-3-into-1", "no-merge-same-type"):
+            V.append({"name": "unchanged-" + sc["name"], "source": "pkg/controllers/disruption/validation.go:120-180",
+                      "before": sc["snapshot"], "after": sc["snapshot"],
+                      "expect": {"command": sc["expect"]["action"], "valid": True, "reason": ""}})
+    # A pending pod nominated to the candidate during the wait (validation.go:99-103)
+    before = snapshot(its, two(([], [])))
+    after = snapshot(its, two(([], [])))
+    for n in after["stateNodes"]:
+        n["nominated"] = True
+    V.append({"name": "candidate-nominated-during-wait", "source": "pkg/controllers/disruption/validation.go:99-103",
+              "before": before, "after": after,
+              "expect": {"command": "delete", "valid": False, "reason": "candidate-nominated"}})
+    # The deleted node's pods no longer fit elsewhere: re-simulation wants a NodeClaim (validation.go:155-160)
+    after = snapshot(its, two(([], [])))
+    for n in after["stateNodes"]:  # whichever node is deleted, the other one is now full
+        n["available"]["pods"] = "0"
+    V.append({"name": "deleted-pods-need-a-new-node", "source": "pkg/controllers/disruption/validation.go:155-160",
+              "before": before, "after": after,
+              "expect": {"command": "delete", "valid": False, "reason": "replacement-needed"}})
+    return V
+
+
 def main():
     # The snapshots (1344 instance types each) are rebuilt from this script by the tests; the fixture
     # keeps the transcribed expectations.
@@ -177,6 +253,10 @@ def main():
     with open(os.path.join(HERE, "consolidation_scenarios.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print("%d scenarios" % len(out))
+    out = [{"name": s["name"], "source": s["source"], "expect": s["expect"]} for s in validation_scenarios()]
+    with open(os.path.join(HERE, "validation_scenarios.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print("%d validation scenarios" % len(out))
 
 
 if __name__ == "__main__":

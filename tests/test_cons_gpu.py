@@ -178,3 +178,74 @@ def test_c5_shape_at_scale_properties():
     assert costs == sorted(costs)
     # determinism
     assert c.consolidate(all_sims=True)["single"] == doc["single"]
+
+
+# ---- Validation.IsValid + ValidateCommand (validation.go:68-180) -----------------------------------
+VFIXTURES = json.load(open(os.path.join(HERE, "golden", "validation_scenarios.json")))
+VSCENARIOS = {s["name"]: s for s in mcf.validation_scenarios()}
+
+
+def _final(doc):
+    m = doc["multi"]["command"]
+    return m if m["action"] != "no-op" else doc["single"]["command"]
+
+
+@pytest.mark.parametrize("fx", VFIXTURES, ids=[f["name"] for f in VFIXTURES])
+def test_reference_validation_scenarios_gpu(fx):
+    """consolidation_test.go TTL-wait known answers: the GPU computes the command on `before` and
+    re-simulates it on `after`; both steps equal the oracle and the Go test's verdict."""
+    scn = VSCENARIOS[fx["name"]]
+    want, got = _both(scn["before"], False)
+    assert _first_diff(want["multi"], got["multi"]) is None
+    assert _first_diff(want["single"], got["single"]) is None
+    cmd = _final(got)
+    assert cmd["action"] == fx["expect"]["command"]
+    v_want = bridge.validate(scn["after"], cmd)
+    v_got = Consolidator(json.dumps(scn["after"])).validate(cmd)
+    assert _first_diff(v_want, v_got) is None, _first_diff(v_want, v_got)
+    assert (v_got["valid"], v_got["reason"]) == (fx["expect"]["valid"], fx["expect"]["reason"])
+
+
+def _perturb(snap, variant, seed):
+    import copy
+    import random
+    after = copy.deepcopy(snap)
+    rng = random.Random(seed)
+    if variant == "pending":  # new pending pods arrive during the wait
+        after["pendingPods"] = list(after.get("pendingPods", [])) + [
+            synth.pod(900000 + i, cpu=rng.choice(["1", "2", "4"]), mem="1Gi") for i in range(3)]
+    elif variant == "full":  # a third of the nodes fill up
+        for n in after["stateNodes"]:
+            if rng.random() < 0.34:
+                n["available"]["pods"] = "0"
+    elif variant == "nominated":
+        for n in after["stateNodes"]:
+            n["nominated"] = rng.random() < 0.2
+    return after
+
+
+@pytest.mark.parametrize("seed,variant", [(s, v) for s in (61, 62, 63) for v in ("same", "pending", "full", "nominated")])
+def test_random_validation_parity(seed, variant):
+    """Commands from a random cluster (multi-node, single-node and every single-node simulation's
+    replacement) re-checked on a perturbed cluster: GPU ValidateCommand == oracle, field by field."""
+    snap = synth.cluster_snapshot(24, 6, n_its=40, it_range=(4, 30), seed=seed, spot_frac=0.3, n_pending=1)
+    doc = Consolidator(json.dumps(snap)).consolidate(all_sims=True)
+    cmds = [doc["multi"]["command"], doc["single"]["command"]]
+    for sim in doc["single"]["sims"][:8]:
+        c = {"action": "replace", "candidates": sim["candidates"]}
+        if sim.get("claim0"):
+            c["replacement"] = {"instanceTypeOptions": sim["claim0"]["instanceTypeOptions"][:5]}
+        cmds.append(c)
+    after = _perturb(snap, variant, seed)
+    h = Consolidator(json.dumps(after))
+    reasons = set()
+    for cmd in cmds:
+        v_want = bridge.validate(after, cmd)
+        v_got = h.validate(cmd)
+        assert _first_diff(v_want, v_got) is None, (cmd, _first_diff(v_want, v_got))
+        reasons.add(v_got["reason"])
+    # the handle's own pass is untouched by the validation runs
+    again = h.consolidate(all_sims=False)
+    want, _ = bridge.consolidate(json.dumps(after), all_sims=False)
+    assert again["single"]["command"] == want["single"]["command"]
+    assert reasons
