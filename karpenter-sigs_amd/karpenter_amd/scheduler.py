@@ -58,6 +58,7 @@ def lib():
     l.ks_results_solve_kernel_ms.restype = ctypes.c_double
     l.ks_results_algorithmic_bytes.argtypes = [vp]
     l.ks_results_algorithmic_bytes.restype = ctypes.c_double
+    l.ks_cluster_state.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
     l.ks_free.argtypes = [vp]
     l.ks_last_error.restype = ctypes.c_char_p
     l.ks_build_info.restype = ctypes.c_char_p
@@ -85,6 +86,16 @@ def inspect(snapshot):
     b = _encode(snapshot)
     out = ctypes.c_void_p()
     _check(lib().ks_problem_inspect(b, len(b), ctypes.byref(out)))
+    return json.loads(_take_str(out))
+
+
+def cluster_state(cluster):
+    """Cluster-state accounting (pkg/controllers/state, cluster.go:220-512 + statenode.go:110-333):
+    the StateNode accessor values the informers converge to for {"nodeClaims", "nodes", "pods"}, as a
+    snapshot "stateNodes" list (host-only; no device)."""
+    b = _encode(cluster)
+    out = ctypes.c_void_p()
+    _check(lib().ks_cluster_state(b, len(b), ctypes.byref(out)))
     return json.loads(_take_str(out))
 
 

@@ -28,6 +28,8 @@ def lib():
         l.oref_consolidate_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_double)]
         l.oref_consolidate_json.restype = ctypes.c_int
+        l.oref_cluster_state.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+        l.oref_cluster_state.restype = ctypes.c_int
         l.oref_validate_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
         l.oref_validate_json.restype = ctypes.c_int
         l.oref_time_cons_sims.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
@@ -75,6 +77,17 @@ def consolidate(snapshot, all_sims=False):
     if l.oref_consolidate_json(s.encode(), 1 if all_sims else 0, ctypes.byref(out), ctypes.byref(secs)) != 0:
         raise RuntimeError("oracle: " + l.oref_last_error().decode())
     return json.loads(_take(out)), secs.value
+
+
+def cluster_state(cluster):
+    """Oracle cluster-state accounting (pkg/controllers/state): StateNode accessors from
+    {"nodeClaims", "nodes", "pods"}; each node reports `podCount` (its bound pods) instead of the pods."""
+    l = lib()
+    s = cluster if isinstance(cluster, str) else json.dumps(cluster)
+    out = ctypes.c_void_p()
+    if l.oref_cluster_state(s.encode(), ctypes.byref(out)) != 0:
+        raise RuntimeError("oracle: " + l.oref_last_error().decode())
+    return json.loads(_take(out))
 
 
 def validate(snapshot, command):

@@ -1516,6 +1516,7 @@ string Scheduler::ResultsJSON() const {
 }
 
 #include "consolidation.inc"
+#include "cluster_state.inc"
 
 // ---------------------------------------------------------------------------------------------
 // Requirement-algebra evaluator for the reference's golden vectors (requirement_test.go,
@@ -1650,6 +1651,18 @@ int oref_consolidate_json(const char* snapshot, int all_sims, char** out, double
     std::string r = oref::consolidateJSON(cp, all_sims != 0);
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (out) *out = dupstr(r);
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// Cluster-state accounting: StateNode accessor values from Node / NodeClaim / Pod lists.
+int oref_cluster_state(const char* cluster, char** out) {
+  try {
+    ojson::Value root = ojson::parse(cluster);
+    if (out) *out = dupstr(oref::clusterStateJSON(root));
     return 0;
   } catch (const std::exception& e) {
     g_err = e.what();

@@ -249,3 +249,23 @@ def test_random_validation_parity(seed, variant):
     want, _ = bridge.consolidate(json.dumps(after), all_sims=False)
     assert again["single"]["command"] == want["single"]["command"]
     assert reasons
+
+
+@pytest.mark.parametrize("seed", (3, 4))
+def test_consolidation_over_derived_cluster_state(seed):
+    """Consolidation over stateNodes derived by ks_cluster_state from Node / NodeClaim / Pod listings
+    (cluster-state accounting, pkg/controllers/state): GPU decisions == oracle."""
+    import test_cluster_state as tcs
+    base = mcf.snapshot(mcf.assorted()[:64], [])
+    c = tcs.random_cluster(seed, n=16)
+    for p in c["pods"]:
+        p["spec"]["containers"][0].pop("ports", None)
+        if not p["metadata"].get("ownerReferences"):
+            p["metadata"]["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "rs",
+                                                 "uid": "rs-uid"}]
+    from karpenter_amd import cluster_state
+    state = cluster_state(json.dumps(c))
+    base["stateNodes"] = state
+    base["candidates"] = [n["name"] for n in state]
+    want, got = _both(base, True)
+    assert _first_diff(want, got) is None, _first_diff(want, got)
