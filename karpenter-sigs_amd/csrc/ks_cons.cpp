@@ -241,8 +241,16 @@ struct ks_cons {
 namespace {
 
 // Parse the cluster snapshot into the resident problem + candidates + sims.
-void build_cons(ks_cons& c, const Value& root) {
-  if (!root.is_obj()) throw KsError(KS_ERR_PARSE, "snapshot is not an object");
+void build_cons(ks_cons& c, const Value& rootIn) {
+  if (!rootIn.is_obj()) throw KsError(KS_ERR_PARSE, "snapshot is not an object");
+  // "cluster": {nodeClaims, nodes, pods} listings instead of "stateNodes": derive the StateNodes the
+  // cluster-state informers would hold (ks_cluster_state)
+  Value root = rootIn;
+  if (const Value* cl = rootIn.get("cluster"); cl && !rootIn.get("stateNodes")) {
+    const std::string sn = cluster_state_json(*cl);
+    root.o = std::make_shared<ksjson::Object>(rootIn.obj());
+    (*root.o)["stateNodes"] = ksjson::Parser(sn.data(), sn.size()).parse();
+  }
   const Value* nodesV = root.get("stateNodes");
   // Active nodes (nodes.Active(): not marked for deletion) enter the problem; the deleting ones only
   // contribute their pods (deletingNodes.Pods, helpers.go:91-95).

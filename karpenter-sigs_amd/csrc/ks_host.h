@@ -70,6 +70,8 @@ struct PodH {
   int32_t priority = 0;
 };
 PodH parse_pod(const ksjson::Value& v);
+// Cluster-state accounting (ks_state.cpp): StateNode accessor values from {nodeClaims, nodes, pods}
+std::string cluster_state_json(const ksjson::Value& cluster);
 
 struct PodState {  // one point of the relaxation chain
   std::vector<uint32_t> rsAll, rsStrict;

@@ -165,6 +165,8 @@ void put_qlist(std::string& o, const QList& q) {
   o += "}";
 }
 
+}  // namespace
+
 std::string cluster_state_json(const Value& root) {
   std::vector<std::string> order;  // providerIDs, canonical order
   std::map<std::string, Entry> byID;
@@ -304,7 +306,6 @@ std::string cluster_state_json(const Value& root) {
   return o + "]";
 }
 
-}  // namespace
 }  // namespace ks
 
 extern "C" int ks_cluster_state(const char* json, size_t len, char** out_json) {

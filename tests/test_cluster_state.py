@@ -120,18 +120,35 @@ def test_random_clusters_match_oracle(seed):
     assert host_view(got) == want
 
 
+def consolidatable(c, its, seed):
+    """Give the nodes of a random cluster the labels NewCandidate reads (an instance type of the pool,
+    its capacity type and zone), and the pods ReplicaSet owners and no host ports (a bound pod holding
+    host ports is refused loudly)."""
+    rng = random.Random(seed)
+    by_name = {}
+    for obj in c["nodeClaims"] + c["nodes"]:
+        name = obj["metadata"]["name"].replace("nc-", "node-")
+        it = by_name.setdefault(name, rng.choice(its))
+        off = it["offerings"][0]
+        obj["metadata"]["labels"].update({"node.kubernetes.io/instance-type": it["name"],
+                                          "karpenter.sh/capacity-type": off["capacityType"],
+                                          "topology.kubernetes.io/zone": off["zone"]})
+    for p in c["pods"]:
+        p["spec"]["containers"][0].pop("ports", None)
+        if not p["metadata"].get("ownerReferences"):
+            p["metadata"]["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "rs",
+                                                 "uid": "rs-uid"}]
+    return c
+
+
 def test_derived_state_feeds_consolidation():
     """The derived stateNodes are a consolidation snapshot's stateNodes: candidates and costs agree with
     the oracle reading the same snapshot."""
     sys.path.insert(0, os.path.join(HERE, "golden"))
     import make_consolidation_fixtures as mcf
-    base = mcf.snapshot(mcf.assorted()[:64], [])
-    c = random_cluster(3, n=16)
-    for p in c["pods"]:  # consolidation's eviction cost reads ReplicaSet-owned pods
-        p["spec"]["containers"][0].pop("ports", None)  # (a bound pod holding host ports is refused loudly)
-        if not p["metadata"].get("ownerReferences"):
-            p["metadata"]["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "rs",
-                                                 "uid": "rs-uid"}]
+    its = mcf.assorted()[:64]
+    base = mcf.snapshot(its, [])
+    c = consolidatable(random_cluster(3, n=16), its, 3)
     state = cluster_state(json.dumps(c))
     base["stateNodes"] = state
     base["candidates"] = [n["name"] for n in state]
@@ -139,3 +156,32 @@ def test_derived_state_feeds_consolidation():
     want, _ = bridge.consolidate(json.dumps(base), all_sims=False)
     assert [(x["name"], x["disruptionCost"]) for x in got["candidates"]] == \
         [(x["name"], x["disruptionCost"]) for x in want["candidates"]]
+    assert got["candidates"]
+
+
+def _cons_inputs(seed):
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import make_consolidation_fixtures as mcf
+    its = mcf.assorted()[:64]
+    c = consolidatable(random_cluster(seed, n=16), its, seed)
+    base = mcf.snapshot(its, [])
+    base.pop("stateNodes")
+    # the oracle reads stateNodes: its own derivation, with each node's bound pods attached in listing order
+    state = bridge.cluster_state(c)
+    for n in state:
+        n["pods"] = [p for p in c["pods"] if n["podCount"] and p["spec"]["nodeName"] == n["name"]]
+    with_state = dict(base, stateNodes=state, candidates=[n["name"] for n in state])
+    with_cluster = dict(base, cluster=c, candidates=[n["name"] for n in state])
+    return with_state, with_cluster
+
+
+@pytest.mark.parametrize("seed", (5, 6))
+def test_consolidation_snapshot_from_listings(seed):
+    """ks_cons_create / ks_cons_inspect accept the raw listings ("cluster") in place of "stateNodes"
+    and derive the same candidates as the oracle over its own derived state."""
+    with_state, with_cluster = _cons_inputs(seed)
+    got = inspect_consolidation(json.dumps(with_cluster))
+    want, _ = bridge.consolidate(json.dumps(with_state), all_sims=False)
+    assert [(x["name"], x["disruptionCost"]) for x in got["candidates"]] == \
+        [(x["name"], x["disruptionCost"]) for x in want["candidates"]]
+    assert got["candidates"]

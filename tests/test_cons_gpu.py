@@ -256,16 +256,23 @@ def test_consolidation_over_derived_cluster_state(seed):
     """Consolidation over stateNodes derived by ks_cluster_state from Node / NodeClaim / Pod listings
     (cluster-state accounting, pkg/controllers/state): GPU decisions == oracle."""
     import test_cluster_state as tcs
-    base = mcf.snapshot(mcf.assorted()[:64], [])
-    c = tcs.random_cluster(seed, n=16)
-    for p in c["pods"]:
-        p["spec"]["containers"][0].pop("ports", None)
-        if not p["metadata"].get("ownerReferences"):
-            p["metadata"]["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "rs",
-                                                 "uid": "rs-uid"}]
+    its = mcf.assorted()[:64]
+    base = mcf.snapshot(its, [])
+    c = tcs.consolidatable(tcs.random_cluster(seed, n=16), its, seed)
     from karpenter_amd import cluster_state
     state = cluster_state(json.dumps(c))
     base["stateNodes"] = state
     base["candidates"] = [n["name"] for n in state]
     want, got = _both(base, True)
+    assert _first_diff(want, got) is None, _first_diff(want, got)
+
+
+def test_consolidation_from_raw_listings():
+    """End to end from Node / NodeClaim / Pod listings: ks_cons_create derives the StateNodes itself;
+    the decisions equal the oracle's over its own derived state."""
+    import test_cluster_state as tcs
+    with_state, with_cluster = tcs._cons_inputs(7)
+    want, _ = bridge.consolidate(json.dumps(with_state), all_sims=True)
+    got = Consolidator(json.dumps(with_cluster)).consolidate(all_sims=True)
+    got.pop("kernel_ms")
     assert _first_diff(want, got) is None, _first_diff(want, got)
