@@ -28,6 +28,8 @@ def lib():
         l.oref_consolidate_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_double)]
         l.oref_consolidate_json.restype = ctypes.c_int
+        l.oref_set_tie_mode.argtypes = [ctypes.c_int, ctypes.c_ulonglong]
+        l.oref_set_tie_mode.restype = ctypes.c_int
         l.oref_cluster_state.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
         l.oref_cluster_state.restype = ctypes.c_int
         l.oref_validate_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
@@ -77,6 +79,13 @@ def consolidate(snapshot, all_sims=False):
     if l.oref_consolidate_json(s.encode(), 1 if all_sims else 0, ctypes.byref(out), ctypes.byref(secs)) != 0:
         raise RuntimeError("oracle: " + l.oref_last_error().decode())
     return json.loads(_take(out)), secs.value
+
+
+def set_tie_mode(mode, seed=0):
+    """Go map-order choice points in the oracle's topology: 0 = canonical (smallest domain name, what the
+    GPU reproduces), 1 = largest name, 2 = seeded pseudo-random; 1 and 2 are other outcomes the
+    reference's random map iteration can produce."""
+    lib().oref_set_tie_mode(mode, seed)
 
 
 def cluster_state(cluster):

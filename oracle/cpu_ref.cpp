@@ -1658,6 +1658,14 @@ int oref_consolidate_json(const char* snapshot, int all_sims, char** out, double
   }
 }
 
+// Tie-enumeration mode for Go map-order choice points (topology.inc TieBreak): 0 canonical, 1 largest
+// domain name, 2 seeded pseudo-random.
+int oref_set_tie_mode(int mode, unsigned long long seed) {
+  oref::TieBreak::mode() = mode;
+  oref::TieBreak::state() = seed ? seed : 0x9E3779B97F4A7C15ull;
+  return 0;
+}
+
 // Cluster-state accounting: StateNode accessor values from Node / NodeClaim / Pod lists.
 int oref_cluster_state(const char* cluster, char** out) {
   try {
