@@ -100,6 +100,16 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
         cpu = {"value": round(n / secs, 2), "unit": "cands/s", "cores": args.cpu_threads, "kind": "port",
                "sample": "first %d single-node simulations of the same cluster (simulateScheduling + "
                          "computeConsolidation, oracle/cpu_ref.cpp, %d host threads, %.1f s)" % (n, args.cpu_threads, secs)}
+    # Validation.IsValid + ValidateCommand (validation.go:68-180) of the command the controller would run
+    # (multi-node first): one re-simulation on the GPU, timed after the passes (it re-plans the launch)
+    final = doc["multi"]["command"] if doc["multi"]["command"]["action"] != "no-op" else doc["single"]["command"]
+    vms = []
+    for _ in range(3):
+        tv = time.perf_counter()
+        v = c.validate(final, device=local)
+        vms.append((time.perf_counter() - tv) * 1000.0)
+    validation = {"command": [final["action"], len(final["candidates"])], "valid": v["valid"], "reason": v["reason"],
+                  "ms": round(sorted(vms)[1], 3)}
     name = "C5" if not topology else "C5 + topology (%d apps: spread, pod affinity, anti-affinity)" % topology
     return {
         "metric": "consolidation cands/sec (%s: %d nodes x 20 pods, 400 instance types)" % (name, args.cons_nodes),
@@ -118,6 +128,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
                      "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("cons_c5" if not topology else "cons_c5t"),
                      "algorithmic_bytes_per_pass": algb, "kernel_ms": round(k_ms, 3), "kernel_ms_max_rank": round(kmax, 3)},
         "cpu_baseline": cpu,
+        "validation": validation,
     }
 
 
