@@ -1661,6 +1661,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 template <bool SIM, bool TOPO>
 hipError_t launch_family(const KsDev& D, const KsWork* works_dev, int n, const Plan& pl, hipStream_t st) {
 #define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, SIM, TOPO>), dim3(n), dim3(kWave), pl.lds, st, D, works_dev, pl)
+  if (n <= 0) return hipSuccess;  // e.g. a consolidation pass with no candidates: nothing to simulate
   const bool tl = pl.talloc != 0;
   switch (D.d.R) {
     case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;
