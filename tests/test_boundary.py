@@ -87,3 +87,31 @@ def test_bad_quantity_is_parse_error():
     with pytest.raises(KsError) as e:
         inspect(snap)
     assert e.value.code == -1
+
+
+def test_more_than_64_label_keys_is_capacity_error():
+    """The requirement encoding holds at most 64 label keys; beyond that the library
+    refuses with KS_ERR_CAPACITY instead of approximating."""
+    snap = synth.config2(70)
+    for i, p in enumerate(snap["pods"]):
+        p["spec"]["nodeSelector"] = {"example.com/key-%03d" % i: "v"}
+    with pytest.raises(KsError) as e:
+        inspect(snap)
+    assert e.value.code == -3, e.value
+
+
+def test_64_label_keys_or_fewer_encode():
+    snap = synth.config2(40)
+    for i, p in enumerate(snap["pods"]):
+        p["spec"]["nodeSelector"] = {"example.com/key-%03d" % i: "v"}
+    assert inspect(snap)["keys"] <= 64
+
+
+def test_cluster_state_rejects_bad_input_loudly():
+    from karpenter_amd import cluster_state
+    with pytest.raises(KsError) as e:
+        cluster_state("[1, 2]")
+    assert e.value.code == -1
+    with pytest.raises(KsError):
+        cluster_state('{"nodes": [{"metadata": {"name": "n"}, "spec": {"providerID": "p"}, '
+                      '"status": {"allocatable": {"cpu": "12q"}}}]}')
