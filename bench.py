@@ -193,6 +193,12 @@ def c4_bench(args, local):
     return out
 
 
+def _pct(xs, q):
+    """Nearest-rank percentile."""
+    ys = sorted(xs)
+    return ys[min(len(ys) - 1, max(0, -(-q * len(ys) // 100) - 1))]
+
+
 def _traffic(tag):
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % tag)
     if os.path.exists(tpath):
@@ -328,7 +334,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_solve", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": bytes_per_launch, "kernel_ms": round(k_ms, 3),
-                     "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3)},
+                     "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3),
+                     # SURVEY §8d timing protocol: median and p90 (nearest rank) of the timed Solves
+                     "kernel_ms_p50": round(_pct(solve_ms, 50), 3), "kernel_ms_p90": round(_pct(solve_ms, 90), 3)},
         "cpu_baseline": cpu,
         "solve_c3": c3,
         "solve_c4": c4,
