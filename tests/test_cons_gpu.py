@@ -276,3 +276,19 @@ def test_consolidation_from_raw_listings():
     got = Consolidator(json.dumps(with_cluster)).consolidate(all_sims=True)
     got.pop("kernel_ms")
     assert _first_diff(want, got) is None, _first_diff(want, got)
+
+
+def test_validation_at_scale_unchanged_cluster():
+    """A command validated against the cluster it was computed on is valid (validation.go:120-180 on an
+    unchanged cluster), for both the multi-node and the single-node command, and the GPU verdict equals
+    the oracle's at 600 nodes x 20 pods (the C5 shape, scaled down for the oracle)."""
+    snap = json.dumps(synth.config5(600))
+    h = Consolidator(snap)
+    doc = h.consolidate()
+    for kind in ("multi", "single"):
+        cmd = doc[kind]["command"]
+        if cmd["action"] == "no-op":
+            continue
+        got = h.validate(cmd)
+        assert got["valid"], (kind, got)
+        assert _first_diff(bridge.validate(snap, cmd), got) is None
