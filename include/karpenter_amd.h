@@ -137,10 +137,11 @@ double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int worl
 
 /* Cluster-state accounting (pkg/controllers/state: Cluster.UpdateNodeClaim / UpdateNode / UpdatePod,
  * cluster.go:220-512, and the StateNode accessors, statenode.go:110-333): from {"nodeClaims":
- * [v1beta1.NodeClaim], "nodes": [v1.Node], "pods": [v1.Pod]} derive the state the informers converge to,
- * as the snapshot's "stateNodes" array: {name, providerID, hostName, labels, taints, capacity,
- * allocatable, available, podRequests, daemonSetRequests, initialized, ready, markedForDeletion,
- * creationTimestamp, hostPortUsage, pods}.  Host-only (no device).  Free with ks_free. */
+ * [v1beta1.NodeClaim], "nodes": [v1.Node], "pods": [v1.Pod], "volumeDrivers": {"ns/pvc": driver},
+ * "csiNodes": [storagev1.CSINode]} derive the state the informers converge to, as the snapshot's
+ * "stateNodes" array: {name, providerID, hostName, labels, taints, capacity, allocatable, available,
+ * podRequests, daemonSetRequests, initialized, ready, markedForDeletion, creationTimestamp,
+ * hostPortUsage, volumeUsage, volumeLimits, pods}.  Host-only (no device).  Free with ks_free. */
 int ks_cluster_state(const char* cluster_json, size_t len, char** state_nodes_json);
 
 void ks_free(void* p);

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -74,6 +75,7 @@ struct Entry {
   const Value* claim = nullptr;
   std::map<std::string, QList> podRequests, dsRequests;  // by pod key "ns/name" (sorted: canonical sums)
   std::map<std::string, std::vector<HostPortH>> ports;
+  std::map<std::string, std::map<std::string, std::set<std::string>>> volumes;  // pod key -> driver -> PVC ids
   std::vector<const Value*> pods;  // bound pods (GetNodePods' listing, unfiltered)
 
   std::map<std::string, std::string> nodeLabels() const { return smap(path(node, {"metadata", "labels"})); }
@@ -194,6 +196,7 @@ std::string cluster_state_json(const Value& root) {
       entry(id).node = &n;
       nodeNameToID[sget(path(&n, {"metadata"}), "name")] = id;
     }
+  const Value* drivers = root.get("volumeDrivers");
   if (const Value* ps = root.get("pods"))
     for (auto& pv : ps->arr()) {
       PodH p = parse_pod(pv);
@@ -208,6 +211,14 @@ std::string cluster_state_json(const Value& root) {
       if (p.ownedByDaemonSet) e.dsRequests[key] = p.requests;
       else e.dsRequests.erase(key);
       e.ports[key] = p.ports;
+      // GetVolumes (volumeusage.go:82-113): PVC id "ns/claim" -> CSI driver; unresolved ones are skipped
+      auto& vol = e.volumes[key];
+      vol.clear();
+      for (auto& claim : p.pvcNames) {
+        const std::string id = p.ns + "/" + claim;
+        const Value* drv = drivers ? drivers->get(id) : nullptr;
+        if (drv && drv->is_str() && !drv->s.empty()) vol[drv->s].insert(id);
+      }
     }
   std::string o = "[";
   bool firstNode = true;
@@ -296,6 +307,44 @@ std::string cluster_state_json(const Value& root) {
       }
       o += "]";
     }
+    // VolumeUsage (union of the pods' volumes) and populateVolumeLimits (cluster.go:457-471: CSINode
+    // drivers with an allocatable count)
+    std::map<std::string, std::set<std::string>> vu;
+    for (auto& kv : e.volumes)
+      for (auto& dv : kv.second) vu[dv.first].insert(dv.second.begin(), dv.second.end());
+    o += "},\"volumeUsage\":{";
+    first = true;
+    for (auto& kv : vu) {
+      if (!first) o += ",";
+      first = false;
+      ksjson::quote(o, kv.first);
+      o += ":[";
+      bool f2 = true;
+      for (auto& id : kv.second) {
+        if (!f2) o += ",";
+        f2 = false;
+        ksjson::quote(o, id);
+      }
+      o += "]";
+    }
+    o += "},\"volumeLimits\":{";
+    first = true;
+    if (e.node)
+      if (const Value* csis = root.get("csiNodes"))
+        for (auto& cn : csis->arr()) {
+          if (sget(path(&cn, {"metadata"}), "name") != sget(path(e.node, {"metadata"}), "name")) continue;
+          if (const Value* ds = path(&cn, {"spec", "drivers"}))
+            for (auto& dv : ds->arr()) {
+              const Value* alloc = dv.get("allocatable");
+              if (!alloc || alloc->is_null()) continue;
+              const Value* cnt = alloc->get("count");
+              if (!first) o += ",";
+              first = false;
+              ksjson::quote(o, sget(&dv, "name"));
+              o += ":" + std::to_string(cnt ? cnt->i64() : 0);
+            }
+          break;
+        }
     o += "},\"pods\":[";
     for (size_t i = 0; i < e.pods.size(); i++) {
       if (i) o += ",";

@@ -37,7 +37,7 @@ def nodeclaim(name, provider_id, labels=None, allocatable=None, capacity=None, t
                        "capacity": dict(capacity or allocatable or {})}}
 
 
-def pod(name, requests=None, node_name="", phase="Running", daemonset=False, host_ports=(), ns="default"):
+def pod(name, requests=None, node_name="", phase="Running", daemonset=False, host_ports=(), ns="default", pvcs=()):
     c = {"name": "c", "resources": {"requests": dict(requests or {})}}
     if host_ports:
         c["ports"] = [{"containerPort": 8080, "hostPort": p, "protocol": "TCP"} for p in host_ports]
@@ -45,7 +45,10 @@ def pod(name, requests=None, node_name="", phase="Running", daemonset=False, hos
     if daemonset:
         md["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "DaemonSet", "name": "ds", "uid": "ds-uid",
                                   "controller": True}]
-    return {"metadata": md, "spec": {"nodeName": node_name, "containers": [c]}, "status": {"phase": phase}}
+    spec = {"nodeName": node_name, "containers": [c]}
+    if pvcs:
+        spec["volumes"] = [{"name": "v%d" % i, "persistentVolumeClaim": {"claimName": n}} for i, n in enumerate(pvcs)]
+    return {"metadata": md, "spec": spec, "status": {"phase": phase}}
 
 
 MANAGED = {"karpenter.sh/nodepool": "default", "node.kubernetes.io/instance-type": "1-cpu-1-mem-amd64-linux"}
@@ -91,6 +94,16 @@ def scenarios():
               "cluster": {"nodes": [node("node-1", {"cpu": "4"}, MANAGED)],
                           "pods": [pod("hp-%d" % i, None, "node-1", host_ports=[i]) for i in range(1, 10)]},
               "expect": {"count": 1, "nodes": {"node-1": {"hostPorts": [5]}}}})
+    # "should hydrate the volume usage on a Node update" (:143-163): 10 bound pods with one PVC each of
+    # a StorageClass provisioned by the CSI driver; the CSINode allows 10 volumes of that driver
+    csi = "fake.csi.provider"
+    S.append({"name": "volume-hydration", "source": src + ":100-163",
+              "cluster": {"nodes": [node("node-1", {"cpu": "4"}, MANAGED)],
+                          "pods": [pod("vp-%d" % i, None, "node-1", pvcs=["pvc-%d" % i]) for i in range(10)],
+                          "volumeDrivers": {"default/pvc-%d" % i: csi for i in range(10)},
+                          "csiNodes": [{"metadata": {"name": "node-1"},
+                                        "spec": {"drivers": [{"name": csi, "allocatable": {"count": 10}}]}}]},
+              "expect": {"count": 1, "nodes": {"node-1": {"volumes": {csi: 10}, "volumeLimits": {csi: 10}}}}})
     nc = nodeclaim("nodeclaim-1", "fake:///nodeclaim-1", MANAGED, {"cpu": "4"})
     S.append({"name": "nodeclaim-and-node-same-name", "source": src + ":323-350",
               "cluster": {"nodeClaims": [nc], "nodes": [node("nodeclaim-1", {"cpu": "4"}, MANAGED)], "pods": []},

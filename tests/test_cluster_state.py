@@ -53,6 +53,9 @@ def test_state_scenarios(fx):
         for field in ("podRequests", "daemonSetRequests"):
             for r, v in exp.get(field, {}).items():  # ExpectResources: missing = 0
                 assert qty(n[field].get(r, "0")) == qty(v), (field, r, n[field])
+        for drv, cnt in exp.get("volumes", {}).items():  # ExceedsLimits of one more volume: at the limit
+            assert len(n["volumeUsage"][drv]) == cnt
+        assert n.get("volumeLimits", {}) == exp.get("volumeLimits", n.get("volumeLimits", {}))
         for port in exp.get("hostPorts", []):
             assert any(p["port"] == port for ps in n["hostPortUsage"].values() for p in ps)
         for r, v in n["allocatable"].items():  # Available = Allocatable - PodRequests
@@ -108,8 +111,21 @@ def random_cluster(seed, n=24):
         req = {"cpu": rng.choice(["100m", "250m", "1", "1.5"]), "memory": rng.choice(["128Mi", "1Gi", "1.5G"])}
         pods.append(msf.pod("pod-%03d" % j, req, bound, phase=rng.choice(["Running"] * 6 + ["Failed", "Succeeded"]),
                             daemonset=rng.random() < 0.15, host_ports=[8000 + j] if rng.random() < 0.1 else (),
-                            ns=rng.choice(["default", "kube-system"])))
-    return {"nodeClaims": ncs, "nodes": nodes, "pods": pods}
+                            ns=rng.choice(["default", "kube-system"]),
+                            pvcs=["pvc-%d" % rng.randrange(40)] if rng.random() < 0.3 else ()))
+    # PVC -> CSI driver (resolved, "" = no driver, or absent = NotFound) and CSINode limits
+    drivers = {}
+    for k in range(40):
+        for ns in ("default", "kube-system"):
+            r = rng.random()
+            if r < 0.7:
+                drivers["%s/pvc-%d" % (ns, k)] = rng.choice(["ebs.csi", "efs.csi"])
+            elif r < 0.85:
+                drivers["%s/pvc-%d" % (ns, k)] = ""
+    csis = [{"metadata": {"name": nm}, "spec": {"drivers": [
+        {"name": "ebs.csi", "allocatable": {"count": rng.randint(1, 30)}},
+        {"name": "efs.csi", "allocatable": None}]}} for nm in names if rng.random() < 0.6]
+    return {"nodeClaims": ncs, "nodes": nodes, "pods": pods, "volumeDrivers": drivers, "csiNodes": csis}
 
 
 @pytest.mark.parametrize("seed", range(12))
