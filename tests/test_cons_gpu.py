@@ -292,3 +292,21 @@ def test_validation_at_scale_unchanged_cluster():
         got = h.validate(cmd)
         assert got["valid"], (kind, got)
         assert _first_diff(bridge.validate(snap, cmd), got) is None
+
+
+@pytest.mark.parametrize("seed,topo", [(71, 0), (72, 8), (73, 24)])
+def test_validation_of_arbitrary_candidate_subsets(seed, topo):
+    """Commands whose candidates are not a prefix of the disruption-cost order (a command from an earlier
+    snapshot, whose order has since changed): the re-simulation removes an arbitrary subset, with its
+    topology counts and hostnames, and its verdict equals the oracle's."""
+    import random
+    snap = synth.cluster_snapshot(20, 6, n_its=40, it_range=(4, 30), seed=seed, n_pending=1, topology=topo)
+    s = json.dumps(snap)
+    h = Consolidator(s)
+    names = [c["name"] for c in bridge.consolidate(s)[0]["candidates"]]
+    rng = random.Random(seed)
+    for _ in range(10):
+        cands = rng.sample(names, rng.randint(1, min(5, len(names))))
+        cmd = {"action": "delete", "candidates": cands}
+        want, got = bridge.validate(s, cmd), h.validate(cmd)
+        assert _first_diff(want, got) is None, (cands, _first_diff(want, got))
