@@ -181,6 +181,7 @@ void ks_upload(ks_problem* pb) {
   size_t o_op = put(t.off_price.data(), t.off_price.size() * 8);
   size_t o_phc = put(t.pod_hpc.data(), t.pod_hpc.size() * 8);
   size_t o_phu = put(t.pod_hpu.data(), t.pod_hpu.size() * 8);
+  size_t o_pho = put(t.pod_hpo.data(), t.pod_hpo.size() * 8);
   size_t o_nhp = put(t.n_hp0.data(), t.n_hp0.size() * 8);
   size_t o_pvm = put(t.pod_vm.data(), t.pod_vm.size() * 8);
   size_t o_vdm = put(t.vol_dm.data(), t.vol_dm.size() * 8);
@@ -241,6 +242,7 @@ void ks_upload(ks_problem* pb) {
   D.off_price = (const double*)(b + o_op);
   D.pod_hpc = (const uint64_t*)(b + o_phc);
   D.pod_hpu = (const uint64_t*)(b + o_phu);
+  D.pod_hpo = (const uint64_t*)(b + o_pho);
   D.n_hp0 = (const uint64_t*)(b + o_nhp);
   D.pod_vm = (const uint64_t*)(b + o_pvm);
   D.vol_dm = (const uint64_t*)(b + o_vdm);
@@ -542,6 +544,10 @@ int ks_problem_create(const char* json, size_t len, ks_problem** out) {
     HIPCHK(hipMalloc(&pb->svals, 2 * n * sizeof(int32_t)));
     pb->stempBytes = std::max<size_t>(queue_sort_temp_bytes((int)n), 256);
     HIPCHK(hipMalloc(&pb->stemp, pb->stempBytes));
+    if (!pb->host.hostQueue.empty()) {
+      HIPCHK(hipMalloc(&pb->hqorder, 4 * n));
+      HIPCHK(hipMemcpy(pb->hqorder, pb->host.hostQueue.data(), 4 * pb->host.hostQueue.size(), hipMemcpyHostToDevice));
+    }
   }
   *out = pb.release();
   return KS_OK;
@@ -561,6 +567,8 @@ int ks_problem_inspect(const char* json, size_t len, char** out) {
   kv("R", d.R); kv("keys", d.NK); kv("W", d.W); kv("NB", d.NB); kv("RSW", d.RSW); kv("T", d.T); kv("templates", d.NTPL);
   kv("pools", d.NPOOL); kv("nodes", d.N); kv("pods", d.P); kv("states", d.S); kv("uids", d.NU); kv("TW", d.TW);
   kv("Kcap", d.Kcap); kv("taints", (long long)h.taints.size()); kv("G", d.G); kv("G1", d.G1);
+  kv("hostQueue", h.hostQueue.empty() ? 0 : 1); kv("hostPorts", (long long)h.hostPortUniverse.size());
+  kv("lateGroups", __builtin_popcountll(d.tgLate)); kv("unlabelledNodes", d.tgUnlab);
   // LDS plans (ks_solve.hip make_plan) at the default and a few reduced budgets
   o += ",\"plans\":{";
   const size_t budgets[] = {160 * 1024 - 256, 6000, 9000, 14000, 24000, 40000};
@@ -588,7 +596,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   API_TRY
   if (!pb || !out) throw KsError(KS_ERR_ARG, "null argument");
   int reps = opts && opts->replicas > 1 ? opts->replicas : 1;
-  if (opts && opts->device >= 0) HIPCHK(hipSetDevice(opts->device));
+  DeviceGuard guard(pb->device, opts);
   const KsDims& d = pb->host.dims;
   // one Solve per CU gets the whole 160 KiB; larger batches trade LDS for waves per CU
   size_t budget = 160 * 1024 - 256;
@@ -622,7 +630,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   for (int attempt = 0; attempt < 2; attempt++) {
     HIPCHK(hipEventRecord(e0, pb->stream));
     HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp,
-                        pb->stempBytes, pb->stream, em));
+                        pb->stempBytes, pb->stream, em, pb->hqorder));
     HIPCHK(hipEventRecord(e1, pb->stream));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));

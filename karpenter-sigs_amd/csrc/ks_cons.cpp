@@ -189,7 +189,10 @@ struct ks_cons {
     bool multi = false;
   };
   std::unique_ptr<ks_problem> pb;
+  // [0, nPass): the pass's candidates in disruption-cost order; [nPass, size): nodes only
+  // Validation.ShouldDisrupt admits (their pool has consolidateAfter Never), for validation's mapping
   std::vector<Cand> cands;
+  int nPass = 0;
   std::vector<Sim> sims;  // multi-node prefixes first (largest first), then one per candidate
   int multiHi = 0;        // multi-node prefix lengths mid+1 for mid in [1, multiHi]
   std::vector<int> pending, deleting;
@@ -197,44 +200,46 @@ struct ks_cons {
   int64_t hostnameSeed = 0;
   int recWords = 0;
 
-  // cached launch for (rank, world)
-  int lrank = -1, lworld = -1;
-  std::vector<int> lsims;  // simulation ids of this rank, launch order
-  void* lbuf = nullptr;    // workspaces + pod maps + views
-  KsWork* lworks = nullptr;
-  int32_t* lrec = nullptr;
-  int32_t* lentries = nullptr;
-  int32_t* lentrySim = nullptr;
-  int32_t* lpodmap = nullptr;
-  uint64_t* lkeys = nullptr;
-  int32_t* lvals = nullptr;
-  void* ltemp = nullptr;
-  size_t ltempBytes = 0;
-  int lnent = 0, lrbits = 0, lsbits = 0;
-  Plan lplan{};
-  std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
+  // A launch of one rank's simulations, cached per (rank, world).  Validation runs its one
+  // re-simulation in a launch of its own, so the pass's launch (records, requirement records,
+  // counters) survives it.
+  struct Launch {
+    int lrank = -1, lworld = -1;
+    std::vector<int> lsims;  // simulation ids of this rank, launch order
+    void* lbuf = nullptr;    // workspaces + pod maps + views
+    KsWork* lworks = nullptr;
+    int32_t* lrec = nullptr;
+    int32_t* lentries = nullptr;
+    int32_t* lentrySim = nullptr;
+    int32_t* lpodmap = nullptr;
+    uint64_t* lkeys = nullptr;
+    int32_t* lvals = nullptr;
+    void* ltemp = nullptr;
+    size_t ltempBytes = 0;
+    int lnent = 0, lrbits = 0, lsbits = 0;
+    Plan lplan{};
+    std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
+    void release() {
+      for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
+                      (void*)lkeys, (void*)lvals, ltemp})
+        if (p) (void)hipFree(p);
+      *this = Launch{};  // stale lookups (claim requirements, counters) now fail cleanly
+    }
+  };
+  Launch L;
   int32_t* rank = nullptr;  // global NewQueue rank of every pod
 
   int sim_of_multi(int mid) const { return multiHi - mid; }  // mid in [1, multiHi]
   int sim_of_single(int i) const { return multiHi + i; }
   int per_rank(int world) const { return ((int)sims.size() + world - 1) / world; }
 
-  void free_launch() {
-    for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
-                    (void*)lkeys, (void*)lvals, ltemp})
-      if (p) (void)hipFree(p);
-    lbuf = nullptr;
-    lworks = nullptr;
-    lrec = lentries = lentrySim = lpodmap = nullptr;
-    lkeys = nullptr;
-    lvals = nullptr;
-    ltemp = nullptr;
-    lrank = lworld = -1;
-  }
+  void free_launch() { L.release(); }
   ~ks_cons() {
-    if (pb) (void)hipSetDevice(pb->device);
+    int prev = -1;
+    if (pb && hipGetDevice(&prev) == hipSuccess) (void)hipSetDevice(pb->device);
     free_launch();
     if (rank) (void)hipFree(rank);
+    if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
 
@@ -314,9 +319,10 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   std::map<std::string, int> hostNode;  // node name -> host.nodes index (sorted order)
   for (size_t i = 0; i < h.nodes.size(); i++) hostNode[h.nodes[i].name] = (int)i;
 
-  // NodePools: expireAfter for lifetimeRemaining
+  // NodePools: expireAfter for lifetimeRemaining; consolidationPolicy (CRD default WhenUnderutilized) and
+  // consolidateAfter ("Never": a NillableDuration with a nil Duration) for ShouldDisrupt
   std::map<std::string, int64_t> expire;
-  std::set<std::string> poolNames;
+  std::set<std::string> poolNames, policyOff, afterNever;
   if (const Value* ps = root.get("nodePools"))
     for (auto& v : ps->arr()) {
       const std::string name = jstr(v.get("metadata"), "name");
@@ -325,6 +331,11 @@ void build_cons(ks_cons& c, const Value& rootIn) {
       int64_t ns = 0;
       if (d && d->get("expireAfter") && d->get("expireAfter")->is_str() && go_duration(d->get("expireAfter")->str(), ns))
         expire[name] = ns;
+      if (d && d->get("consolidationPolicy") && d->get("consolidationPolicy")->is_str() &&
+          d->get("consolidationPolicy")->str() != "WhenUnderutilized")
+        policyOff.insert(name);
+      if (d && d->get("consolidateAfter") && d->get("consolidateAfter")->is_str() && d->get("consolidateAfter")->str() == "Never")
+        afterNever.insert(name);
     }
   std::map<std::string, std::map<std::string, int>> poolTypes;
   if (const Value* bp = root.get("instanceTypesByNodePool"))
@@ -338,7 +349,7 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   const std::vector<Pdb> pdbs = parse_pdbs(root);
 
   // NewCandidate for the listed nodes; nodes that would fail it are not candidates
-  std::vector<ks_cons::Cand> cands;
+  std::vector<ks_cons::Cand> cands, valOnly;
   if (const Value* cs = root.get("candidates"))
     for (auto& v : cs->arr()) {
       const std::string name = v.str();
@@ -350,12 +361,20 @@ void build_cons(ks_cons& c, const Value& rootIn) {
       if (hn == hostNode.end()) continue;
       const Host::Node& n = h.nodes[(size_t)hn->second];
       if (!n.initialized) continue;
+      const Value* ann = nv.get("annotations");
+      if (ann && ann->is_obj() && ann->get("karpenter.sh/do-not-disrupt")) continue;  // types.go:78-81 (key presence)
       auto lct = n.labels.find(kCTKey), lz = n.labels.find(kZoneKey), lp = n.labels.find(kPoolKey);
       if (lct == n.labels.end() || lz == n.labels.end() || lp == n.labels.end()) continue;
       auto pt = poolTypes.find(lp->second);
       if (!poolNames.count(lp->second) || pt == poolTypes.end()) continue;
       auto lit = n.labels.find(kITKey);
       if (lit == n.labels.end() || !pt->second.count(lit->second)) continue;
+      if (c.nominated.count(name)) continue;  // types.go:110-113
+      // ShouldDisrupt: consolidation.go:96-108 for the pass; validation.go:112-118 (no consolidateAfter
+      // test) admits the rest for mapCandidates after the wait
+      if (ann && ann->is_obj() && jstr(ann, "karpenter.sh/do-not-consolidate") == "true") continue;
+      if (policyOff.count(lp->second)) continue;
+      const bool passOk = !afterNever.count(lp->second);
       ks_cons::Cand k;
       k.node = hn->second;
       k.name = name;
@@ -377,7 +396,7 @@ void build_cons(ks_cons& c, const Value& rootIn) {
       // filterCandidates (helpers.go:47-71): a PDB allowing no eviction or a do-not-disrupt pod blocks it
       bool blocked = false;
       for (int p : k.pods) blocked = blocked || !can_evict(pdbs, podMeta[(size_t)p]) || do_not_disrupt(podMeta[(size_t)p]);
-      if (!blocked) cands.push_back(std::move(k));
+      if (!blocked) (passOk ? cands : valOnly).push_back(std::move(k));
     }
   // sort.Slice(candidates, disruptionCost <): pdqsort only observes less(), so the costs' dense ranks
   // reproduce its swap sequence exactly.
@@ -395,8 +414,10 @@ void build_cons(ks_cons& c, const Value& rootIn) {
     g.run(n);
     for (int i = 0; i < n; i++) c.cands.push_back(cands[(size_t)idx[i]]);
   }
+  c.nPass = (int)c.cands.size();
+  for (auto& k : valOnly) c.cands.push_back(std::move(k));
   // the simulations: multi-node prefixes (firstNConsolidationOption's search space) and single nodes
-  const int n = (int)c.cands.size();
+  const int n = c.nPass;
   if (n >= 2) {
     int hi = std::min(n, 100);
     if (n <= hi) hi = n - 1;
@@ -464,7 +485,9 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
     const int g = e.first.first, v = e.first.second;
     const bool host = h.groups[(size_t)g].keyId == hostKey;
     // still registered with no pod: a universe domain, or the hostname of a node the simulation keeps
-    const bool keep = h.topoUniverse[(size_t)g][(size_t)v] || (host && h.activeHost(v) && !goneHosts.count(v));
+    // (a late group never registered the nodes' hostnames: it was created after NewExistingNode)
+    const bool keep = h.topoUniverse[(size_t)g][(size_t)v] ||
+                      (host && !h.groups[(size_t)g].late && h.activeHost(v) && !goneHosts.count(v));
     if (v < 0 || v >= h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_NV])
       throw KsError(KS_ERR_CAPACITY, "topology domain outside its group's value range");
     out.push_back(h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_CNT] + v);
@@ -480,7 +503,7 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
 
 // Build and upload the launch of this rank's simulations (cached per (rank, world)).
 void prepare_launch(ks_cons& c, int rank, int world) {
-  if (c.lrank == rank && c.lworld == world) return;
+  if (c.L.lrank == rank && c.L.lworld == world) return;
   c.free_launch();
   ks_problem& pb = *c.pb;
   Host& h = pb.host;
@@ -489,7 +512,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   std::vector<int> mine;
   for (int s = rank; s < (int)c.sims.size(); s += world) mine.push_back(s);
   const int ns = (int)mine.size();
-  c.lsims = mine;
+  c.L.lsims = mine;
   // per-node capacity in device units (limits are restored for the removed candidates)
   auto nodeCap = [&](int node, int r) -> int64_t {
     auto it = h.nodes[(size_t)node].capacity.find(h.resNames[(size_t)r]);
@@ -562,26 +585,26 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       o.tdel = a.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
     }
   }
-  c.lnent = (int)entries.size();
-  HIPCHK(hipMalloc(&c.lbuf, std::max<size_t>(a.total, 256)));
-  char* base = (char*)c.lbuf;
-  HIPCHK(hipMalloc(&c.lworks, sizeof(KsWork) * std::max(ns, 1)));
-  HIPCHK(hipMalloc(&c.lrec, 4 * (size_t)c.recWords * std::max(ns, 1)));
-  HIPCHK(hipMalloc(&c.lentries, 4 * (size_t)std::max(c.lnent, 1)));
-  HIPCHK(hipMalloc(&c.lentrySim, 4 * (size_t)std::max(c.lnent, 1)));
-  HIPCHK(hipMalloc(&c.lpodmap, 4 * (size_t)std::max(c.lnent, 1)));
-  HIPCHK(hipMalloc(&c.lkeys, 16 * (size_t)std::max(c.lnent, 1)));
-  HIPCHK(hipMalloc(&c.lvals, 8 * (size_t)std::max(c.lnent, 1)));
-  c.ltempBytes = std::max<size_t>(queue_sort_temp_bytes(std::max(c.lnent, 1)), 256);
-  HIPCHK(hipMalloc(&c.ltemp, c.ltempBytes));
-  if (c.lnent) {
-    HIPCHK(hipMemcpy(c.lentries, entries.data(), 4 * entries.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c.lentrySim, entrySim.data(), 4 * entrySim.size(), hipMemcpyHostToDevice));
+  c.L.lnent = (int)entries.size();
+  HIPCHK(hipMalloc(&c.L.lbuf, std::max<size_t>(a.total, 256)));
+  char* base = (char*)c.L.lbuf;
+  HIPCHK(hipMalloc(&c.L.lworks, sizeof(KsWork) * std::max(ns, 1)));
+  HIPCHK(hipMalloc(&c.L.lrec, 4 * (size_t)c.recWords * std::max(ns, 1)));
+  HIPCHK(hipMalloc(&c.L.lentries, 4 * (size_t)std::max(c.L.lnent, 1)));
+  HIPCHK(hipMalloc(&c.L.lentrySim, 4 * (size_t)std::max(c.L.lnent, 1)));
+  HIPCHK(hipMalloc(&c.L.lpodmap, 4 * (size_t)std::max(c.L.lnent, 1)));
+  HIPCHK(hipMalloc(&c.L.lkeys, 16 * (size_t)std::max(c.L.lnent, 1)));
+  HIPCHK(hipMalloc(&c.L.lvals, 8 * (size_t)std::max(c.L.lnent, 1)));
+  c.L.ltempBytes = std::max<size_t>(queue_sort_temp_bytes(std::max(c.L.lnent, 1)), 256);
+  HIPCHK(hipMalloc(&c.L.ltemp, c.L.ltempBytes));
+  if (c.L.lnent) {
+    HIPCHK(hipMemcpy(c.L.lentries, entries.data(), 4 * entries.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c.L.lentrySim, entrySim.data(), 4 * entrySim.size(), hipMemcpyHostToDevice));
   }
-  c.lrbits = 1;
-  while ((1ll << c.lrbits) < std::max(d.P, 2)) c.lrbits++;
-  c.lsbits = 1;
-  while ((1ll << c.lsbits) < std::max(ns, 2)) c.lsbits++;
+  c.L.lrbits = 1;
+  while ((1ll << c.L.lrbits) < std::max(d.P, 2)) c.L.lrbits++;
+  c.L.lsbits = 1;
+  while ((1ll << c.L.lsbits) < std::max(ns, 2)) c.L.lsbits++;
 
   // per-simulation inputs: removed nodes, limits, prices
   std::vector<char> stage(a.total, 0);
@@ -668,12 +691,12 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     w.counters = (int64_t*)(base + o.counters);
     w.n_hp = (uint64_t*)(base + o.n_hp);
     w.c_hp = (uint64_t*)(base + o.c_hp);
-    w.pod_map = c.lpodmap + entBeg[k];
+    w.pod_map = c.L.lpodmap + entBeg[k];
     w.P = simP[k];
     w.nrm = (int32_t)rm.size();
     w.rm = (const int32_t*)(base + o.rm);
     w.pool0 = (const int64_t*)(base + o.pool0);
-    w.rec = c.lrec + (size_t)k * c.recWords;
+    w.rec = c.L.lrec + (size_t)k * c.recWords;
     w.price = price;
     w.cflags = cflags;
     w.ccs = simP[k] + 1;
@@ -692,17 +715,17 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     }
     works[k] = w;
   }
-  HIPCHK(hipMemcpy(c.lbuf, stage.data(), a.total, hipMemcpyHostToDevice));
-  if (ns) HIPCHK(hipMemcpy(c.lworks, works.data(), sizeof(KsWork) * ns, hipMemcpyHostToDevice));
-  c.lhost = works;
+  HIPCHK(hipMemcpy(c.L.lbuf, stage.data(), a.total, hipMemcpyHostToDevice));
+  if (ns) HIPCHK(hipMemcpy(c.L.lworks, works.data(), sizeof(KsWork) * ns, hipMemcpyHostToDevice));
+  c.L.lhost = works;
   // LDS plan: a small budget per simulation so several simulations share a CU
   KsDims dd = d;
   dd.Kcap = std::max(1, std::min(maxP, 16384));
-  c.lplan = make_plan(dd, 40 * 1024, true);
-  if (c.lplan.lds > 64 * 1024 || c.lplan.KO < 1) c.lplan = make_plan(dd, 160 * 1024 - 256, true);
-  if (c.lplan.lds > 160 * 1024 || c.lplan.KO < 1) throw KsError(KS_ERR_CAPACITY, "simulation state does not fit in LDS");
-  c.lrank = rank;
-  c.lworld = world;
+  c.L.lplan = make_plan(dd, 40 * 1024, true);
+  if (c.L.lplan.lds > 64 * 1024 || c.L.lplan.KO < 1) c.L.lplan = make_plan(dd, 160 * 1024 - 256, true);
+  if (c.L.lplan.lds > 160 * 1024 || c.L.lplan.KO < 1) throw KsError(KS_ERR_CAPACITY, "simulation state does not fit in LDS");
+  c.L.lrank = rank;
+  c.L.lworld = world;
 }
 
 std::string names_json(const Host& h, const std::vector<int>& its) {
@@ -738,7 +761,7 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
     if (rec((int)s)[RF_ERROR] != KE_OK)
       throw KsError(rec((int)s)[RF_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
                     "simulation " + std::to_string(s) + " reported kernel error " + std::to_string(rec((int)s)[RF_ERROR]));
-  const int n = (int)c.cands.size();
+  const int n = c.nPass;
   int64_t counter = c.hostnameSeed;
   std::map<int, int64_t> before;  // sim -> hostname counter before it ran
   auto run = [&](int sim) {
@@ -872,14 +895,14 @@ namespace {
 double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
   prepare_launch(c, rank, world);
   ks_problem& pb = *c.pb;
-  const int ns = (int)c.lsims.size();
+  const int ns = (int)c.L.lsims.size();
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
   HIPCHK(hipEventRecord(e0, pb.stream));
-  HIPCHK(sim_queue_sort(c.rank, c.lentries, c.lentrySim, c.lnent, c.lrbits, c.lsbits, c.lkeys, c.lvals, c.ltemp,
-                        c.ltempBytes, c.lpodmap, pb.stream));
-  HIPCHK(launch_sims(pb.dev, c.lworks, ns, c.lplan, pb.stream));
+  HIPCHK(sim_queue_sort(c.rank, c.L.lentries, c.L.lentrySim, c.L.lnent, c.L.lrbits, c.L.lsbits, c.L.lkeys, c.L.lvals, c.L.ltemp,
+                        c.L.ltempBytes, c.L.lpodmap, pb.stream));
+  HIPCHK(launch_sims(pb.dev, c.L.lworks, ns, c.L.lplan, pb.stream));
   HIPCHK(hipEventRecord(e1, pb.stream));
   HIPCHK(hipEventSynchronize(e1));
   float ms = 0;
@@ -889,10 +912,10 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
   const size_t bytes = 4 * (size_t)c.recWords * ns, all = 4 * (size_t)c.recWords * c.per_rank(world);
   if (onDevice) {
     HIPCHK(hipMemsetAsync(records, 0, all, pb.stream));
-    if (bytes) HIPCHK(hipMemcpyAsync(records, c.lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
+    if (bytes) HIPCHK(hipMemcpyAsync(records, c.L.lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
   } else {
     memset(records, 0, all);
-    if (bytes) HIPCHK(hipMemcpyAsync(records, c.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
+    if (bytes) HIPCHK(hipMemcpyAsync(records, c.L.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
   }
   HIPCHK(hipStreamSynchronize(pb.stream));
   return ms;
@@ -927,21 +950,25 @@ std::string validate_json(ks_cons& c, const Value& cmd) {
   for (int i : mapped)
     if (c.nominated.count(c.cands[(size_t)i].name)) return out(false, "candidate-nominated", "");
   if (mapped.empty()) return out(false, "no-candidates", "");
-  // a plan holding only this simulation, then the pass's plan back
+  // a plan holding only this simulation in a launch of its own; the pass's plan and launch come back
   std::vector<ks_cons::Sim> saved(1);
   saved[0].cands = mapped;
   saved.swap(c.sims);
-  c.free_launch();
+  ks_cons::Launch pass;
+  std::swap(pass, c.L);
+  auto restore = [&]() {
+    c.free_launch();
+    std::swap(pass, c.L);
+    c.sims.swap(saved);
+  };
   std::vector<int32_t> r((size_t)c.recWords, 0);
   try {
     (void)run_sims(c, 0, 1, r.data(), false);
   } catch (...) {
-    c.sims.swap(saved);
-    c.free_launch();
+    restore();
     throw;
   }
-  c.sims.swap(saved);
-  c.free_launch();
+  restore();
   if (r[RF_ERROR] != KE_OK)
     throw KsError(r[RF_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
                   "validation simulation reported kernel error " + std::to_string(r[RF_ERROR]));
@@ -1011,7 +1038,7 @@ int ks_cons_inspect(const char* json, size_t len, char** out) {
   ks_cons c;
   build_cons(c, root);
   std::string o = "{\"candidates\":[";
-  for (size_t i = 0; i < c.cands.size(); i++) {
+  for (size_t i = 0; i < (size_t)c.nPass; i++) {
     if (i) o += ",";
     o += "{\"name\":";
     ksjson::quote(o, c.cands[i].name);
@@ -1029,7 +1056,7 @@ int ks_cons_inspect(const char* json, size_t len, char** out) {
 
 void ks_cons_free(ks_cons* c) { delete c; }
 
-int ks_cons_num_candidates(const ks_cons* c) { return c ? (int)c->cands.size() : 0; }
+int ks_cons_num_candidates(const ks_cons* c) { return c ? c->nPass : 0; }
 int ks_cons_num_sims(const ks_cons* c) { return c ? (int)c->sims.size() : 0; }
 int ks_cons_record_bytes(const ks_cons* c) { return c ? 4 * c->recWords : 0; }
 int ks_cons_records_per_rank(const ks_cons* c, int world) { return c && world > 0 ? c->per_rank(world) : 0; }
@@ -1038,7 +1065,7 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
                 double* kernel_ms) {
   API_TRY
   if (!c || !records || world < 1 || rank < 0 || rank >= world) throw KsError(KS_ERR_ARG, "bad argument");
-  if (opts && opts->device >= 0) HIPCHK(hipSetDevice(opts->device));
+  DeviceGuard guard(c->pb->device, opts);
   const double ms = run_sims(*c, rank, world, records, records_on_device != 0);
   if (kernel_ms) *kernel_ms = ms;
   return KS_OK;
@@ -1048,7 +1075,7 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
 int ks_cons_validate(ks_cons* c, const char* command_json, size_t len, const ks_solve_opts* opts, char** json_out) {
   API_TRY
   if (!c || !command_json || !json_out) throw KsError(KS_ERR_ARG, "null argument");
-  if (opts && opts->device >= 0) HIPCHK(hipSetDevice(opts->device));
+  DeviceGuard guard(c->pb->device, opts);
   ksjson::Value cmd = ksjson::Parser(command_json, len ? len : strlen(command_json)).parse();
   if (!cmd.is_obj()) throw KsError(KS_ERR_PARSE, "command is not an object");
   *json_out = strdup(validate_json(*c, cmd).c_str());
@@ -1089,12 +1116,12 @@ int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out) {
   API_TRY
   if (!c || !out) throw KsError(KS_ERR_ARG, "bad argument");
   const int RSW = c->pb->host.dims.RSW;
-  for (size_t k = 0; k < c->lsims.size(); k++)
-    if (c->lsims[k] == sim) {
+  for (size_t k = 0; k < c->L.lsims.size(); k++)
+    if (c->L.lsims[k] == sim) {
       int32_t claim = -1;
-      HIPCHK(hipMemcpy(&claim, c->lrec + k * c->recWords + RF_CLAIM, 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(&claim, c->L.lrec + k * c->recWords + RF_CLAIM, 4, hipMemcpyDeviceToHost));
       if (claim < 0) throw KsError(KS_ERR_ARG, "simulation has no NodeClaim");
-      HIPCHK(hipMemcpy(out, c->lhost[k].c_rs + (size_t)claim * RSW, 4 * (size_t)RSW, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(out, c->L.lhost[k].c_rs + (size_t)claim * RSW, 4 * (size_t)RSW, hipMemcpyDeviceToHost));
       return KS_OK;
     }
   throw KsError(KS_ERR_ARG, "simulation not in this rank's launch");
@@ -1123,9 +1150,9 @@ int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, 
 int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out) {
   API_TRY
   if (!c || !out) throw KsError(KS_ERR_ARG, "bad argument");
-  for (size_t k = 0; k < c->lsims.size(); k++)
-    if (c->lsims[k] == sim) {
-      HIPCHK(hipMemcpy(out, c->lhost[k].counters, 8 * CT_NCOUNTERS, hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < c->L.lsims.size(); k++)
+    if (c->L.lsims[k] == sim) {
+      HIPCHK(hipMemcpy(out, c->L.lhost[k].counters, 8 * CT_NCOUNTERS, hipMemcpyDeviceToHost));
       return KS_OK;
     }
   throw KsError(KS_ERR_ARG, "simulation not in this rank's launch");

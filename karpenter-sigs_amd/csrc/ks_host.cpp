@@ -869,29 +869,41 @@ void Host::build(const Value& root) {
   tab.n_taint.assign((size_t)std::max(N, 1) * 2, 0);
   tab.n_flags.assign(std::max(N, 1), 0);
   tab.n_hp0.assign(std::max(N, 1), 0);
-  // --- host ports: masks over the distinct (IP, port, protocol) triples.  A node's reserved set and a
-  // pod's ports conflict iff some pair Matches (hostportusage.go:74-85); the pod-key exception of
-  // Conflicts never applies because no pod being scheduled is in a node's initial usage (checked).
-  std::set<std::string> podKeys;
-  for (auto& p : pods) podKeys.insert(p.ns + "/" + p.name);
-  auto internHP = [&](const HostPortH& h) {
+  // --- host ports: masks over a universe of (IP, port, protocol) triples (HostPort.Matches,
+  // hostportusage.go:45-58).  HostPortUsage.reserved is keyed by pod (namespace/name): Conflicts skips
+  // the entries of the pod being checked and Add replaces that pod's entries (hostportusage.go:70-85).
+  // A node's initial entries whose pod key is also a pod being scheduled (e.g. a re-created StatefulSet
+  // pod whose predecessor still holds the ports) get universe elements of their own, tagged with that
+  // key: the pod's conflict mask leaves them out, and its commit clears them (pod_hpo).
+  std::map<std::string, int> podKeyCount;
+  for (auto& p : pods) podKeyCount[p.ns + "/" + p.name]++;
+  hostPortOwner.clear();
+  auto internHP = [&](const HostPortH& h, const std::string& owner) {
     for (size_t i = 0; i < hostPortUniverse.size(); i++)
-      if (hostPortUniverse[i].ip == h.ip && hostPortUniverse[i].port == h.port && hostPortUniverse[i].proto == h.proto)
+      if (hostPortUniverse[i].ip == h.ip && hostPortUniverse[i].port == h.port && hostPortUniverse[i].proto == h.proto &&
+          hostPortOwner[i] == owner)
         return (int)i;
     hostPortUniverse.push_back(h);
+    hostPortOwner.push_back(owner);
     return (int)hostPortUniverse.size() - 1;
   };
-  for (auto& p : pods) for (auto& h : p.ports) internHP(h);
+  for (auto& p : pods) for (auto& h : p.ports) internHP(h, "");
+  std::set<std::string> ownerKeys;  // pods being scheduled with entries on some existing node
   for (auto& n : nodes)
     for (auto& e : n.hostPorts) {
-      if (podKeys.count(e.first))
-        throw KsError(-2, "pod " + e.first + " is scheduled while it holds host ports on node " + n.name);
-      internHP(e.second);
+      const bool pending = podKeyCount.count(e.first) != 0;
+      if (pending) ownerKeys.insert(e.first);
+      internHP(e.second, pending ? e.first : "");
     }
+  for (auto& p : pods) {  // Add on a NodeClaim replaces a same-key pod's entries: not modelled
+    const std::string key = p.ns + "/" + p.name;
+    if (podKeyCount[key] > 1 && (!p.ports.empty() || ownerKeys.count(key)))
+      throw KsError(-2, "pods being scheduled share the key " + key + " and host ports");
+  }
   if (hostPortUniverse.size() > 64) throw KsError(-3, "more than 64 distinct host ports");
   auto hpMask = [&](const std::vector<std::pair<std::string, HostPortH>>& v) {
     uint64_t m = 0;
-    for (auto& e : v) m |= 1ull << internHP(e.second);
+    for (auto& e : v) m |= 1ull << internHP(e.second, podKeyCount.count(e.first) ? e.first : "");
     return m;
   };
   dims.hpAny = hostPortUniverse.empty() ? 0 : 1;
@@ -1037,13 +1049,18 @@ void Host::build(const Value& root) {
   tab.pod_flags.assign(std::max(P, 1), 0);
   tab.pod_hpc.assign(std::max(P, 1), 0);
   tab.pod_hpu.assign(std::max(P, 1), 0);
+  tab.pod_hpo.assign(std::max(P, 1), 0);
   for (int i = 0; i < P; i++) {
     tab.pod_flags[i] = pods[i].provisionable ? PF_PROVISIONABLE : 0;
+    const std::string key = pods[i].ns + "/" + pods[i].name;
+    for (size_t u = 0; u < hostPortUniverse.size(); u++)
+      if (hostPortOwner[u] == key) tab.pod_hpo[i] |= 1ull << u;  // its own entries: never a conflict, replaced by Add
     for (auto& h : pods[i].ports) {
       for (size_t u = 0; u < hostPortUniverse.size(); u++) {
-        if (hostPortUniverse[u].ip == h.ip && hostPortUniverse[u].port == h.port && hostPortUniverse[u].proto == h.proto)
+        if (hostPortUniverse[u].ip == h.ip && hostPortUniverse[u].port == h.port && hostPortUniverse[u].proto == h.proto &&
+            hostPortOwner[u].empty())
           tab.pod_hpu[i] |= 1ull << u;
-        if (h.matches(hostPortUniverse[u])) tab.pod_hpc[i] |= 1ull << u;
+        if (h.matches(hostPortUniverse[u]) && hostPortOwner[u] != key) tab.pod_hpc[i] |= 1ull << u;
       }
     }
   }
@@ -1143,16 +1160,36 @@ void Host::build(const Value& root) {
   for (int64_t v : tab.pod_req) dims.negReq |= v < 0;
   for (int64_t v : tab.tpl_daemon) dims.negReq |= v < 0;
   {
+    // NewQueue: sort.Slice(pods, byCPUAndMemoryDescending) (queue.go:37-43,83-112).  Its less() is the
+    // lexicographic order of (-cpu, -memory, creationTimestamp, uid); without ties every unstable sort
+    // agrees and the device radix-sorts the keys.  With ties the order is pdqsort's swap sequence over
+    // the input order: emulate sort.Slice on the keys' dense ranks (less() is all pdqsort observes).
     std::vector<int> idx(P);
     for (int i = 0; i < P; i++) idx[i] = i;
     std::sort(idx.begin(), idx.end(), [&](int a, int b) { return sk[a] < sk[b]; });
-    for (int i = 1; i < P; i++)
-      if (sk[idx[i]] == sk[idx[i - 1]])
-        throw KsError(-2, "pods " + pods[idx[i - 1]].name + " and " + pods[idx[i]].name +
-                              " tie on (cpu, memory, creationTimestamp, uid); queue order would depend on sort.Slice tie order");
+    bool ties = false;
+    for (int i = 1; i < P && !ties; i++) ties = sk[idx[i]] == sk[idx[i - 1]];
+    hostQueue.clear();
+    if (ties) {
+      std::vector<int32_t> key(P), val(P);
+      int rank = 0;
+      for (int i = 0; i < P; i++) {
+        if (i > 0 && sk[idx[i]] != sk[idx[i - 1]]) rank++;
+        key[idx[i]] = rank;
+      }
+      for (int i = 0; i < P; i++) val[i] = i;
+      GoSortExact g{GoSort{key.data(), val.data()}};
+      g.run(P);
+      hostQueue = val;
+    }
   }
   dims.S = std::max(S, 1);
   buildTopology();
+  // Topology ownership is keyed by UID (TopologyGroup.owners, topologygroup.go; Topology.Update removes
+  // the UID from every group first, topology.go:91-122): pods sharing a UID share their groups, which
+  // the per-pod relaxation states here do not model.
+  if (dims.dupUids && !groups.empty())
+    throw KsError(-2, "pods sharing a UID own topology groups (TopologyGroup owners are keyed by UID)");
   tab.st_rs.assign((size_t)dims.S * dims.RSW, 0);
   tab.st_tol.assign((size_t)dims.S * 2, 0);
   tab.st_flags.assign(dims.S, 0);

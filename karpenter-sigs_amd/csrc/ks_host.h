@@ -93,6 +93,7 @@ struct TopoGroup {
   bool filterNil = true;
   std::vector<std::vector<uint32_t>> filter;  // OR of requirement records (TopologyNodeFilter)
   std::map<std::string, int32_t> domains;    // registered domain -> count (initial state)
+  bool late = false;  // created by a relaxed state's Topology.Update mid-Solve (topology.go:102-119)
 };
 
 struct Host {
@@ -115,6 +116,7 @@ struct Host {
   // taints
   std::vector<TaintH> taints;
   std::vector<HostPortH> hostPortUniverse;  // distinct (IP, port, protocol), bit i of the host-port masks
+  std::vector<std::string> hostPortOwner;   // per element: "" or the key of the pod being scheduled whose initial entry it is
   std::map<std::string, std::string> volumeDrivers;  // "ns/pvc" -> resolved CSI driver (resolveDriver, volumeusage.go:115-172)
   std::vector<std::string> volDrivers, volUniverse;  // limited drivers; the pending pods' PVC keys (bit i)
   // instance types
@@ -165,6 +167,11 @@ struct Host {
   std::set<int> topoHostActive;                                         // hostname value ids of the nodes (Register)
   bool activeHost(int v) const { return topoHostActive.count(v) != 0; }
   int64_t hostnameSeed = 0;
+  // NewQueue order computed on the host (set only when some pods tie on the whole sort key, i.e. share
+  // cpu, memory, creation time and UID, as the benchmark's un-applied pods do): sort.Slice's order of
+  // tied pods is its swap sequence over the input order (ks_gosort.h), not a key order the radix sort
+  // on the device can reproduce.
+  std::vector<int32_t> hostQueue;
   bool emptyTopology = false;  // the benchmark's &scheduling.Topology{}: no groups (scheduling_benchmark_test.go:124)
   KsDims dims{};
 
@@ -173,7 +180,7 @@ struct Host {
     std::vector<int64_t> tsort_alloc, it_alloc, it_cap, tpl_daemon, pool_rem0, pod_req, pod_sortkey, n_avail, n_req0;
     std::vector<double> off_price;
     std::vector<int32_t> n_flags, pod_flags;
-    std::vector<uint64_t> pod_hpc, pod_hpu, n_hp0;
+    std::vector<uint64_t> pod_hpc, pod_hpu, pod_hpo, n_hp0;
     std::vector<uint64_t> pod_vm, vol_dm, n_vm0;  // volume limits (volumeusage.go:183-227)
     std::vector<int32_t> n_vc0, n_vlim;
     // topology groups (ks_topo.cpp)

@@ -68,6 +68,8 @@ struct KsDims {
   int32_t FSW;             // fail_rs words per (pod, template): RSW, or counts + registered bits if larger
   int32_t volAny;          // some pending pod mounts a PVC of a driver an existing node limits
   int32_t VD;              // limited drivers (<= kMaxVD); vol_dm[VD] partitions the pods' PVC universe
+  int32_t tgUnlab;         // some existing node lacks the label of a topology group's key (k_solve node_slow)
+  uint64_t tgLate;         // groups a relaxed state creates mid-Solve: inactive until that relaxation
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
@@ -126,6 +128,7 @@ struct KsDev {
   const double KS_G* off_price;    // available offerings' prices (worstLaunchPrice, helpers.go:235-258)
   const uint64_t KS_G* pod_hpc;    // [P] host-port triples a pod's ports Match (conflict mask)
   const uint64_t KS_G* pod_hpu;    // [P] host-port triples a pod reserves
+  const uint64_t KS_G* pod_hpo;    // [P] elements of the pod's own initial entries on existing nodes
   const uint64_t KS_G* n_hp0;      // [N] host-port triples reserved on an existing node
   // volume limits (volumeusage.go:183-227): the pending pods' PVCs of limited drivers are a <=64-bit
   // universe; a node's usage per driver is a count (all its PVCs) plus the universe bits it mounts

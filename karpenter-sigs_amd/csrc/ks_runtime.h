@@ -12,7 +12,7 @@
 namespace ks {
 hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
-                        hipEvent_t mid);
+                        hipEvent_t mid, const int32_t* fixed_order = nullptr);
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st);
 Plan make_plan(const KsDims& d, size_t budget, bool sim = false, bool wideKO = false);
 size_t queue_sort_temp_bytes(int n);
@@ -60,16 +60,42 @@ struct ks_problem {
   int32_t* svals = nullptr;
   void* stemp = nullptr;
   size_t stempBytes = 0;
+  int32_t* hqorder = nullptr;  // [P] NewQueue order from the host (Host::hostQueue), when pods tie
   ~ks_problem() {
+    int prev = -1;
+    if (device >= 0 && hipGetDevice(&prev) == hipSuccess && prev != device) (void)hipSetDevice(device);
     if (skeys) (void)hipFree(skeys);
     if (svals) (void)hipFree(svals);
     if (stemp) (void)hipFree(stemp);
+    if (hqorder) (void)hipFree(hqorder);
     if (dbuf) (void)hipFree(dbuf);
     if (wbuf) (void)hipFree(wbuf);
     if (works_dev) (void)hipFree(works_dev);
     if (stream) (void)hipStreamDestroy(stream);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
   }
 };
+
+namespace ks {
+// One C-ABI call on a handle: its buffers and stream live on the device it was created on, so that
+// device is made current for the call (an opts->device naming another one is an argument error) and
+// the caller's current device is restored afterwards.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard(int dev, const ks_solve_opts* opts) {
+    if (opts && opts->device >= 0 && opts->device != dev)
+      throw KsError(KS_ERR_ARG, "opts->device " + std::to_string(opts->device) + " is not the device the handle was created on (" +
+                                    std::to_string(dev) + ")");
+    HIPCHK(hipGetDevice(&prev));
+    if (prev != dev) HIPCHK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+}  // namespace ks
 
 // Upload the host tables to one HBM allocation and point pb->dev at them.
 void ks_upload(ks_problem* pb);

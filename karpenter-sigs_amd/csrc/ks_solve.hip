@@ -129,7 +129,7 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 template <int RT>
 struct Window {
   int p, g, uid, s, flags, toltpl, pf, st;
-  uint64_t ll, tol0, tol1, hpc, hpu, vm;
+  uint64_t ll, tol0, tol1, hpc, hpu, hpo, vm;
   int64_t req[RT > 0 ? RT : kMaxR];
 };
 
@@ -177,8 +177,10 @@ struct Solver {
   uint64_t t_inv = 0;   // inverse groups the popped pod owns
   int t_s = 0;          // the popped pod's relaxation state
   bool t_nonode = false;  // some matching group admits no domain at all: no existing node can pass
+  uint64_t t_active = ~0ull;  // groups in t.topologies so far (late groups join at their relaxation)
   int64_t algbytes = 0;
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
+  uint64_t cur_hpo = 0;               // its own initial entries on existing nodes (HostPortUsage.Add replaces them)
   uint64_t cur_vm = 0;                // the popped pod's PVCs of limited drivers (Solve only; SIM refuses them)
 
   __device__ Solver(const KsDev& D_, const KsWork& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
@@ -294,9 +296,11 @@ struct Solver {
   // Existing-node check for two nodes per lane (positions n and n + 64 of the first-fit order):
   // every load of both is issued before any test, so a 128-node step of the scan costs one memory
   // round trip.  Out-of-range positions are clamped for the loads and masked.  nf: NodeFlag bits.
+  // sl0 / sl1: the node passed every check but lacks the label of a matching group's key, so only the
+  // wave-cooperative node_slow can decide it (ok is false then).
   __device__ __forceinline__ void node_ok2(int n0, int s, int sflags, const int64_t* pod, uint64_t tol0,
                                            uint64_t tol1, bool& ok0, bool& ok1, int& nf0, int& nf1,
-                                           int64_t* q0, int64_t* q1) const {
+                                           int64_t* q0, int64_t* q1, bool& sl0, bool& sl1) const {
     const int n1 = n0 + kWave;
     const int c0 = n0 < d.N ? n0 : d.N - 1, c1 = n1 < d.N ? n1 : d.N - 1;
     const bool own0 = !SIM || tbit(s_tch, c0), own1 = !SIM || tbit(s_tch, c1);
@@ -343,9 +347,18 @@ struct Solver {
       if (ok0) ok0 = rs_compatible(L, node_rs(c0), D.st_rs + (int64_t)s * d.RSW, 0);
       if (ok1) ok1 = rs_compatible(L, node_rs(c1), D.st_rs + (int64_t)s * d.RSW, 0);
     }
+    sl0 = sl1 = false;
     if (TOPO && t_mask) {  // topology (existingnode.go:106-114)
-      if (ok0) ok0 = topo_node_ok(c0);
-      if (ok1) ok1 = topo_node_ok(c1);
+      if (ok0) {
+        const int t = topo_node_state(c0);
+        ok0 = t == 1;
+        sl0 = t == 2;
+      }
+      if (ok1) {
+        const int t = topo_node_state(c1);
+        ok1 = t == 1;
+        sl1 = t == 2;
+      }
     }
   }
   __device__ __forceinline__ const uint32_t KS_G* node_rs(int n) const {
@@ -355,7 +368,7 @@ struct Solver {
   // Solve: commit of a pod to node j by its owner lane.
   __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod) {
     for (int r = 0; r < R(); r++) W.n_req[(int64_t)j * R() + r] += pod[r];
-    if (d.hpAny) W.n_hp[j] |= cur_hpu;
+    if (d.hpAny) W.n_hp[j] = (W.n_hp[j] & ~cur_hpo) | cur_hpu;  // HostPortUsage.Add (hostportusage.go:70-72)
     if (d.volAny && cur_vm) vol_commit(j);
     if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
   }
@@ -376,7 +389,7 @@ struct Solver {
         if (RT == 0 && r >= d.R) break;
         W.n_req[(int64_t)j * R() + r] = q[r] + pod[r];
       }
-      if (d.hpAny) W.n_hp[j] = (fresh ? D.n_hp0[j] : W.n_hp[j]) | cur_hpu;
+      if (d.hpAny) W.n_hp[j] = ((fresh ? D.n_hp0[j] : W.n_hp[j]) & ~cur_hpo) | cur_hpu;
       if (d.volAny && cur_vm) vol_commit(j);
       if (fresh) s_tch[j >> 5] |= 1u << (j & 31);
     }
@@ -484,29 +497,75 @@ struct Solver {
   }
   // ExistingNode.Add's topology step for node n (one lane): the node's single domain of each
   // matching group must be the one TopologyGroup.Get returns (existingnode.go:106-114).
-  __device__ __forceinline__ bool topo_node_ok(int n) const {
+  // Returns 0 (fails), 1 (passes) or 2 (every labelled group passes, but the node lacks the label of
+  // some group's key: its domain then comes from the requirements it accumulated, node_slow decides).
+  __device__ __forceinline__ int topo_node_state(int n) const {
+    int st = 1;
     for (uint64_t m = t_mask; m; m &= m - 1) {
       const int g = ctz64(m);
       const int v = D.n_tdom[(int64_t)g * d.N + n];
-      if (v < 0) return false;
+      if (v < 0) {
+        st = 2;
+        continue;
+      }
       const int c = tcnt(g, v);
-      if (c < 0) return false;  // unregistered: Get never returns it
+      if (c < 0) return 0;  // unregistered: Get never returns it
       const int type = tg(g, TGM_TYPE);
       if (type == TG_SPREAD) {
         const int self = (int)((t_sel >> g) & 1ull);
-        if ((int64_t)c + self - s_tmin[g] > tg(g, TGM_SKEW)) return false;
+        if ((int64_t)c + self - s_tmin[g] > tg(g, TGM_SKEW)) return 0;
       } else if (type == TG_AFFINITY) {  // a selected pod's domain, or the bootstrap for a self-selecting pod
-        if (!tpod_has(g, v)) return false;
-        if (s_tmin[g] ? c == 0 : !((t_sel >> g) & 1ull)) return false;
+        if (!tpod_has(g, v)) return 0;
+        if (s_tmin[g] ? c == 0 : !((t_sel >> g) & 1ull)) return 0;
       } else if (c != 0 || !tpod_has(g, v)) {
-        return false;
+        return 0;
       }
     }
-    return true;
+    return st;
+  }
+  // ExistingNode.Add's requirement and topology steps for node j, wave-wide, for a node lacking the
+  // label of a matching group's key (existingnode.go:91-115): nodeRequirements = the node's requirements
+  // + the pod's, then AddRequirements picks the domains over nodeRequirements.Get(key) exactly as for a
+  // NodeClaim (a missing key reads as Exists, a pod's NotIn leaves the complement), and the strict
+  // Compatible decides.  The other checks already passed.  On success s_rs holds the node's new
+  // requirements (the pod's and the topology's added).
+  __device__ __forceinline__ bool node_slow(int j, int s, int sflags) {
+    wsync();
+    copy_words(s_rs, node_rs(j), d.RSW);
+    wsync();
+    if ((sflags & SF_HAS_KEYS) && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
+    wsync();
+    return topo_apply(s_rs, -1, 0) == 0;
+  }
+  // The node's requirements after a node_slow commit (n.requirements = nodeRequirements): s_rs.
+  // SIM: into the node's copy-on-write slot.
+  __device__ __forceinline__ void node_store_rs(int j, int& nrs) {
+    wsync();
+    if (!SIM) {
+      copy_words(W.n_rs + (int64_t)j * d.RSW, s_rs, d.RSW);
+    } else {
+      const int owner = j & (kWave - 1);
+      const bool rsfresh = !tbit(s_tchr, j);
+      int slot;
+      if (rsfresh) {
+        slot = nrs++;
+      } else {
+        int v = 0;
+        if (lane() == owner) v = W.n_slot[j];
+        slot = rdl(v, owner);
+      }
+      copy_words(W.n_rs + (int64_t)slot * d.RSW, s_rs, d.RSW);
+      if (lane() == owner && rsfresh) W.n_slot[j] = slot;
+      if (lane() == 0) s_tchr[j >> 5] |= 1u << (j & 31);
+    }
+    hbm_release();
+    wsync();
   }
   // Topology.AddRequirements + Compatible on a NodeClaim's candidate record `rs` (LDS), wave-wide.
   // Returns 0, FC_TOPO | group << 16, or FC_TOPO_COMPAT; on success rs holds the final requirements.
-  __device__ __forceinline__ uint32_t topo_apply(LU32 rs, int claim) {
+  // claim < 0: an existing node's record (node_slow; no hostname placeholder); allow: the final
+  // Compatible's AllowUndefined keys (NodeClaim: well-known labels, nodeclaim.go:96; node: none).
+  __device__ __forceinline__ uint32_t topo_apply(LU32 rs, int claim, uint64_t allow) {
     copy_words(s_trs0, rs, d.RSW);
     wsync();
     for (uint64_t m = t_mask; m; m &= m - 1) {
@@ -514,7 +573,7 @@ struct Solver {
       const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
       const bool host = tg(g, TGM_HOST) != 0;
       const KeyMeta km = L.keys[k];
-      const int nslot = nv + (host ? 1 : 0);  // + the claim's own hostname-placeholder (private bit)
+      const int nslot = nv + (host && claim >= 0 ? 1 : 0);  // + the claim's own hostname-placeholder (private bit)
       for (int i = lane(); i < d.RSW; i += kWave) s_trs1[i] = 0;
       wsync();
       if (tg(g, TGM_TYPE) == TG_SPREAD) {  // nextDomainTopologySpread: smallest count, then smallest name
@@ -552,7 +611,7 @@ struct Solver {
           // placeholder is its only node domain, and any other insert drops out in Add)
           uint32_t z1 = ~0u, z2 = ~0u;
           for (int v = lane(); v < nslot; v += kWave) {
-            const int c = v < nv ? tcnt(g, v) : 0;
+            const int c = v < nv ? tcnt(g, v) : tccnt(g, claim);  // a placeholder: -1 if not registered
             if (c < 0 || !tpod_has(g, v)) continue;
             if (v < nv) z2 = (uint32_t)v < z2 ? (uint32_t)v : z2;
             if (rs_member(L, s_trs0, k, v)) z1 = (uint32_t)v < z1 ? (uint32_t)v : z1;
@@ -599,7 +658,7 @@ struct Solver {
     }
     // Compatible(nodeRequirements, topologyRequirements, AllowUndefinedWellKnownLabels)
     int ok = 1;
-    if (lane() == 0) ok = rs_compatible(L, s_trs0, rs, d.allowWK) ? 1 : 0;
+    if (lane() == 0) ok = rs_compatible(L, s_trs0, rs, allow) ? 1 : 0;
     ok = rdl(ok, 0);
     return ok ? 0u : (uint32_t)FC_TOPO_COMPAT;
   }
@@ -614,7 +673,7 @@ struct Solver {
     hbm_release();
     const uint64_t owned = d.G1 >= 64 ? ~0ull : ((1ull << d.G1) - 1);
     const uint64_t pres = rs_present(F), compl_ = rs_compl(F);
-    for (uint64_t m = (t_sel & owned) | t_inv; m; m &= m - 1) {
+    for (uint64_t m = (t_sel & owned & t_active) | t_inv; m; m &= m - 1) {
       const int g = ctz64(m);
       const bool ownedGroup = g < d.G1;
       if (ownedGroup && tg(g, TGM_TYPE) == TG_SPREAD && tg(g, TGM_FEND) > tg(g, TGM_FBEG)) {  // nodeFilter
@@ -649,11 +708,11 @@ struct Solver {
           const int v = w * 32 + __builtin_ctz(x);
           x &= x - 1;
           if (v >= nv) {
-            if (claim >= 0) {
+            if (claim >= 0) {  // -1: not registered in a late group (recording registers it)
               const int64_t at = (int64_t)g * W.ccs + claim;
               const int cc = W.tg_ccnt[at];
-              W.tg_ccnt[at] = cc + 1;
-              if (cc == 0) W.tg_cpos[g] += 1;  // one more placeholder holding a counted pod
+              W.tg_ccnt[at] = cc < 0 ? 1 : cc + 1;
+              if (cc <= 0) W.tg_cpos[g] += 1;  // one more placeholder holding a counted pod
             }
           } else {
             const int c = W.tg_cnt[tg(g, TGM_CNT) + v];
@@ -661,6 +720,18 @@ struct Solver {
           }
         }
       }
+    }
+    hbm_release();
+    wsync();
+  }
+
+  // Topology.Update creating the late groups `m` (topology.go:102-119), wave-wide: the NodeClaims made so
+  // far registered their placeholders before these groups existed (NewNodeClaim's Register only reaches
+  // t.topologies), so their placeholder domains start unregistered.
+  __device__ __forceinline__ void topo_activate(uint64_t m, int nclaims) {
+    for (; m; m &= m - 1) {
+      const int g = ctz64(m);
+      for (int c = lane(); c < nclaims; c += kWave) W.tg_ccnt[(int64_t)g * W.ccs + c] = -1;
     }
     hbm_release();
     wsync();
@@ -694,7 +765,7 @@ struct Solver {
       wsync();
       if ((sflags & SF_HAS_KEYS) && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
       wsync();
-      if (TOPO && t_mask && topo_apply(s_rs, c) != 0) {  // topology requirements (nodeclaim.go:92-100)
+      if (TOPO && t_mask && topo_apply(s_rs, c, d.allowWK) != 0) {  // topology requirements (nodeclaim.go:92-100)
         ncnt = 0;
         return false;
       }
@@ -871,7 +942,7 @@ struct Solver {
             wsync();
           }
           if (TOPO && ok && t_mask) {  // topology requirements of the fresh NodeClaim (nodeclaim.go:92-100)
-            const uint32_t tc = topo_apply(s_rs, nclaims);
+            const uint32_t tc = topo_apply(s_rs, nclaims, d.allowWK);
             if (tc) {
               ok = false;
               code = tc;
@@ -1254,6 +1325,7 @@ struct Solver {
       w.tol1 = D.st_tol[2 * w.s + 1];
       w.hpc = D.pod_hpc[w.g];
       w.hpu = D.pod_hpu[w.g];
+      w.hpo = D.pod_hpo[w.g];
       w.vm = D.pod_vm[w.g];
 #pragma unroll
       for (int r = 0; r < RM; r++) {
@@ -1272,6 +1344,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const KsWork W = works[blockIdx.x];
   const KsDims d = D.d;
   Solver<RT, TL, SIM, TOPO> S(D, W, pl);
+  if (TOPO) S.t_active = ~d.tgLate;
   const int R = S.R();
   char KS_L* sp = smem;
   auto take = [&](size_t bytes) { char KS_L* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
@@ -1451,6 +1524,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (d.hpAny) {
       S.cur_hpc = (uint64_t)rdl64((int64_t)w.hpc, wi);
       S.cur_hpu = (uint64_t)rdl64((int64_t)w.hpu, wi);
+      S.cur_hpo = (uint64_t)rdl64((int64_t)w.hpo, wi);
     }
     if (d.volAny) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
     if (TOPO) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
@@ -1464,10 +1538,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     bool placed = false;
     // 1) existing nodes in order (none can pass when a matching group admits no domain)
     PH_BEGIN(t1);
-    const bool skipNodes = TOPO && S.t_nonode;
+    // (unlabelled nodes choose their domain from their requirements: no shortcut then)
+    const bool skipNodes = TOPO && S.t_nonode && !d.tgUnlab;
     int scanFrom = 0;
     if constexpr (NW > 0) {
-      if (d.N > 0 && !skipNodes) {
+      // (problems with unlabelled nodes scan every node through node_ok2, which handles them)
+      if (d.N > 0 && !skipNodes && !(TOPO && d.tgUnlab)) {
         int kj = -1;
         uint64_t mj = 0;
         asm volatile("; KS_MARK window_begin");
@@ -1481,7 +1557,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           ok &= (whp[k] & S.cur_hpc) == 0;
           if (d.volAny && S.cur_vm && ok) ok = S.vol_ok(n);
           if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), D.st_rs + (int64_t)s * d.RSW, 0);
-          if (TOPO && S.t_mask && ok) ok = S.topo_node_ok(n);
+          if (TOPO && S.t_mask && ok) ok = S.topo_node_state(n) == 1;  // every node is labelled here
           const uint64_t m = wballot(ok);
           if (m) {
             kj = k;
@@ -1500,7 +1576,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
               if (lane() == owner) {
 #pragma unroll
                 for (int r = 0; r < RM; r++) wrq[k][r] += pod[r];
-                whp[k] |= S.cur_hpu;
+                whp[k] = (whp[k] & ~S.cur_hpo) | S.cur_hpu;
                 if (d.volAny && S.cur_vm) S.vol_commit(j);
               }
             }
@@ -1523,26 +1599,51 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
     for (int base = skipNodes ? d.N : scanFrom; base < d.N && !placed; base += 2 * kWave) {
-      bool ok0, ok1;
+      bool ok0, ok1, sl0, sl1;
       int nf0, nf1;
       int64_t q0[RM], q1[RM];
-      S.node_ok2(base + lane(), s, sflags, pod, tol0, tol1, ok0, ok1, nf0, nf1, q0, q1);
-      const uint64_t m0 = wballot(ok0), m1 = wballot(ok1);
-      if (m0 | m1) {
-        const int j = m0 ? base + ctz64(m0) : base + kWave + ctz64(m1);
+      S.node_ok2(base + lane(), s, sflags, pod, tol0, tol1, ok0, ok1, nf0, nf1, q0, q1, sl0, sl1);
+      uint64_t m0 = wballot(ok0), m1 = wballot(ok1);
+      int j = -1;
+      bool slowj = false;
+      if (m0 | m1) j = m0 ? base + ctz64(m0) : base + kWave + ctz64(m1);
+      if (TOPO && d.tgUnlab) {  // unlabelled nodes before the first fast fit are decided wave-wide, in order
+        uint64_t s0 = wballot(sl0), s1 = wballot(sl1);
+        for (int half = 0; half < 2 && !slowj; half++) {
+          uint64_t sm = half ? s1 : s0;
+          const uint64_t fm = half ? m1 : m0;
+          if (fm) sm &= (fm & (~fm + 1)) - 1;  // only those before the half's first fast fit
+          for (; sm && !slowj; sm &= sm - 1) {
+            const int jj = base + half * kWave + ctz64(sm);
+            if (S.node_slow(jj, s, sflags)) {
+              j = jj;
+              slowj = true;
+            }
+          }
+          if (fm) break;
+        }
+      }
+      if (j >= 0) {
+        const bool hi = j - base >= kWave;
         S.algbytes += (int64_t)(j - base + 1) * (16 * R + 16);
         PH_BEGIN(t7);
+        const int fl = slowj ? (sflags & ~SF_HAS_KEYS) : sflags;  // node_slow's record replaces rs_add
         if constexpr (SIM) {
           int64_t qs[RM];
 #pragma unroll
-          for (int r = 0; r < RM; r++) qs[r] = m0 ? q0[r] : q1[r];
-          S.sim_node_commit(j, s, sflags, pod, qs, nrs, false);
-          const int nf = rdl(m0 ? nf0 : nf1, j & (kWave - 1));
+          for (int r = 0; r < RM; r++) qs[r] = hi ? q1[r] : q0[r];
+          S.sim_node_commit(j, s, fl, pod, qs, nrs, false);
+          const int nf = rdl(hi ? nf1 : nf0, j & (kWave - 1));
           if ((nf & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
         } else if (lane() == (j & (kWave - 1))) {
-          S.node_commit(j, s, sflags, pod);  // the owner lane of node j
+          S.node_commit(j, s, fl, pod);  // the owner lane of node j
         }
-        if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, j, 0);  // existingnode.go:121
+        if (TOPO && slowj) {
+          S.node_store_rs(j, nrs);
+          if (S.t_sel | S.t_inv) S.topo_record(S.s_rs, -1, -1, 0);  // existingnode.go:121
+        } else if (TOPO && (S.t_sel | S.t_inv)) {
+          S.topo_record(S.node_rs(j), -1, j, 0);  // existingnode.go:121
+        }
         S.log_commit(p, -(j + 1), nlog);
         PH_END(t7, 7);
         placed = true;
@@ -1621,6 +1722,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       if (relaxed) W.pod_state[p] = s + 1;
     }
     if (relaxed) epoch++;
+    if (TOPO && relaxed && d.tgLate) {  // Topology.Update (scheduler.go:160-170): groups the new state creates
+      const uint64_t fresh = D.st_gown[s + 1] & ~S.t_active;
+      if (fresh) {
+        S.topo_activate(fresh, nclaims);
+        S.t_active |= fresh;
+      }
+    }
     int tail = qhead + qlen;
     if (tail >= P) tail -= P;
     if (lane() == 0) W.queue[tail] = p;
@@ -1743,13 +1851,17 @@ hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp,
 // One ks_solve: queue sort -> workspace init -> [mid event] -> k_solve (all on one stream).
 // Topology problems get their own instantiation: the group state would otherwise occupy SGPRs (and
 // their spills) across the whole commit loop of every topology-free Solve.
+// fixed_order: NewQueue's order computed on the host (pods tying on the whole sort key), no radix sort.
 hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
-                        hipEvent_t mid) {
+                        hipEvent_t mid, const int32_t* fixed_order) {
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
-  hipError_t e = queue_sort(D, skeys, svals, stemp, stempBytes, qorder, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep, (const int32_t*)qorder);
+  if (!fixed_order) {
+    hipError_t e = queue_sort(D, skeys, svals, stemp, stempBytes, qorder, st);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep,
+                     fixed_order ? fixed_order : (const int32_t*)qorder);
   if (mid) (void)hipEventRecord(mid, st);
   return (D.d.G ? launch_solve_topo : launch_solve_plain)(D, works_dev, nrep, pl, st);
 }

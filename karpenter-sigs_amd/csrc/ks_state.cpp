@@ -260,6 +260,15 @@ std::string cluster_state_json(const Value& root) {
       o += ":";
       ksjson::quote(o, kv.second);
     }
+    o += "},\"annotations\":{";  // StateNode.Annotations() (statenode.go:148-161): the same object as Labels()
+    first = true;
+    for (auto& kv : smap(path(e.face(), {"metadata", "annotations"}))) {
+      if (!first) o += ",";
+      first = false;
+      ksjson::quote(o, kv.first);
+      o += ":";
+      ksjson::quote(o, kv.second);
+    }
     o += "},\"taints\":[";
     first = true;
     for (auto& t : e.taintList()) {

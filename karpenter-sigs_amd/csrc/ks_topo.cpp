@@ -10,9 +10,13 @@
 //   registration        NewExistingNode registers every node's hostname (existingnode.go:60)
 //
 // Device view: groups [0, G1) are t.topologies in creation order, [G1, G) t.inverseTopologies; the
-// kernels iterate them in that order.  Every relaxation state of a pod must own a subset of the
-// groups the initial Update pass created: a group created later (a relaxed required node-affinity
-// term changes a spread group's node filter) would start counting mid-Solve, which is refused.
+// kernels iterate them in that order.  A relaxed state whose groups the initial Update pass did not
+// create (a dropped required node-affinity term changes a spread group's node filter, so its hash)
+// makes Topology.Update create them mid-Solve (topology.go:102-119): countDomains over the cluster's
+// bound pods, the universe domains, and no hostname Register of the existing nodes or of the
+// NodeClaims made so far.  Those "late" groups are built here too, after the initial ones (in pod and
+// relaxation order), and k_solve activates each one at the relaxation that creates it: before that
+// it records nothing, and NodeClaims created before it are not registered in it.
 // namespaceSelector terms resolve against the snapshot's namespace list ("namespaces").
 #include <algorithm>
 #include <climits>
@@ -277,8 +281,7 @@ void Host::buildTopology() {
     }
     states[(size_t)p][0].gown = gown;
   }
-  if (own.size() + inv.size() > 64) throw KsError(-3, "more than 64 topology groups");
-  const int G1 = (int)own.size(), G = G1 + (int)inv.size();
+  uint64_t late = 0;
   for (int p = 0; p < P; p++)
     for (size_t k = 1; k < states[(size_t)p].size(); k++) {
       PodState& st = states[(size_t)p][k];
@@ -286,18 +289,30 @@ void Host::buildTopology() {
       uint64_t gown = 0;
       for (auto& g : ownedSpecGroups(*st.spec)) {
         auto it = ownByHash.find(g.hash);
-        if (it == ownByHash.end())
-          throw KsError(-2, "pod " + pods[(size_t)p].ns + "/" + pods[(size_t)p].name +
-                                ": a relaxed state creates a new topology group mid-Solve (not encoded by this build)");
-        gown |= 1ull << it->second;
+        int idx;
+        if (it == ownByHash.end()) {  // created by this relaxation's Update (topology.go:102-119)
+          idx = (int)own.size();
+          if (idx >= 64) throw KsError(-3, "more than 64 topology groups");
+          countDomains(g, idx);
+          g.late = true;
+          ownByHash[g.hash] = idx;
+          own.push_back(g);
+          late |= 1ull << idx;
+        } else {
+          idx = it->second;
+        }
+        gown |= 1ull << idx;
       }
       st.gown = gown;
     }
+  if (own.size() + inv.size() > 64) throw KsError(-3, "more than 64 topology groups");
+  const int G1 = (int)own.size(), G = G1 + (int)inv.size();
+  dims.tgLate = late;
   groups = own;
   groups.insert(groups.end(), inv.begin(), inv.end());
   groupsOwned = G1;
   for (auto& g : groups)  // NewExistingNode registers every node's hostname (existingnode.go:60)
-    if (g.key == kHostnameKey)
+    if (g.key == kHostnameKey && !g.late)  // in the groups that exist by then
       for (auto& n : nodes) g.domains.emplace(n.hostName, 0);
   for (int p = 0; p < P; p++) {
     tab.pod_ginv[(size_t)p] = invOwned[(size_t)p] << G1;
@@ -355,19 +370,9 @@ void Host::buildTopology() {
     }
   // A node without a group's label takes that key only from a pod's NotIn requirement
   // (existingnode.go:97-115: the strict Compatible admits nothing else), after which the topology
-  // domain would be chosen like a NodeClaim's.  The kernel treats an unlabelled node as failing the
-  // group; refuse the one input where that differs.
-  for (int g = 0; g < G; g++) {
-    const int k = groups[(size_t)g].keyId;
-    bool unlabelled = false;
-    for (int n = 0; n < N && !unlabelled; n++) unlabelled = tab.n_tdom[(size_t)g * N + n] < 0;
-    if (!unlabelled) continue;
-    for (auto& chain : states)
-      for (auto& st : chain)
-        if (bit(rs_present(st.rsAll.data()), k) && bit(rs_compl(st.rsAll.data()), k))
-          throw KsError(-2, "topology key " + groups[(size_t)g].key +
-                                                " is missing on an existing node while a pod constrains it with NotIn");
-  }
+  // domain is chosen like a NodeClaim's; k_solve decides such nodes wave-wide (node_slow).
+  dims.tgUnlab = 0;
+  for (size_t i = 0; i < tab.n_tdom.size() && G > 0 && N > 0; i++) dims.tgUnlab |= tab.n_tdom[i] < 0;
   if (topoExcluded) {  // the consolidation view: what each simulation's exclusions take away
     for (auto& kv : contrib)
       for (auto& gd : kv.second) {

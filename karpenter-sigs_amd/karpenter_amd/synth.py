@@ -152,9 +152,12 @@ def make_diverse_pods(count, rng):
     return out
 
 
-def benchmark_snapshot(n_pods, n_its=400, seed=42, diverse=True):
+def benchmark_snapshot(n_pods, n_its=400, seed=42, diverse=True, literal=False):
     """BenchmarkScheduling (scheduling_benchmark_test.go:116-182): one template from test.NodePool(),
-    no NodePools (so no limits), empty Topology, fake.InstanceTypes(n_its)."""
+    no NodePools (so no limits), empty Topology, fake.InstanceTypes(n_its).
+    literal: the benchmark's pods exactly as test.Pod() builds them without an apiserver: no UID and a
+    zero CreationTimestamp (pkg/test/pods.go, metadata.go), so NewQueue breaks cpu/memory ties with
+    sort.Slice's tie order and every pod shares the staleness key "" (queue.go:38,54-69)."""
     rng = np.random.default_rng(seed)
     its = fake_instance_types(n_its)
     np_obj = node_pool("default-pool")
@@ -165,6 +168,9 @@ def benchmark_snapshot(n_pods, n_its=400, seed=42, diverse=True):
         for i in range(n_pods):
             pods.append(pod(i, cpu=CPU_CHOICES[rng.integers(5)], mem=MEM_CHOICES[rng.integers(6)],
                             labels={"my-label": LABEL_VALUES[rng.integers(7)]}))
+    if literal:
+        for p in pods:
+            p["metadata"].pop("uid", None)
     return {
         "wellKnownLabels": FAKE_WELL_KNOWN,
         "instanceTypes": its,
@@ -178,9 +184,10 @@ def benchmark_snapshot(n_pods, n_its=400, seed=42, diverse=True):
     }
 
 
-def config1(seed=42):
-    """C1: BenchmarkScheduling2000 — makeDiversePods(2000) x fake.InstanceTypes(400)."""
-    return benchmark_snapshot(2000, 400, seed, diverse=True)
+def config1(seed=42, literal=False):
+    """C1: BenchmarkScheduling2000 — makeDiversePods(2000) x fake.InstanceTypes(400).
+    literal=True: the benchmark's own pods (empty UIDs, zero timestamps)."""
+    return benchmark_snapshot(2000, 400, seed, diverse=True, literal=literal)
 
 
 def config2(n_pods=50000, seed=42):

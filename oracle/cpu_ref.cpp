@@ -1700,7 +1700,7 @@ int oref_time_cons_sims(const char* snapshot, int count, int threads, double* se
   try {
     ojson::Value root = ojson::parse(snapshot);
     oref::ConsProblem cp = oref::parseConsProblem(root);
-    const int n = std::min<int>(count, (int)cp.candidates.size());
+    const int n = std::min<int>(count, cp.nPass);
     const int nt = std::max(1, std::min(threads, n));
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;

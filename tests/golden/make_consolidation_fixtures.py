@@ -57,9 +57,10 @@ def od_sorted(its):
     return sorted(ods, key=cheapest_price)
 
 
-def nodepool(requirements=None):
+def nodepool(requirements=None, disruption=None):
     np_ = synth.node_pool("default", requirements=requirements)
     np_["spec"]["disruption"] = {"consolidationPolicy": "WhenUnderutilized", "expireAfter": "720h"}
+    np_["spec"]["disruption"].update(disruption or {})
     return np_
 
 
@@ -76,8 +77,8 @@ def rs_pod(i, cpu=None, bound_to=None, annotations=None, pending=False):
     return p
 
 
-def node(name, it, alloc, pods, initialized=True):
-    """test.NodeClaimAndNode with the NodeClaim's labels and Status.Allocatable."""
+def node(name, it, alloc, pods, initialized=True, annotations=None):
+    """test.NodeClaimAndNode with the NodeClaim's labels, annotations and Status.Allocatable."""
     off = it["offerings"][0]
     labels = {synth.NODEPOOL: "default", synth.IT_LABEL: it["name"], synth.CT: off["capacityType"],
               synth.ZONE: off["zone"], synth.HOSTNAME: name}
@@ -92,13 +93,16 @@ def node(name, it, alloc, pods, initialized=True):
                 used_m += int(float(c) * 1000) if not c.endswith("m") else int(c[:-1])
         total_m = int(float(alloc["cpu"]) * 1000)
         avail["cpu"] = "%dm" % (total_m - used_m)
-    return {"name": name, "hostName": name, "labels": labels, "taints": [], "capacity": dict(alloc),
-            "available": avail, "daemonSetRequests": {}, "initialized": initialized, "ready": initialized,
-            "creationTimestamp": synth._fmt_time(NOW - 600), "pods": pods}
+    out = {"name": name, "hostName": name, "labels": labels, "taints": [], "capacity": dict(alloc),
+           "available": avail, "daemonSetRequests": {}, "initialized": initialized, "ready": initialized,
+           "creationTimestamp": synth._fmt_time(NOW - 600), "pods": pods}
+    if annotations:  # NodeClaimLinkedNode copies the NodeClaim's annotations (pkg/test/nodes.go:70-84)
+        out["annotations"] = dict(annotations)
+    return out
 
 
-def snapshot(its, nodes, pending=(), requirements=None):
-    np_ = nodepool(requirements)
+def snapshot(its, nodes, pending=(), requirements=None, disruption=None):
+    np_ = nodepool(requirements, disruption)
     return {"wellKnownLabels": synth.FAKE_WELL_KNOWN, "instanceTypes": its,
             "instanceTypesByNodePool": {"default": list(range(len(its)))},
             "nodeClaimTemplates": [np_], "nodePools": [np_], "daemonSetPods": [],
@@ -171,6 +175,40 @@ def scenarios():
     n2 = node("node-b", least, alloc, [rs_pod(1, bound_to="node-b"), rs_pod(2, bound_to="node-b")])
     S.append({"name": "no-merge-same-type", "source": src + ":2849-2926", "snapshot": snapshot(its, [n1, n2]),
               "expect": {"action": "delete", "candidates": ["node-a"]}})
+    # Node annotations block candidates: NewCandidate's do-not-disrupt key (types.go:78-81) and
+    # ShouldDisrupt's do-not-consolidate == "true" (consolidation.go:96-101).
+    # "can delete nodes, considers karpneter.sh/do-not-consolidate on nodes" (:1319-1370) and
+    # "... karpenter.sh/do-not-disrupt on nodes" (:1371-1422): the non-annotated node (more pods) goes
+    for key, lines in (("karpenter.sh/do-not-consolidate", "1319-1370"), ("karpenter.sh/do-not-disrupt", "1371-1422")):
+        n1 = node("node-a", least, alloc, [rs_pod(0, bound_to="node-a"), rs_pod(1, bound_to="node-a")])
+        n2 = node("node-b", least, alloc, [rs_pod(2, bound_to="node-b")], annotations={key: "true"})
+        S.append({"name": "delete-considers-%s-on-nodes" % key.split("/")[1], "source": src + ":" + lines,
+                  "snapshot": snapshot(its, [n1, n2]), "expect": {"action": "delete", "candidates": ["node-a"]}})
+    # "can replace nodes, considers karpenter.sh/do-not-consolidate on nodes" (:536-614) and
+    # "... karpenter.sh/do-not-disrupt on nodes" (:615-693): 2 pods of 2 cpu on the 32-cpu node are
+    # replaced; the annotated 5-cpu node keeps its pod
+    for key, lines in (("karpenter.sh/do-not-consolidate", "536-614"), ("karpenter.sh/do-not-disrupt", "615-693")):
+        n1 = node("node-a", most, {"cpu": "32"}, [rs_pod(0, cpu="2", bound_to="node-a"), rs_pod(1, cpu="2", bound_to="node-a")])
+        n2 = node("node-b", most, {"cpu": "5", "pods": "100"}, [rs_pod(2, cpu="2", bound_to="node-b")],
+                  annotations={key: "true"})
+        S.append({"name": "replace-considers-%s-on-nodes" % key.split("/")[1], "source": src + ":" + lines,
+                  "snapshot": snapshot(its, [n1, n2]),
+                  "expect": {"action": "replace", "candidates": ["node-a"], "replacement_excludes": most["name"]}})
+    # ShouldDisrupt's NodePool rule (consolidation.go:102-106): consolidation is disabled for a pool whose
+    # consolidationPolicy is not WhenUnderutilized, or whose consolidateAfter is Never
+    for tag, dis in (("when-empty-policy", {"consolidationPolicy": "WhenEmpty", "consolidateAfter": "30s"}),
+                     ("consolidate-after-never", {"consolidateAfter": "Never"})):
+        n1 = node("node-a", least, alloc, [rs_pod(0, bound_to="node-a"), rs_pod(1, bound_to="node-a")])
+        n2 = node("node-b", least, alloc, [rs_pod(2, bound_to="node-b")])
+        S.append({"name": "pool-%s-disables-consolidation" % tag,
+                  "source": "pkg/controllers/disruption/consolidation.go:102-106",
+                  "snapshot": snapshot(its, [n1, n2], disruption=dis), "expect": {"action": "no-op", "candidates": []}})
+    # A node nominated for a pending pod is not a candidate (NewCandidate, types.go:110-113)
+    n1 = node("node-a", least, alloc, [rs_pod(0, bound_to="node-a"), rs_pod(1, bound_to="node-a")])
+    n2 = node("node-b", least, alloc, [rs_pod(2, bound_to="node-b")])
+    n2["nominated"] = True
+    S.append({"name": "nominated-node-is-not-a-candidate", "source": "pkg/controllers/disruption/types.go:110-113",
+              "snapshot": snapshot(its, [n1, n2]), "expect": {"action": "delete", "candidates": ["node-a"]}})
     return S
 
 
@@ -228,14 +266,28 @@ def validation_scenarios():
             V.append({"name": "unchanged-" + sc["name"], "source": "pkg/controllers/disruption/validation.go:120-180",
                       "before": sc["snapshot"], "after": sc["snapshot"],
                       "expect": {"command": sc["expect"]["action"], "valid": True, "reason": ""}})
-    # A pending pod nominated to the candidate during the wait (validation.go:99-103)
+    # A pending pod nominated to the candidate during the wait: NewCandidate drops a nominated node
+    # (types.go:110-113), so the candidate no longer maps and the command is invalid before the
+    # IsNodeNominated check of validation.go:99-103 is reached
     before = snapshot(its, two(([], [])))
     after = snapshot(its, two(([], [])))
     for n in after["stateNodes"]:
         n["nominated"] = True
-    V.append({"name": "candidate-nominated-during-wait", "source": "pkg/controllers/disruption/validation.go:99-103",
+    V.append({"name": "candidate-nominated-during-wait", "source": "pkg/controllers/disruption/types.go:110-113",
               "before": before, "after": after,
-              "expect": {"command": "delete", "valid": False, "reason": "candidate-nominated"}})
+              "expect": {"command": "delete", "valid": False, "reason": "candidates-changed"}})
+    # The pool's consolidateAfter turns to Never during the wait: Validation.ShouldDisrupt checks only the
+    # policy and do-not-consolidate (validation.go:112-118), so the command is still valid
+    after = snapshot(its, two(([], [])), disruption={"consolidateAfter": "Never"})
+    V.append({"name": "consolidate-after-never-during-wait", "source": "pkg/controllers/disruption/validation.go:112-118",
+              "before": before, "after": after, "expect": {"command": "delete", "valid": True, "reason": ""}})
+    # ... while a do-not-consolidate annotation added during the wait invalidates it
+    after = snapshot(its, two(([], [])))
+    for n in after["stateNodes"]:
+        n["annotations"] = {"karpenter.sh/do-not-consolidate": "true"}
+    V.append({"name": "do-not-consolidate-during-wait", "source": "pkg/controllers/disruption/validation.go:112-118",
+              "before": before, "after": after,
+              "expect": {"command": "delete", "valid": False, "reason": "candidates-changed"}})
     # The deleted node's pods no longer fit elsewhere: re-simulation wants a NodeClaim (validation.go:155-160)
     after = snapshot(its, two(([], [])))
     for n in after["stateNodes"]:  # whichever node is deleted, the other one is now full

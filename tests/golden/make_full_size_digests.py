@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Full-size parity digests for the BASELINE.json configs, computed by the oracle in this container.
+
+The GPU box has no reference and the oracle needs minutes at these sizes (C3 20k: ~8 min, C4 10k x 2k:
+~4 min, single thread), so the oracle's canonical results are committed as sha256 digests and the
+-m gpu tests (tests/test_full_size_gpu.py) compare the HIP path's results against them:
+
+  C1  BenchmarkScheduling2000 (scheduling_benchmark_test.go:72-74,116-182), literal pods (empty UIDs,
+      zero creation timestamps, so NewQueue's order comes from sort.Slice's tie order, queue.go:38)
+  C2  50k resource-only pods x 400 fake instance types (scheduler.go:140-189)
+  C3  20k pods, 800 instance types x 8 offerings, 3 tainted NodePools, selectors / affinity / tolerations
+  C4  10k pods onto 2k existing nodes, zonal + hostname spread and hostname anti-affinity
+  C5  5k-node / 100k-pod cluster: every multi-node prefix simulation firstNConsolidationOption can
+      probe (multinodeconsolidation.go:87-137) and every single-node simulation
+      (singlenodeconsolidation.go:42-88), with the chosen commands
+
+Per config: one digest of the whole canonical Results document (json.dumps with sorted keys and no
+whitespace) and one digest per NewNodeClaim / existing node / simulation, so a mismatch names the
+first differing element.  Re-run: python tests/golden/make_full_size_digests.py [names...]
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "karpenter-sigs_amd"))
+from karpenter_amd import synth  # noqa: E402
+
+OUT = os.path.join(HERE, "full_size_digests.json")
+
+
+def canon(x):
+    return json.dumps(x, sort_keys=True, separators=(",", ":"), ensure_ascii=False)
+
+
+def sha(x):
+    return hashlib.sha256(canon(x).encode()).hexdigest()
+
+
+def solve_digest(results):
+    """Digests of a Solve's canonical Results (stats dropped)."""
+    r = {k: v for k, v in results.items() if k != "stats"}
+    return {"all": sha(r), "newNodeClaims": [sha(c) for c in r["newNodeClaims"]],
+            "existingNodes": sha(r["existingNodes"]), "podErrors": sha(r["podErrors"]),
+            "counts": {"newNodeClaims": len(r["newNodeClaims"]), "podErrors": len(r["podErrors"]),
+                       "podsOnExistingNodes": sum(len(n["pods"]) for n in r["existingNodes"])}}
+
+
+def cons_digest(doc):
+    """Digests of a consolidation pass with every simulation reported (all_sims)."""
+    return {"all": sha(doc), "candidates": sha(doc["candidates"]),
+            "multi": {"command": sha(doc["multi"]["command"]), "sims": [sha(s) for s in doc["multi"]["sims"]]},
+            "single": {"command": sha(doc["single"]["command"]), "sims": [sha(s) for s in doc["single"]["sims"]]},
+            "summary": {"multi": doc["multi"]["command"]["action"], "single": doc["single"]["command"]["action"],
+                        "candidates": len(doc["candidates"])}}
+
+
+CONFIGS = {
+    "C1": lambda: synth.config1(literal=True),
+    "C2": lambda: synth.config2(50000),
+    "C3": lambda: synth.config3(20000),
+    "C4": lambda: synth.config4(10000, 2000),
+    "C5": lambda: synth.config5(5000),
+}
+
+
+def main(names):
+    from oracle import bridge
+
+    out = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    for name in names:
+        t = time.time()
+        snap = json.dumps(CONFIGS[name]())
+        if name == "C5":
+            doc, secs = bridge.consolidate(snap, all_sims=True)
+            out[name] = cons_digest(doc)
+        else:
+            res, secs = bridge.solve(snap)
+            out[name] = solve_digest(res)
+        out[name]["snapshot"] = hashlib.sha256(snap.encode()).hexdigest()
+        out[name]["oracle_seconds"] = round(secs, 1)
+        print("%s: %.1f s oracle, %.1f s wall" % (name, secs, time.time() - t), flush=True)
+        with open(OUT, "w") as f:
+            json.dump(out, f, indent=0, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or list(CONFIGS))

@@ -178,7 +178,7 @@ def _anti_term(rng, app):
     return {"labelSelector": _app_selector(rng, app), "topologyKey": _pick(rng, [synth.HOSTNAME, synth.HOSTNAME, synth.ZONE])}
 
 
-def add_topology(rng, pods, nodes, affinity=False):
+def add_topology(rng, pods, nodes, affinity=False, or_terms=False):
     """Topology spread (zone / hostname / capacity-type, maxSkew 1-3, minDomains, DoNotSchedule and
     ScheduleAnyway), required + preferred pod anti-affinity (topology.go, topologygroup.go) per app,
     plus bound cluster pods on the existing nodes that seed the counts (countDomains) and inverse
@@ -205,6 +205,11 @@ def add_topology(rng, pods, nodes, affinity=False):
             elif f < 0.5:
                 spec["req"] = [{"matchExpressions": [{"key": synth.ZONE, "operator": "In",
                                                       "values": sorted(_pick(rng, ZONES, 2))}]}]
+            if or_terms and rng.random() < 0.7:  # OR'd terms: relaxing term[0] re-hashes the spread group
+                spec.pop("sel", None)
+                spec["req"] = [{"matchExpressions": [{"key": synth.ZONE, "operator": "In",
+                                                      "values": sorted(_pick(rng, ZONES, int(rng.integers(1, 3))))}]}
+                               for _ in range(int(rng.integers(2, 4)))]
         if rng.random() < 0.35:
             spec["anti"] = [_anti_term(rng, app)]
         if rng.random() < 0.25:
@@ -300,7 +305,10 @@ def add_namespaces(rng, pods, cluster):
 
 
 def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False, topology=False,
-                   affinity=False, volumes=False, namespaces=False):
+                   affinity=False, volumes=False, namespaces=False, same_pod_ports=False, or_terms=False):
+    """same_pod_ports: existing nodes' HostPortUsage also holds entries keyed by pods being scheduled
+    (their own ports, or others), the case HostPortUsage.Conflicts skips and Add replaces
+    (hostportusage.go:70-85)."""
     rng = np.random.default_rng(seed)
     its = random_its(rng, n_its)
     n_templates = int(rng.integers(1, 4)) if n_templates is None else n_templates
@@ -361,7 +369,19 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
         for p in pods:
             if rng.random() < 0.4:
                 add_host_ports(rng, p)
-    cluster = add_topology(rng, pods, nodes, affinity) if topology else []
+    if same_pod_ports and nodes:
+        for p in pods:
+            if rng.random() < 0.1:
+                n = nodes[int(rng.integers(len(nodes)))]
+                own = p["spec"]["containers"][0].get("ports") or []
+                if own and rng.random() < 0.7:
+                    entries = [{"ip": e.get("hostIP", "0.0.0.0"), "port": e["hostPort"], "protocol": e["protocol"]}
+                               for e in own]
+                else:
+                    ip, port, proto = HOST_PORTS[int(rng.integers(len(HOST_PORTS)))]
+                    entries = [{"ip": ip or "0.0.0.0", "port": port, "protocol": proto}]
+                n.setdefault("hostPortUsage", {})["%s/%s" % (p["metadata"]["namespace"], p["metadata"]["name"])] = entries
+    cluster = add_topology(rng, pods, nodes, affinity, or_terms) if topology else []
     nss = add_namespaces(rng, pods, cluster) if namespaces else []
     vdrivers = add_volumes(rng, pods, nodes) if volumes else {}
     return {
@@ -383,3 +403,28 @@ def canonical(results):
     d = dict(results)
     d.pop("stats", None)
     return d
+
+
+def unlabel_topology_nodes(snap, seed, frac=0.3):
+    """Existing nodes without the zone / capacity-type label a topology group keys on, and pods that
+    admit them through a NotIn (or DoesNotExist) requirement on that key: ExistingNode.Add then takes
+    the key from the pod's requirements and picks the domain like a NodeClaim's (existingnode.go:91-115)."""
+    rng = np.random.default_rng(seed)
+    for n in snap["stateNodes"]:
+        if rng.random() < frac:
+            for key in (synth.ZONE, synth.CT):
+                if rng.random() < 0.6:
+                    n["labels"].pop(key, None)
+    for p in snap["pods"]:
+        if rng.random() >= 0.35:
+            continue
+        key = synth.ZONE if rng.random() < 0.7 else synth.CT
+        op = "NotIn" if rng.random() < 0.85 else "DoesNotExist"
+        expr = {"key": key, "operator": op}
+        if op == "NotIn":
+            expr["values"] = sorted(_pick(rng, ZONES if key == synth.ZONE else CTS, 1))
+        na = p["spec"].setdefault("affinity", {}).setdefault("nodeAffinity", {})
+        req = na.setdefault("requiredDuringSchedulingIgnoredDuringExecution", {"nodeSelectorTerms": [{"matchExpressions": []}]})
+        for term in req["nodeSelectorTerms"]:
+            term.setdefault("matchExpressions", []).append(dict(expr))
+    return snap

@@ -61,21 +61,50 @@ def test_host_ports_are_encoded():
     assert inspect(snap)["pods"] == 10
 
 
-def test_scheduled_pod_holding_host_ports_is_loud():
-    """Conflicts' same-pod exception (hostportusage.go:78) is not encoded: a pod being scheduled that
-    already holds ports on an existing node is refused."""
+def test_pod_holding_its_own_host_ports_encodes():
+    """Conflicts' same-pod exception (hostportusage.go:78): a pod being scheduled whose key already holds
+    ports on an existing node is encoded (its own entries are left out of its conflict mask)."""
     snap = problems.random_problem(3, n_nodes=2)
     snap["pods"][0]["spec"]["containers"][0]["ports"] = [{"hostPort": 80, "containerPort": 80}]
     p0 = snap["pods"][0]["metadata"]
     snap["stateNodes"][0]["hostPortUsage"] = {"%s/%s" % (p0["namespace"], p0["name"]): [{"port": 80}]}
+    assert inspect(snap)["pods"] == len(snap["pods"])
+
+
+def test_same_key_pods_with_host_ports_are_loud():
+    """Two pods being scheduled under one namespace/name with host ports: HostPortUsage.Add on a NodeClaim
+    would replace one's entries with the other's, which is not encoded."""
+    snap = problems.random_problem(3, n_nodes=2)
+    snap["pods"][0]["spec"]["containers"][0]["ports"] = [{"hostPort": 80, "containerPort": 80}]
+    snap["pods"][1]["metadata"]["name"] = snap["pods"][0]["metadata"]["name"]
     with pytest.raises(KsError) as e:
         inspect(snap)
     assert e.value.code == -2
 
 
-def test_duplicate_queue_key_is_loud():
+def test_queue_key_ties_encode():
+    """Pods tying on the whole NewQueue key (cpu, memory, creation time, UID — BenchmarkScheduling's
+    un-applied pods) get their order from the host's sort.Slice emulation (queue.go:38)."""
     snap = synth.config2(10)
     snap["pods"][1] = dict(snap["pods"][0])
+    d = inspect(snap)
+    assert d["hostQueue"] == 1 and d["uids"] == 9
+    assert inspect(synth.config1(literal=True))["hostQueue"] == 1
+    assert inspect(synth.config1())["hostQueue"] == 0
+
+
+def test_groups_created_mid_solve_encode():
+    """A relaxed state whose spread group re-hashes (OR'd required terms, topology.go:102-119) gets a
+    late group, activated by the kernel at that relaxation."""
+    snap = problems.random_problem(460, n_pods=150, topology=True, or_terms=True)
+    assert inspect(snap)["lateGroups"] > 0
+
+
+def test_shared_uids_with_topology_are_loud():
+    """TopologyGroup owners are keyed by UID: pods sharing one with topology groups are refused."""
+    snap = problems.random_problem(5, topology=True)
+    for p in snap["pods"]:
+        p["metadata"]["uid"] = ""
     with pytest.raises(KsError) as e:
         inspect(snap)
     assert e.value.code == -2

@@ -164,16 +164,20 @@ def test_sharded_runs_gather_to_the_same_decision():
 
 
 def test_c5_shape_at_scale_properties():
-    """1000-node slice of the C5 cluster: every single-node simulation is evaluated; a delete must
-    leave every rescheduled pod placed (size-independent properties; the oracle checks the small
-    cases exactly)."""
+    """1000-node slice of the C5 cluster: every single-node simulation is evaluated.  The cluster has the
+    headroom for any one node's 20 pods, so every single-node simulation reschedules all of them onto
+    the remaining nodes without a new NodeClaim (a delete), and the multi-node search reaches the
+    largest prefix (101 candidates, multinodeconsolidation.go:93-95) as a delete — as the oracle
+    computes for this cluster (the full 5k-node pass is compared to it in test_full_size_gpu.py)."""
     snap = synth.cluster_snapshot(1000, 20, 400, seed=4205)
     c = Consolidator(json.dumps(snap))
     assert c.num_candidates == 1000 and c.num_sims == 1000 + 100
     doc = c.consolidate(all_sims=True)
     assert len(doc["single"]["sims"]) == 1000
-    for s in doc["single"]["sims"]:
-        assert s["allNonPendingScheduled"] or s["newNodeClaims"] >= 0
+    assert all(s["allNonPendingScheduled"] and s["newNodeClaims"] == 0 for s in doc["single"]["sims"])
+    assert doc["single"]["command"]["action"] == "delete"
+    assert doc["single"]["command"]["candidates"] == [doc["candidates"][0]["name"]]
+    assert doc["multi"]["command"]["action"] == "delete" and len(doc["multi"]["command"]["candidates"]) == 101
     costs = [x["disruptionCost"] for x in doc["candidates"]]
     assert costs == sorted(costs)
     # determinism
@@ -310,3 +314,26 @@ def test_validation_of_arbitrary_candidate_subsets(seed, topo):
         cmd = {"action": "delete", "candidates": cands}
         want, got = bridge.validate(s, cmd), h.validate(cmd)
         assert _first_diff(want, got) is None, (cands, _first_diff(want, got))
+
+
+def test_validate_keeps_the_pass_launch():
+    """ks_cons_validate re-simulates in a launch of its own: after run -> validate on one handle, the
+    pass's records still decide identically, and the requirement records and counters the decision
+    reads (ks_cons_claim_requirements, ks_cons_sim_counters) still come from the pass's launch."""
+    snap = json.dumps(synth.cluster_snapshot(24, 10, n_its=60, it_range=(6, 30), seed=2, spot_frac=0.6))
+    c = Consolidator(snap)
+    recs, _ = c.run(0, 1)
+    before = c.decide(recs, 1, all_sims=True)
+    need = c.needed_sims(recs, 1, all_sims=True)
+    assert need, "the scenario's multi-node command is a replace, which needs a requirement record"
+    reqs = {s: c.claim_requirements(s) for s in need}
+    counters = c.sim_counters(need[0])
+    for cmd in (before["multi"]["command"], before["single"]["command"]):
+        v = c.validate(cmd)
+        assert v["valid"], v
+    assert c.decide(recs, 1, all_sims=True) == before
+    assert {s: c.claim_requirements(s) for s in need} == reqs
+    assert c.sim_counters(need[0]) == counters
+    want, _ = bridge.consolidate(snap, all_sims=True)
+    got = dict(before)
+    assert _first_diff(want, got) is None

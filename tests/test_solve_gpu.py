@@ -182,3 +182,35 @@ def test_volume_reference_scenarios_gpu(name):
     d = _diff(want, got)
     assert d is None, d
     assert not mvf.check(scn, want)
+
+
+def test_config1_literal_benchmark_pods():
+    """BenchmarkScheduling2000 with the benchmark's own pods (no UID, zero CreationTimestamp; they are never
+    applied to an apiserver): NewQueue breaks cpu/memory ties by sort.Slice's swap order over the input
+    (queue.go:38, the host's pdqsort emulation) and every pod shares the staleness key "" (queue.go:54-69)."""
+    want, got = _solve_both(synth.config1(literal=True))
+    d = _diff(want, got)
+    assert d is None, d
+
+
+@pytest.mark.parametrize("seed", list(range(400, 412)))
+def test_queue_ties_parity(seed):
+    """Random problems whose pods share UIDs and timestamps in groups, so NewQueue's order of equal
+    (cpu, memory) pods comes from sort.Slice's tie order and staleness is shared per UID."""
+    snap = problems.random_problem(seed, n_pods=200, n_nodes=int(seed % 3) * 5)
+    for i, p in enumerate(snap["pods"]):
+        p["metadata"]["uid"] = "" if seed == 401 else "shared-%d" % (i % 25)
+        p["metadata"].pop("creationTimestamp", None)
+    want, got = _solve_both(snap)
+    d = _diff(want, got)
+    assert d is None, d
+
+
+@pytest.mark.parametrize("seed", list(range(420, 436)))
+def test_same_pod_host_ports_parity(seed):
+    """Existing nodes whose HostPortUsage holds entries of the pods being scheduled: Conflicts skips the
+    pod's own entries and Add replaces them (hostportusage.go:70-85)."""
+    snap = problems.random_problem(seed, n_pods=150, n_nodes=8 + seed % 5, host_ports=True, same_pod_ports=True)
+    want, got = _solve_both(snap)
+    d = _diff(want, got)
+    assert d is None, d

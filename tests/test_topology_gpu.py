@@ -149,3 +149,32 @@ def test_config4_full_size_properties():
             app = snap["pods"][p]["metadata"]["labels"]["app"]
             assert host_apps[(app, where)] == 1, (p, where)
     assert all(w in node_zone or w.startswith("claim-") for w in seen.values())
+
+
+@pytest.mark.parametrize("seed", list(range(440, 456)))
+def test_unlabelled_nodes_with_not_in_parity(seed):
+    """Existing nodes lacking a topology key's label, with pods admitting them through NotIn /
+    DoesNotExist on that key: the node takes the key from the pod's requirements and its domain is
+    chosen like a NodeClaim's, then recorded (existingnode.go:91-121); k_solve decides such nodes
+    wave-wide (node_slow) and keeps their accumulated requirements."""
+    snap = problems.random_problem(seed, n_pods=150, n_nodes=10, topology=True, affinity=seed % 2 == 1)
+    problems.unlabel_topology_nodes(snap, seed)
+    want, got = _solve_both(snap)
+    d = _diff(want, got)
+    assert d is None, d
+
+
+@pytest.mark.parametrize("seed", list(range(460, 480)))
+def test_groups_created_mid_solve_parity(seed):
+    """Spread pods with OR'd required node-affinity terms: relaxing term[0] changes the group's node
+    filter, so Topology.Update creates a new group mid-Solve (topology.go:102-119) with countDomains over
+    the cluster's bound pods only, no hostnames of the existing nodes or earlier NodeClaims registered,
+    and no earlier placements recorded."""
+    from karpenter_amd import inspect
+
+    snap = problems.random_problem(seed, n_pods=150, n_nodes=int(seed % 3) * 6, topology=True,
+                                   affinity=seed % 2 == 1, or_terms=True)
+    assert inspect(snap)["lateGroups"] > 0
+    want, got = _solve_both(snap)
+    d = _diff(want, got)
+    assert d is None, d
