@@ -7,12 +7,18 @@ Solve does not shard (every placement depends on all earlier ones), so N GPUs ru
 replicas, one per rank ("replicas only"); value = pods solved by all ranks / max-rank time.
 
 Prints ONE JSON line on rank 0 (the driver's contract), including:
-  roofline     : dominant kernel k_solve, algorithmic bytes (counted by the kernel) /
-                 its HIP-event duration vs the 8 TB/s HBM peak; traffic from profiles/ PMC data if any
-  cpu_baseline : the oracle (C++ restatement of the reference Solve, single thread) timed on this
-                 host on the same workload
+  create_ms / e2e_*  what a drop-in caller pays: ks_problem_create (parse + encode + upload, the
+                     NewScheduler-time work) and the rate including it and the results copy-back
+  roofline     : dominant kernel k_solve, HIP-event duration vs the 8 TB/s HBM peak, for two byte
+                 counts: the kernel's own scan (algorithmic_bytes_per_launch) and SURVEY.md §8d's
+                 reference scan (algorithmic_bytes_ref, counted by the oracle); traffic = PMC HBM bytes
+                 from the committed profile named in traffic_source
+  cpu_baseline : the oracle (C++ restatement of the reference Solve) timed on this host on the same
+                 workload, with the host's nproc / CPU model and the threads used
+  solve_c1/c3/c4, consolidation(_topology): the other BASELINE.json configs, each with the same fields
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -23,6 +29,80 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "karpenter-sigs_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+DIGESTS = os.path.join(ROOT, "tests", "golden", "full_size_digests.json")
+
+
+def _host():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
+def _baseline(value, unit, threads, sample, secs):
+    d = {"value": round(value, 2), "unit": unit, "cores": threads, "threads": threads, "kind": "port",
+         "sample": sample + " (oracle/cpu_ref.cpp, %d host thread%s, %.1f s)" % (threads, "" if threads == 1 else "s", secs),
+         "gomaxprocs": "n/a (no Go reference on this host)"}
+    d.update(_host())
+    return d
+
+
+def _ref_bytes(name, snap_json):
+    """SURVEY.md §8d algorithmic bytes of the reference's scan for a BASELINE config, as the oracle counted
+    them when tests/golden/full_size_digests.json was made (the oracle needs minutes at these sizes);
+    None if the workload is not the committed one."""
+    try:
+        d = json.load(open(DIGESTS)).get(name)
+    except OSError:
+        return None
+    if not d or hashlib.sha256(snap_json.encode()).hexdigest() != d.get("snapshot"):
+        return None
+    return d.get("algBytesRef")
+
+
+def _traffic(tag):
+    tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % tag)
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            t = json.load(f)
+        return t.get("hbm_bytes_per_launch"), "profiles/traffic_%s.json (rocprofv3 PMC, profile tag %s)" % (tag, t.get("tag"))
+    return None, None
+
+
+def _roofline(kernel, k_ms, alg_bytes, ref_bytes, traffic_tag, per_gpu_div=1, extra=None):
+    achieved = alg_bytes / (k_ms / 1000.0) / 1e9 / per_gpu_div
+    traffic, src = _traffic(traffic_tag)
+    r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+         "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(k_ms, 3),
+         "algorithmic_bytes_ref": ref_bytes, "achieved_ref": None, "frac_ref": None}
+    if ref_bytes:
+        ar = ref_bytes / (k_ms / 1000.0) / 1e9 / per_gpu_div
+        r["achieved_ref"] = round(ar, 3)
+        r["frac_ref"] = ar / HBM_PEAK_GBS
+    if extra:
+        r.update(extra)
+    return r
+
+
+def _pct(xs, q):
+    """Nearest-rank percentile."""
+    ys = sorted(xs)
+    return ys[min(len(ys) - 1, max(0, -(-q * len(ys) // 100) - 1))]
+
+
+def _create(cls, snap_json):
+    """(handle, create_ms): the second of two constructions (the first pays the process's HIP init)."""
+    cls(snap_json).close()
+    t = time.perf_counter()
+    h = cls(snap_json)
+    return h, (time.perf_counter() - t) * 1000.0
 
 
 def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0):
@@ -38,7 +118,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
 
     snap = json.dumps(synth.config5(args.cons_nodes) if not topology else
                       synth.cluster_snapshot(args.cons_nodes, 20, 400, seed=4205, topology=topology))
-    c = Consolidator(snap)
+    c, create_ms = _create(Consolidator, snap)
     per, rb = c.records_per_rank(world), c.record_bytes
     dev = "cuda:%d" % local
     out = gathered = None
@@ -71,6 +151,9 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
             doc = c.decide(recs, world, fetch=table.__getitem__, candidates=False) if rank == 0 else None
         return ms, recs, doc
 
+    t0 = time.perf_counter()
+    one_pass()  # first pass: includes the launch plan's build and upload (prepare_launch)
+    first_ms = (time.perf_counter() - t0) * 1000.0
     for _ in range(args.warmup):
         one_pass()
     barrier_sync()
@@ -91,17 +174,21 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
         return None
     k_ms = sum(kms) / len(kms)
     algb = c.alg_bytes(recs, world)
-    achieved = algb / (k_ms / 1000.0) / 1e9 / world  # per GPU: each rank scans its own shard
-    cpu = None
+    ref = _ref_bytes("C5", snap) if not topology else None
+    cpu = cpu1 = None
     if not args.no_cpu_baseline and world == 1:
         from oracle import bridge
 
-        n, secs = bridge.time_cons_sims(snap, args.cpu_sims if not topology else args.cpu_topo_sims, args.cpu_threads)
-        cpu = {"value": round(n / secs, 2), "unit": "cands/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": "first %d single-node simulations of the same cluster (simulateScheduling + "
-                         "computeConsolidation, oracle/cpu_ref.cpp, %d host threads, %.1f s)" % (n, args.cpu_threads, secs)}
+        n_sims = args.cpu_sims if not topology else args.cpu_topo_sims
+        n, secs = bridge.time_cons_sims(snap, n_sims, args.cpu_threads)
+        cpu = _baseline(n / secs, "cands/s", args.cpu_threads,
+                        "first %d single-node simulations of the same cluster (simulateScheduling + "
+                        "computeConsolidation)" % n, secs)
+        n1, secs1 = bridge.time_cons_sims(snap, max(n_sims // (4 * args.cpu_threads), 8), 1)
+        cpu1 = _baseline(n1 / secs1, "cands/s", 1, "first %d single-node simulations of the same cluster "
+                         "(sequential, as the reference's single goroutine runs them)" % n1, secs1)
     # Validation.IsValid + ValidateCommand (validation.go:68-180) of the command the controller would run
-    # (multi-node first): one re-simulation on the GPU, timed after the passes (it re-plans the launch)
+    # (multi-node first): one re-simulation on the GPU, timed after the passes (its own launch)
     final = doc["multi"]["command"] if doc["multi"]["command"]["action"] != "no-op" else doc["single"]["command"]
     vms = []
     for _ in range(3):
@@ -111,100 +198,71 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
     validation = {"command": [final["action"], len(final["candidates"])], "valid": v["valid"], "reason": v["reason"],
                   "ms": round(sorted(vms)[1], 3)}
     name = "C5" if not topology else "C5 + topology (%d apps: spread, pod affinity, anti-affinity)" % topology
+    pass_ms = elapsed * 1000.0 / args.cons_steps
     return {
         "metric": "consolidation cands/sec (%s: %d nodes x 20 pods, 400 instance types)" % (name, args.cons_nodes),
         "value": round(c.num_sims * args.cons_steps / elapsed, 1),
         "unit": "cands/s",
         "n_gpus": world,
         "steps": args.cons_steps,
-        "ms_per_pass": round(elapsed * 1000.0 / args.cons_steps, 3),
+        "ms_per_pass": round(pass_ms, 3),
         "scaling": "strong",
         "simulations_per_pass": c.num_sims,
         "candidates": c.num_candidates,
+        # ks_cons_create: parse + NewCandidate + encode + upload of the cluster snapshot (once per pass in
+        # the reference's terms); e2e = a fresh snapshot every pass: create + first pass (plan + run + decide)
+        "create_ms": round(create_ms, 3),
+        "first_pass_ms": round(first_ms, 3),
+        "e2e_cands_per_s": round(c.num_sims / ((create_ms + first_ms) / 1000.0), 1),
         "decision": {"multi": [doc["multi"]["command"]["action"], len(doc["multi"]["command"]["candidates"])],
                      "single": [doc["single"]["command"]["action"], doc["single"]["command"]["candidates"]]},
-        "roofline": {"bound": "hbm", "kernel": "k_solve<SIM%s>" % (", TOPO" if topology else ""),
-                     "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("cons_c5" if not topology else "cons_c5t"),
-                     "algorithmic_bytes_per_pass": algb, "kernel_ms": round(k_ms, 3), "kernel_ms_max_rank": round(kmax, 3)},
+        "roofline": _roofline("k_solve<SIM%s>" % (", TOPO" if topology else ""), k_ms, algb, ref,
+                              "cons_c5" if not topology else "cons_c5t", per_gpu_div=world,
+                              extra={"kernel_ms_max_rank": round(kmax, 3)}),
         "cpu_baseline": cpu,
+        "cpu_baseline_1thread": cpu1,
         "validation": validation,
     }
 
 
-def c3_bench(args, local):
-    """C3 (BASELINE.json configs[2]): requirement-heavy Solve, 1 GPU, reported beside the C2 line."""
-    from karpenter_amd import Scheduler, synth
+def solve_line(args, local, name, snap, metric, reps, cpu_sample=None, extra=None, traffic_tag=None):
+    """A Solve workload beside the C2 line: GPU time of `reps` Solves, create / e2e cost, the kernel's
+    roofline against both byte counts, and the oracle on `cpu_sample` = (snapshot, pods, description)."""
+    from karpenter_amd import Scheduler
 
-    sch = Scheduler(json.dumps(synth.config3(args.c3_pods)))
+    snap_json = json.dumps(snap)
+    npods = len(snap["pods"])
+    sch, create_ms = _create(Scheduler, snap_json)
+    t = time.perf_counter()
     r = sch.solve(device=local)
-    placed = sum(len(c["pods"]) for c in r.new_nodeclaims)
+    full_ms = (time.perf_counter() - t) * 1000.0
     for _ in range(max(args.warmup - 1, 0)):
         sch.solve(device=local, timing_only=True)
     t0 = time.perf_counter()
-    ks = []
-    for _ in range(2):
-        ks.append(sch.solve(device=local, timing_only=True).solve_kernel_ms)
-    el = (time.perf_counter() - t0) / 2
-    out = {"metric": "pods/sec in Scheduler.Solve (C3: %d pods, 800 instance types x 8 offerings, 3 tainted "
-                     "NodePools, selectors/affinity/tolerations)" % args.c3_pods,
-           "value": round(args.c3_pods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1000, 3),
-           "kernel_ms": round(sum(ks) / len(ks), 3), "new_nodeclaims": len(r.new_nodeclaims),
-           "pods_placed": placed, "pod_errors": len(r.pod_errors), "cpu_baseline": None}
-    if not args.no_cpu_baseline:
+    ks, algb = [], []
+    for _ in range(reps):
+        x = sch.solve(device=local, timing_only=True)
+        ks.append(x.solve_kernel_ms)
+        algb.append(x.algorithmic_bytes)
+    el = (time.perf_counter() - t0) / reps
+    k_ms = sum(ks) / len(ks)
+    out = {"metric": metric, "value": round(npods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1000, 3),
+           "kernel_ms": round(k_ms, 3), "create_ms": round(create_ms, 3),
+           "e2e_pods_per_s": round(npods / ((create_ms + full_ms) / 1000.0), 1),
+           "new_nodeclaims": len(r.new_nodeclaims), "pods_on_existing_nodes": sum(len(n["pods"]) for n in r.existing_nodes),
+           "pod_errors": len(r.pod_errors),
+           "roofline": _roofline("k_solve", k_ms, sum(algb) / len(algb), _ref_bytes(name, snap_json), traffic_tag),
+           "cpu_baseline": None}
+    if extra:
+        out.update(extra)
+    if cpu_sample and not args.no_cpu_baseline:
         from oracle import bridge
 
-        sp = min(args.c3_cpu_pods, args.c3_pods)
-        secs = bridge.time_solve(json.dumps(synth.config3(sp)), 1)
-        out["cpu_baseline"] = {"value": round(sp / secs, 1), "unit": "pods/s", "cores": 1, "kind": "port",
-                               "sample": "1 Solve of C3 with %d pods (oracle/cpu_ref.cpp, single thread, %.1f s); "
-                                         "the oracle's per-pod cost grows with the pod count" % (sp, secs)}
+        csnap, cpods, desc, creps = cpu_sample
+        secs = bridge.time_solve(json.dumps(csnap), creps)
+        out["cpu_baseline"] = _baseline(cpods * creps / secs, "pods/s", 1, desc, secs)
+    sch.close()
     return out
-
-
-def c4_bench(args, local):
-    """C4 (BASELINE.json configs[3]): topology Solve onto existing nodes, 1 GPU, beside the C2 line.
-    The oracle leg times a bounded sample of the same shape (fewer pods and nodes)."""
-    from karpenter_amd import Scheduler, synth
-
-    sch = Scheduler(json.dumps(synth.config4(args.c4_pods, args.c4_nodes)))
-    r = sch.solve(device=local)
-    on_nodes = sum(len(n["pods"]) for n in r.existing_nodes)
-    for _ in range(max(args.warmup - 1, 0)):
-        sch.solve(device=local, timing_only=True)
-    t0 = time.perf_counter()
-    ks = []
-    for _ in range(3):
-        ks.append(sch.solve(device=local, timing_only=True).solve_kernel_ms)
-    el = (time.perf_counter() - t0) / 3
-    out = {"metric": "pods/sec in Scheduler.Solve (C4: %d pods onto %d existing nodes, zonal + hostname spread, "
-                     "hostname anti-affinity, 20 apps)" % (args.c4_pods, args.c4_nodes),
-           "value": round(args.c4_pods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1000, 3),
-           "kernel_ms": round(sum(ks) / len(ks), 3), "new_nodeclaims": len(r.new_nodeclaims),
-           "pods_on_existing_nodes": on_nodes, "pod_errors": len(r.pod_errors), "cpu_baseline": None}
-    if not args.no_cpu_baseline:
-        from oracle import bridge
-
-        sp, sn = max(args.c4_pods // 4, 1), max(args.c4_nodes // 4, 1)
-        secs = bridge.time_solve(json.dumps(synth.config4(sp, sn)), 1)
-        out["cpu_baseline"] = {"value": round(sp / secs, 1), "unit": "pods/s", "cores": 1, "kind": "port",
-                               "sample": "1 Solve of C4 with %d pods onto %d nodes (oracle/cpu_ref.cpp, single "
-                                         "thread, %.1f s)" % (sp, sn, secs)}
-    return out
-
-
-def _pct(xs, q):
-    """Nearest-rank percentile."""
-    ys = sorted(xs)
-    return ys[min(len(ys) - 1, max(0, -(-q * len(ys) // 100) - 1))]
-
-
-def _traffic(tag):
-    tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % tag)
-    if os.path.exists(tpath):
-        with open(tpath) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    return None
 
 
 def main():
@@ -217,12 +275,14 @@ def main():
     ap.add_argument("--cpu-pods", type=int, default=50000, help="oracle sample size (same workload shape)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--no-c1", action="store_true")
     ap.add_argument("--no-c3", action="store_true")
     ap.add_argument("--c3-pods", type=int, default=20000)
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--c4-pods", type=int, default=10000)
     ap.add_argument("--c4-nodes", type=int, default=2000)
     ap.add_argument("--only-consolidation", action="store_true", help="profiling: skip the Solve section")
+    ap.add_argument("--only-solve", default="", help="profiling: run only this Solve line (c2, c3, c4)")
     ap.add_argument("--cons-nodes", type=int, default=5000, help="C5 cluster size (20 pods per node)")
     ap.add_argument("--cons-steps", type=int, default=20)
     ap.add_argument("--cpu-sims", type=int, default=2400, help="oracle consolidation sample (simulations)")
@@ -261,13 +321,23 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
+    if args.only_solve in ("c3", "c4"):
+        if args.only_solve == "c3":
+            line = solve_line(args, local, "C3", synth.config3(args.c3_pods), "C3 profile", 2, traffic_tag="c3")
+        else:
+            line = solve_line(args, local, "C4", synth.config4(args.c4_pods, args.c4_nodes), "C4 profile", 3,
+                              traffic_tag="c4")
+        print(json.dumps(line))
+        return
 
     snap = synth.config2(args.pods) if args.its == 400 else synth.benchmark_snapshot(args.pods, args.its, 42, False)
     snap_json = json.dumps(snap)
-    sch = Scheduler(snap_json)
+    sch, create_ms = _create(Scheduler, snap_json)
 
-    # one full solve to verify the result shape (every pod placed once) outside the timed region
+    # one full solve (results copied back and rendered) to verify the result shape outside the timed region
+    t = time.perf_counter()
     check = sch.solve(device=local)
+    full_ms = (time.perf_counter() - t) * 1000.0
     placed = sum(len(c["pods"]) for c in check.new_nodeclaims)
     assert placed + len(check.pod_errors) == args.pods, "solve lost pods"
     nclaims = len(check.new_nodeclaims)
@@ -294,19 +364,41 @@ def main():
     value = args.pods * world * args.steps / elapsed
     k_ms = sum(solve_ms) / len(solve_ms)
     bytes_per_launch = sum(algb) / len(algb)
-    achieved = bytes_per_launch / (k_ms / 1000.0) / 1e9
-    traffic = _traffic("c2")
+    ref = _ref_bytes("C2", snap_json)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         from oracle import bridge
 
-        csnap = synth.config2(args.cpu_pods) if args.cpu_pods != args.pods else snap
-        secs = bridge.time_solve(json.dumps(csnap), 1)
-        cpu = {"value": round(args.cpu_pods / secs, 1), "unit": "pods/s", "cores": 1, "kind": "port",
-               "sample": "1 Solve of C2 with %d pods x %d instance types (oracle/cpu_ref.cpp, single thread, "
-                         "%.1f s)" % (args.cpu_pods, args.its, secs)}
-    c3 = None if args.no_c3 or world > 1 else c3_bench(args, local)
-    c4 = None if args.no_c4 or world > 1 else c4_bench(args, local)
+        csnap = json.dumps(synth.config2(args.cpu_pods)) if args.cpu_pods != args.pods else snap_json
+        res, secs = bridge.solve(csnap)
+        if ref is None and args.cpu_pods == args.pods:
+            ref = res.get("stats", {}).get("algBytesRef")
+        cpu = _baseline(args.cpu_pods / secs, "pods/s", 1, "1 Solve of C2 with %d pods x %d instance types" %
+                        (args.cpu_pods, args.its), secs)
+    lines = {}
+    if world == 1:
+        if not args.no_c1:
+            c1 = synth.config1(literal=True)
+            lines["solve_c1"] = solve_line(
+                args, local, "C1", c1, "pods/sec in Scheduler.Solve (C1: BenchmarkScheduling2000, the benchmark's "
+                "literal pods: empty UIDs, zero timestamps; 400 fake instance types, empty topology)", 10,
+                cpu_sample=(c1, 2000, "20 Solves of C1", 20), traffic_tag="c1")
+        if not args.no_c3:
+            sp = min(args.c3_cpu_pods, args.c3_pods)
+            lines["solve_c3"] = solve_line(
+                args, local, "C3", synth.config3(args.c3_pods),
+                "pods/sec in Scheduler.Solve (C3: %d pods, 800 instance types x 8 offerings, 3 tainted NodePools, "
+                "selectors/affinity/tolerations)" % args.c3_pods, 2,
+                cpu_sample=(synth.config3(sp), sp, "1 Solve of C3 with %d pods (the oracle's per-pod cost grows with "
+                            "the pod count: at 20k it takes ~460 s)" % sp, 1), traffic_tag="c3")
+        if not args.no_c4:
+            sp, sn = max(args.c4_pods // 4, 1), max(args.c4_nodes // 4, 1)
+            lines["solve_c4"] = solve_line(
+                args, local, "C4", synth.config4(args.c4_pods, args.c4_nodes),
+                "pods/sec in Scheduler.Solve (C4: %d pods onto %d existing nodes, zonal + hostname spread, hostname "
+                "anti-affinity, 20 apps)" % (args.c4_pods, args.c4_nodes), 3,
+                cpu_sample=(synth.config4(sp, sn), sp, "1 Solve of C4 with %d pods onto %d nodes" % (sp, sn), 1),
+                traffic_tag="c4")
     cons = None if args.no_consolidation else consolidation_bench(args, rank, world, local, dist, barrier_sync)
     ctopo = None
     if not args.no_consolidation and args.cons_topo_apps:
@@ -331,18 +423,20 @@ def main():
                                "empty topology (BenchmarkScheduling shape)" % (args.pods, args.its),
                    "pods": args.pods, "instance_types": args.its, "parallelism": "replicas%d" % world,
                    "new_nodeclaims": nclaims},
-        "roofline": {"bound": "hbm", "kernel": "k_solve", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes_per_launch": bytes_per_launch, "kernel_ms": round(k_ms, 3),
-                     "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3),
-                     # SURVEY §8d timing protocol: median and p90 (nearest rank) of the timed Solves
-                     "kernel_ms_p50": round(_pct(solve_ms, 50), 3), "kernel_ms_p90": round(_pct(solve_ms, 90), 3)},
+        # the drop-in caller's cost (never `value`): ks_problem_create = parse + encode + upload of the
+        # snapshot; e2e = create + one Solve with its results copied back and rendered
+        "create_ms": round(create_ms, 3),
+        "full_solve_ms": round(full_ms, 3),
+        "e2e_pods_per_s": round(args.pods / ((create_ms + full_ms) / 1000.0), 1),
+        "roofline": _roofline("k_solve", k_ms, bytes_per_launch, ref, "c2", extra={
+            "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3),
+            # SURVEY §8d timing protocol: median and p90 (nearest rank) of the timed Solves
+            "kernel_ms_p50": round(_pct(solve_ms, 50), 3), "kernel_ms_p90": round(_pct(solve_ms, 90), 3)}),
         "cpu_baseline": cpu,
-        "solve_c3": c3,
-        "solve_c4": c4,
-        "consolidation": cons,
-        "consolidation_topology": ctopo,
     }
+    out.update(lines)
+    out["consolidation"] = cons
+    out["consolidation_topology"] = ctopo
     print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

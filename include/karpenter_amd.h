@@ -74,6 +74,25 @@ int ks_results_existing_node(const ks_results* r, int i, int* state_node_index, 
 int ks_results_num_pod_errors(const ks_results* r);
 int ks_results_pod_error(const ks_results* r, int i, int* pod_index, const char** message);
 
+/* One key of a NodeClaim's Requirements (pkg/scheduling/requirement.go:33-280), as a cgo shim rebuilds
+ * it: Operator() ("In", "NotIn", "Exists", "DoesNotExist"; Gt/Lt read as "Exists" with bounds,
+ * requirement.go:197-208), the value set in sorted order, and the Gt / Lt bounds. */
+typedef struct ks_requirement {
+  const char* key;
+  const char* op;
+  int n_values;
+  const char* const* values;
+  int has_gt, has_lt;
+  int64_t gt, lt;
+} ks_requirement;
+/* NodeClaim i's Spec.Resources.Requests (nodeclaim.go:35-42, scheduler.go:102-106): resource names in
+ * name order with canonical resource.Quantity.String() text.  Arrays live as long as r. */
+int ks_results_nodeclaim_requests(const ks_results* r, int i, int* n, const char* const** names,
+                                  const char* const** quantities);
+/* NodeClaim i's Requirements after FinalizeScheduling (hostname removed, nodeclaim.go:123-128), one entry
+ * per key in key order (what consolidation.go:134-188 reads from NewNodeClaims[0]). */
+int ks_results_nodeclaim_requirements(const ks_results* r, int i, int* n, const ks_requirement** reqs);
+
 /* Device time of the solve kernel(s) of the last ks_solve, measured with HIP events on the
  * stream the kernel ran on (milliseconds). */
 double ks_results_kernel_ms(const ks_results* r);
@@ -120,6 +139,19 @@ int ks_cons_needed_sims(const ks_cons* c, const void* records, int world, int fl
 int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out);
 int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
                    char** json_out);
+/* The methods' timeouts (MultiNodeConsolidationTimeoutDuration = 1 min, multinodeconsolidation.go:34,99-110;
+ * SingleNodeConsolidationTimeoutDuration = 3 min, singlenodeconsolidation.go:29,58-65) on a virtual clock
+ * that advances sim_seconds per simulation the sequential replay consults: the multi-node search returns
+ * its last saved command once the clock passes its timeout, the single-node scan abandons with no command.
+ * The GPU has already run every simulation, so sim_seconds models the reference's per-simulation cost
+ * (0: no timeout ever fires, which is ks_cons_decide). */
+typedef struct ks_cons_clock {
+  double multi_timeout_s;
+  double single_timeout_s;
+  double sim_seconds;
+} ks_cons_clock;
+int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
+                         const ks_cons_clock* clock, char** json_out);
 /* Validation.IsValid after its wait + ValidateCommand (disruption/validation.go:68-180): the handle
  * holds the current cluster snapshot (stateNodes may carry "nominated": Cluster.IsNodeNominated);
  * command_json is a command as ks_cons_decide reports it ({"candidates": [names], "replacement":

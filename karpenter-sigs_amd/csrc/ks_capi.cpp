@@ -119,6 +119,32 @@ struct ks_results {
     int64_t host;
     std::vector<int32_t> pods, its;
     std::string json;
+    // structured accessors (ks_results_nodeclaim_requests / _requirements); the pointer arrays point
+    // into the string vectors, rebuilt by bind() after every move
+    std::vector<std::string> reqNames, reqQty;
+    std::vector<const char*> reqNameP, reqQtyP;
+    struct Req {
+      std::string key, op;
+      std::vector<std::string> values;
+      int hasGt = 0, hasLt = 0;
+      int64_t gt = 0, lt = 0;
+    };
+    std::vector<Req> reqs;
+    std::vector<std::vector<const char*>> reqValP;
+    std::vector<ks_requirement> reqC;
+    void bind() {
+      reqNameP.clear();
+      reqQtyP.clear();
+      for (auto& x : reqNames) reqNameP.push_back(x.c_str());
+      for (auto& x : reqQty) reqQtyP.push_back(x.c_str());
+      reqValP.assign(reqs.size(), {});
+      reqC.clear();
+      for (size_t i = 0; i < reqs.size(); i++) {
+        for (auto& v : reqs[i].values) reqValP[i].push_back(v.c_str());
+        reqC.push_back(ks_requirement{reqs[i].key.c_str(), reqs[i].op.c_str(), (int)reqs[i].values.size(),
+                                      reqValP[i].data(), reqs[i].hasGt, reqs[i].hasLt, reqs[i].gt, reqs[i].lt});
+      }
+    }
   };
   struct ENode {
     int index;
@@ -352,6 +378,8 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
       ksjson::quote(j, kv.first);
       j += ":";
       ksjson::quote(j, qty_str(kv.second));
+      cl.reqNames.push_back(kv.first);
+      cl.reqQty.push_back(qty_str(kv.second));
     }
     j += "},\"requirements\":[";
     first = true;
@@ -361,6 +389,25 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
       if (!first) j += ",";
       first = false;
       ksjson::quote(j, h.reqString(rec, kk, true, cl.host));
+      static const char* opn[] = {"In", "NotIn", "Exists", "DoesNotExist"};
+      ks_results::Claim::Req q;
+      q.key = h.keyNames[(size_t)kk];
+      const int op = rs_op(h.L, rec, kk);
+      q.op = opn[op];
+      if (op == OP_IN || op == OP_NOTIN) {
+        const KeyMeta& km = h.keys[(size_t)kk];
+        for (int b = 0; b < km.nv; b++)
+          if ((rec[h.L.HDR + km.off + (b >> 5)] >> (b & 31)) & 1u) q.values.push_back(h.values[(size_t)kk][(size_t)b]);
+        std::sort(q.values.begin(), q.values.end());
+      }
+      const KeyMeta& km = h.keys[(size_t)kk];
+      if (km.bslot >= 0) {
+        q.hasGt = bit(rs_hasgt(rec), kk) ? 1 : 0;
+        q.hasLt = bit(rs_haslt(rec), kk) ? 1 : 0;
+        if (q.hasGt) q.gt = rs_gt(rec, km.bslot);
+        if (q.hasLt) q.lt = rs_lt(rec, km.bslot);
+      }
+      cl.reqs.push_back(std::move(q));
     }
     j += "],\"requirementsString\":";
     ksjson::quote(j, h.reqsString(rec, cl.host));
@@ -394,6 +441,7 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     cl.json = j;
     res->claims.push_back(std::move(cl));
   }
+  for (auto& c : res->claims) c.bind();  // after the last move of the claims vector
   for (int n = 0; n < d.N; n++) res->nodes.push_back(ks_results::ENode{h.nodes[n].origIndex, h.nodes[n].name, nodePods[n]});
   // PodErrors (scheduler.go:179-183 keeps non-nil errors only)
   // k_solve records ST_FAILED at each failed attempt and nothing on success: a pod is an error iff
@@ -710,6 +758,22 @@ int ks_results_nodeclaim(const ks_results* r, int i, int* tpl, const int32_t** p
   if (np) *np = (int)c.pods.size();
   if (its) *its = c.its.data();
   if (nit) *nit = (int)c.its.size();
+  return KS_OK;
+}
+int ks_results_nodeclaim_requests(const ks_results* r, int i, int* n, const char* const** names,
+                                  const char* const** quantities) {
+  if (!r || i < 0 || i >= (int)r->claims.size()) return KS_ERR_ARG;
+  const auto& c = r->claims[(size_t)i];
+  if (n) *n = (int)c.reqNameP.size();
+  if (names) *names = c.reqNameP.data();
+  if (quantities) *quantities = c.reqQtyP.data();
+  return KS_OK;
+}
+int ks_results_nodeclaim_requirements(const ks_results* r, int i, int* n, const ks_requirement** reqs) {
+  if (!r || i < 0 || i >= (int)r->claims.size()) return KS_ERR_ARG;
+  const auto& c = r->claims[(size_t)i];
+  if (n) *n = (int)c.reqC.size();
+  if (reqs) *reqs = c.reqC.data();
   return KS_OK;
 }
 int ks_results_num_existing_nodes(const ks_results* r) { return (int)r->nodes.size(); }

@@ -749,8 +749,12 @@ std::vector<int> bits_to_its(const Host& h, int tpl, const int32_t* bits) {
 // rsOf(sim): NewNodeClaims[0]'s requirement record of simulation `sim` (kept in the workspace of the
 // GPU that ran it; ks_cons_needed_sims lists the simulations whose record the output needs).
 using RsFn = std::function<const uint32_t*(int)>;
+// clk: the methods' timeouts on a virtual clock that advances clk->sim_seconds per simulation the replay
+// consults (MultiNodeConsolidation's 1 min, multinodeconsolidation.go:34,99-110; SingleNodeConsolidation's
+// 3 min, singlenodeconsolidation.go:29,58-65); null or sim_seconds 0: the clock never passes a timeout.
 std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool allSims, const RsFn& rsOf,
-                        bool withCandidates = true) {
+                        bool withCandidates = true, const ks_cons_clock* clk = nullptr) {
+  const double simS = clk ? clk->sim_seconds : 0.0;
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
   const int per = c.per_rank(world);
@@ -847,7 +851,10 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
         run(c.sim_of_multi(mid));
         multiRan.insert(mid);
       }
+    double now = 0;  // the search's clock; timeout = start + MultiNodeConsolidationTimeoutDuration
     while (lo <= hi) {
+      if (clk && now > clk->multi_timeout_s) break;  // m.clock.Now().After(timeout): lastSavedCommand
+      now += simS;
       const int mid = (lo + hi) / 2;
       const int sim = c.sim_of_multi(mid);
       run(sim);
@@ -872,13 +879,20 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
   // SingleNodeConsolidation.ComputeCommand: the first candidate whose simulation yields an action
   int singleSim = -1;
   std::string singleSims;
+  double now = 0;  // ComputeCommand's clock; timeout = start + SingleNodeConsolidationTimeoutDuration
+  bool timedOut = false;
   for (int i = 0; i < n; i++) {
     if (singleSim >= 0 && !allSims) break;
+    if (clk && singleSim < 0 && !timedOut && now > clk->single_timeout_s) {
+      timedOut = true;  // s.clock.Now().After(timeout): abandon with no command
+      if (!allSims) break;
+    }
+    if (!timedOut) now += simS;
     const int sim = c.sim_of_single(i);
     run(sim);
     singleSims += (i ? "," : "") + simJSON(sim);
     const int a = rec(sim)[RF_ACTION];
-    if (singleSim >= 0 || a == CA_ERROR || a == CA_NOOP) continue;
+    if (singleSim >= 0 || timedOut || a == CA_ERROR || a == CA_NOOP) continue;
     singleSim = sim;
   }
   o += "],\"multi\":{\"command\":" + cmdJSON(multiSim, multiErr) + ",\"sims\":[" + multiSims + "]}";
@@ -1130,6 +1144,11 @@ int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out) {
 
 int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
                    char** json_out) {
+  return ks_cons_decide_clock(c, records, world, flags, rs_table, nullptr, json_out);
+}
+
+int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
+                         const ks_cons_clock* clock, char** json_out) {
   API_TRY
   if (!c || !records || !json_out || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
   const int32_t* recs = (const int32_t*)records;
@@ -1139,7 +1158,7 @@ int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, 
   std::map<int, const uint32_t*> table;
   for (size_t i = 0; i < need.size(); i++) table[need[i]] = rs_table + i * c->pb->host.dims.RSW;
   *json_out = strdup(decide_json(*c, recs, world, all_sims, [&](int sim) { return table.at(sim); },
-                                 (flags & KS_CONS_CANDIDATES) != 0)
+                                 (flags & KS_CONS_CANDIDATES) != 0, clock)
                          .c_str());
   return KS_OK;
   API_CATCH

@@ -12,9 +12,10 @@ import json
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# KS_LIB_VARIANT=stats loads the diagnostic build with per-phase cycle counters.
-_LIB_PATH = os.path.join(_HERE, "libkarpenter_amd_stats.so" if os.environ.get("KS_LIB_VARIANT") == "stats"
-                         else "libkarpenter_amd.so")
+# KS_LIB_VARIANT=stats loads the diagnostic build with per-phase cycle counters; =asan the ASan + UBSan
+# build of the host translation units (make -C karpenter-sigs_amd asan; scripts/asan_cpu_suite.sh).
+_VARIANTS = {"stats": "libkarpenter_amd_stats.so", "asan": "libkarpenter_amd_asan.so"}
+_LIB_PATH = os.path.join(_HERE, _VARIANTS.get(os.environ.get("KS_LIB_VARIANT", ""), "libkarpenter_amd.so"))
 _lib = None
 
 KS_ERRORS = {-1: "KS_ERR_PARSE", -2: "KS_ERR_UNSUPPORTED", -3: "KS_ERR_CAPACITY", -4: "KS_ERR_HIP",
@@ -31,6 +32,11 @@ class _Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("simulation_mode", ctypes.c_int), ("replicas", ctypes.c_int),
                 ("timing_only", ctypes.c_int), ("lds_budget", ctypes.c_int),
                 ("reserved", ctypes.c_int * 3)]
+
+
+class _Clock(ctypes.Structure):  # ks_cons_clock
+    _fields_ = [("multi_timeout_s", ctypes.c_double), ("single_timeout_s", ctypes.c_double),
+                ("sim_seconds", ctypes.c_double)]
 
 
 def library_path():
@@ -171,6 +177,7 @@ def _cons_lib():
         l.ks_cons_run.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_Opts), vp, ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_double)]
         l.ks_cons_decide.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+        l.ks_cons_decide_clock.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(_Clock), ctypes.POINTER(vp)]
         l.ks_cons_requirement_words.argtypes = [vp]
         l.ks_cons_needed_sims.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
         l.ks_cons_claim_requirements.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
@@ -253,10 +260,11 @@ class Consolidator:
         _check(l.ks_cons_claim_requirements(self._h, sim, out))
         return bytes(out)
 
-    def decide(self, records, world=1, all_sims=False, fetch=None, candidates=True):
+    def decide(self, records, world=1, all_sims=False, fetch=None, candidates=True, clock=None):
         """Sequential selection over the gathered records ([rank][slot] layout, bytes).  fetch(sim)
         returns the requirement record bytes of a needed simulation (default: this handle's run);
-        candidates=False leaves out the ordered candidate list (the commands are unchanged)."""
+        candidates=False leaves out the ordered candidate list (the commands are unchanged);
+        clock=(multi_timeout_s, single_timeout_s, sim_seconds): the methods' timeouts on a virtual clock."""
         l = _cons_lib()
         need = self.needed_sims(records, world, all_sims)
         fetch = fetch or self.claim_requirements
@@ -265,8 +273,13 @@ class Consolidator:
         buf = ctypes.create_string_buffer(bytes(records), len(records))
         js = ctypes.c_void_p()
         flags = (1 if all_sims else 0) | (2 if candidates else 0)
-        _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, flags,
-                                ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(js)))
+        if clock is None:
+            _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, flags,
+                                    ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(js)))
+        else:
+            clk = _Clock(*clock)
+            _check(l.ks_cons_decide_clock(self._h, ctypes.cast(buf, ctypes.c_void_p), world, flags,
+                                          ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(clk), ctypes.byref(js)))
         return json.loads(_take_str(js))
 
     def validate(self, command, device=-1):
@@ -289,9 +302,9 @@ class Consolidator:
         buf = ctypes.create_string_buffer(bytes(records), len(records))
         return _cons_lib().ks_cons_records_alg_bytes(self._h, ctypes.cast(buf, ctypes.c_void_p), world)
 
-    def consolidate(self, all_sims=False, device=-1):
+    def consolidate(self, all_sims=False, device=-1, clock=None):
         recs, ms = self.run(0, 1, device)
-        doc = self.decide(recs, 1, all_sims)
+        doc = self.decide(recs, 1, all_sims, clock=clock)
         doc["kernel_ms"] = ms
         return doc
 

@@ -5,7 +5,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "_build", "liboracle.so")
+_LIB = os.path.join(_HERE, "_build", "liboracle_asan.so" if os.environ.get("KS_ORACLE_VARIANT") == "asan"
+                    else "liboracle.so")
 _lib = None
 
 
@@ -28,6 +29,9 @@ def lib():
         l.oref_consolidate_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_double)]
         l.oref_consolidate_json.restype = ctypes.c_int
+        l.oref_consolidate_clock_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                                  ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]
+        l.oref_consolidate_clock_json.restype = ctypes.c_int
         l.oref_set_tie_mode.argtypes = [ctypes.c_int, ctypes.c_ulonglong]
         l.oref_set_tie_mode.restype = ctypes.c_int
         l.oref_cluster_state.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
@@ -69,8 +73,9 @@ def time_solve(snapshot, reps):
     return secs.value
 
 
-def consolidate(snapshot, all_sims=False):
-    """Oracle multi-node then single-node consolidation over a cluster snapshot; returns (doc, seconds).
+def consolidate(snapshot, all_sims=False, with_stats=False):
+    """Oracle multi-node then single-node consolidation over a cluster snapshot; returns (doc, seconds)
+    (with_stats: (doc, seconds, stats), stats = {"algBytesRef": SURVEY §8d bytes over the simulations run}).
     all_sims: simulate every candidate / prefix (what the GPU computes) and report each outcome."""
     l = lib()
     s = snapshot if isinstance(snapshot, str) else json.dumps(snapshot)
@@ -78,7 +83,22 @@ def consolidate(snapshot, all_sims=False):
     secs = ctypes.c_double()
     if l.oref_consolidate_json(s.encode(), 1 if all_sims else 0, ctypes.byref(out), ctypes.byref(secs)) != 0:
         raise RuntimeError("oracle: " + l.oref_last_error().decode())
-    return json.loads(_take(out)), secs.value
+    doc = json.loads(_take(out))
+    stats = doc.pop("stats", {})
+    return (doc, secs.value, stats) if with_stats else (doc, secs.value)
+
+
+def consolidate_clock(snapshot, multi_timeout_s, single_timeout_s, sim_seconds, all_sims=False):
+    """consolidate() with the methods' timeouts on a virtual clock advancing sim_seconds per simulation."""
+    l = lib()
+    s = snapshot if isinstance(snapshot, str) else json.dumps(snapshot)
+    out = ctypes.c_void_p()
+    if l.oref_consolidate_clock_json(s.encode(), 1 if all_sims else 0, multi_timeout_s, single_timeout_s, sim_seconds,
+                                     ctypes.byref(out)) != 0:
+        raise RuntimeError("oracle: " + l.oref_last_error().decode())
+    doc = json.loads(_take(out))
+    doc.pop("stats", None)
+    return doc
 
 
 def set_tie_mode(mode, seed=0):

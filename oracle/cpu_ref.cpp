@@ -1041,6 +1041,7 @@ class Scheduler {
   explicit Scheduler(Problem& pb) : pb_(pb) {
     nodeID_ = pb.hostnameSeed;
     buildTopology();
+    initAlgBytes();
     // NewScheduler (scheduler.go:49-83)
     for (auto& np : pb.nodePools) if (np.preferNoSchedule) toleratePreferNoSchedule_ = true;
     for (size_t t = 0; t < pb.templates.size(); t++) {  // getDaemonOverhead :324-341
@@ -1129,6 +1130,7 @@ class Scheduler {
   int64_t nodeIDCounter() const { return nodeID_; }
 
   long long attempts = 0;  // statistics: NodeClaim.Add calls
+  int64_t algBytes() const { return algBytes_; }
 
  private:
   Problem& pb_;
@@ -1167,6 +1169,49 @@ class Scheduler {
   vector<ResourceList> reqsCache_;
 
   ResourceList CeilingRequestsFor(int p) { return RequestsForPods({&pb_.pods[p]}); }
+
+  // SURVEY.md §8d algorithmic bytes: the bytes of every candidate the reference scans per pod step, in a
+  // fixed-width encoding (R int64 resource vectors, W 32-bit requirement words per object with
+  // W = sum over its keys of ceil((|V_key| + 1) / 32) + 1, a T-bit instance-type set):
+  //   existing node tried   16R + 4W_node + 8 per topology group evaluated
+  //   NodeClaim tried       16R + 4W_claim + T/8 (+ per remaining instance type scanned 8R + 4W_it + 4)
+  //   commit                 8R + 4W + T/8
+  // A measurement of this restatement (test infrastructure), not part of the reference.
+  int64_t algBytes_ = 0;
+  int64_t R_ = 0, T8_ = 0;
+  map<string, int64_t> keyWords_;
+  vector<int64_t> itW_;
+  void initAlgBytes() {
+    map<string, set<string>> uni;
+    set<string> res;
+    auto addReqs = [&](const Requirements& r) {
+      for (auto& kv : r.m) for (auto& v : kv.second.values) uni[kv.first].insert(v);
+      for (auto& kv : r.m) uni[kv.first];
+    };
+    for (auto& it : pb_.its) {
+      addReqs(it.reqs);
+      for (auto& kv : it.allocatable) res.insert(kv.first);
+    }
+    for (auto& t : pb_.templates) addReqs(t.reqs);
+    for (auto& n : pb_.nodes) for (auto& kv : n.labels) uni[kv.first].insert(kv.second);
+    for (auto& p : pb_.pods) {
+      Pod cp = p;
+      addReqs(NewPodRequirements(cp));
+      for (auto& kv : RequestsForPods({&p})) res.insert(kv.first);
+    }
+    for (auto& kv : uni) keyWords_[kv.first] = ((int64_t)kv.second.size() + 1 + 31) / 32 + 1;
+    R_ = (int64_t)res.size();
+    T8_ = ((int64_t)pb_.its.size() + 7) / 8;
+    for (auto& it : pb_.its) itW_.push_back(W(it.reqs));
+  }
+  int64_t W(const Requirements& r) const {
+    int64_t w = 0;
+    for (auto& kv : r.m) {
+      auto k = keyWords_.find(kv.first);
+      w += k == keyWords_.end() ? 2 : k->second;
+    }
+    return w;
+  }
 
   bool byCPUAndMemoryDescending(int a, int b) {  // queue.go:83-112
     const ResourceList& l = reqsCache_[a];
@@ -1251,6 +1296,13 @@ class Scheduler {
   bool existingAdd(ExistingNode& n, int p) {
     Pod& pod = pb_.pods[p];
     const StateNodeSnap& sn = pb_.nodes[n.node];
+    algBytes_ += 16 * R_ + 4 * W(n.reqs);
+    const int64_t applied0 = topo_.applied;
+    struct Touch {  // the topology groups AddRequirements evaluated, however the attempt ends
+      Scheduler* s;
+      int64_t a0;
+      ~Touch() { s->algBytes_ += 8 * (s->topo_.applied - a0); }
+    } touch{this, applied0};
     if (!Tolerates(sn.taints, pod).empty()) return false;
     vector<HostPort> hp = GetHostPorts(pod);
     string key = pod.ns + "/" + pod.name;
@@ -1273,6 +1325,7 @@ class Scheduler {
     n.pods.push_back(p);
     n.requests = requests;
     n.reqs = nodeReqs;
+    algBytes_ += 8 * R_ + 4 * W(nodeReqs) + T8_;
     topo_.Record(pod, nodeReqs, nullptr);
     n.hostPorts.Add(key, hp);
     n.volumes.Add(vols);  // existingnode.go:122
@@ -1311,6 +1364,12 @@ class Scheduler {
     attempts++;
     Pod& pod = pb_.pods[p];
     Result res;
+    algBytes_ += 16 * R_ + 4 * W(n.reqs) + T8_;
+    struct Touch {
+      Scheduler* s;
+      int64_t a0;
+      ~Touch() { s->algBytes_ += 8 * (s->topo_.applied - a0); }
+    } touch{this, topo_.applied};
     Errs te = Tolerates(pb_.templates[n.tpl].taints, pod);
     if (!te.empty()) { res.ok = false; res.errs = {joinErrs(te)}; return res; }
     vector<HostPort> hp = GetHostPorts(pod);
@@ -1340,6 +1399,7 @@ class Scheduler {
     ResourceList podReq = RequestsForPods({&pod});
     ResourceList requests = Merge({&n.requests, &podReq});
     FilterResults f = filterInstanceTypes(n.itOptions, ncReqs, requests);
+    for (int i : n.itOptions) algBytes_ += 8 * R_ + 4 * itW_[(size_t)i] + 4;
     if (f.remaining.empty()) {
       ResourceList cum = Merge({&n.daemonResources, &podReq});
       res.ok = false;
@@ -1351,6 +1411,7 @@ class Scheduler {
     n.itOptions = f.remaining;
     n.requests = requests;
     n.reqs = ncReqs;
+    algBytes_ += 8 * R_ + 4 * W(ncReqs) + T8_;
     topo_.Record(pod, ncReqs, &pb_.wellKnown);
     n.hostPorts.Add(key, hp);
     return res;
@@ -1511,7 +1572,7 @@ string Scheduler::ResultsJSON() const {
     o += ":";
     ojson::quote(o, joinErrs(errors_[p].errs));
   }
-  o += "},\"stats\":{\"claimAddCalls\":" + std::to_string(attempts) + "}}";
+  o += "},\"stats\":{\"claimAddCalls\":" + std::to_string(attempts) + ",\"algBytesRef\":" + std::to_string(algBytes_) + "}}";
   return o;
 }
 
@@ -1651,6 +1712,24 @@ int oref_consolidate_json(const char* snapshot, int all_sims, char** out, double
     std::string r = oref::consolidateJSON(cp, all_sims != 0);
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (out) *out = dupstr(r);
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// consolidate_json with the methods' timeouts on a virtual clock (ConsClock).
+int oref_consolidate_clock_json(const char* snapshot, int all_sims, double multi_timeout_s, double single_timeout_s,
+                                double sim_seconds, char** out) {
+  try {
+    ojson::Value root = ojson::parse(snapshot);
+    oref::ConsProblem cp = oref::parseConsProblem(root);
+    oref::ConsClock clk;
+    clk.multiTimeout = multi_timeout_s;
+    clk.singleTimeout = single_timeout_s;
+    clk.simSeconds = sim_seconds;
+    if (out) *out = dupstr(oref::consolidateJSON(cp, all_sims != 0, &clk));
     return 0;
   } catch (const std::exception& e) {
     g_err = e.what();

@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "karpenter-sigs_amd"))
 from karpenter_amd import synth  # noqa: E402
 
-OUT = os.path.join(HERE, "full_size_digests.json")
+OUT = os.environ.get("KS_DIGEST_OUT", os.path.join(HERE, "full_size_digests.json"))
 
 
 def canon(x):
@@ -76,11 +76,15 @@ def main(names):
         t = time.time()
         snap = json.dumps(CONFIGS[name]())
         if name == "C5":
-            doc, secs = bridge.consolidate(snap, all_sims=True)
+            doc, secs, stats = bridge.consolidate(snap, all_sims=True, with_stats=True)
             out[name] = cons_digest(doc)
         else:
             res, secs = bridge.solve(snap)
+            stats = res.get("stats", {})
             out[name] = solve_digest(res)
+        # SURVEY.md §8d algorithmic bytes of the reference's scan (the oracle's count), for bench.py's
+        # roofline where the oracle is too slow to run inside the benchmark
+        out[name]["algBytesRef"] = stats.get("algBytesRef")
         out[name]["snapshot"] = hashlib.sha256(snap.encode()).hexdigest()
         out[name]["oracle_seconds"] = round(secs, 1)
         print("%s: %.1f s oracle, %.1f s wall" % (name, secs, time.time() - t), flush=True)

@@ -337,3 +337,18 @@ def test_validate_keeps_the_pass_launch():
     want, _ = bridge.consolidate(snap, all_sims=True)
     got = dict(before)
     assert _first_diff(want, got) is None
+
+
+@pytest.mark.parametrize("clock", [(60.0, 180.0, 0.0), (60.0, 180.0, 25.0), (60.0, 180.0, 100.0), (60.0, 180.0, 250.0),
+                                   (1.0, 2.0, 0.5)])
+@pytest.mark.parametrize("which", [("c", 1), ("c", 6), ("t", 1), ("t", 24)])
+def test_consolidation_timeouts_parity(clock, which):
+    """MultiNodeConsolidation's 1 min and SingleNodeConsolidation's 3 min timeouts (multinodeconsolidation.go:
+    99-110: return the last saved command; singlenodeconsolidation.go:58-65: abandon) on a virtual clock
+    that advances per simulation the sequential replay consults: GPU replay == oracle."""
+    case = [c for c in (CASES if which[0] == "c" else TOPO_CASES) if c["seed"] == which[1]][0]
+    snap = json.dumps(synth.cluster_snapshot(**case))
+    want = bridge.consolidate_clock(snap, *clock)
+    got = Consolidator(snap).consolidate(clock=clock)
+    got.pop("kernel_ms")
+    assert _first_diff(want, got) is None, _first_diff(want, got)
