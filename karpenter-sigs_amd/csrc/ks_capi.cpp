@@ -581,6 +581,7 @@ int ks_problem_create(const char* json, size_t len, ks_problem** out) {
   ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
   std::unique_ptr<ks_problem> pb(new ks_problem());
   pb->host.build(root);
+  ksjson::release_async(std::move(root));
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw KsError(KS_ERR_HIP, "no HIP device visible");
   HIPCHK(hipGetDevice(&pb->device));

@@ -247,6 +247,7 @@ namespace {
 
 // Parse the cluster snapshot into the resident problem + candidates + sims.
 void build_cons(ks_cons& c, const Value& rootIn) {
+  PhaseTimer pt("build_cons");
   if (!rootIn.is_obj()) throw KsError(KS_ERR_PARSE, "snapshot is not an object");
   // "cluster": {nodeClaims, nodes, pods} listings instead of "stateNodes": derive the StateNodes the
   // cluster-state informers would hold (ks_cluster_state)
@@ -263,11 +264,21 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   auto pods = std::make_shared<ksjson::Array>();
   std::vector<std::vector<int>> nodePods;  // per snapshot node: global pod indices (GetNodePods)
   std::vector<PodH> podMeta;
-  if (const Value* pv = root.get("pendingPods"))
-    for (auto& v : pv->arr()) {
+  // every pod of the snapshot, parsed by worker threads (pods are independent)
+  std::vector<const Value*> allPodV;
+  const Value* pendV = root.get("pendingPods");
+  for (auto& v : pendV ? pendV->arr() : ksjson::Array{}) allPodV.push_back(&v);
+  for (auto& nv : nodesV ? nodesV->arr() : ksjson::Array{})
+    if (const Value* ps = nv.get("pods"))
+      for (auto& pv : ps->arr()) allPodV.push_back(&pv);
+  std::vector<PodH> allPods(allPodV.size());
+  parallel_for((int)allPodV.size(), 256, [&](int i) { allPods[(size_t)i] = parse_pod(*allPodV[(size_t)i]); });
+  size_t next = 0;
+  if (pendV)
+    for (auto& v : pendV->arr()) {
       c.pending.push_back((int)pods->size());
       pods->push_back(v);
-      podMeta.push_back(parse_pod(v));
+      podMeta.push_back(std::move(allPods[next++]));
     }
   std::map<std::string, int> nodeByName;
   std::vector<char> deletingNode;
@@ -282,7 +293,7 @@ void build_cons(ks_cons& c, const Value& rootIn) {
     std::vector<int> mine;
     if (const Value* ps = nv.get("pods"))
       for (auto& pv : ps->arr()) {
-        PodH p = parse_pod(pv);
+        PodH& p = allPods[next++];
         if (p.ownedByNode || p.ownedByDaemonSet || p.terminal || p.deleting) continue;  // node.go:32-53
         mine.push_back((int)pods->size());
         pods->push_back(pv);
@@ -293,6 +304,7 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   for (size_t i = 0; i < nodePods.size(); i++)
     if (deletingNode[i]) for (int p : nodePods[i]) c.deleting.push_back(p);
 
+  pt.mark("parse pods + nodes");
   // the Solve snapshot the problem is encoded from
   Value solveRoot;
   solveRoot.kind = Value::Obj;
@@ -312,8 +324,12 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   for (int p : c.pending) always.insert(podMeta[(size_t)p].uid);
   for (int p : c.deleting) always.insert(podMeta[(size_t)p].uid);
   h.topoExcluded = &always;
+  h.preParsedPods = &podMeta;  // the Solve snapshot's "pods", already parsed above (moved into h.pods)
   h.build(solveRoot);
   h.topoExcluded = nullptr;
+  h.preParsedPods = nullptr;
+  const std::vector<PodH>& podH = h.pods;
+  pt.mark("Host::build");
   if (h.dims.dupUids) throw KsError(KS_ERR_UNSUPPORTED, "consolidation snapshot has duplicate pod UIDs");
   c.hostnameSeed = h.hostnameSeed;
   std::map<std::string, int> hostNode;  // node name -> host.nodes index (sorted order)
@@ -384,7 +400,7 @@ void build_cons(ks_cons& c, const Value& rootIn) {
       k.it = pt->second.at(lit->second);
       k.pods = nodePods[(size_t)it->second];
       double cost = 0;
-      for (int p : k.pods) cost += eviction_cost(podMeta[(size_t)p]);  // disruptionCost helpers.go:170-176
+      for (int p : k.pods) cost += eviction_cost(podH[(size_t)p]);  // disruptionCost helpers.go:170-176
       double remaining = 1.0;                                           // lifetimeRemaining types.go:136-145
       auto ex = expire.find(k.pool);
       if (ex != expire.end()) {
@@ -395,9 +411,10 @@ void build_cons(ks_cons& c, const Value& rootIn) {
       k.cost = cost * remaining;
       // filterCandidates (helpers.go:47-71): a PDB allowing no eviction or a do-not-disrupt pod blocks it
       bool blocked = false;
-      for (int p : k.pods) blocked = blocked || !can_evict(pdbs, podMeta[(size_t)p]) || do_not_disrupt(podMeta[(size_t)p]);
+      for (int p : k.pods) blocked = blocked || !can_evict(pdbs, podH[(size_t)p]) || do_not_disrupt(podH[(size_t)p]);
       if (!blocked) (passOk ? cands : valOnly).push_back(std::move(k));
     }
+  pt.mark("candidates");
   // sort.Slice(candidates, disruptionCost <): pdqsort only observes less(), so the costs' dense ranks
   // reproduce its swap sequence exactly.
   {
@@ -435,6 +452,7 @@ void build_cons(ks_cons& c, const Value& rootIn) {
     c.sims.push_back(s);
   }
   c.recWords = rec_words(h.dims.TW);
+  pt.mark("sort + sims");
 }
 
 // Offerings.Get(capacityType, zone) (all offerings, available or not): first match
@@ -1019,6 +1037,7 @@ int ks_cons_create(const char* json, size_t len, ks_cons** out) {
   ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
   std::unique_ptr<ks_cons> c(new ks_cons());
   build_cons(*c, root);
+  ksjson::release_async(std::move(root));
   ks_problem& pb = *c->pb;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw KsError(KS_ERR_HIP, "no HIP device visible");
@@ -1048,9 +1067,14 @@ int ks_cons_create(const char* json, size_t len, ks_cons** out) {
 int ks_cons_inspect(const char* json, size_t len, char** out) {
   API_TRY
   if (!json || !out) throw KsError(KS_ERR_ARG, "null argument");
+  PhaseTimer pt("ks_cons_inspect");
   ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  pt.mark("json parse");
   ks_cons c;
   build_cons(c, root);
+  pt.mark("build_cons");
+  root = ksjson::Value();
+  pt.mark("json free");
   std::string o = "{\"candidates\":[";
   for (size_t i = 0; i < (size_t)c.nPass; i++) {
     if (i) o += ",";

@@ -465,10 +465,17 @@ std::string Host::placeholder(int64_t id) const {
 // build: the NewScheduler half of the boundary
 // ---------------------------------------------------------------------------------------------
 void Host::build(const Value& root) {
+  PhaseTimer pt("Host::build");
   if (auto* t = root.get("topology"); t && !t->is_null())
     throw KsError(-2, "explicit topology groups are not accepted: pass the pods' topology spread / pod "
                       "(anti-)affinity terms and the cluster's bound pods (clusterPods, clusterNodes)");
-  if (auto* cps = root.get("clusterPods")) for (auto& v : cps->arr()) clusterPods.push_back(parse_pod(v));
+  auto parsePods = [](const Value* v, std::vector<PodH>& out) {  // independent per pod: worker threads
+    if (!v) return;
+    const ksjson::Array& a = v->arr();
+    out.resize(a.size());
+    parallel_for((int)a.size(), 256, [&](int i) { out[(size_t)i] = parse_pod(a[(size_t)i]); });
+  };
+  parsePods(root.get("clusterPods"), clusterPods);
   if (auto* nss = root.get("namespaces"))  // the cluster's Namespace list, for namespaceSelector terms
     for (auto& v : nss->arr()) {
       const Value* md = v.get("metadata") ? v.get("metadata") : &v;
@@ -486,6 +493,7 @@ void Host::build(const Value& root) {
   if (auto* hs = root.get("hostnameSeed")) hostnameSeed = hs->i64();
   if (auto* et = root.get("emptyTopology")) emptyTopology = et->boolean();
 
+  pt.mark("head");
   // --- instance types
   if (auto* v = root.get("instanceTypes"))
     for (auto& e : v->arr()) {
@@ -587,11 +595,14 @@ void Host::build(const Value& root) {
     if (a.initialized != b.initialized) return a.initialized;
     return a.name < b.name;
   });
+  pt.mark("its+templates+nodes");
   if (auto* v = root.get("daemonSetPods")) for (auto& e : v->arr()) daemons.push_back(parse_pod(e));
-  if (auto* v = root.get("pods")) for (auto& e : v->arr()) pods.push_back(parse_pod(e));
+  if (preParsedPods) pods = std::move(*preParsedPods);
+  else parsePods(root.get("pods"), pods);
   if (auto* v = root.get("volumeDrivers"))
     for (auto& kv : v->obj()) volumeDrivers[kv.first] = kv.second.str();
 
+  pt.mark("parse pods");
   // --- universe of keys and values
   internKey(kHostname);
   internKey(kZone);
@@ -708,6 +719,7 @@ void Host::build(const Value& root) {
   L.vIsInt = vIsInt.data();
   L.vInt = vInt.data();
 
+  pt.mark("universe");
   // --- resources
   std::map<std::string, std::vector<__int128>> seen;
   auto visitQ = [&](const QList& q) { for (auto& kv : q) seen[kv.first].push_back(kv.second.n); };
@@ -860,6 +872,7 @@ void Host::build(const Value& root) {
     }
   }
 
+  pt.mark("resources+taints+its+templates");
   // --- existing nodes (NewExistingNode, calculateExistingNodeClaims)
   int N = (int)nodes.size();
   dims.N = N;
@@ -875,8 +888,12 @@ void Host::build(const Value& root) {
   // A node's initial entries whose pod key is also a pod being scheduled (e.g. a re-created StatefulSet
   // pod whose predecessor still holds the ports) get universe elements of their own, tagged with that
   // key: the pod's conflict mask leaves them out, and its commit clears them (pod_hpo).
+  bool anyPorts = false;
+  for (auto& p : pods) anyPorts = anyPorts || !p.ports.empty();
+  for (auto& n : nodes) anyPorts = anyPorts || !n.hostPorts.empty();
   std::map<std::string, int> podKeyCount;
-  for (auto& p : pods) podKeyCount[p.ns + "/" + p.name]++;
+  if (anyPorts)
+    for (auto& p : pods) podKeyCount[p.ns + "/" + p.name]++;
   hostPortOwner.clear();
   auto internHP = [&](const HostPortH& h, const std::string& owner) {
     for (size_t i = 0; i < hostPortUniverse.size(); i++)
@@ -896,6 +913,7 @@ void Host::build(const Value& root) {
       internHP(e.second, pending ? e.first : "");
     }
   for (auto& p : pods) {  // Add on a NodeClaim replaces a same-key pod's entries: not modelled
+    if (!anyPorts) break;
     const std::string key = p.ns + "/" + p.name;
     if (podKeyCount[key] > 1 && (!p.ports.empty() || ownerKeys.count(key)))
       throw KsError(-2, "pods being scheduled share the key " + key + " and host ports");
@@ -1011,6 +1029,7 @@ void Host::build(const Value& root) {
     std::copy(lab.begin(), lab.end(), tab.n_rs0.begin() + (size_t)i * dims.RSW);
     taintMask(n.taints, &tab.n_taint[(size_t)i * 2]);
   }
+  pt.mark("nodes+hostports+volumes");
   // --- limits: remaining = Limits - capacity of existing nodes in the pool
   int NP = (int)pools.size();
   dims.NPOOL = NP;
@@ -1038,6 +1057,7 @@ void Host::build(const Value& root) {
     }
   }
 
+  pt.mark("limits");
   // --- pods: requests, queue sort keys, relaxation chains
   int P = (int)pods.size();
   dims.P = P;
@@ -1052,6 +1072,7 @@ void Host::build(const Value& root) {
   tab.pod_hpo.assign(std::max(P, 1), 0);
   for (int i = 0; i < P; i++) {
     tab.pod_flags[i] = pods[i].provisionable ? PF_PROVISIONABLE : 0;
+    if (hostPortUniverse.empty()) continue;
     const std::string key = pods[i].ns + "/" + pods[i].name;
     for (size_t u = 0; u < hostPortUniverse.size(); u++)
       if (hostPortOwner[u] == key) tab.pod_hpo[i] |= 1ull << u;  // its own entries: never a conflict, replaced by Add
@@ -1072,18 +1093,21 @@ void Host::build(const Value& root) {
   int cpuR = resId.count("cpu") ? resId["cpu"] : -1, memR = resId.count("memory") ? resId["memory"] : -1;
   std::vector<std::array<int64_t, 4>> sk(P);
   int S = 0;
-  for (int i = 0; i < P; i++) {
+  states.assign((size_t)P, {});
+  // per pod (independent: worker threads): requests, queue key, relaxation chain
+  parallel_for(P, 128, [&](int i) {
     PodH& p = pods[i];
     vec(p.requests, &tab.pod_req[(size_t)i * R]);
     int64_t cpu = cpuR >= 0 ? tab.pod_req[(size_t)i * R + cpuR] : 0;
     int64_t mem = memR >= 0 ? tab.pod_req[(size_t)i * R + memR] : 0;
     int64_t* k4 = &tab.pod_sortkey[(size_t)i * 4];
+    const int uidRank = uids.at(p.uid);
     k4[0] = -cpu;  // descending
     k4[1] = -mem;
     k4[2] = p.created;
-    k4[3] = uids[p.uid];
+    k4[3] = uidRank;
     sk[i] = {k4[0], k4[1], k4[2], k4[3]};
-    tab.pod_uid[i] = uids[p.uid];
+    tab.pod_uid[i] = uidRank;
     // relaxation chain
     PodH cur = p;
     std::vector<PodState> chain;
@@ -1137,10 +1161,12 @@ void Host::build(const Value& root) {
       }
       if (!relaxed) break;
     }
+    states[(size_t)i] = std::move(chain);
+  });
+  for (int i = 0; i < P; i++) {
     tab.pod_state0[i] = S;
-    tab.pod_nstate[i] = (int)chain.size();
-    S += (int)chain.size();
-    states.push_back(std::move(chain));
+    tab.pod_nstate[i] = (int)states[(size_t)i].size();
+    S += (int)states[(size_t)i].size();
   }
   for (int c = 0; c < 4; c++) {
     int64_t mn = 0, mx = 0;
@@ -1183,8 +1209,10 @@ void Host::build(const Value& root) {
       hostQueue = val;
     }
   }
+  pt.mark("pods encode");
   dims.S = std::max(S, 1);
   buildTopology();
+  pt.mark("topology");
   // Topology ownership is keyed by UID (TopologyGroup.owners, topologygroup.go; Topology.Update removes
   // the UID from every group first, topology.go:91-122): pods sharing a UID share their groups, which
   // the per-pod relaxation states here do not model.

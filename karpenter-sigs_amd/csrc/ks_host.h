@@ -1,5 +1,8 @@
 // ks_host.h — host-side problem model, encoder and renderer (declarations).
 #pragma once
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <array>
 #include <cstdint>
 #include <functional>
@@ -160,6 +163,7 @@ struct Host {
   // Consolidation view (ks_cons.cpp): NewTopology excludes only these UIDs (the pods every simulation
   // schedules); each simulation then subtracts its candidates' pods from the counts it records below.
   const std::set<std::string>* topoExcluded = nullptr;
+  std::vector<PodH>* preParsedPods = nullptr;  // set: the snapshot's "pods" already parsed (moved in by build)
   std::map<std::string, std::vector<std::pair<int, int>>> topoContrib;  // cluster pod UID -> (group, value) counted
   std::map<std::string, uint64_t> topoInvOwner;                         // cluster pod UID -> inverse groups it owns
   std::vector<int> topoInvOwners;                                       // per group: owning cluster pods
@@ -219,6 +223,20 @@ struct Host {
   void intern(const std::string& key, const std::string& val);
   void internKey(const std::string& key);
   std::map<std::string, std::set<std::string>> valueSet_;
+};
+
+// Host-side phase timing for diagnostics: KS_HOST_TIMING=1 prints each mark's milliseconds to stderr.
+struct PhaseTimer {
+  const char* what;
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseTimer(const char* w) : what(w), on(std::getenv("KS_HOST_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* phase) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[%s] %-34s %8.2f ms\n", what, phase, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
 };
 
 std::string qlist_json(const QList& l);  // resources.String (pretty.Concise)

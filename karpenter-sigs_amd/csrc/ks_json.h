@@ -1,23 +1,46 @@
-// ks_json.h — minimal JSON DOM reader/writer for snapshot input and results output.
-// Objects keep keys in a std::map (Go maps are unordered; every consumer here either sorts or
-// ignores order), arrays keep order. Numbers are kept as their literal text so int64 / float64
-// callers can parse them exactly.
+// ks_json.h — JSON DOM reader/writer for snapshot input and results output.
+// Objects are key-sorted flat vectors (iteration order equals a std::map's: Go maps are unordered and
+// every consumer here either sorts or ignores order; a duplicate key keeps its last value), arrays keep
+// order.  Numbers are kept as their literal text so int64 / float64 callers can parse them exactly.
+// Snapshots are tens of MB (C5: 45 MB, 100k pods): large arrays near the top of the document (pods,
+// stateNodes, clusterPods) are split at element boundaries by a skip scan and their elements parsed by
+// worker threads (ks_parallel.h), each into its own slot.
 #pragma once
+#include <algorithm>
 #include <cctype>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
-#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <string_view>
+#include <thread>
+#include <utility>
 #include <vector>
+
+#include "ks_parallel.h"
 
 namespace ksjson {
 
 struct Value;
-using Object = std::map<std::string, Value>;
 using Array = std::vector<Value>;
+
+// Key-sorted (key, value) pairs: the subset of std::map's interface the decoders use.
+struct Object {
+  using Entry = std::pair<std::string, Value>;
+  std::vector<Entry> e;
+  Object() = default;
+  std::vector<Entry>::const_iterator begin() const { return e.begin(); }
+  std::vector<Entry>::const_iterator end() const { return e.end(); }
+  std::vector<Entry>::iterator begin() { return e.begin(); }
+  std::vector<Entry>::iterator end() { return e.end(); }
+  size_t size() const { return e.size(); }
+  bool empty() const { return e.empty(); }
+  const Value* find(std::string_view k) const;
+  Value& operator[](const std::string& k);
+  void finish();  // sort by key; on duplicates the last one parsed wins
+};
 
 struct Value {
   enum Kind { Null, Bool, Number, String, Arr, Obj } kind = Null;
@@ -30,11 +53,7 @@ struct Value {
   bool is_obj() const { return kind == Obj; }
   bool is_arr() const { return kind == Arr; }
   bool is_str() const { return kind == String; }
-  const Value* get(const std::string& k) const {
-    if (kind != Obj) return nullptr;
-    auto it = o->find(k);
-    return it == o->end() ? nullptr : &it->second;
-  }
+  const Value* get(std::string_view k) const { return kind == Obj ? o->find(k) : nullptr; }
   const Array& arr() const {
     static const Array empty;
     return kind == Arr ? *a : empty;
@@ -55,11 +74,36 @@ struct Value {
   bool boolean(bool dflt = false) const { return kind == Bool ? b : dflt; }
 };
 
+inline const Value* Object::find(std::string_view k) const {
+  if (e.size() <= 8) {  // decoder objects are small: a scan beats the binary search
+    for (auto& x : e)
+      if (x.first == k) return &x.second;
+    return nullptr;
+  }
+  auto it = std::lower_bound(e.begin(), e.end(), k, [](const Entry& x, std::string_view key) { return x.first < key; });
+  return it != e.end() && it->first == k ? &it->second : nullptr;
+}
+inline Value& Object::operator[](const std::string& k) {
+  auto it = std::lower_bound(e.begin(), e.end(), k, [](const Entry& x, const std::string& key) { return x.first < key; });
+  if (it != e.end() && it->first == k) return it->second;
+  return e.insert(it, Entry(k, Value()))->second;
+}
+inline void Object::finish() {
+  std::stable_sort(e.begin(), e.end(), [](const Entry& x, const Entry& y) { return x.first < y.first; });
+  size_t w = 0;
+  for (size_t i = 0; i < e.size(); i++) {
+    if (w > 0 && e[w - 1].first == e[i].first) e[w - 1].second = std::move(e[i].second);  // last wins
+    else if (w != i) e[w++] = std::move(e[i]);
+    else w++;
+  }
+  e.resize(w);
+}
+
 class Parser {
  public:
   Parser(const char* p, size_t n) : p_(p), end_(p + n) {}
   Value parse() {
-    Value v = value();
+    Value v = value(0);
     ws();
     if (p_ != end_) fail("trailing characters");
     return v;
@@ -68,11 +112,81 @@ class Parser {
  private:
   const char* p_;
   const char* end_;
+  static constexpr int kParallelDepth = 3;          // arrays this close to the root may be split
+  static constexpr size_t kParallelBytes = 1 << 20;  // ... when they span at least this many bytes
+  static constexpr size_t kParallelMinElems = 256;
   [[noreturn]] void fail(const char* m) { throw std::runtime_error(std::string("json: ") + m); }
   void ws() {
     while (p_ < end_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
   }
-  Value value() {
+  // Skip one value without building it (structure only: strings with escapes, nesting).
+  void skip() {
+    ws();
+    if (p_ >= end_) fail("unexpected end");
+    const char c = *p_;
+    if (c == '"') {
+      skip_string();
+    } else if (c == '{' || c == '[') {
+      int depth = 0;
+      while (p_ < end_) {
+        const char x = *p_;
+        if (x == '"') {
+          skip_string();
+          continue;
+        }
+        ++p_;
+        if (x == '{' || x == '[') depth++;
+        else if (x == '}' || x == ']') {
+          if (--depth == 0) return;
+        }
+      }
+      fail("unterminated container");
+    } else {
+      while (p_ < end_ && *p_ != ',' && *p_ != ']' && *p_ != '}' && *p_ != ' ' && *p_ != '\n' && *p_ != '\r' &&
+             *p_ != '\t')
+        ++p_;
+    }
+  }
+  void skip_string() {
+    ++p_;
+    while (p_ < end_) {
+      const char x = *p_++;
+      if (x == '\\') {
+        if (p_ >= end_) fail("bad escape");
+        ++p_;
+      } else if (x == '"') {
+        return;
+      }
+    }
+    fail("unterminated string");
+  }
+  // A large array: element extents by a skip scan, then the elements parsed in parallel.
+  bool array_parallel(Value& v, int depth) {
+    const char* start = p_;
+    std::vector<std::pair<const char*, const char*>> ext;
+    for (;;) {
+      ws();
+      const char* b = p_;
+      skip();
+      ext.push_back({b, p_});
+      ws();
+      if (p_ < end_ && *p_ == ',') { ++p_; continue; }
+      if (p_ < end_ && *p_ == ']') { ++p_; break; }
+      fail("expected ',' or ']'");
+    }
+    if (ext.size() < kParallelMinElems || (size_t)(p_ - start) < kParallelBytes) {
+      p_ = start;  // small after all: the sequential path
+      return false;
+    }
+    v.a->resize(ext.size());
+    Array& out = *v.a;
+    ks::parallel_for((int)ext.size(), 64, [&](int i) {
+      Parser sub(ext[(size_t)i].first, (size_t)(ext[(size_t)i].second - ext[(size_t)i].first));
+      out[(size_t)i] = sub.value(depth + 1);
+    });
+    return true;
+  }
+  Value value(int depth) {
     ws();
     if (p_ >= end_) fail("unexpected end");
     char c = *p_;
@@ -83,6 +197,10 @@ class Parser {
       v.o = std::make_shared<Object>();
       ws();
       if (p_ < end_ && *p_ == '}') { ++p_; return v; }
+      // entries collect on a per-thread stack (nested objects above them), then move into one
+      // exactly sized buffer: no growth reallocations
+      static thread_local std::vector<Object::Entry> stack;
+      const size_t base = stack.size();
       for (;;) {
         ws();
         if (p_ >= end_ || *p_ != '"') fail("expected key");
@@ -90,20 +208,29 @@ class Parser {
         ws();
         if (p_ >= end_ || *p_ != ':') fail("expected ':'");
         ++p_;
-        (*v.o)[k] = value();
+        Value x = value(depth + 1);
+        stack.emplace_back(std::move(k), std::move(x));
         ws();
         if (p_ < end_ && *p_ == ',') { ++p_; continue; }
         if (p_ < end_ && *p_ == '}') { ++p_; break; }
+        stack.resize(base);
         fail("expected ',' or '}'");
       }
+      v.o->e.reserve(stack.size() - base);
+      for (size_t i = base; i < stack.size(); i++) v.o->e.push_back(std::move(stack[i]));
+      stack.resize(base);
+      v.o->finish();
     } else if (c == '[') {
       ++p_;
       v.kind = Value::Arr;
       v.a = std::make_shared<Array>();
       ws();
       if (p_ < end_ && *p_ == ']') { ++p_; return v; }
+      if (depth < kParallelDepth && (size_t)(end_ - p_) >= kParallelBytes && ks::parallel_threads() > 1 &&
+          array_parallel(v, depth))
+        return v;
       for (;;) {
-        v.a->push_back(value());
+        v.a->push_back(value(depth + 1));
         ws();
         if (p_ < end_ && *p_ == ',') { ++p_; continue; }
         if (p_ < end_ && *p_ == ']') { ++p_; break; }
@@ -143,7 +270,14 @@ class Parser {
   }
   std::string string() {
     ++p_;  // opening quote
-    std::string out;
+    const char* b = p_;  // fast path: no escape before the closing quote
+    while (p_ < end_ && *p_ != '"' && *p_ != '\\') ++p_;
+    if (p_ < end_ && *p_ == '"') {
+      std::string out(b, p_);
+      ++p_;
+      return out;
+    }
+    std::string out(b, p_);
     while (p_ < end_ && *p_ != '"') {
       char c = *p_++;
       if (c != '\\') { out += c; continue; }
@@ -180,6 +314,13 @@ class Parser {
 };
 
 inline Value parse(const std::string& s) { return Parser(s.data(), s.size()).parse(); }
+
+// Destroy a (large) document on a detached thread: its ~millions of frees leave the caller's critical
+// path (ks_problem_create / ks_cons_create return while the snapshot DOM is still being released).
+inline void release_async(Value&& v) {
+  auto* p = new Value(std::move(v));
+  std::thread([p]() { delete p; }).detach();
+}
 
 // ---- writer helpers -------------------------------------------------------------------------
 inline void quote(std::string& out, const std::string& s) {
