@@ -222,6 +222,9 @@ void ks_upload(ks_problem* pb) {
   size_t o_pgi = put(t.pod_ginv.data(), t.pod_ginv.size() * 8);
   size_t o_srs = put(t.st_rss.data(), t.st_rss.size() * 4);
   size_t o_ntd = put(t.n_tdom.data(), t.n_tdom.size() * 4);
+  size_t o_fkw = put(t.fk_words.data(), t.fk_words.size() * 4);
+  size_t o_fkk = put(t.fk_key_off.data(), t.fk_key_off.size() * 4);
+  size_t o_fkt = put(t.fk_tpl.data(), t.fk_tpl.size() * 4);
   HIPCHK(hipMalloc(&pb->dbuf, a.total));
   std::vector<char> staging(a.total, 0);
   for (auto& it : items)
@@ -283,6 +286,9 @@ void ks_upload(ks_problem* pb) {
   D.pod_ginv = (const uint64_t*)(b + o_pgi);
   D.st_rss = (const uint32_t*)(b + o_srs);
   D.n_tdom = (const int32_t*)(b + o_ntd);
+  D.fk_words = (const uint32_t*)(b + o_fkw);
+  D.fk_key_off = (const int32_t*)(b + o_fkk);
+  D.fk_tpl = (const int32_t*)(b + o_fkt);
 }
 
 // Rebuild Results from the replica-0 workspace.

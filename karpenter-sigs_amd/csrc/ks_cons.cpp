@@ -265,12 +265,14 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   std::vector<std::vector<int>> nodePods;  // per snapshot node: global pod indices (GetNodePods)
   std::vector<PodH> podMeta;
   // every pod of the snapshot, parsed by worker threads (pods are independent)
+  // (arr() of a null pointer's absence is the shared empty array: references stay into the DOM)
+  static const Value kNone;
   std::vector<const Value*> allPodV;
   const Value* pendV = root.get("pendingPods");
-  for (auto& v : pendV ? pendV->arr() : ksjson::Array{}) allPodV.push_back(&v);
-  for (auto& nv : nodesV ? nodesV->arr() : ksjson::Array{})
+  for (const Value& v : (pendV ? *pendV : kNone).arr()) allPodV.push_back(&v);
+  for (const Value& nv : (nodesV ? *nodesV : kNone).arr())
     if (const Value* ps = nv.get("pods"))
-      for (auto& pv : ps->arr()) allPodV.push_back(&pv);
+      for (const Value& pv : ps->arr()) allPodV.push_back(&pv);
   std::vector<PodH> allPods(allPodV.size());
   parallel_for((int)allPodV.size(), 256, [&](int i) { allPods[(size_t)i] = parse_pod(*allPodV[(size_t)i]); });
   size_t next = 0;
@@ -283,7 +285,7 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   std::map<std::string, int> nodeByName;
   std::vector<char> deletingNode;
   int ni = 0;
-  for (auto& nv : nodesV ? nodesV->arr() : ksjson::Array{}) {
+  for (const Value& nv : (nodesV ? *nodesV : kNone).arr()) {
     const std::string name = jstr(&nv, "name");
     const bool del = nv.get("markedForDeletion") ? nv.get("markedForDeletion")->boolean(false) : false;
     nodeByName[name] = ni++;
@@ -1083,6 +1085,23 @@ int ks_cons_inspect(const char* json, size_t len, char** out) {
     char buf[96];
     snprintf(buf, sizeof buf, ",\"disruptionCost\":%.17g,\"pods\":%zu}", c.cands[i].cost, c.cands[i].pods.size());
     o += buf;
+  }
+  // the pending pods every simulation schedules, as encoded (name + device request vector)
+  const Host& h = c.pb->host;
+  o += "],\"pendingPods\":[";
+  for (size_t i = 0; i < c.pending.size(); i++) {
+    const int p = c.pending[i];
+    o += i ? ",{\"name\":" : "{\"name\":";
+    ksjson::quote(o, h.pods[(size_t)p].name);
+    o += ",\"requests\":[";
+    for (int r = 0; r < h.dims.R; r++)
+      o += (r ? "," : "") + std::to_string(h.tab.pod_req[(size_t)p * h.dims.R + r]);
+    o += "]}";
+  }
+  o += "],\"resources\":[";
+  for (int r = 0; r < h.dims.R; r++) {
+    if (r) o += ",";
+    ksjson::quote(o, h.resNames[(size_t)r]);
   }
   o += "],\"sims\":" + std::to_string(c.sims.size()) + ",\"multiPrefixes\":" + std::to_string(c.multiHi) +
        ",\"recordBytes\":" + std::to_string(4 * c.recWords) + ",\"pods\":" + std::to_string(c.pb->host.dims.P) +

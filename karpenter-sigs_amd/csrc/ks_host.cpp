@@ -872,6 +872,70 @@ void Host::build(const Value& root) {
     }
   }
 
+  // --- feasibility tables (k_solve feas_masks): per template, the positions of its instance-type list as
+  // bitsets per (key, value), so Requirements.Intersects(IT, X) and hasOffering(IT, X) of
+  // filterInstanceTypesByRequirements (nodeclaim.go:225-278) evaluate for every position at once as
+  // unions and intersections of bitsets.  Per template: [all positions][irregular] then per key of an
+  // instance type: [lacks the key][DoesNotExist][In][has value 0][has value 1]..., then the available
+  // offerings per (zone, capacity-type) value pair.  An IT requirement that is a complement (NotIn /
+  // Exists / Gt / Lt) makes its position irregular: those keep the exact per-position check.
+  {
+    const int TW = dims.TW, NK = dims.NK;
+    tab.fk_key_off.assign((size_t)std::max(NT, 1) * NK, -1);
+    tab.fk_tpl.assign((size_t)std::max(NT, 1) * 3, 0);
+    tab.fk_words.clear();
+    uint64_t multi = 0;  // keys some instance type constrains with more than one value
+    auto blk = [&](size_t words) {
+      const size_t o = tab.fk_words.size();
+      tab.fk_words.resize(o + words, 0);
+      return o;
+    };
+    auto setb = [&](size_t off, int p) { tab.fk_words[off + (size_t)(p >> 5)] |= 1u << (p & 31); };
+    for (int t = 0; t < NT; t++) {
+      const int tb = tab.tpl_it_beg[t], n = tab.tpl_it_beg[t + 1] - tb;
+      const size_t all = blk((size_t)TW), irr = blk((size_t)TW);
+      for (int p = 0; p < n; p++) setb(all, p);
+      for (uint64_t m = itKeys; m; m &= m - 1) {
+        const int k = __builtin_ctzll(m);
+        const KeyMeta& km = keys[(size_t)k];
+        const size_t base = blk((size_t)(3 + km.nv) * TW);
+        tab.fk_key_off[(size_t)t * NK + k] = (int32_t)base;
+        for (int p = 0; p < n; p++) {
+          const uint32_t* r = &tab.it_rs[(size_t)tab.tpl_its[(size_t)(tb + p)] * dims.RSW];
+          if (!bit(rs_present(r), k)) {
+            setb(base, p);
+            continue;
+          }
+          if (bit(rs_compl(r), k)) {
+            setb(irr, p);
+            continue;
+          }
+          int cnt = 0;
+          for (int v = 0; v < km.nv; v++)
+            if ((r[L.HDR + km.off + (v >> 5)] >> (v & 31)) & 1u) {
+              setb(base + (size_t)(3 + v) * TW, p);
+              cnt++;
+            }
+          setb(base + (size_t)(cnt == 0 ? 1 : 2) * TW, p);
+          if (cnt > 1) multi |= 1ull << k;
+        }
+      }
+      const int nz = keys[(size_t)zoneKey].nv, nc = keys[(size_t)ctKey].nv;
+      const size_t off = blk((size_t)nz * nc * TW);
+      for (int p = 0; p < n; p++) {
+        const int it = tab.tpl_its[(size_t)(tb + p)];
+        for (int o = tab.it_off_beg[(size_t)it]; o < tab.it_off_beg[(size_t)it + 1]; o++)
+          setb(off + ((size_t)tab.off_zone[(size_t)o] * nc + tab.off_ct[(size_t)o]) * TW, p);
+      }
+      tab.fk_tpl[(size_t)t * 3] = (int32_t)all;
+      tab.fk_tpl[(size_t)t * 3 + 1] = (int32_t)irr;
+      tab.fk_tpl[(size_t)t * 3 + 2] = (int32_t)off;
+    }
+    if (tab.fk_words.size() > (size_t)INT32_MAX) throw KsError(-3, "feasibility tables exceed 2^31 words");
+    dims.fkMulti = multi;
+    if (tab.fk_words.empty()) tab.fk_words.push_back(0);
+  }
+
   pt.mark("resources+taints+its+templates");
   // --- existing nodes (NewExistingNode, calculateExistingNodeClaims)
   int N = (int)nodes.size();

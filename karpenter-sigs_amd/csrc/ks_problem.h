@@ -70,6 +70,7 @@ struct KsDims {
   int32_t VD;              // limited drivers (<= kMaxVD); vol_dm[VD] partitions the pods' PVC universe
   int32_t tgUnlab;         // some existing node lacks the label of a topology group's key (k_solve node_slow)
   uint64_t tgLate;         // groups a relaxed state creates mid-Solve: inactive until that relaxation
+  uint64_t fkMulti;        // keys some instance type constrains with more than one value (feas_masks)
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
@@ -146,6 +147,10 @@ struct KsDev {
   const uint64_t KS_G* pod_ginv;   // [P] inverse groups the pod owns
   const uint32_t KS_G* st_rss;     // [S][RSW] strict pod requirements (podDomains)
   const int32_t KS_G* n_tdom;      // [G][N] value of the node's label for the group's key, -1 none
+  // feasibility tables (ks_host.cpp; k_solve feas_masks): per template, position bitsets per (key, value)
+  const uint32_t KS_G* fk_words;
+  const int32_t KS_G* fk_key_off;  // [NTPL][NK]
+  const int32_t KS_G* fk_tpl;      // [NTPL][3]
 };
 
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };

@@ -164,6 +164,9 @@ struct Solver {
   LU32 s_rs;            // [RSW] candidate requirements
   LU32 s_rem;           // [TW+2] candidate options
   LU32 s_cand;          // [TW+2] limit-filtered template options
+  LU32 s_fic;           // [TW+2] feas_masks: Intersects(IT, X) per position
+  LU32 s_fof;           // [TW+2] feas_masks: hasOffering(IT, X) per position
+  LU32 s_firr;          // [TW+2] feas_masks: irregular positions (exact per-position check)
   LU32 s_rmv;           // SIM: [ceil(N/32)] nodes removed by the simulation (the candidates)
   LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose requests live in a W.n_req slot
   LU32 s_tchr;          // SIM: [ceil(N/32)] nodes whose requirements live in a W.n_rs slot
@@ -249,6 +252,77 @@ struct Solver {
       if (rs_member(L, rs, d.zoneKey, D.off_zone[o]) && rs_member(L, rs, d.ctKey, D.off_ct[o])) return true;
     return false;
   }
+  // filterInstanceTypesByRequirements' requirement and offering tests (nodeclaim.go:225-278) for every
+  // position of template t at once, from the host's per-(key, value) position bitsets (ks_host.cpp
+  // "feasibility tables"): for each key of X that instance types constrain, Requirements.Intersects
+  // passes on the positions whose IT lacks the key (only shared keys are checked), on those holding a
+  // value X admits, and -- when X's operator is NotIn / DoesNotExist -- on those whose IT says
+  // DoesNotExist (both negative, requirements.go:248-252); the keys intersect.  hasOffering is the union
+  // over the (zone, capacity-type) pairs X admits (a missing key admits all).  Lane w owns word w:
+  // s_fic, s_fof; s_firr marks positions whose IT holds a complement requirement (checked exactly).
+  __device__ __forceinline__ void feas_masks(LU32 X, int t) {
+    const uint32_t KS_G* F = D.fk_words;
+    const int TW = d.TW;
+    const int ball = D.fk_tpl[3 * t], birr = D.fk_tpl[3 * t + 1], boff = D.fk_tpl[3 * t + 2];
+    const uint64_t keysX = rs_present(X) & d.itKeys;
+    const int nz = L.keys[d.zoneKey].nv, nc = L.keys[d.ctKey].nv;
+    for (int w0 = 0; w0 < TW; w0 += kWave) {
+      const int w = w0 + lane();
+      const int wc = w < TW ? w : TW - 1;
+      uint32_t ic = F[ball + wc];
+      for (uint64_t m = keysX; m; m &= m - 1) {
+        const int k = ctz64(m);
+        const int base = D.fk_key_off[t * d.NK + k];
+        const KeyMeta km = L.keys[k];
+        uint32_t acc = F[base + wc];  // positions whose IT lacks the key
+        const int op = rs_op(L, X, k);
+        if (op == OP_NOTIN || op == OP_DNE) acc |= F[base + TW + wc];
+        if (!bit(rs_compl(X), k)) {  // X In: the positions holding one of its values
+          for (int i = 0; i < km.nw; i++) {
+            uint32_t x = X[L.HDR + km.off + i];
+            while (x) {
+              const int v = i * 32 + __builtin_ctz(x);
+              x &= x - 1;
+              acc |= F[base + (3 + v) * TW + wc];
+            }
+          }
+        } else if (!bit(d.fkMulti, k)) {  // complement, one value per IT: In positions minus the values X excludes
+          uint32_t sub = 0;
+          for (int v0 = 0; v0 < km.nv; v0 += kWave) {
+            uint64_t out = wballot(v0 + lane() < km.nv && !rs_member(L, X, k, v0 + lane()));
+            for (; out; out &= out - 1) sub |= F[base + (3 + v0 + ctz64(out)) * TW + wc];
+          }
+          acc |= F[base + 2 * TW + wc] & ~sub;
+        } else {  // complement over multi-valued ITs: the values X admits
+          for (int v0 = 0; v0 < km.nv; v0 += kWave) {
+            uint64_t in = wballot(v0 + lane() < km.nv && rs_member(L, X, k, v0 + lane()));
+            for (; in; in &= in - 1) acc |= F[base + (3 + v0 + ctz64(in)) * TW + wc];
+          }
+        }
+        ic &= acc;
+      }
+      uint32_t of = 0;
+      for (int c0 = 0; c0 < nc; c0 += kWave) {
+        const uint64_t cm0 = wballot(c0 + lane() < nc && rs_member(L, X, d.ctKey, c0 + lane()));
+        if (!cm0) continue;
+        for (int z0 = 0; z0 < nz; z0 += kWave) {
+          for (uint64_t zm = wballot(z0 + lane() < nz && rs_member(L, X, d.zoneKey, z0 + lane())); zm; zm &= zm - 1) {
+            const int z = z0 + ctz64(zm);
+            for (uint64_t cm = cm0; cm; cm &= cm - 1) of |= F[boff + (z * nc + c0 + ctz64(cm)) * TW + wc];
+          }
+        }
+      }
+      const uint32_t irr = F[birr + wc];
+      if (w < TW) {
+        s_fic[w] = ic;
+        s_fof[w] = of;
+        s_firr[w] = irr;
+      }
+    }
+    wsync();
+  }
+  __device__ __forceinline__ bool fbit(LU32 m, int pos) const { return (m[pos >> 5] >> (pos & 31)) & 1u; }
+
   template <class PD, class PS>
   __device__ __forceinline__ void copy_words(PD dst, PS src, int n) const {
     for (int i = lane(); i < n; i += kWave) dst[i] = src[i];
@@ -815,17 +889,23 @@ struct Solver {
       return ncnt > 0;
     }
     int cnt = 0, scanned = 0;
+    if (changed) feas_masks(s_rs, t);
     for (int base = 0; base < nIT; base += kWave) {
       const int wi = base >> 5;
       const uint64_t bits = (uint64_t)s_rem[wi] | (wi + 1 < d.TW ? (uint64_t)s_rem[wi + 1] << 32 : 0ull);
       uint64_t m = 0;
       if (bits) {
         const int gpos = tb + base + lane();
+        const int pos = base + lane();
         bool ok = (bits >> lane()) & 1ull;
         if (ok) ok = fits_pos(req, gpos);
         if (ok && changed) {
-          const int it = D.tpl_its[gpos];
-          ok = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs) && has_offering(it, s_rs);
+          if (fbit(s_firr, pos)) {
+            const int it = D.tpl_its[gpos];
+            ok = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs) && has_offering(it, s_rs);
+          } else {
+            ok = fbit(s_fic, pos) && fbit(s_fof, pos);
+          }
         }
         m = wballot(ok);
         scanned += __popcll(bits);
@@ -964,15 +1044,21 @@ struct Solver {
             for (int r = 0; r < R(); r++) req[r] = D.tpl_daemon[(int64_t)t * R() + r] + pod[r];
             uint32_t flags = 0;
             uint64_t any = 0;
+            feas_masks(s_rs, t);
             for (int base = 0; base < nIT; base += kWave) {
               const int pos = base + lane();
               const bool in = pos < nIT && ((s_cand[pos >> 5] >> (pos & 31)) & 1u);
               bool ic = false, fi = false, of = false;
               if (in) {
-                const int it = D.tpl_its[tb + pos];
-                ic = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs);
+                if (fbit(s_firr, pos)) {
+                  const int it = D.tpl_its[tb + pos];
+                  ic = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs);
+                  of = has_offering(it, s_rs);
+                } else {
+                  ic = fbit(s_fic, pos);
+                  of = fbit(s_fof, pos);
+                }
                 fi = fits_pos(req, tb + pos);
-                of = has_offering(it, s_rs);
               }
               if (wballot(ic)) flags |= FF_REQ;
               if (wballot(fi)) flags |= FF_FITS;
@@ -1367,6 +1453,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   S.s_rs = (LU32)take(4 * (size_t)d.RSW);
   S.s_rem = (LU32)take(4 * (size_t)d.TW + 8);
   S.s_cand = (LU32)take(4 * (size_t)d.TW + 8);
+  S.s_fic = (LU32)take(4 * (size_t)d.TW + 8);
+  S.s_fof = (LU32)take(4 * (size_t)d.TW + 8);
+  S.s_firr = (LU32)take(4 * (size_t)d.TW + 8);
   const int NWN = (d.N + 31) >> 5;
   S.s_rmv = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tch = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
@@ -1813,7 +1902,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   Plan pl{};
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
-                       r16(4 * (size_t)d.RSW) + 2 * r16(4 * TW + 8) + 16 * 16 +
+                       r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 +
                        (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
                        (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)

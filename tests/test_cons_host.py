@@ -53,3 +53,23 @@ def test_candidates_match_oracle(name, snap):
 def test_prefix_cap_is_101_candidates():
     got = inspect_consolidation(json.dumps(synth.cluster_snapshot(150, 2, n_its=30, it_range=(4, 20), seed=5)))
     assert got["multiPrefixes"] == 100 and got["sims"] == 250
+
+
+@pytest.mark.parametrize("name,snap", SNAPS, ids=[n for n, _ in SNAPS])
+def test_pending_pods_encoded(name, snap):
+    """Every simulation schedules the pending pods (SimulateScheduling, helpers.go:79-85): the encode must
+    hold each of them, in snapshot order, with its own requests (RequestsForPods incl. pods=1)."""
+    got = inspect_consolidation(json.dumps(snap))
+    pend = snap.get("pendingPods", [])
+    assert [p["name"] for p in got["pendingPods"]] == [p["metadata"]["name"] for p in pend]
+    res = got["resources"]
+    for p, q in zip(pend, got["pendingPods"]):
+        asked = {}
+        for c in p["spec"].get("containers", []):
+            for k, v in c.get("resources", {}).get("requests", {}).items():
+                asked[k] = asked.get(k, 0) + (0 if str(v).strip("0.m") == "" else 1)
+        enc = dict(zip(res, q["requests"]))
+        assert enc.get("pods") == 1
+        for k, nz in asked.items():
+            if nz and k in enc:
+                assert enc[k] > 0, (name, p["metadata"]["name"], k)
