@@ -748,8 +748,8 @@ int ks_results_json(const ks_results* r, char** json_out) {
   static const char* names[] = {"nclaims", "ncommits", "hostnameCounter", "error", "pops", "algBytes",
                                 "sorts", "sortsWithDescent", "claimFull", "claimQuickFail", "windows",
                                 "cycPop", "cycNodes", "cycSort", "cycQuick", "cycFull", "cycCommit", "cycTemplates",
-                                "cycTotal", "cycNodeCommit"};
-  for (int i = 0; i < 20; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
+                                "cycTotal", "cycNodeCommit", "cycFullRs", "cycFullThr", "cycFullMasks", "cycFullApply"};
+  for (int i = 0; i < 24; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
   o += "}}";
   *json_out = strdup(o.c_str());
   return KS_OK;

@@ -16,9 +16,11 @@
 #if defined(__HIP_DEVICE_COMPILE__)
 #define KS_G __attribute__((address_space(1)))
 #define KS_L __attribute__((address_space(3)))
+#define KS_C __attribute__((address_space(4)))  // read-only for the whole launch: scalar loads
 #else
 #define KS_G
 #define KS_L
+#define KS_C
 #endif
 
 namespace ks {
@@ -241,6 +243,7 @@ enum Counter {
   // diagnostic build (-DKS_PHASE_STATS): s_memtime cycles per phase
   CT_CYC_POP, CT_CYC_NODES, CT_CYC_SORT, CT_CYC_QUICK, CT_CYC_FULL, CT_CYC_COMMIT, CT_CYC_TPL, CT_CYC_TOTAL,
   CT_CYC_NCOMMIT,  // existing-node commit (inside CT_CYC_NODES)
+  CT_CYC_SUB,      // [4] claim_full sub-phases (inside CT_CYC_FULL): requirements, thresholds, masks, apply
   CT_NCOUNTERS = 24
 };
 enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3 };

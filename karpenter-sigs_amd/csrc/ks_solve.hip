@@ -78,9 +78,11 @@ __device__ __forceinline__ uint32_t lds_and(LU32 p, uint32_t v) {  // ds_and_rtn
 #ifdef KS_PHASE_STATS
 #define PH_BEGIN(v) uint64_t v = __builtin_amdgcn_s_memtime()
 #define PH_END(v, slot) cyc[slot] += __builtin_amdgcn_s_memtime() - v
+#define PHS_END(v, slot) scyc[slot] += __builtin_amdgcn_s_memtime() - v  // sub-phases (Solver member)
 #else
 #define PH_BEGIN(v)
 #define PH_END(v, slot)
+#define PHS_END(v, slot)
 #endif
 
 // ------------------------------------------------------------------------------------------------
@@ -140,15 +142,84 @@ struct Window {
 // SIM: a consolidation simulation (helpers.go:73-127) over the shared cluster problem: pods are
 // the simulation's local subset (W.pod_map), the candidates' nodes are masked out, and existing
 // node state is copy-on-write (a node's HBM slot is initialised the first time a pod lands on it).
+// Requirements.Add (requirements.go:118-125) of `in` into `out`, both in LDS: the rs_add of
+// ks_reqset.h with each key's words spread over the lanes (headers are wave-uniform; one wave,
+// so every lane's reads of a key precede lane 0's header stores).  Returns whether a key of
+// `mask` changed (what rs_equal_keys against the old record would report).
+// A free function kept out of line (no Solver `this` escapes): inlined into claim_full, the compiled Solve diverged from the oracle on the
+// reference scenarios (device requests vs the replayed Merge) although the flag it returned and the
+// record it built matched rs_add + rs_equal_keys lane for lane; the call costs a few instructions.
+__device__ __attribute__((noinline)) bool rs_add_wave(const DevLayout L, LU32 out, LU32 in, uint64_t mask) {
+  const uint64_t pi = rs_present(in), po = rs_present(out);
+  uint64_t cm = rs_compl(out), hg = rs_hasgt(out), hl = rs_haslt(out);
+  const uint64_t icm = rs_compl(in), ihg = rs_hasgt(in), ihl = rs_haslt(in);
+  bool diff = false;
+  for (uint64_t m = pi; m; m &= m - 1) {
+    const int k = ctz64(m);
+    const uint64_t one = 1ull << k;
+    const KeyMeta km = L.keys[k];
+    const bool watched = (mask & one) != 0;
+    if (po & one) {
+      const KeyIx x = key_ix_header(L, out, in, k);
+      for (int i = lane(); i < km.nw; i += kWave) {
+        const uint32_t old = out[L.HDR + km.off + i];
+        const uint32_t nw = key_ix_word(L, out, in, k, i, x);
+        out[L.HDR + km.off + i] = nw;
+        diff |= watched && nw != old;
+      }
+      const bool keep = !x.dne && x.compl_;
+      const uint64_t ncm = keep ? (cm | one) : (cm & ~one);
+      const uint64_t nhg = (keep && x.hg) ? (hg | one) : (hg & ~one);
+      const uint64_t nhl = (keep && x.hl) ? (hl | one) : (hl & ~one);
+      diff |= watched && (((ncm ^ cm) | (nhg ^ hg) | (nhl ^ hl)) & one) != 0;
+      cm = ncm;
+      hg = nhg;
+      hl = nhl;
+      if (km.bslot >= 0) {
+        const int64_t ngt = keep && x.hg ? x.gt : 0, nlt = keep && x.hl ? x.lt : 0;
+        diff |= watched && (ngt != rs_gt(out, km.bslot) || nlt != rs_lt(out, km.bslot));
+        wsync();
+        if (lane() == 0) {
+          rs_set_gt(out, km.bslot, ngt);
+          rs_set_lt(out, km.bslot, nlt);
+        }
+      }
+    } else {  // rs_copy_key
+      for (int i = lane(); i < km.nw; i += kWave) out[L.HDR + km.off + i] = in[L.HDR + km.off + i];
+      diff |= watched;  // the key appears
+      cm = (cm & ~one) | (icm & one);
+      hg = (hg & ~one) | (ihg & one);
+      hl = (hl & ~one) | (ihl & one);
+      if (km.bslot >= 0 && lane() == 0) {
+        rs_set_gt(out, km.bslot, rs_gt(in, km.bslot));
+        rs_set_lt(out, km.bslot, rs_lt(in, km.bslot));
+      }
+    }
+  }
+  wsync();
+  if (lane() == 0) {
+    wr64(out, 0, po | pi);
+    wr64(out, 2, cm);
+    wr64(out, 4, hg);
+    wr64(out, 6, hl);
+  }
+  wsync();
+  return wballot(diff) != 0;
+}
+
 template <int RT, bool TL, bool SIM, bool TOPO>
 struct Solver {
   static constexpr int RM = RT > 0 ? RT : kMaxR;
   // By value: a reference to a byval kernel argument forces a scratch copy of the whole struct
   // (every field access then becomes a scratch load); values scalarise into SGPRs.
-  const KsDev D;
-  const KsDims d;
-  const KsWork W;
-  const Plan pl;
+  // Launch constants by reference, not by copy: the kernel arguments stay in the kernarg segment and
+  // the work descriptor in constant memory, read with scalar loads where used.  (Copies of these
+  // ~1 KB structs did not fit the SGPRs and lived in scratch memory: a private-memory round trip
+  // on many hot-path reads.)
+  const KsDev& D;
+  const KsDims& d;
+  const KsWork KS_C& W;
+  const Plan& pl;
   DevLayout L;
   ClaimView<true> lc;   // claims [0, KL)
   ClaimView<false> gc;  // claims [KL, KO)
@@ -162,6 +233,7 @@ struct Solver {
   LI32 s_tbeg;          // [NTPL+1]
   LI64 s_pool;          // [NPOOL][R] remaining limits
   LU32 s_rs;            // [RSW] candidate requirements
+  LU32 s_pin;           // [RSW] the popped pod's requirement record (its relaxation state), when it has keys
   LU32 s_rem;           // [TW+2] candidate options
   LU32 s_cand;          // [TW+2] limit-filtered template options
   LU32 s_fic;           // [TW+2] feas_masks: Intersects(IT, X) per position
@@ -185,8 +257,11 @@ struct Solver {
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
   uint64_t cur_hpo = 0;               // its own initial entries on existing nodes (HostPortUsage.Add replaces them)
   uint64_t cur_vm = 0;                // the popped pod's PVCs of limited drivers (Solve only; SIM refuses them)
+#ifdef KS_PHASE_STATS
+  uint64_t scyc[4] = {0, 0, 0, 0};  // claim_full sub-phases: requirements, thresholds, masks, apply
+#endif
 
-  __device__ Solver(const KsDev& D_, const KsWork& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
+  __device__ Solver(const KsDev& D_, const KsWork KS_C& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
   __device__ __forceinline__ int R() const { return RT > 0 ? RT : d.R; }
 
   template <bool INL>
@@ -340,6 +415,7 @@ struct Solver {
     return uni(c);
   }
 
+
   // --- existing nodes (ExistingNode.Add, existingnode.go:64-124) -------------------------------
   // VolumeUsage.ExceedsLimits (volumeusage.go:202-209) for the popped pod's PVCs: per limited driver,
   // the node's count plus the pod's PVCs it does not mount yet.  Nodes over a limit before the Solve
@@ -418,8 +494,8 @@ struct Solver {
       if (ok1) ok1 = vol_ok(c1);
     }
     if (sflags & SF_HAS_KEYS) {  // strict Compatible: no AllowUndefinedWellKnownLabels
-      if (ok0) ok0 = rs_compatible(L, node_rs(c0), D.st_rs + (int64_t)s * d.RSW, 0);
-      if (ok1) ok1 = rs_compatible(L, node_rs(c1), D.st_rs + (int64_t)s * d.RSW, 0);
+      if (ok0) ok0 = rs_compatible(L, node_rs(c0), s_pin, 0);
+      if (ok1) ok1 = rs_compatible(L, node_rs(c1), s_pin, 0);
     }
     sl0 = sl1 = false;
     if (TOPO && t_mask) {  // topology (existingnode.go:106-114)
@@ -444,7 +520,7 @@ struct Solver {
     for (int r = 0; r < R(); r++) W.n_req[(int64_t)j * R() + r] += pod[r];
     if (d.hpAny) W.n_hp[j] = (W.n_hp[j] & ~cur_hpo) | cur_hpu;  // HostPortUsage.Add (hostportusage.go:70-72)
     if (d.volAny && cur_vm) vol_commit(j);
-    if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+    if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)j * d.RSW, s_pin);
   }
   // SIM: copy-on-write commit (wave-uniform).  W.n_req is indexed by node but only the nodes a pod
   // landed on are ever written (s_tch marks them), so a fresh simulation needs no initialisation.
@@ -480,8 +556,7 @@ struct Solver {
         copy_words(s_rs, W.n_rs + (int64_t)slot * d.RSW, d.RSW);
       }
       wsync();
-      if (lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
-      wsync();
+      rs_add_wave(L, s_rs, s_pin, 0);
       copy_words(W.n_rs + (int64_t)slot * d.RSW, s_rs, d.RSW);
       if (lane() == owner && rsfresh) W.n_slot[j] = slot;
       if (lane() == 0) s_tchr[j >> 5] |= 1u << (j & 31);
@@ -607,8 +682,7 @@ struct Solver {
     wsync();
     copy_words(s_rs, node_rs(j), d.RSW);
     wsync();
-    if ((sflags & SF_HAS_KEYS) && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
-    wsync();
+    if (sflags & SF_HAS_KEYS) rs_add_wave(L, s_rs, s_pin, 0);
     return topo_apply(s_rs, -1, 0) == 0;
   }
   // The node's requirements after a node_slow commit (n.requirements = nodeRequirements): s_rs.
@@ -822,7 +896,7 @@ struct Solver {
       ok &= pod[r] <= s_phead[(int64_t)j * R() + r];
     }
     if (ok && (sflags & SF_HAS_KEYS))
-      ok = rs_compatible(L, W.c_rs + (int64_t)s_order[j] * d.RSW, D.st_rs + (int64_t)s * d.RSW, d.allowWK);
+      ok = rs_compatible(L, W.c_rs + (int64_t)s_order[j] * d.RSW, s_pin, d.allowWK);
     return ok;
   }
 
@@ -833,18 +907,20 @@ struct Solver {
                                              int& ncnt) {
     const ClaimView<INL>& v = cv<INL>();
     bool changed = false;
+    PH_BEGIN(u0);
     if ((sflags & SF_HAS_KEYS) || (TOPO && t_mask)) {
       const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
       copy_words(s_rs, crs, d.RSW);
       wsync();
-      if ((sflags & SF_HAS_KEYS) && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
-      wsync();
-      if (TOPO && t_mask && topo_apply(s_rs, c, d.allowWK) != 0) {  // topology requirements (nodeclaim.go:92-100)
-        ncnt = 0;
-        return false;
+      if (sflags & SF_HAS_KEYS)
+        changed = rs_add_wave(L, s_rs, s_pin, (sflags & SF_TOUCHES_IT_KEYS) ? d.itKeys : 0);
+      if (TOPO && t_mask) {
+        if (topo_apply(s_rs, c, d.allowWK) != 0) {  // topology requirements (nodeclaim.go:92-100)
+          ncnt = 0;
+          return false;
+        }
+        changed = !rs_equal_keys(L, s_rs, crs, d.itKeys);
       }
-      changed = (((sflags & SF_HAS_KEYS) && (sflags & SF_TOUCHES_IT_KEYS)) || (TOPO && t_mask)) &&
-                !rs_equal_keys(L, s_rs, crs, d.itKeys);
       algbytes += 8 * d.RSW;
     }
     const int t = uni(v.tpl[c]);
@@ -855,11 +931,13 @@ struct Solver {
       nthr[r] = uni(v.thr[(int64_t)c * R() + r]);
     }
     const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
+    PHS_END(u0, 0);
+    PH_BEGIN(u1);
     copy_words(s_rem, v.rem + (int64_t)c * d.TW, d.TW);
     wsync();
-    if (!changed && !d.negReq) {
-      // Requirements unchanged: the options dropped are exactly those some growing request no longer
-      // fits, a prefix of each resource's Allocatable-ascending order beyond its threshold.
+    if (!d.negReq) {
+      // Requests only grow: the options a request no longer fits are a prefix of each resource's
+      // Allocatable-ascending order beyond its threshold.
       int removed = 0, examined = 0;
       for (int r = 0; r < R(); r++) {
         const int64_t base = (int64_t)tb * R() + (int64_t)r * nIT;
@@ -883,9 +961,45 @@ struct Solver {
         }
         nthr[r] = k;
       }
-      ncnt = uni(v.cnt[c]) - removed;
       algbytes += 8 * d.TW + 16 * R() + 4 * R() + (int64_t)examined * 12;
       wsync();
+      PHS_END(u1, 1);
+      if (!changed) {
+        ncnt = uni(v.cnt[c]) - removed;
+        return ncnt > 0;
+      }
+      // Requirements changed: the options left are those the new requirements still admit, from
+      // the feasibility masks (one word per lane), exact per position only for irregular ones.
+      PH_BEGIN(u2);
+      feas_masks(s_rs, t);
+      PHS_END(u2, 2);
+      PH_BEGIN(u3);
+      for (int w0 = 0; w0 < d.TW; w0 += kWave) {
+        const int w = w0 + lane();
+        uint32_t keep = 0, irr = 0;
+        if (w < d.TW) {
+          const uint32_t rem = s_rem[w];
+          irr = rem & s_firr[w];
+          keep = rem & ~s_firr[w] & s_fic[w] & s_fof[w];
+        }
+        for (uint64_t any = wballot(irr != 0); any; any &= any - 1) {  // rare: complement IT requirements
+          const int ow = w0 + ctz64(any);
+          const uint32_t bits = (uint32_t)rdl((int)irr, ow - w0);
+          const bool mine = lane() < 32 && ((bits >> lane()) & 1u);
+          bool ok = false;
+          if (mine) {
+            const int it = D.tpl_its[tb + ow * 32 + lane()];
+            ok = rs_intersects(L, D.it_rs + (int64_t)it * d.RSW, s_rs) && has_offering(it, s_rs);
+          }
+          const uint32_t okb = (uint32_t)wballot(ok);
+          if (w == ow) keep |= okb;
+        }
+        if (w < d.TW) s_rem[w] = keep;
+      }
+      wsync();
+      ncnt = popc_words(s_rem, d.TW);
+      algbytes += 12 * (int64_t)d.TW;
+      PHS_END(u3, 3);
       return ncnt > 0;
     }
     int cnt = 0, scanned = 0;
@@ -928,14 +1042,31 @@ struct Solver {
     const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
     for (int r = 0; r < R(); r++) {
       int64_t m = INT64_MIN;
-      for (int q = lane(); q < nIT; q += kWave)
-        if ((bits[q >> 5] >> (q & 31)) & 1u) {
-          const int64_t a = alloc_pos(tb + q, r);
-          m = a > m ? a : m;
+      if (!d.negReq) {  // the first option from the top of the Allocatable-ascending order
+        const int64_t base = (int64_t)tb * R() + (int64_t)r * nIT;
+        for (int k = nIT - 1; k >= 0; k -= kWave) {
+          const int i = k - lane();
+          bool in = false;
+          if (i >= 0) {
+            const int q = tsort_p(base + i);
+            in = (bits[q >> 5] >> (q & 31)) & 1u;
+          }
+          const uint64_t hit = wballot(in);
+          if (hit) {
+            m = tsort_a(base + k - ctz64(hit));
+            break;
+          }
         }
-      for (int off = 32; off >= 1; off >>= 1) {
-        const int64_t o = __shfl_xor(m, off);
-        m = o > m ? o : m;
+      } else {
+        for (int q = lane(); q < nIT; q += kWave)
+          if ((bits[q >> 5] >> (q & 31)) & 1u) {
+            const int64_t a = alloc_pos(tb + q, r);
+            m = a > m ? a : m;
+          }
+        for (int off = 32; off >= 1; off >>= 1) {
+          const int64_t o = __shfl_xor(m, off);
+          m = o > m ? o : m;
+        }
       }
       if (lane() == 0) {
         v.max[(int64_t)c * R() + r] = m;
@@ -1017,9 +1148,8 @@ struct Solver {
           wsync();
           bool ok = true;
           if (sflags & SF_HAS_KEYS) {
-            ok = rs_compatible(L, s_rs, D.st_rs + (int64_t)s * d.RSW, d.allowWK);
-            if (ok && lane() == 0) rs_add(L, s_rs, D.st_rs + (int64_t)s * d.RSW);
-            wsync();
+            ok = rs_compatible(L, s_rs, s_pin, d.allowWK);
+            if (ok) rs_add_wave(L, s_rs, s_pin, 0);
           }
           if (TOPO && ok && t_mask) {  // topology requirements of the fresh NodeClaim (nodeclaim.go:92-100)
             const uint32_t tc = topo_apply(s_rs, nclaims, d.allowWK);
@@ -1427,8 +1557,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   constexpr int RM = Solver<RT, TL, SIM, TOPO>::RM;
   extern __shared__ __attribute__((aligned(16))) char smem_generic[];
   char KS_L* smem = (char KS_L*)smem_generic;
-  const KsWork W = works[blockIdx.x];
-  const KsDims d = D.d;
+  const KsWork KS_C& W = ((const KsWork KS_C*)works)[blockIdx.x];
+  const KsDims& d = D.d;
   Solver<RT, TL, SIM, TOPO> S(D, W, pl);
   if (TOPO) S.t_active = ~d.tgLate;
   const int R = S.R();
@@ -1451,6 +1581,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   S.s_tbeg = (LI32)take(4 * (size_t)(d.NTPL + 1));
   S.s_pool = (LI64)take(8 * (size_t)(d.NPOOL + 1) * R);
   S.s_rs = (LU32)take(4 * (size_t)d.RSW);
+  S.s_pin = (LU32)take(4 * (size_t)d.RSW);
   S.s_rem = (LU32)take(4 * (size_t)d.TW + 8);
   S.s_cand = (LU32)take(4 * (size_t)d.TW + 8);
   S.s_fic = (LU32)take(4 * (size_t)d.TW + 8);
@@ -1616,6 +1747,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       S.cur_hpo = (uint64_t)rdl64((int64_t)w.hpo, wi);
     }
     if (d.volAny) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
+    if (sflags & SF_HAS_KEYS) {  // the state's record, read by every check of this pop
+      S.copy_words(S.s_pin, D.st_rs + (int64_t)s * d.RSW, d.RSW);
+      wsync();
+    }
     if (TOPO) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
 #pragma unroll
     for (int r = 0; r < RM; r++) {
@@ -1645,7 +1780,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
           ok &= (whp[k] & S.cur_hpc) == 0;
           if (d.volAny && S.cur_vm && ok) ok = S.vol_ok(n);
-          if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), D.st_rs + (int64_t)s * d.RSW, 0);
+          if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), S.s_pin, 0);
           if (TOPO && S.t_mask && ok) ok = S.topo_node_state(n) == 1;  // every node is labelled here
           const uint64_t m = wballot(ok);
           if (m) {
@@ -1674,7 +1809,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             if (sflags & SF_HAS_KEYS) S.sim_node_commit(j, s, sflags, pod, pod, nrs, true);
             if ((rdl(nfv, owner) & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
           } else if ((sflags & SF_HAS_KEYS) && lane() == owner) {
-            rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, D.st_rs + (int64_t)s * d.RSW);
+            rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, S.s_pin);
           }
           if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, j, 0);  // existingnode.go:121
           S.log_commit(p, -(j + 1), nlog);
@@ -1847,6 +1982,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     for (int i = 0; i < 7; i++) W.counters[CT_CYC_POP + i] = (int64_t)cyc[i];
     W.counters[CT_CYC_TOTAL] = (int64_t)(__builtin_amdgcn_s_memtime() - tstart);
     W.counters[CT_CYC_NCOMMIT] = (int64_t)cyc[7];
+    for (int i = 0; i < 4; i++) W.counters[CT_CYC_SUB + i] = (int64_t)S.scyc[i];
 #endif
   }
   if constexpr (SIM) S.sim_record(P, nclaims, hostCtr, allSched, err);
@@ -1902,7 +2038,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   Plan pl{};
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
-                       r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 +
+                       2 * r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 +
                        (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
                        (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)

@@ -15,7 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # KS_LIB_VARIANT=stats loads the diagnostic build with per-phase cycle counters; =asan the ASan + UBSan
 # build of the host translation units (make -C karpenter-sigs_amd asan; scripts/asan_cpu_suite.sh).
 _VARIANTS = {"stats": "libkarpenter_amd_stats.so", "asan": "libkarpenter_amd_asan.so"}
-_LIB_PATH = os.path.join(_HERE, _VARIANTS.get(os.environ.get("KS_LIB_VARIANT", ""), "libkarpenter_amd.so"))
+_VARIANT = os.environ.get("KS_LIB_VARIANT", "")
+_LIB_PATH = os.path.join(_HERE, _VARIANTS.get(_VARIANT, "libkarpenter_amd_%s.so" % _VARIANT if _VARIANT else "libkarpenter_amd.so"))
 _lib = None
 
 KS_ERRORS = {-1: "KS_ERR_PARSE", -2: "KS_ERR_UNSUPPORTED", -3: "KS_ERR_CAPACITY", -4: "KS_ERR_HIP",

@@ -18,7 +18,8 @@ r = Scheduler(json.dumps(snap)).solve()
 st = r.stats
 tot = max(st["cycTotal"], 1)
 print(json.dumps(st))
-for k in ["cycPop", "cycNodes", "cycNodeCommit", "cycSort", "cycQuick", "cycFull", "cycCommit", "cycTemplates"]:
+for k in ["cycPop", "cycNodes", "cycNodeCommit", "cycSort", "cycQuick", "cycFull", "cycFullRs", "cycFullThr",
+          "cycFullMasks", "cycFullApply", "cycCommit", "cycTemplates"]:
     print("%-14s %6.1f%%  %8.1f cyc/pod" % (k, 100.0 * st[k] / tot, st[k] / n))
 print("total cyc/pod %.1f  pops %d  sorts %d slow %d  claims %d  solve_kernel_ms %.2f" % (
     tot / n, st["pops"], st["sorts"], st["sortsWithDescent"], st["nclaims"], r.solve_kernel_ms))
