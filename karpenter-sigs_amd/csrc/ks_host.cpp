@@ -1318,6 +1318,9 @@ void Host::build(const Value& root) {
   dims.itKeys = itKeys;
   dims.hostnameSeed = (int32_t)hostnameSeed;
   dims.Kcap = std::max(1, std::min(P, 16384));
+  bool anyKeys = false;
+  for (int32_t f : tab.st_flags) anyKeys |= (f & SF_HAS_KEYS) != 0;
+  dims.lean = !dims.hpAny && !dims.volAny && !dims.dupUids && !dims.negReq && groups.empty() && !anyKeys ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------------

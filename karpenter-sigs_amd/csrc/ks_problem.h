@@ -73,6 +73,8 @@ struct KsDims {
   int32_t tgUnlab;         // some existing node lacks the label of a topology group's key (k_solve node_slow)
   uint64_t tgLate;         // groups a relaxed state creates mid-Solve: inactive until that relaxation
   uint64_t fkMulti;        // keys some instance type constrains with more than one value (feas_masks)
+  int32_t lean;            // none of host ports, limited volumes, pod label requirements, shared UIDs,
+                           // negative requests, topology: k_solve's LEAN instantiation applies
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.

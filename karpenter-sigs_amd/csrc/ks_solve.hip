@@ -207,9 +207,18 @@ __device__ __attribute__((noinline)) bool rs_add_wave(const DevLayout L, LU32 ou
   return wballot(diff) != 0;
 }
 
-template <int RT, bool TL, bool SIM, bool TOPO>
+template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN>
 struct Solver {
   static constexpr int RM = RT > 0 ? RT : kMaxR;
+  // LEAN: the problem uses none of host ports, limited volumes, pod label requirements, shared UIDs,
+  // negative requests or topology (KsDims::lean, set by the encoder).  Those paths compile out, which
+  // frees the registers they pinned (SGPR spills) and the instructions they cost on every pop.
+  static_assert(!(LEAN && TOPO), "LEAN excludes topology");
+  __device__ __forceinline__ bool hpA() const { return !LEAN && d.hpAny; }
+  __device__ __forceinline__ bool volA() const { return !LEAN && d.volAny; }
+  __device__ __forceinline__ bool negR() const { return !LEAN && d.negReq; }
+  __device__ __forceinline__ bool dupU() const { return !LEAN && d.dupUids; }
+  __device__ __forceinline__ bool keys(int sflags) const { return !LEAN && (sflags & SF_HAS_KEYS); }
   // By value: a reference to a byval kernel argument forces a scratch copy of the whole struct
   // (every field access then becomes a scratch load); values scalarise into SGPRs.
   // Launch constants by reference, not by copy: the kernel arguments stay in the kernarg segment and
@@ -473,7 +482,7 @@ struct Solver {
     nf0 = SIM ? D.n_flags[c0] : 0;
     nf1 = SIM ? D.n_flags[c1] : 0;
     uint64_t h0 = 0, h1 = 0;
-    if (d.hpAny) {  // HostPortUsage.Conflicts (hostportusage.go:74-85)
+    if (hpA()) {  // HostPortUsage.Conflicts (hostportusage.go:74-85)
       h0 = own0 ? W.n_hp[c0] : D.n_hp0[c0];
       h1 = own1 ? W.n_hp[c1] : D.n_hp0[c1];
     }
@@ -489,11 +498,11 @@ struct Solver {
       ok0 &= (a0[r] >= 0) & (q0[r] + pod[r] <= a0[r]);
       ok1 &= (a1[r] >= 0) & (q1[r] + pod[r] <= a1[r]);
     }
-    if (d.volAny && cur_vm) {
+    if (volA() && cur_vm) {
       if (ok0) ok0 = vol_ok(c0);
       if (ok1) ok1 = vol_ok(c1);
     }
-    if (sflags & SF_HAS_KEYS) {  // strict Compatible: no AllowUndefinedWellKnownLabels
+    if (keys(sflags)) {  // strict Compatible: no AllowUndefinedWellKnownLabels
       if (ok0) ok0 = rs_compatible(L, node_rs(c0), s_pin, 0);
       if (ok1) ok1 = rs_compatible(L, node_rs(c1), s_pin, 0);
     }
@@ -518,9 +527,9 @@ struct Solver {
   // Solve: commit of a pod to node j by its owner lane.
   __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod) {
     for (int r = 0; r < R(); r++) W.n_req[(int64_t)j * R() + r] += pod[r];
-    if (d.hpAny) W.n_hp[j] = (W.n_hp[j] & ~cur_hpo) | cur_hpu;  // HostPortUsage.Add (hostportusage.go:70-72)
-    if (d.volAny && cur_vm) vol_commit(j);
-    if (sflags & SF_HAS_KEYS) rs_add(L, W.n_rs + (int64_t)j * d.RSW, s_pin);
+    if (hpA()) W.n_hp[j] = (W.n_hp[j] & ~cur_hpo) | cur_hpu;  // HostPortUsage.Add (hostportusage.go:70-72)
+    if (volA() && cur_vm) vol_commit(j);
+    if (keys(sflags)) rs_add(L, W.n_rs + (int64_t)j * d.RSW, s_pin);
   }
   // SIM: copy-on-write commit (wave-uniform).  W.n_req is indexed by node but only the nodes a pod
   // landed on are ever written (s_tch marks them), so a fresh simulation needs no initialisation.
@@ -539,11 +548,11 @@ struct Solver {
         if (RT == 0 && r >= d.R) break;
         W.n_req[(int64_t)j * R() + r] = q[r] + pod[r];
       }
-      if (d.hpAny) W.n_hp[j] = ((fresh ? D.n_hp0[j] : W.n_hp[j]) & ~cur_hpo) | cur_hpu;
-      if (d.volAny && cur_vm) vol_commit(j);
+      if (hpA()) W.n_hp[j] = ((fresh ? D.n_hp0[j] : W.n_hp[j]) & ~cur_hpo) | cur_hpu;
+      if (volA() && cur_vm) vol_commit(j);
       if (fresh) s_tch[j >> 5] |= 1u << (j & 31);
     }
-    if (sflags & SF_HAS_KEYS) {
+    if (keys(sflags)) {
       const bool rsfresh = !tbit(s_tchr, j);
       int slot;
       if (rsfresh) {
@@ -682,7 +691,7 @@ struct Solver {
     wsync();
     copy_words(s_rs, node_rs(j), d.RSW);
     wsync();
-    if (sflags & SF_HAS_KEYS) rs_add_wave(L, s_rs, s_pin, 0);
+    if (keys(sflags)) rs_add_wave(L, s_rs, s_pin, 0);
     return topo_apply(s_rs, -1, 0) == 0;
   }
   // The node's requirements after a node_slow commit (n.requirements = nodeRequirements): s_rs.
@@ -888,14 +897,14 @@ struct Solver {
   // --- NodeClaim quick reject at sorted position j: necessary conditions of NodeClaim.Add ------
   __device__ __forceinline__ bool claim_quick(int j, int s, int sflags, uint32_t toltpl, const int64_t* pod) const {
     if (!((toltpl >> s_ptpl[j]) & 1u)) return false;  // Taints.Tolerates (nodeclaim.go:68-71)
-    if (d.hpAny && (W.c_hp[s_order[j]] & cur_hpc)) return false;  // host port conflicts (:72-75)
+    if (hpA() && (W.c_hp[s_order[j]] & cur_hpc)) return false;  // host port conflicts (:72-75)
     bool ok = true;
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
       ok &= pod[r] <= s_phead[(int64_t)j * R() + r];
     }
-    if (ok && (sflags & SF_HAS_KEYS))
+    if (ok && keys(sflags))
       ok = rs_compatible(L, W.c_rs + (int64_t)s_order[j] * d.RSW, s_pin, d.allowWK);
     return ok;
   }
@@ -908,11 +917,11 @@ struct Solver {
     const ClaimView<INL>& v = cv<INL>();
     bool changed = false;
     PH_BEGIN(u0);
-    if ((sflags & SF_HAS_KEYS) || (TOPO && t_mask)) {
+    if (keys(sflags) || (TOPO && t_mask)) {
       const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
       copy_words(s_rs, crs, d.RSW);
       wsync();
-      if (sflags & SF_HAS_KEYS)
+      if (keys(sflags))
         changed = rs_add_wave(L, s_rs, s_pin, (sflags & SF_TOUCHES_IT_KEYS) ? d.itKeys : 0);
       if (TOPO && t_mask) {
         if (topo_apply(s_rs, c, d.allowWK) != 0) {  // topology requirements (nodeclaim.go:92-100)
@@ -935,7 +944,7 @@ struct Solver {
     PH_BEGIN(u1);
     copy_words(s_rem, v.rem + (int64_t)c * d.TW, d.TW);
     wsync();
-    if (!d.negReq) {
+    if (!negR()) {
       // Requests only grow: the options a request no longer fits are a prefix of each resource's
       // Allocatable-ascending order beyond its threshold.
       int removed = 0, examined = 0;
@@ -1042,7 +1051,7 @@ struct Solver {
     const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
     for (int r = 0; r < R(); r++) {
       int64_t m = INT64_MIN;
-      if (!d.negReq) {  // the first option from the top of the Allocatable-ascending order
+      if (!negR()) {  // the first option from the top of the Allocatable-ascending order
         const int64_t base = (int64_t)tb * R() + (int64_t)r * nIT;
         for (int k = nIT - 1; k >= 0; k -= kWave) {
           const int i = k - lane();
@@ -1094,17 +1103,17 @@ struct Solver {
       }
       v.cnt[c] = ncnt;
       s_okey[pos] = okNew;
-      if (d.hpAny) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
+      if (hpA()) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
     }
-    if ((sflags & SF_HAS_KEYS) || (TOPO && t_mask)) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
+    if (keys(sflags) || (TOPO && t_mask)) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
     copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     log_commit(p, c, nlog);
     // The max bound stays valid as the options only shrink; it is tightened lazily when a full check
     // fails.  HBM-resident claim state is re-read by other lanes: drain the stores first.
-    if ((sflags & SF_HAS_KEYS) || !INL || d.hpAny) hbm_release();
+    if (keys(sflags) || !INL || hpA()) hbm_release();
     wsync();
     if (TOPO && (t_sel | t_inv)) {  // Topology.Record on the claim's final requirements (nodeclaim.go:121)
-      if ((sflags & SF_HAS_KEYS) || t_mask) topo_record(s_rs, c, -1, d.allowWK);
+      if (keys(sflags) || t_mask) topo_record(s_rs, c, -1, d.allowWK);
       else topo_record(W.c_rs + (int64_t)c * d.RSW, c, -1, d.allowWK);
     }
     algbytes += 24 * R() + 4 * d.TW + 8;
@@ -1147,7 +1156,7 @@ struct Solver {
           copy_words(s_rs, D.tpl_rs + (int64_t)t * d.RSW, d.RSW);
           wsync();
           bool ok = true;
-          if (sflags & SF_HAS_KEYS) {
+          if (keys(sflags)) {
             ok = rs_compatible(L, s_rs, s_pin, d.allowWK);
             if (ok) rs_add_wave(L, s_rs, s_pin, 0);
           }
@@ -1552,14 +1561,14 @@ struct Solver {
   }
 };
 
-template <int RT, bool TL, bool SIM, bool TOPO>
+template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_solve(KsDev D, const KsWork* works, Plan pl) {
-  constexpr int RM = Solver<RT, TL, SIM, TOPO>::RM;
+  constexpr int RM = Solver<RT, TL, SIM, TOPO, LEAN>::RM;
   extern __shared__ __attribute__((aligned(16))) char smem_generic[];
   char KS_L* smem = (char KS_L*)smem_generic;
   const KsWork KS_C& W = ((const KsWork KS_C*)works)[blockIdx.x];
   const KsDims& d = D.d;
-  Solver<RT, TL, SIM, TOPO> S(D, W, pl);
+  Solver<RT, TL, SIM, TOPO, LEAN> S(D, W, pl);
   if (TOPO) S.t_active = ~d.tgLate;
   const int R = S.R();
   char KS_L* sp = smem;
@@ -1729,7 +1738,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const int g = SIM ? rdl(w.g, wi) : p;
     const int uid = rdl(w.uid, wi);
     uint64_t ll = (uint64_t)rdl64((int64_t)w.ll, wi);
-    if (d.dupUids) {
+    if (S.dupU()) {
       hbm_release();
       ll = uni64((int64_t)ld_sc1(W.last_len + uid));
     }
@@ -1741,13 +1750,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const int sflags = rdl(w.flags, wi);
     const uint32_t toltpl = (uint32_t)rdl((int)w.toltpl, wi);
     const uint64_t tol0 = (uint64_t)rdl64((int64_t)w.tol0, wi), tol1 = (uint64_t)rdl64((int64_t)w.tol1, wi);
-    if (d.hpAny) {
+    if (S.hpA()) {
       S.cur_hpc = (uint64_t)rdl64((int64_t)w.hpc, wi);
       S.cur_hpu = (uint64_t)rdl64((int64_t)w.hpu, wi);
       S.cur_hpo = (uint64_t)rdl64((int64_t)w.hpo, wi);
     }
-    if (d.volAny) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
-    if (sflags & SF_HAS_KEYS) {  // the state's record, read by every check of this pop
+    if (S.volA()) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
+    if (S.keys(sflags)) {  // the state's record, read by every check of this pop
       S.copy_words(S.s_pin, D.st_rs + (int64_t)s * d.RSW, d.RSW);
       wsync();
     }
@@ -1779,8 +1788,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
           for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
           ok &= (whp[k] & S.cur_hpc) == 0;
-          if (d.volAny && S.cur_vm && ok) ok = S.vol_ok(n);
-          if ((sflags & SF_HAS_KEYS) && ok) ok = rs_compatible(S.L, S.node_rs(n), S.s_pin, 0);
+          if (S.volA() && S.cur_vm && ok) ok = S.vol_ok(n);
+          if (S.keys(sflags) && ok) ok = rs_compatible(S.L, S.node_rs(n), S.s_pin, 0);
           if (TOPO && S.t_mask && ok) ok = S.topo_node_state(n) == 1;  // every node is labelled here
           const uint64_t m = wballot(ok);
           if (m) {
@@ -1801,14 +1810,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                 for (int r = 0; r < RM; r++) wrq[k][r] += pod[r];
                 whp[k] = (whp[k] & ~S.cur_hpo) | S.cur_hpu;
-                if (d.volAny && S.cur_vm) S.vol_commit(j);
+                if (S.volA() && S.cur_vm) S.vol_commit(j);
               }
             }
           PH_BEGIN(t7);
           if constexpr (SIM) {
-            if (sflags & SF_HAS_KEYS) S.sim_node_commit(j, s, sflags, pod, pod, nrs, true);
+            if (S.keys(sflags)) S.sim_node_commit(j, s, sflags, pod, pod, nrs, true);
             if ((rdl(nfv, owner) & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
-          } else if ((sflags & SF_HAS_KEYS) && lane() == owner) {
+          } else if (S.keys(sflags) && lane() == owner) {
             rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, S.s_pin);
           }
           if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, j, 0);  // existingnode.go:121
@@ -1993,13 +2002,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 // include this file), so the four compile in parallel.
 template <bool SIM, bool TOPO>
 hipError_t launch_family(const KsDev& D, const KsWork* works_dev, int n, const Plan& pl, hipStream_t st) {
-#define KS_LAUNCH(RT_, TL_) hipLaunchKernelGGL((k_solve<RT_, TL_, SIM, TOPO>), dim3(n), dim3(kWave), pl.lds, st, D, works_dev, pl)
+#define KS_LAUNCH(RT_, TL_, LEAN_) \
+  hipLaunchKernelGGL((k_solve<RT_, TL_, SIM, TOPO, LEAN_>), dim3(n), dim3(kWave), pl.lds, st, D, works_dev, pl)
   if (n <= 0) return hipSuccess;  // e.g. a consolidation pass with no candidates: nothing to simulate
   const bool tl = pl.talloc != 0;
+  // the lean instantiations exist for the common shapes only: 3 or 4 resources, LDS-resident tables
+  const bool lean = !TOPO && D.d.lean && tl;
   switch (D.d.R) {
-    case 3: if (tl) KS_LAUNCH(3, true); else KS_LAUNCH(3, false); break;
-    case 4: if (tl) KS_LAUNCH(4, true); else KS_LAUNCH(4, false); break;
-    default: if (tl) KS_LAUNCH(0, true); else KS_LAUNCH(0, false); break;
+    case 3: if (lean) KS_LAUNCH(3, true, !TOPO); else if (tl) KS_LAUNCH(3, true, false); else KS_LAUNCH(3, false, false); break;
+    case 4: if (lean) KS_LAUNCH(4, true, !TOPO); else if (tl) KS_LAUNCH(4, true, false); else KS_LAUNCH(4, false, false); break;
+    default: if (tl) KS_LAUNCH(0, true, false); else KS_LAUNCH(0, false, false); break;
   }
 #undef KS_LAUNCH
   return hipGetLastError();
