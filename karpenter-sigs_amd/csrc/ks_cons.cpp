@@ -538,7 +538,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     auto it = h.nodes[(size_t)node].capacity.find(h.resNames[(size_t)r]);
     return it == h.nodes[(size_t)node].capacity.end() ? 0 : h.toDev(r, it->second);
   };
-  Arena a;
+  Arena a;   // device workspaces (zeroed on the device, never staged on the host)
+  Arena ai;  // per-simulation inputs (staged and uploaded): removed nodes, limits, prices, topology deltas
   struct Off {
     size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
         last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price, n_hp,
@@ -590,9 +591,9 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     o.counters = a.add(8 * CT_NCOUNTERS);
     o.n_hp = a.add(d.hpAny ? 8 * (size_t)N : 8);
     o.c_hp = a.add(8 * K);
-    o.rm = a.add(4 * std::max<size_t>(sm.cands.size(), 1));
-    o.pool0 = a.add(8 * (size_t)NP * R);
-    o.st_price = sm.multi ? a.add(8 * (size_t)std::max(d.T, 1)) : 0;
+    o.rm = ai.add(4 * std::max<size_t>(sm.cands.size(), 1));
+    o.pool0 = ai.add(8 * (size_t)NP * R);
+    o.st_price = sm.multi ? ai.add(8 * (size_t)std::max(d.T, 1)) : 0;
     if (d.volAny) {  // indexed by node, written only where a pod with PVCs lands (copy-on-write)
       o.n_vm = a.add(8 * (size_t)N);
       o.n_vc = a.add(4 * (size_t)N * std::max(d.VD, 1));
@@ -602,12 +603,14 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       o.tg_ccnt = a.add(4 * (size_t)d.G * (P + 1));
       o.tg_cpos = a.add(4 * (size_t)d.G);
       tdel[k] = sim_topology(c, sm, simPods[k], tdead[k]);
-      o.tdel = a.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
+      o.tdel = ai.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
     }
   }
   c.L.lnent = (int)entries.size();
-  HIPCHK(hipMalloc(&c.L.lbuf, std::max<size_t>(a.total, 256)));
+  const size_t inBase = a.total;
+  HIPCHK(hipMalloc(&c.L.lbuf, std::max<size_t>(inBase + ai.total, 256)));
   char* base = (char*)c.L.lbuf;
+  char* ibase = base + inBase;
   HIPCHK(hipMalloc(&c.L.lworks, sizeof(KsWork) * std::max(ns, 1)));
   HIPCHK(hipMalloc(&c.L.lrec, 4 * (size_t)c.recWords * std::max(ns, 1)));
   HIPCHK(hipMalloc(&c.L.lentries, 4 * (size_t)std::max(c.L.lnent, 1)));
@@ -627,7 +630,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   while ((1ll << c.L.lsbits) < std::max(ns, 2)) c.L.lsbits++;
 
   // per-simulation inputs: removed nodes, limits, prices
-  std::vector<char> stage(a.total, 0);
+  std::vector<char> stage(ai.total, 0);
   std::vector<KsWork> works(ns);
   for (int k = 0; k < ns; k++) {
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
@@ -683,7 +686,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
           st[(size_t)t] = f == prices.end() ? 0.0 : f->second;  // a missing map entry reads as 0
         }
       memcpy(stage.data() + o.st_price, st.data(), 8 * st.size());
-      w.st_price = (const double*)(base + o.st_price);
+      w.st_price = (const double*)(ibase + o.st_price);
     }
     w.c_tpl = (int32_t*)(base + o.c_tpl);
     w.c_cnt = (int32_t*)(base + o.c_cnt);
@@ -714,8 +717,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     w.pod_map = c.L.lpodmap + entBeg[k];
     w.P = simP[k];
     w.nrm = (int32_t)rm.size();
-    w.rm = (const int32_t*)(base + o.rm);
-    w.pool0 = (const int64_t*)(base + o.pool0);
+    w.rm = (const int32_t*)(ibase + o.rm);
+    w.pool0 = (const int64_t*)(ibase + o.pool0);
     w.rec = c.L.lrec + (size_t)k * c.recWords;
     w.price = price;
     w.cflags = cflags;
@@ -729,13 +732,16 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       w.tg_ccnt = (int32_t*)(base + o.tg_ccnt);
       w.tg_cpos = (int32_t*)(base + o.tg_cpos);
       memcpy(stage.data() + o.tdel, tdel[k].data(), 4 * tdel[k].size());
-      w.tdel = (const int32_t*)(base + o.tdel);
+      w.tdel = (const int32_t*)(ibase + o.tdel);
       w.ntdel = (int32_t)(tdel[k].size() / 2);
       w.tdead = tdead[k];
     }
     works[k] = w;
   }
-  HIPCHK(hipMemcpy(c.L.lbuf, stage.data(), a.total, hipMemcpyHostToDevice));
+  // The workspaces (~120 KB per simulation on C5, mostly the node-indexed copy-on-write request slots)
+  // are zeroed on the device; only the inputs cross PCIe.
+  HIPCHK(hipMemset(c.L.lbuf, 0, inBase));
+  if (ai.total) HIPCHK(hipMemcpy(ibase, stage.data(), ai.total, hipMemcpyHostToDevice));
   if (ns) HIPCHK(hipMemcpy(c.L.lworks, works.data(), sizeof(KsWork) * ns, hipMemcpyHostToDevice));
   c.L.lhost = works;
   // LDS plan: a small budget per simulation so several simulations share a CU

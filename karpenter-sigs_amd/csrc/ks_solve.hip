@@ -50,6 +50,11 @@ __device__ __forceinline__ int lane() { return (int)threadIdx.x; }
 __device__ __forceinline__ uint64_t wballot(bool p) { return __ballot(p ? 1 : 0); }
 __device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// A wave-uniform branch condition.  The commit chain's control flow is uniform by construction, but
+// the compiler cannot prove it for values that pass through LDS atomics or lane-indexed loads; a
+// condition it believes divergent turns the whole Solve loop into exec-masked code (every loop-carried
+// scalar in a VGPR, mask bookkeeping spilled to VGPR lanes).  readfirstlane makes the branch scalar.
+__device__ __forceinline__ bool ub(bool x) { return __builtin_amdgcn_readfirstlane((int)x) != 0; }
 __device__ __forceinline__ int64_t uni64(int64_t x) {
   return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
                    (uint32_t)__builtin_amdgcn_readfirstlane((int)x));
@@ -1564,6 +1569,10 @@ struct Solver {
 template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_solve(KsDev D, const KsWork* works, Plan pl) {
   constexpr int RM = Solver<RT, TL, SIM, TOPO, LEAN>::RM;
+  // Simulations force their loop's branch conditions scalar (ub); measured on the Solve instantiations
+  // the extra scalar registers cost more (spills) than the exec-mask bookkeeping they remove.
+  auto U = [](bool x) { return SIM ? ub(x) : x; };
+  auto UI = [](int x) { return SIM ? uni(x) : x; };
   extern __shared__ __attribute__((aligned(16))) char smem_generic[];
   char KS_L* smem = (char KS_L*)smem_generic;
   const KsWork KS_C& W = ((const KsWork KS_C*)works)[blockIdx.x];
@@ -1681,8 +1690,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // flags.  A pod that fits there costs no memory round trip; commits update the owner's registers.
   constexpr int NW = RT > 0 ? 4 : 0;
   constexpr int NWA = NW > 0 ? NW : 1;
+  // LEAN (no negative requests): the window keeps each node's free capacity Available - requests, so
+  // Fits(requests + pod, Available) is one compare per resource; a node that can never fit (negative
+  // Available, beyond N, removed by the simulation) holds INT64_MIN, which no request (>= 0) fits.
+  constexpr int NWQ = LEAN ? 1 : NWA;
   uint64_t wtx[NWA], wty[NWA], whp[NWA];
-  int64_t wav[NWA][RM], wrq[NWA][RM];
+  int64_t wav[NWA][RM], wrq[NWQ][RM];  // LEAN: wav = free capacity, wrq unused
   int wnf[NWA];
   if constexpr (NW > 0) {
     if (d.N > 0) {
@@ -1691,11 +1704,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         const int n = k * kWave + lane(), c = n < d.N ? n : d.N - 1;
         wtx[k] = D.n_taint[2 * c];
         wty[k] = D.n_taint[2 * c + 1];
+        bool never = n >= d.N;
+        if (SIM) never |= S.tbit(S.s_rmv, c);
 #pragma unroll
         for (int r = 0; r < RM; r++) {
-          wav[k][r] = D.n_avail[(int64_t)c * RM + r];
-          wrq[k][r] = D.n_req0[(int64_t)c * RM + r];
+          const int64_t a = D.n_avail[(int64_t)c * RM + r], q = D.n_req0[(int64_t)c * RM + r];
+          if constexpr (LEAN) {
+            never |= a < 0;
+            wav[k][r] = a - q;
+          } else {
+            wav[k][r] = a;
+            wrq[k][r] = q;
+          }
         }
+        if constexpr (LEAN)
+#pragma unroll
+          for (int r = 0; r < RM; r++) wav[k][r] = never ? INT64_MIN : wav[k][r];
         wnf[k] = SIM ? D.n_flags[c] : 0;
         whp[k] = D.n_hp0[c];
       }
@@ -1724,7 +1748,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const uint64_t tstart = __builtin_amdgcn_s_memtime();
 #endif
 
-  while (qlen > 0) {
+  while (true) {
+    qlen = UI(qlen);
+    qhead = UI(qhead);
+    wi = UI(wi);
+    wn = UI(wn);
+    if (qlen <= 0) break;
     PH_BEGIN(t0);
     if (wi == wn) {
       S.refill(w, qhead, qlen, P, pushed);
@@ -1732,6 +1761,57 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       wn = qlen < kWave ? qlen : kWave;
       wi = 0;
       windows++;
+    }
+    if constexpr (LEAN && SIM && NW > 0) {
+      // Fast path of a simulation over resource-only pods (what consolidation re-schedules): while the
+      // next pops each fit a node of the register window, the step is Queue.Pop + the window's
+      // first-fit ballots + the commit to the owner lane's registers, with nothing else live.  A pod
+      // that fits no window node (or a stale queue) leaves it un-popped for the general step below.
+      if (d.N > 0) {
+        while (wi < wn) {
+          const uint64_t fll = (uint64_t)rdl64((int64_t)w.ll, wi);
+          if ((uint32_t)(fll >> 32) == epoch && (uint32_t)fll == (uint32_t)qlen) break;
+          const uint64_t ft0 = (uint64_t)rdl64((int64_t)w.tol0, wi), ft1 = (uint64_t)rdl64((int64_t)w.tol1, wi);
+          int64_t fp[RM];
+#pragma unroll
+          for (int r = 0; r < RM; r++) fp[r] = rdl64(w.req[r], wi);
+          int kj = -1;
+          uint64_t mj = 0;
+#pragma unroll
+          for (int k = 0; k < NW; k++) {
+            bool ok = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
+#pragma unroll
+            for (int r = 0; r < RM; r++) ok &= fp[r] <= wav[k][r];
+            const uint64_t m = wballot(ok);
+            if (m) {
+              kj = k;
+              mj = m;
+              break;
+            }
+          }
+          if (kj < 0) break;
+          const int fpod = rdl(w.p, wi);
+          const int j = kj * kWave + ctz64(mj), owner = j & (kWave - 1);
+          int nfv = 0;
+#pragma unroll
+          for (int k = 0; k < NW; k++)
+            if (k == kj) {
+              nfv = wnf[k];
+              if (lane() == owner)
+#pragma unroll
+                for (int r = 0; r < RM; r++) wav[k][r] -= fp[r];
+            }
+          if ((rdl(nfv, owner) & NF_UNUSABLE) && !(rdl(w.pf, wi) & PF_PROVISIONABLE)) allSched = false;
+          if (rdl(w.st, wi) == ST_FAILED && lane() == 0) W.pod_status[fpod] = ST_SCHEDULED;
+          S.log_commit(fpod, -(j + 1), nlog);
+          S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
+          qhead = qhead + 1 == P ? 0 : qhead + 1;
+          qlen--;
+          pops++;
+          wi++;
+        }
+        if (wi == wn) continue;  // window drained: refill (or finish) at the loop head
+      }
     }
     // Queue.Pop (queue.go:46-61)
     const int p = rdl(w.p, wi);
@@ -1742,7 +1822,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       hbm_release();
       ll = uni64((int64_t)ld_sc1(W.last_len + uid));
     }
-    if ((uint32_t)(ll >> 32) == epoch && (uint32_t)ll == (uint32_t)qlen) break;
+    if (U((uint32_t)(ll >> 32) == epoch && (uint32_t)ll == (uint32_t)qlen)) break;
     qhead = qhead + 1 == P ? 0 : qhead + 1;
     qlen--;
     if (++pops > popCap) { err = KE_ITER_CAP; break; }
@@ -1783,10 +1863,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
         for (int k = 0; k < NW; k++) {
           const int n = k * kWave + lane();
-          bool ok = (n < d.N) & (((wtx[k] & ~tol0) | (wty[k] & ~tol1)) == 0);
-          if (SIM) ok &= !S.tbit(S.s_rmv, n < d.N ? n : 0);
+          bool ok = (((wtx[k] & ~tol0) | (wty[k] & ~tol1)) == 0);
+          if constexpr (LEAN) {
 #pragma unroll
-          for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
+            for (int r = 0; r < RM; r++) ok &= pod[r] <= wav[k][r];
+          } else {
+            ok &= n < d.N;
+            if (SIM) ok &= !S.tbit(S.s_rmv, n < d.N ? n : 0);
+#pragma unroll
+            for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
+          }
           ok &= (whp[k] & S.cur_hpc) == 0;
           if (S.volA() && S.cur_vm && ok) ok = S.vol_ok(n);
           if (S.keys(sflags) && ok) ok = rs_compatible(S.L, S.node_rs(n), S.s_pin, 0);
@@ -1799,7 +1885,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           }
         }
         asm volatile("; KS_MARK window_end");
-        if (kj >= 0) {
+        if (U(kj >= 0)) {
           const int j = kj * kWave + ctz64(mj), owner = j & (kWave - 1);
           int nfv = 0;
 #pragma unroll
@@ -1808,7 +1894,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
               nfv = wnf[k];
               if (lane() == owner) {
 #pragma unroll
-                for (int r = 0; r < RM; r++) wrq[k][r] += pod[r];
+                for (int r = 0; r < RM; r++) {
+                  if constexpr (LEAN) wav[k][r] -= pod[r];
+                  else wrq[k][r] += pod[r];
+                }
                 whp[k] = (whp[k] & ~S.cur_hpo) | S.cur_hpu;
                 if (S.volA() && S.cur_vm) S.vol_commit(j);
               }
@@ -1831,7 +1920,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         scanFrom = NW * kWave;
       }
     }
-    for (int base = skipNodes ? d.N : scanFrom; base < d.N && !placed; base += 2 * kWave) {
+    for (int base = skipNodes ? d.N : scanFrom; U(base < d.N && !placed); base += 2 * kWave) {
       bool ok0, ok1, sl0, sl1;
       int nf0, nf1;
       int64_t q0[RM], q1[RM];
@@ -1856,6 +1945,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           if (fm) break;
         }
       }
+      j = UI(j);
       if (j >= 0) {
         const bool hi = j - base >= kWave;
         S.algbytes += (int64_t)(j - base + 1) * (16 * R + 16);
@@ -1886,37 +1976,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
     PH_END(t1, 1);
     // 2) in-flight NodeClaims, sorted by pod count
-    if (!placed && nclaims > 0) {
+    if (U(!placed && nclaims > 0)) {
       PH_BEGIN(t2);
       sorts++;
-      if (!srt) {
+      if (!U(srt)) {
         S.sort_claims(nclaims);
         slow++;
         srt = true;
       }
       PH_END(t2, 2);
-      for (int base = 0; base < nclaims && !placed; base += kWave) {
+      for (int base = 0; U(base < nclaims && !placed); base += kWave) {
         PH_BEGIN(t3);
         const int j = base + lane();
         const bool q = j < nclaims && S.claim_quick(j, s, sflags, toltpl, pod);
         uint64_t m = wballot(q);
         S.algbytes += (int64_t)min(kWave, nclaims - base) * (8 * R + 4);
         PH_END(t3, 3);
-        while (m && !placed) {
+        while (U(m != 0 && !placed)) {
           const int jj = base + ctz64(m);
           m &= m - 1;
           const int c = uni(S.s_order[jj]);
           PH_BEGIN(t4);
           const bool inl = c < pl.KL;
           int ncnt = 0;
-          const bool ok = inl ? S.template claim_full<true>(c, s, sflags, pod, req, nthr, ncnt)
-                              : S.template claim_full<false>(c, s, sflags, pod, req, nthr, ncnt);
+          const bool ok = U(inl ? S.template claim_full<true>(c, s, sflags, pod, req, nthr, ncnt)
+                                 : S.template claim_full<false>(c, s, sflags, pod, req, nthr, ncnt));
           fulls++;
           PH_END(t4, 4);
           PH_BEGIN(t5);
           if (ok) {
-            srt = inl ? S.template commit_claim<true>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog)
-                      : S.template commit_claim<false>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog);
+            srt = U(inl ? S.template commit_claim<true>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog)
+                         : S.template commit_claim<false>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog));
             placed = true;
           } else {
             // the quick bound was stale: tighten it to the exact max over the current options
@@ -1930,10 +2020,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
     // 3) new NodeClaim per template
-    if (!placed) {
+    if (!U(placed)) {
       PH_BEGIN(t6);
-      const int r = S.try_templates(p, s, sflags, toltpl, pod, nclaims, nlog, hostCtr, srt);
+      const int r = UI(S.try_templates(p, s, sflags, toltpl, pod, nclaims, nlog, hostCtr, srt));
       PH_END(t6, 6);
+      nclaims = UI(nclaims);
+      hostCtr = UI(hostCtr);
+      srt = U(srt);
       if (r < 0) { err = KE_CLAIM_CAP; break; }
       if (r == 1) placed = true;
       if (r == 2) {  // no templates: add() returns a nil error
@@ -1941,14 +2034,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         placed = true;
       }
     }
-    if (placed) {
+    if (U(placed)) {
       // SIM: the epilogue reads the final status; only a pod that failed before needs a store
       if (SIM && rdl(w.st, wi - 1) == ST_FAILED && lane() == 0) W.pod_status[p] = ST_SCHEDULED;
       continue;
     }
     // failure: Preferences.Relax (preferences.go:38) + Queue.Push (queue.go:64-71)
     const int s0 = D.pod_state0[g], ns = D.pod_nstate[g];
-    const bool relaxed = s - s0 + 1 < ns;
+    const bool relaxed = U(s - s0 + 1 < ns);
     if (lane() == 0) {
       W.pod_status[p] = ST_FAILED;
       W.pod_fstate[p] = s;
