@@ -232,6 +232,14 @@ void ks_upload(ks_problem* pb) {
   HIPCHK(hipMemcpy(pb->dbuf, staging.data(), a.total, hipMemcpyHostToDevice));
   char* b = (char*)pb->dbuf;
   KsDev& D = pb->dev;
+  // k_feasibility's output: one row of TW words per (relaxation state, template), rewritten by every
+  // Solve / pass; skipped (the kernel evaluates every key itself) if it would exceed 1 GiB
+  const size_t fmBytes = 4 * (size_t)h.dims.S * h.dims.NTPL * h.dims.TW;
+  // (LEAN problems carry no pod label requirements: no step would read a row)
+  h.dims.fmOn = fmBytes > 0 && fmBytes <= ((size_t)1 << 30) && h.dims.NK <= 64 && !h.dims.lean &&
+                !getenv("KS_NO_FEASIBILITY");
+  if (h.dims.fmOn) HIPCHK(hipMalloc(&pb->fmbuf, fmBytes));
+  D.st_fm = (uint32_t*)pb->fmbuf;
   D.d = h.dims;
   D.keys = (const KeyMeta*)(b + o_keys);
   D.wordValid = (const uint32_t*)(b + o_wv);
@@ -362,7 +370,11 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     for (auto& kv : req) {
       int r = h.resId.at(kv.first);
       if (h.toDev(r, kv.second) != creq[(size_t)c * d.R + r])
-        throw KsError(KS_ERR_INTERNAL, "device requests diverge from the replayed Merge for " + kv.first);
+        throw KsError(KS_ERR_INTERNAL, "device requests diverge from the replayed Merge for " + kv.first + " (claim " +
+                                           std::to_string(c) + " at position " + std::to_string(k) + " of " +
+                                           std::to_string(nc) + ": device " + std::to_string(creq[(size_t)c * d.R + r]) +
+                                           ", replay " + std::to_string(h.toDev(r, kv.second)) + " over " +
+                                           std::to_string(cl.pods.size()) + " pods)");
     }
     const uint32_t* rec = &crs[(size_t)c * d.RSW];
     std::string j = "{\"nodePoolName\":";

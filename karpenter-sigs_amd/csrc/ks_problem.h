@@ -67,12 +67,14 @@ struct KsDims {
   int32_t G, G1;           // topology groups (ks_topo.cpp): [0, G1) t.topologies, [G1, G) inverse
   int32_t tgMaxNv;         // largest value universe of a topology key
   int32_t tgCntWords;      // size of the count table
+  int32_t tgSmall;         // count words [0, tgSmall): the non-hostname groups, LDS-resident in k_solve
   int32_t FSW;             // fail_rs words per (pod, template): RSW, or counts + registered bits if larger
   int32_t volAny;          // some pending pod mounts a PVC of a driver an existing node limits
   int32_t VD;              // limited drivers (<= kMaxVD); vol_dm[VD] partitions the pods' PVC universe
   int32_t tgUnlab;         // some existing node lacks the label of a topology group's key (k_solve node_slow)
   uint64_t tgLate;         // groups a relaxed state creates mid-Solve: inactive until that relaxation
   uint64_t fkMulti;        // keys some instance type constrains with more than one value (feas_masks)
+  int32_t fmOn;            // st_fm is computed (k_feasibility) and k_solve reads it
   int32_t lean;            // none of host ports, limited volumes, pod label requirements, shared UIDs,
                            // negative requests, topology: k_solve's LEAN instantiation applies
 };
@@ -155,6 +157,10 @@ struct KsDev {
   const uint32_t KS_G* fk_words;
   const int32_t KS_G* fk_key_off;  // [NTPL][NK]
   const int32_t KS_G* fk_tpl;      // [NTPL][3]
+  // k_feasibility's output: per (relaxation state, template), the template positions whose instance type
+  // Intersects both the template's and the state's requirements on every key no instance type constrains
+  // with more than one value (fkMulti excluded); [S][NTPL][TW]
+  uint32_t KS_G* st_fm;
 };
 
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };

@@ -47,6 +47,7 @@ struct ks_problem {
   ks::Host host;
   ks::KsDev dev{};
   void* dbuf = nullptr;
+  void* fmbuf = nullptr;  // k_feasibility rows (KsDev::st_fm)
   void* wbuf = nullptr;
   size_t wbytes = 0;
   ks::KsWork* works_dev = nullptr;
@@ -69,6 +70,7 @@ struct ks_problem {
     if (stemp) (void)hipFree(stemp);
     if (hqorder) (void)hipFree(hqorder);
     if (dbuf) (void)hipFree(dbuf);
+    if (fmbuf) (void)hipFree(fmbuf);
     if (wbuf) (void)hipFree(wbuf);
     if (works_dev) (void)hipFree(works_dev);
     if (stream) (void)hipStreamDestroy(stream);

@@ -28,6 +28,9 @@
 // of thousands of them fills the 256 CUs.  Nothing here is a dense contraction: no MFMA.
 #include <hip/hip_runtime.h>
 
+#ifndef KS_FM_OFF
+#define KS_FM_OFF 0
+#endif
 #ifndef KS_TU
 #define KS_TU 0
 #endif
@@ -212,6 +215,88 @@ __device__ __attribute__((noinline)) bool rs_add_wave(const DevLayout L, LU32 ou
   return wballot(diff) != 0;
 }
 
+// Requirements.Intersects(IT, X) (requirements.go:241-258) on the keys `keys` of X, for word wc of template
+// t's position bitset, from the host's per-(key, value) position tables (ks_host.cpp "feasibility tables"):
+// per key, the positions whose IT lacks the key (only shared keys are checked), those holding a value X
+// admits, and -- when X's operator is NotIn / DoesNotExist -- those whose IT says DoesNotExist (both
+// negative).  Every lane of the wave calls it with the same X, t and keys (ballots over X's values).
+template <class PX>
+__device__ __forceinline__ uint32_t fk_intersects_word(const KsDev& D, const DevLayout& L, PX X, int t, int wc,
+                                                       uint64_t keys) {
+  const uint32_t KS_G* F = D.fk_words;
+  const KsDims& d = D.d;
+  const int TW = d.TW;
+  uint32_t ic = ~0u;
+  for (uint64_t m = keys; m; m &= m - 1) {
+    const int k = ctz64(m);
+    const int base = D.fk_key_off[t * d.NK + k];
+    const KeyMeta km = L.keys[k];
+    uint32_t acc = F[base + wc];  // positions whose IT lacks the key
+    const int op = rs_op(L, X, k);
+    if (op == OP_NOTIN || op == OP_DNE) acc |= F[base + TW + wc];
+    if (!bit(rs_compl(X), k)) {  // X In: the positions holding one of its values
+      for (int i = 0; i < km.nw; i++) {
+        uint32_t x = X[L.HDR + km.off + i];
+        while (x) {
+          const int v = i * 32 + __builtin_ctz(x);
+          x &= x - 1;
+          acc |= F[base + (3 + v) * TW + wc];
+        }
+      }
+    } else if (!bit(d.fkMulti, k)) {  // complement, one value per IT: In positions minus the values X excludes
+      uint32_t sub = 0;
+      for (int v0 = 0; v0 < km.nv; v0 += kWave) {
+        uint64_t out = wballot(v0 + lane() < km.nv && !rs_member(L, X, k, v0 + lane()));
+        for (; out; out &= out - 1) sub |= F[base + (3 + v0 + ctz64(out)) * TW + wc];
+      }
+      acc |= F[base + 2 * TW + wc] & ~sub;
+    } else {  // complement over multi-valued ITs: the values X admits
+      for (int v0 = 0; v0 < km.nv; v0 += kWave) {
+        uint64_t in = wballot(v0 + lane() < km.nv && rs_member(L, X, k, v0 + lane()));
+        for (; in; in &= in - 1) acc |= F[base + (3 + v0 + ctz64(in)) * TW + wc];
+      }
+    }
+    ic &= acc;
+  }
+  return ic;
+}
+
+#if KS_TU == 0
+// k_feasibility (north_star "feasibility matrix"): the static part of the pod x
+// instance-type feasibility, one wavefront per (relaxation state, template) row, lanes over the words of
+// the template's position bitset.  Row = Intersects(IT, template) AND Intersects(IT, state) on the keys
+// no instance type constrains with more than one value (nodeclaim.go:225-260; requirements.go:241-258).
+// k_solve ANDs the row where it would otherwise re-evaluate those keys per step (feas_masks).
+// HBM-bound: reads the state's and template's records and the template's position tables, writes TW words.
+__global__ __launch_bounds__(64) void k_feasibility(KsDev D) {
+  const KsDims& d = D.d;
+  __shared__ __attribute__((aligned(16))) uint32_t s_kraw[64 * sizeof(KeyMeta) / 4];
+  for (int i = lane(); i < d.NK * (int)(sizeof(KeyMeta) / 4); i += kWave) s_kraw[i] = ((const uint32_t KS_G*)D.keys)[i];
+  __syncthreads();
+  DevLayout L;
+  L.nkeys = d.NK;
+  L.W = d.W;
+  L.NB = d.NB;
+  L.HDR = d.HDR;
+  L.RSW = d.RSW;
+  L.keys = (const KeyMeta KS_L*)s_kraw;
+  L.wordValid = D.wordValid;
+  L.vIsInt = D.vIsInt;
+  L.vInt = D.vInt;
+  const int row = blockIdx.x, s = row / d.NTPL, t = row - s * d.NTPL;
+  const uint32_t KS_G* X = D.st_rs + (int64_t)s * d.RSW;
+  const uint32_t KS_G* T = D.tpl_rs + (int64_t)t * d.RSW;
+  const uint64_t km = d.itKeys & ~d.fkMulti;
+  const uint64_t kx = rs_present(X) & km, kt = rs_present(T) & km;
+  for (int w0 = 0; w0 < d.TW; w0 += kWave) {
+    const int w = w0 + lane();
+    const int wc = w < d.TW ? w : d.TW - 1;
+    const uint32_t v = fk_intersects_word(D, L, X, t, wc, kx) & fk_intersects_word(D, L, T, t, wc, kt);
+    if (w < d.TW) D.st_fm[(int64_t)row * d.TW + w] = v;
+  }
+}
+#endif
+
 template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN>
 struct Solver {
   static constexpr int RM = RT > 0 ? RT : kMaxR;
@@ -261,6 +346,8 @@ struct Solver {
   LI32 s_tmin;          // [G] domainMinCount of the popped pod, per spread group
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
   LU32 s_trs1;          // [RSW] one group's domains as a single-key record
+  LI32 s_tcs;           // [tgSmall] counts of the small-key groups (the count table's LDS-resident prefix)
+  LU32 s_tcd;           // SIM: dirty bits over count words [tgSmall, tgCntWords): set once W.tg_cnt holds the word
   uint64_t t_mask = 0;  // groups matching the popped pod (owned in its state | inverse groups selecting it)
   uint64_t t_sel = 0;   // groups whose selector selects the popped pod
   uint64_t t_inv = 0;   // inverse groups the popped pod owns
@@ -349,47 +436,23 @@ struct Solver {
   // DoesNotExist (both negative, requirements.go:248-252); the keys intersect.  hasOffering is the union
   // over the (zone, capacity-type) pairs X admits (a missing key admits all).  Lane w owns word w:
   // s_fic, s_fof; s_firr marks positions whose IT holds a complement requirement (checked exactly).
-  __device__ __forceinline__ void feas_masks(LU32 X, int t) {
+  // fmrow: k_feasibility's row for (the popped pod's state, t) -- the keys no instance type constrains
+  // with more than one value, already intersected for the template and the state -- when X is the
+  // template's or a claim's requirements plus that state's (Compatible with it) and nothing else: per
+  // such key the test factorises (an IT's single value is admitted by X = A + B iff by A and by B; its
+  // DoesNotExist passes iff both are negative, which Compatible implies), and the claim's options already
+  // satisfy A's part.  Only the multi-valued keys are evaluated here then.
+  __device__ __forceinline__ void feas_masks(LU32 X, int t, const uint32_t KS_G* fmrow = nullptr) {
     const uint32_t KS_G* F = D.fk_words;
     const int TW = d.TW;
     const int ball = D.fk_tpl[3 * t], birr = D.fk_tpl[3 * t + 1], boff = D.fk_tpl[3 * t + 2];
-    const uint64_t keysX = rs_present(X) & d.itKeys;
+    const uint64_t keysX = rs_present(X) & d.itKeys & (fmrow ? d.fkMulti : ~0ull);
     const int nz = L.keys[d.zoneKey].nv, nc = L.keys[d.ctKey].nv;
     for (int w0 = 0; w0 < TW; w0 += kWave) {
       const int w = w0 + lane();
       const int wc = w < TW ? w : TW - 1;
-      uint32_t ic = F[ball + wc];
-      for (uint64_t m = keysX; m; m &= m - 1) {
-        const int k = ctz64(m);
-        const int base = D.fk_key_off[t * d.NK + k];
-        const KeyMeta km = L.keys[k];
-        uint32_t acc = F[base + wc];  // positions whose IT lacks the key
-        const int op = rs_op(L, X, k);
-        if (op == OP_NOTIN || op == OP_DNE) acc |= F[base + TW + wc];
-        if (!bit(rs_compl(X), k)) {  // X In: the positions holding one of its values
-          for (int i = 0; i < km.nw; i++) {
-            uint32_t x = X[L.HDR + km.off + i];
-            while (x) {
-              const int v = i * 32 + __builtin_ctz(x);
-              x &= x - 1;
-              acc |= F[base + (3 + v) * TW + wc];
-            }
-          }
-        } else if (!bit(d.fkMulti, k)) {  // complement, one value per IT: In positions minus the values X excludes
-          uint32_t sub = 0;
-          for (int v0 = 0; v0 < km.nv; v0 += kWave) {
-            uint64_t out = wballot(v0 + lane() < km.nv && !rs_member(L, X, k, v0 + lane()));
-            for (; out; out &= out - 1) sub |= F[base + (3 + v0 + ctz64(out)) * TW + wc];
-          }
-          acc |= F[base + 2 * TW + wc] & ~sub;
-        } else {  // complement over multi-valued ITs: the values X admits
-          for (int v0 = 0; v0 < km.nv; v0 += kWave) {
-            uint64_t in = wballot(v0 + lane() < km.nv && rs_member(L, X, k, v0 + lane()));
-            for (; in; in &= in - 1) acc |= F[base + (3 + v0 + ctz64(in)) * TW + wc];
-          }
-        }
-        ic &= acc;
-      }
+      uint32_t ic = F[ball + wc] & fk_intersects_word(D, L, X, t, wc, keysX);
+      if (fmrow) ic &= fmrow[wc];
       uint32_t of = 0;
       for (int c0 = 0; c0 < nc; c0 += kWave) {
         const uint64_t cm0 = wballot(c0 + lane() < nc && rs_member(L, X, d.ctKey, c0 + lane()));
@@ -409,6 +472,12 @@ struct Solver {
       }
     }
     wsync();
+  }
+  // k_feasibility's row for (state s, template t), or null where it does not apply: not computed, or
+  // topology requirements were added to the record (they are not part of the row).
+  __device__ __forceinline__ const uint32_t KS_G* fm_row(int s, int t) const {
+    if (KS_FM_OFF || !d.fmOn || (TOPO && t_mask)) return nullptr;
+    return D.st_fm + ((int64_t)s * d.NTPL + t) * d.TW;
   }
   __device__ __forceinline__ bool fbit(LU32 m, int pos) const { return (m[pos >> 5] >> (pos & 31)) & 1u; }
 
@@ -583,7 +652,34 @@ struct Solver {
   // Counts and registered bits are written by one lane and read by others: loads bypass the L1.
   __device__ __forceinline__ int tg(int g, int f) const { return s_tgm[g * TGM_WORDS + f]; }
   // count of domain v, -1 while the domain is not registered (absent from TopologyGroup.domains)
-  __device__ __forceinline__ int tcnt(int g, int v) const { return ld_sc1(W.tg_cnt + tg(g, TGM_CNT) + v); }
+  // Small-key groups read LDS.  The hostname groups (one word per node) live in HBM: a Solve's workspace
+  // holds a full copy (k_init); a simulation reads the shared NewTopology counts until it first writes a
+  // word (copy-on-write, s_tcd), so no simulation copies the table.
+  __device__ __forceinline__ int tcnt_at(int off) const {
+    if (off < d.tgSmall) return s_tcs[off];
+    if constexpr (SIM) {
+      const int b = off - d.tgSmall;
+      const int own = ld_sc1(W.tg_cnt + off), shared = D.tg_cnt0[off];
+      return ((s_tcd[b >> 5] >> (b & 31)) & 1u) ? own : shared;
+    }
+    return ld_sc1(W.tg_cnt + off);
+  }
+  __device__ __forceinline__ int tcnt(int g, int v) const { return tcnt_at(tg(g, TGM_CNT) + v); }
+  // Topology.Record's count increment of word `off` (recording registers the domain), by one lane;
+  // concurrent callers touch distinct words.
+  __device__ __forceinline__ void tcnt_inc(int off) const {
+    const int c = tcnt_at(off);
+    const int n = c < 0 ? 1 : c + 1;
+    if (off < d.tgSmall) {
+      s_tcs[off] = n;
+      return;
+    }
+    W.tg_cnt[off] = n;
+    if constexpr (SIM) {
+      const int b = off - d.tgSmall;
+      __hip_atomic_fetch_or(s_tcd + (b >> 5), 1u << (b & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  }
   __device__ __forceinline__ int tccnt(int g, int claim) const { return ld_sc1(W.tg_ccnt + (int64_t)g * W.ccs + claim); }  // claim <= Kcap (a fresh claim at the cap)
   __device__ __forceinline__ bool tpod_has(int g, int v) const {  // podDomains.Has (strict pod requirements)
     return rs_member(L, D.st_rss + (int64_t)t_s * d.RSW, tg(g, TGM_KEY), v);
@@ -848,10 +944,7 @@ struct Solver {
       if (node >= 0) {
         if (lane() == 0) {
           const int v = D.n_tdom[(int64_t)g * d.N + node];
-          if (v >= 0) {
-            const int c = W.tg_cnt[tg(g, TGM_CNT) + v];  // recording registers the domain
-            W.tg_cnt[tg(g, TGM_CNT) + v] = c < 0 ? 1 : c + 1;
-          }
+          if (v >= 0) tcnt_inc(tg(g, TGM_CNT) + v);  // recording registers the domain
         }
         continue;
       }
@@ -877,8 +970,7 @@ struct Solver {
               if (cc <= 0) W.tg_cpos[g] += 1;  // one more placeholder holding a counted pod
             }
           } else {
-            const int c = W.tg_cnt[tg(g, TGM_CNT) + v];
-            W.tg_cnt[tg(g, TGM_CNT) + v] = c < 0 ? 1 : c + 1;
+            tcnt_inc(tg(g, TGM_CNT) + v);
           }
         }
       }
@@ -985,7 +1077,7 @@ struct Solver {
       // Requirements changed: the options left are those the new requirements still admit, from
       // the feasibility masks (one word per lane), exact per position only for irregular ones.
       PH_BEGIN(u2);
-      feas_masks(s_rs, t);
+      feas_masks(s_rs, t, fm_row(s, t));
       PHS_END(u2, 2);
       PH_BEGIN(u3);
       for (int w0 = 0; w0 < d.TW; w0 += kWave) {
@@ -1017,7 +1109,7 @@ struct Solver {
       return ncnt > 0;
     }
     int cnt = 0, scanned = 0;
-    if (changed) feas_masks(s_rs, t);
+    if (changed) feas_masks(s_rs, t, fm_row(s, t));
     for (int base = 0; base < nIT; base += kWave) {
       const int wi = base >> 5;
       const uint64_t bits = (uint64_t)s_rem[wi] | (wi + 1 < d.TW ? (uint64_t)s_rem[wi + 1] << 32 : 0ull);
@@ -1188,7 +1280,7 @@ struct Solver {
             for (int r = 0; r < R(); r++) req[r] = D.tpl_daemon[(int64_t)t * R() + r] + pod[r];
             uint32_t flags = 0;
             uint64_t any = 0;
-            feas_masks(s_rs, t);
+            feas_masks(s_rs, t, fm_row(s, t));
             for (int base = 0; base < nIT; base += kWave) {
               const int pos = base + lane();
               const bool in = pos < nIT && ((s_cand[pos >> 5] >> (pos & 31)) & 1u);
@@ -1569,10 +1661,15 @@ struct Solver {
 template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_solve(KsDev D, const KsWork* works, Plan pl) {
   constexpr int RM = Solver<RT, TL, SIM, TOPO, LEAN>::RM;
-  // Simulations force their loop's branch conditions scalar (ub); measured on the Solve instantiations
-  // the extra scalar registers cost more (spills) than the exec-mask bookkeeping they remove.
-  auto U = [](bool x) { return SIM ? ub(x) : x; };
-  auto UI = [](int x) { return SIM ? uni(x) : x; };
+  // The loop's branch conditions are forced scalar (ub / uni): its control flow is wave-uniform by
+  // construction, and left to prove that itself the compiler falls back to exec-masked code for the whole
+  // commit loop, which costs time and, in one build of the requirement-carrying instantiation, lost a
+  // claim-state write-back (two reference Binpacking scenarios; device requests 0 for one NodeClaim).
+  // The LEAN Solve instantiation (resource-only pods, C1/C2) keeps the compiler's choice: there the
+  // scalar form's extra SGPR spills cost 15 % of C2, and its parity is pinned by the full-size digests.
+  constexpr bool FORCEU = SIM || !LEAN;
+  auto U = [](bool x) { return FORCEU ? ub(x) : x; };
+  auto UI = [](int x) { return FORCEU ? uni(x) : x; };
   extern __shared__ __attribute__((aligned(16))) char smem_generic[];
   char KS_L* smem = (char KS_L*)smem_generic;
   const KsWork KS_C& W = ((const KsWork KS_C*)works)[blockIdx.x];
@@ -1614,6 +1711,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   S.s_tmin = (LI32)take(4 * (size_t)d.G);
   S.s_trs0 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
   S.s_trs1 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
+  S.s_tcs = (LI32)take(d.G ? 4 * (size_t)d.tgSmall : 0);
+  const int NWC = SIM && d.G ? (d.tgCntWords - d.tgSmall + 31) >> 5 : 0;
+  S.s_tcd = (LU32)take(4 * (size_t)NWC);
+  for (int i = lane(); i < (d.G ? d.tgSmall : 0); i += kWave) S.s_tcs[i] = D.tg_cnt0[i];
+  for (int i = lane(); i < NWC; i += kWave) S.s_tcd[i] = 0;
   for (int i = lane(); i < d.G * TGM_WORDS; i += kWave) S.s_tgm[i] = D.tg_meta[i];
   S.gc.tpl = W.c_tpl;
   S.gc.req = W.c_req;
@@ -1646,15 +1748,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       // NewTopology for this simulation: the shared counts minus the candidates' pods, which the
       // simulation schedules and NewTopology therefore excludes (topology.go:72-75,262-265); a
       // domain left with no pod and no other registration drops out of TopologyGroup.domains.
-      for (int i = lane(); i < d.tgCntWords; i += kWave) W.tg_cnt[i] = D.tg_cnt0[i];
+      // (copy-on-write: only the words these entries touch get a private copy)
       for (int i = lane(); i < d.G * W.ccs; i += kWave) W.tg_ccnt[i] = 0;
       for (int i = lane(); i < d.G; i += kWave) W.tg_cpos[i] = 0;
-      hbm_release();
       wsync();
       for (int i = lane(); i < W.ntdel; i += kWave) {  // offsets are distinct within one simulation
         const int off = W.tdel[2 * i], x = W.tdel[2 * i + 1];
         const int c = D.tg_cnt0[off] - (x >> 1);
-        W.tg_cnt[off] = (c == 0 && (x & 1)) ? -1 : c;
+        const int n = (c == 0 && (x & 1)) ? -1 : c;
+        if (off < d.tgSmall) {
+          S.s_tcs[off] = n;
+        } else {
+          W.tg_cnt[off] = n;
+          const int b = off - d.tgSmall;
+          __hip_atomic_fetch_or(S.s_tcd + (b >> 5), 1u << (b & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
       }
       hbm_release();
     }
@@ -1693,9 +1801,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // LEAN (no negative requests): the window keeps each node's free capacity Available - requests, so
   // Fits(requests + pod, Available) is one compare per resource; a node that can never fit (negative
   // Available, beyond N, removed by the simulation) holds INT64_MIN, which no request (>= 0) fits.
-  constexpr int NWQ = LEAN ? 1 : NWA;
+  constexpr bool FREEW = LEAN && SIM;  // (the Solve instantiations keep Available + requests: measured faster there)
+  constexpr int NWQ = FREEW ? 1 : NWA;
   uint64_t wtx[NWA], wty[NWA], whp[NWA];
-  int64_t wav[NWA][RM], wrq[NWQ][RM];  // LEAN: wav = free capacity, wrq unused
+  int64_t wav[NWA][RM], wrq[NWQ][RM];  // FREEW: wav = free capacity, wrq unused
   int wnf[NWA];
   if constexpr (NW > 0) {
     if (d.N > 0) {
@@ -1709,7 +1818,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
         for (int r = 0; r < RM; r++) {
           const int64_t a = D.n_avail[(int64_t)c * RM + r], q = D.n_req0[(int64_t)c * RM + r];
-          if constexpr (LEAN) {
+          if constexpr (FREEW) {
             never |= a < 0;
             wav[k][r] = a - q;
           } else {
@@ -1717,7 +1826,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             wrq[k][r] = q;
           }
         }
-        if constexpr (LEAN)
+        if constexpr (FREEW)
 #pragma unroll
           for (int r = 0; r < RM; r++) wav[k][r] = never ? INT64_MIN : wav[k][r];
         wnf[k] = SIM ? D.n_flags[c] : 0;
@@ -1762,7 +1871,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       wi = 0;
       windows++;
     }
-    if constexpr (LEAN && SIM && NW > 0) {
+    if constexpr (FREEW && NW > 0) {
       // Fast path of a simulation over resource-only pods (what consolidation re-schedules): while the
       // next pops each fit a node of the register window, the step is Queue.Pop + the window's
       // first-fit ballots + the commit to the owner lane's registers, with nothing else live.  A pod
@@ -1864,7 +1973,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int k = 0; k < NW; k++) {
           const int n = k * kWave + lane();
           bool ok = (((wtx[k] & ~tol0) | (wty[k] & ~tol1)) == 0);
-          if constexpr (LEAN) {
+          if constexpr (FREEW) {
 #pragma unroll
             for (int r = 0; r < RM; r++) ok &= pod[r] <= wav[k][r];
           } else {
@@ -1895,7 +2004,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
               if (lane() == owner) {
 #pragma unroll
                 for (int r = 0; r < RM; r++) {
-                  if constexpr (LEAN) wav[k][r] -= pod[r];
+                  if constexpr (FREEW) wav[k][r] -= pod[r];
                   else wrq[k][r] += pod[r];
                 }
                 whp[k] = (whp[k] & ~S.cur_hpo) | S.cur_hpu;
@@ -2145,7 +2254,9 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
                        2 * r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 +
                        (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
-                       (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) : 0);
+                       (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) +
+                                  r16(4 * (size_t)d.tgSmall) + (sim ? r16(4 * (size_t)((d.tgCntWords - d.tgSmall + 31) / 32)) : 0)
+                              : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)
   const size_t clmB = 16 + 16 * R + 4 * TW + 4 * R;      // tpl, cnt, req, max, rem, thr (+ rounding)
   const size_t slack = 10 * 16;                          // per-array 16-byte rounding
@@ -2190,6 +2301,7 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
     hipError_t e = queue_sort(D, skeys, svals, stemp, stempBytes, qorder, st);
     if (e != hipSuccess) return e;
   }
+  if (D.d.fmOn) hipLaunchKernelGGL(k_feasibility, dim3(D.d.S * D.d.NTPL), dim3(kWave), 0, st, D);
   hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep,
                      fixed_order ? fixed_order : (const int32_t*)qorder);
   if (mid) (void)hipEventRecord(mid, st);
@@ -2201,6 +2313,7 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st) {
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
   if (nsims <= 0) return hipSuccess;
+  if (D.d.fmOn) hipLaunchKernelGGL(k_feasibility, dim3(D.d.S * D.d.NTPL), dim3(kWave), 0, st, D);
   return (D.d.G ? launch_sims_topo : launch_sims_plain)(D, works_dev, nsims, pl, st);
 }
 #endif

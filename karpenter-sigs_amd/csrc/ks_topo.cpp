@@ -89,6 +89,7 @@ void Host::buildTopology() {
   if (!any) {
     dims.G = dims.G1 = 0;
     dims.tgCntWords = 1;
+    dims.tgSmall = 0;
     dims.FSW = dims.RSW;
     tab.tg_meta.assign(TGM_WORDS, 0);
     tab.tg_cnt0.assign(1, 0);
@@ -326,6 +327,25 @@ void Host::buildTopology() {
   tab.tg_cnt0.clear();
   tab.tg_frs.clear();
   int maxNv = 0;
+  // Count-table layout: the groups over small keys (zone, capacity type, ...) first, up to kTgSmallCap
+  // words -- k_solve keeps that prefix in LDS -- then the hostname groups (one word per node), which stay
+  // in HBM (copy-on-write per simulation).
+  constexpr size_t kTgSmallCap = 2048;
+  std::vector<int> order;
+  std::vector<char> isSmall((size_t)G, 0);
+  size_t smallWords = 0;
+  for (int g = 0; g < G; g++) {
+    const size_t nv = std::max<size_t>(values[(size_t)groups[(size_t)g].keyId].size(), 1);
+    if (groups[(size_t)g].key != kHostnameKey && smallWords + nv <= kTgSmallCap) {
+      isSmall[(size_t)g] = 1;
+      smallWords += nv;
+      order.push_back(g);
+    }
+  }
+  for (int g = 0; g < G; g++)
+    if (!isSmall[(size_t)g]) order.push_back(g);
+  dims.tgSmall = 0;
+  std::vector<std::vector<int32_t>> cnts((size_t)G);
   for (int g = 0; g < G; g++) {
     TopoGroup& tg = groups[(size_t)g];
     int32_t* m = &tab.tg_meta[(size_t)g * TGM_WORDS];
@@ -335,7 +355,6 @@ void Host::buildTopology() {
     m[TGM_KEY] = tg.keyId;
     m[TGM_SKEW] = tg.maxSkew;
     m[TGM_MIND] = tg.minDomains;
-    m[TGM_CNT] = (int32_t)tab.tg_cnt0.size();
     m[TGM_NV] = nv;
     m[TGM_FBEG] = (int32_t)(tab.tg_frs.size() / dims.RSW);
     m[TGM_HOST] = tg.key == kHostnameKey ? 1 : 0;
@@ -346,7 +365,7 @@ void Host::buildTopology() {
         throw KsError(-5, "topology domain " + kv.first + " outside the value universe of " + tg.key);
       cnt[(size_t)vi->second] = kv.second;
     }
-    tab.tg_cnt0.insert(tab.tg_cnt0.end(), cnt.begin(), cnt.end());
+    cnts[(size_t)g] = std::move(cnt);
     bool trivial = false;  // an empty term is Compatible with everything: the filter always matches
     for (auto& f : tg.filter) trivial = trivial || rs_present(f.data()) == 0;
     if (!trivial)
@@ -354,6 +373,12 @@ void Host::buildTopology() {
     m[TGM_FEND] = (int32_t)(tab.tg_frs.size() / dims.RSW);
   }
   if (tab.tg_frs.empty()) tab.tg_frs.assign(dims.RSW, 0);
+  for (size_t i = 0; i < order.size(); i++) {
+    const int g = order[i];
+    tab.tg_meta[(size_t)g * TGM_WORDS + TGM_CNT] = (int32_t)tab.tg_cnt0.size();
+    tab.tg_cnt0.insert(tab.tg_cnt0.end(), cnts[(size_t)g].begin(), cnts[(size_t)g].end());
+    if (isSmall[(size_t)g]) dims.tgSmall = (int32_t)tab.tg_cnt0.size();
+  }
   tab.n_tdom.assign((size_t)std::max(N, 1) * G, -1);  // [G][N]: a wave reads 64 nodes of one group
   for (int n = 0; n < N; n++)
     for (int g = 0; g < G; g++) {
