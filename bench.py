@@ -239,11 +239,13 @@ def solve_line(args, local, name, snap, metric, reps, cpu_sample=None, extra=Non
     for _ in range(max(args.warmup - 1, 0)):
         sch.solve(device=local, timing_only=True)
     t0 = time.perf_counter()
-    ks, algb = [], []
+    ks, algb, fms, fbytes = [], [], [], 0.0
     for _ in range(reps):
         x = sch.solve(device=local, timing_only=True)
         ks.append(x.solve_kernel_ms)
         algb.append(x.algorithmic_bytes)
+        fms.append(x.feasibility_ms)
+        fbytes = x.feasibility_bytes
     el = (time.perf_counter() - t0) / reps
     k_ms = sum(ks) / len(ks)
     out = {"metric": metric, "value": round(npods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1000, 3),
@@ -253,6 +255,10 @@ def solve_line(args, local, name, snap, metric, reps, cpu_sample=None, extra=Non
            "pod_errors": len(r.pod_errors),
            "roofline": _roofline("k_solve", k_ms, sum(algb) / len(algb), _ref_bytes(name, snap_json), traffic_tag),
            "cpu_baseline": None}
+    if fbytes > 0:  # k_feasibility (pod-state x instance-type rows) launched inside each Solve: its own roofline
+        f_ms = sum(fms) / len(fms)
+        out["feasibility"] = _roofline("k_feasibility", f_ms, fbytes, None, (traffic_tag or name.lower()) + "_feasibility"
+                                       if traffic_tag else None)
     if extra:
         out.update(extra)
     if cpu_sample and not args.no_cpu_baseline:

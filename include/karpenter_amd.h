@@ -98,6 +98,10 @@ int ks_results_nodeclaim_requirements(const ks_results* r, int i, int* n, const 
 double ks_results_kernel_ms(const ks_results* r);
 /* The k_solve launch alone (the dominant kernel; excludes workspace init and the queue sort). */
 double ks_results_solve_kernel_ms(const ks_results* r);
+/* k_feasibility (the static pod-state x instance-type rows) inside this Solve: HIP-event time and its
+ * algorithmic bytes; 0 when the problem has no pod label requirements (the kernel is not launched). */
+double ks_results_feasibility_ms(const ks_results* r);
+double ks_results_feasibility_bytes(const ks_results* r);
 /* Algorithmic bytes the solve scanned (SURVEY.md §8d formula, counted by the kernel). */
 double ks_results_algorithmic_bytes(const ks_results* r);
 

@@ -154,7 +154,7 @@ struct ks_results {
   std::vector<Claim> claims;
   std::vector<ENode> nodes;
   std::vector<std::pair<int32_t, std::string>> errors;
-  double kernel_ms = 0, solve_ms = 0, algbytes = 0;
+  double kernel_ms = 0, solve_ms = 0, algbytes = 0, feas_ms = 0, feas_bytes = 0;
   std::vector<int64_t> counters;
 };
 
@@ -235,9 +235,36 @@ void ks_upload(ks_problem* pb) {
   // k_feasibility's output: one row of TW words per (relaxation state, template), rewritten by every
   // Solve / pass; skipped (the kernel evaluates every key itself) if it would exceed 1 GiB
   const size_t fmBytes = 4 * (size_t)h.dims.S * h.dims.NTPL * h.dims.TW;
-  // (LEAN problems carry no pod label requirements: no step would read a row)
-  h.dims.fmOn = fmBytes > 0 && fmBytes <= ((size_t)1 << 30) && h.dims.NK <= 64 && !h.dims.lean &&
-                !getenv("KS_NO_FEASIBILITY");
+  // (only steps of pods with label requirements read a row)
+  bool keys = false;
+  for (int32_t f : t.st_flags) keys = keys || (f & SF_HAS_KEYS);
+  h.dims.fmOn = fmBytes > 0 && fmBytes <= ((size_t)1 << 30) && h.dims.NK <= 64 && keys && !getenv("KS_NO_FEASIBILITY");
+  // algorithmic bytes of one k_feasibility launch: per (state, template) row the TW words written, the
+  // two records' headers and the key words read, and one position-table word per lane for every table
+  // row the per-key test ORs (the lacks / DoesNotExist rows, plus one per admitted In value)
+  pb->fmBytes = 0;
+  if (h.dims.fmOn) {
+    const uint64_t km = h.dims.itKeys & ~h.dims.fkMulti;
+    auto tableWords = [&](const uint32_t* rec) {
+      double w = 0;
+      for (uint64_t m = rs_present(rec) & km; m; m &= m - 1) {
+        const int k = __builtin_ctzll(m);
+        const KeyMeta& kmeta = h.keys[(size_t)k];
+        w += 2;
+        if (!bit(rs_compl(rec), k))
+          for (int i = 0; i < kmeta.nw; i++) w += __builtin_popcount(rec[h.dims.HDR + kmeta.off + i]);
+        else
+          w += kmeta.nv;
+      }
+      return w;
+    };
+    double tplW = 0;
+    for (int tt = 0; tt < h.dims.NTPL; tt++) tplW += tableWords(&t.tpl_rs[(size_t)tt * h.dims.RSW]);
+    for (int s = 0; s < h.dims.S; s++) {
+      const double sw = tableWords(&t.st_rs[(size_t)s * h.dims.RSW]);
+      pb->fmBytes += 4.0 * h.dims.TW * (h.dims.NTPL * (1 + sw) + tplW) + 4.0 * 2 * h.dims.HDR * h.dims.NTPL;
+    }
+  }
   if (h.dims.fmOn) HIPCHK(hipMalloc(&pb->fmbuf, fmBytes));
   D.st_fm = (uint32_t*)pb->fmbuf;
   D.d = h.dims;
@@ -689,19 +716,28 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
     pb->wreps = reps;
   }
   KsWork w0 = work_ptrs((char*)pb->wbuf, wl);
-  hipEvent_t e0, em, e1;
+  hipEvent_t e0, em, e1, ef[2];
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&em));
   HIPCHK(hipEventCreate(&e1));
-  float ms = 0, setup = 0;
+  HIPCHK(hipEventCreate(&ef[0]));
+  HIPCHK(hipEventCreate(&ef[1]));
+  // A Solve that outgrows the default plan's NodeClaim capacity runs again with the wide plan; the
+  // caller pays both launches, so the reported times are their sums (the re-plan is remembered).
+  float ms = 0, setup = 0, fms = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     HIPCHK(hipEventRecord(e0, pb->stream));
     HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp,
-                        pb->stempBytes, pb->stream, em, pb->hqorder));
+                        pb->stempBytes, pb->stream, em, pb->hqorder, ef));
     HIPCHK(hipEventRecord(e1, pb->stream));
     HIPCHK(hipEventSynchronize(e1));
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-    HIPCHK(hipEventElapsedTime(&setup, e0, em));
+    float a = 0, b = 0, f = 0;
+    HIPCHK(hipEventElapsedTime(&a, e0, e1));
+    HIPCHK(hipEventElapsedTime(&b, e0, em));
+    if (pb->dev.d.fmOn) HIPCHK(hipEventElapsedTime(&f, ef[0], ef[1]));
+    ms += a;
+    setup += b;
+    fms += f;
     int64_t err = 0;
     HIPCHK(hipMemcpy(&err, w0.counters + CT_ERROR, 8, hipMemcpyDeviceToHost));
     if (err != KE_CLAIM_CAP || pb->wideKO) break;
@@ -715,6 +751,8 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(em);
   (void)hipEventDestroy(e1);
+  (void)hipEventDestroy(ef[0]);
+  (void)hipEventDestroy(ef[1]);
   ks_results* r;
   if (opts && opts->timing_only) {
     r = new ks_results();
@@ -731,6 +769,8 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   }
   r->kernel_ms = ms;
   r->solve_ms = ms - setup;
+  r->feas_ms = fms;
+  r->feas_bytes = pb->dev.d.fmOn ? pb->fmBytes : 0;
   *out = r;
   return KS_OK;
   API_CATCH
@@ -812,6 +852,8 @@ int ks_results_pod_error(const ks_results* r, int i, int* pod, const char** msg)
 }
 double ks_results_kernel_ms(const ks_results* r) { return r->kernel_ms; }
 double ks_results_solve_kernel_ms(const ks_results* r) { return r->solve_ms; }
+double ks_results_feasibility_ms(const ks_results* r) { return r->feas_ms; }
+double ks_results_feasibility_bytes(const ks_results* r) { return r->feas_bytes; }
 double ks_results_algorithmic_bytes(const ks_results* r) { return r->algbytes; }
 
 }  // extern "C"

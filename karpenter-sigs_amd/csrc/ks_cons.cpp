@@ -209,6 +209,7 @@ struct ks_cons {
     void* lbuf = nullptr;    // workspaces + pod maps + views
     KsWork* lworks = nullptr;
     int32_t* lrec = nullptr;
+    int32_t* hrec = nullptr;  // pinned host staging of the records (one DMA per pass, no pageable bounce)
     int32_t* lentries = nullptr;
     int32_t* lentrySim = nullptr;
     int32_t* lpodmap = nullptr;
@@ -223,6 +224,7 @@ struct ks_cons {
       for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
                       (void*)lkeys, (void*)lvals, ltemp})
         if (p) (void)hipFree(p);
+      if (hrec) (void)hipHostFree(hrec);
       *this = Launch{};  // stale lookups (claim requirements, counters) now fail cleanly
     }
   };
@@ -613,6 +615,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   char* ibase = base + inBase;
   HIPCHK(hipMalloc(&c.L.lworks, sizeof(KsWork) * std::max(ns, 1)));
   HIPCHK(hipMalloc(&c.L.lrec, 4 * (size_t)c.recWords * std::max(ns, 1)));
+  HIPCHK(hipHostMalloc((void**)&c.L.hrec, 4 * (size_t)c.recWords * std::max(ns, 1), hipHostMallocDefault));
   HIPCHK(hipMalloc(&c.L.lentries, 4 * (size_t)std::max(c.L.lnent, 1)));
   HIPCHK(hipMalloc(&c.L.lentrySim, 4 * (size_t)std::max(c.L.lnent, 1)));
   HIPCHK(hipMalloc(&c.L.lpodmap, 4 * (size_t)std::max(c.L.lnent, 1)));
@@ -954,10 +957,13 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
     HIPCHK(hipMemsetAsync(records, 0, all, pb.stream));
     if (bytes) HIPCHK(hipMemcpyAsync(records, c.L.lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
   } else {
-    memset(records, 0, all);
-    if (bytes) HIPCHK(hipMemcpyAsync(records, c.L.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
+    if (bytes) HIPCHK(hipMemcpyAsync(c.L.hrec, c.L.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
   }
   HIPCHK(hipStreamSynchronize(pb.stream));
+  if (!onDevice) {
+    memcpy(records, c.L.hrec, bytes);
+    memset((char*)records + bytes, 0, all - bytes);
+  }
   return ms;
 }
 

@@ -12,7 +12,7 @@
 namespace ks {
 hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
-                        hipEvent_t mid, const int32_t* fixed_order = nullptr);
+                        hipEvent_t mid, const int32_t* fixed_order = nullptr, hipEvent_t* feas = nullptr);
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st);
 Plan make_plan(const KsDims& d, size_t budget, bool sim = false, bool wideKO = false);
 size_t queue_sort_temp_bytes(int n);
@@ -48,6 +48,7 @@ struct ks_problem {
   ks::KsDev dev{};
   void* dbuf = nullptr;
   void* fmbuf = nullptr;  // k_feasibility rows (KsDev::st_fm)
+  double fmBytes = 0;     // k_feasibility's algorithmic bytes per launch
   void* wbuf = nullptr;
   size_t wbytes = 0;
   ks::KsWork* works_dev = nullptr;

@@ -834,10 +834,26 @@ struct Solver {
       const int nslot = nv + (host && claim >= 0 ? 1 : 0);  // + the claim's own hostname-placeholder (private bit)
       for (int i = lane(); i < d.RSW; i += kWave) s_trs1[i] = 0;
       wsync();
+      // The values a domain scan visits.  When the record holds the key as an In set (a NodeClaim's
+      // hostname: its own placeholder), Requirements.Add below keeps only values of that set (rs only
+      // shrinks from the snapshot s_trs0), so the scan over the set's bits leaves rs exactly as the scan
+      // over the whole universe would -- 5000 hostnames become one word per lane.
+      const bool inSet = bit(rs_present(s_trs0), k) && !bit(rs_compl(s_trs0), k);
+      auto scan = [&](bool restrict, auto&& body) {
+        if (restrict && inSet) {
+          for (int wd = lane(); wd < km.nw; wd += kWave)
+            for (uint32_t x = s_trs0[L.HDR + km.off + wd]; x; x &= x - 1) {
+              const int v = wd * 32 + __builtin_ctz(x);
+              if (v < nslot) body(v);
+            }
+        } else {
+          for (int v = lane(); v < nslot; v += kWave) body(v);
+        }
+      };
       if (tg(g, TGM_TYPE) == TG_SPREAD) {  // nextDomainTopologySpread: smallest count, then smallest name
         const int self = (int)((t_sel >> g) & 1ull), mn = s_tmin[g], skew = tg(g, TGM_SKEW);
         uint64_t best = ~0ull;
-        for (int v = lane(); v < nslot; v += kWave) {
+        scan(true, [&](int v) {
           const bool nodeHas = rs_member(L, s_trs0, k, v);
           int c = -1;
           if (nodeHas) c = v < nv ? tcnt(g, v) : tccnt(g, claim);  // placeholders are always registered
@@ -847,7 +863,7 @@ struct Solver {
             const uint64_t key = ((uint64_t)(uint32_t)c << 32) | (uint32_t)v;
             best = key < best ? key : best;
           }
-        }
+        });
         for (int off = 32; off >= 1; off >>= 1) {
           const uint64_t o = __shfl_xor(best, off);
           best = o < best ? o : best;
@@ -858,12 +874,12 @@ struct Solver {
       } else if (tg(g, TGM_TYPE) == TG_AFFINITY) {  // nextDomainAffinity
         const bool self = (t_sel >> g) & 1ull;
         if (s_tmin[g]) {  // the domains already holding a selected pod (other placeholders drop out in Add)
-          for (int v = lane(); v < nslot; v += kWave) {
+          scan(true, [&](int v) {
             const int c = v < nv ? tcnt(g, v) : tccnt(g, claim);
             if (c > 0 && tpod_has(g, v))
               __hip_atomic_fetch_or(s_trs1 + L.HDR + km.off + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_WAVEFRONT);
-          }
+          });
         } else if (self) {  // bootstrap: first registered pod∩node domain, then first registered pod domain
           // (canonical map order = sorted names = value order; for hostname keys the claim's own
           // placeholder is its only node domain, and any other insert drops out in Add)
@@ -889,8 +905,10 @@ struct Solver {
           return FC_TOPO | ((uint32_t)g << 16);
         }
       } else {  // nextDomainAntiAffinity: registered zero-count domains the pod's domains allow
+        // (a Solve renders which check failed -- no zero-count domain at all vs none the record allows --
+        // so only simulations, which report success alone, restrict this scan)
         bool any = false;
-        for (int v = lane(); v < nslot; v += kWave) {
+        scan(SIM, [&](int v) {
           bool in;
           if (v < nv) {
             in = tcnt(g, v) == 0 && tpod_has(g, v);
@@ -904,7 +922,7 @@ struct Solver {
                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
             any = true;
           }
-        }
+        });
         if (wballot(any) == 0) return FC_TOPO | ((uint32_t)g << 16);
       }
       wsync();
@@ -2295,13 +2313,17 @@ hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp,
 // fixed_order: NewQueue's order computed on the host (pods tying on the whole sort key), no radix sort.
 hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
-                        hipEvent_t mid, const int32_t* fixed_order) {
+                        hipEvent_t mid, const int32_t* fixed_order, hipEvent_t* feas) {
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
   if (!fixed_order) {
     hipError_t e = queue_sort(D, skeys, svals, stemp, stempBytes, qorder, st);
     if (e != hipSuccess) return e;
   }
-  if (D.d.fmOn) hipLaunchKernelGGL(k_feasibility, dim3(D.d.S * D.d.NTPL), dim3(kWave), 0, st, D);
+  if (D.d.fmOn) {
+    if (feas) (void)hipEventRecord(feas[0], st);
+    hipLaunchKernelGGL(k_feasibility, dim3(D.d.S * D.d.NTPL), dim3(kWave), 0, st, D);
+    if (feas) (void)hipEventRecord(feas[1], st);
+  }
   hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep,
                      fixed_order ? fixed_order : (const int32_t*)qorder);
   if (mid) (void)hipEventRecord(mid, st);

@@ -65,6 +65,10 @@ def lib():
     l.ks_results_solve_kernel_ms.restype = ctypes.c_double
     l.ks_results_algorithmic_bytes.argtypes = [vp]
     l.ks_results_algorithmic_bytes.restype = ctypes.c_double
+    l.ks_results_feasibility_ms.argtypes = [vp]
+    l.ks_results_feasibility_ms.restype = ctypes.c_double
+    l.ks_results_feasibility_bytes.argtypes = [vp]
+    l.ks_results_feasibility_bytes.restype = ctypes.c_double
     l.ks_cluster_state.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
     l.ks_free.argtypes = [vp]
     l.ks_last_error.restype = ctypes.c_char_p
@@ -86,6 +90,14 @@ def _take_str(ptr):
 
 def _encode(snapshot):
     return (snapshot if isinstance(snapshot, str) else json.dumps(snapshot)).encode()
+
+
+def _records_buffer(records):
+    """A ctypes buffer over gathered records: a run's own buffer (the memoryview run() returns) as is,
+    anything else bytes-like copied once."""
+    if isinstance(records, memoryview) and isinstance(records.obj, ctypes.Array):
+        return records.obj
+    return ctypes.create_string_buffer(bytes(records), len(records))
 
 
 def inspect(snapshot):
@@ -118,6 +130,8 @@ class Results:
         self.kernel_ms = kernel_ms
         self.solve_kernel_ms = solve_kernel_ms
         self.algorithmic_bytes = alg_bytes
+        self.feasibility_ms = 0.0     # k_feasibility inside this Solve (0: not launched)
+        self.feasibility_bytes = 0.0  # its algorithmic bytes
 
     def canonical(self):
         d = dict(self.doc)
@@ -142,14 +156,18 @@ class Scheduler:
         _check(lib().ks_solve(self._h, ctypes.byref(o), ctypes.byref(r)))
         try:
             if timing_only:
-                return Results({"newNodeClaims": [], "existingNodes": [], "podErrors": {}},
-                               lib().ks_results_kernel_ms(r), lib().ks_results_algorithmic_bytes(r),
-                               lib().ks_results_solve_kernel_ms(r))
-            js = ctypes.c_void_p()
-            _check(lib().ks_results_json(r, ctypes.byref(js)))
-            doc = json.loads(_take_str(js))
-            return Results(doc, lib().ks_results_kernel_ms(r), lib().ks_results_algorithmic_bytes(r),
-                           lib().ks_results_solve_kernel_ms(r))
+                out = Results({"newNodeClaims": [], "existingNodes": [], "podErrors": {}},
+                              lib().ks_results_kernel_ms(r), lib().ks_results_algorithmic_bytes(r),
+                              lib().ks_results_solve_kernel_ms(r))
+            else:
+                js = ctypes.c_void_p()
+                _check(lib().ks_results_json(r, ctypes.byref(js)))
+                doc = json.loads(_take_str(js))
+                out = Results(doc, lib().ks_results_kernel_ms(r), lib().ks_results_algorithmic_bytes(r),
+                              lib().ks_results_solve_kernel_ms(r))
+            out.feasibility_ms = lib().ks_results_feasibility_ms(r)
+            out.feasibility_bytes = lib().ks_results_feasibility_bytes(r)
+            return out
         finally:
             lib().ks_results_free(r)
 
@@ -233,17 +251,21 @@ class Consolidator:
         o = _Opts(device, 1, 1, 0, 0)
         ms = ctypes.c_double()
         if out_ptr is None:
-            buf = ctypes.create_string_buffer(self.records_per_rank(world) * self.record_bytes)
-            _check(l.ks_cons_run(self._h, rank, world, ctypes.byref(o), ctypes.cast(buf, ctypes.c_void_p), 0,
+            # one host buffer per handle, reused by every pass and handed on without copies (a memoryview,
+            # valid until the handle's next run; bytes(view) keeps a copy)
+            n = self.records_per_rank(world) * self.record_bytes
+            if getattr(self, "_recbuf", None) is None or len(self._recbuf) != n:
+                self._recbuf = ctypes.create_string_buffer(n)
+            _check(l.ks_cons_run(self._h, rank, world, ctypes.byref(o), ctypes.cast(self._recbuf, ctypes.c_void_p), 0,
                                  ctypes.byref(ms)))
-            return buf.raw, ms.value
+            return memoryview(self._recbuf), ms.value
         _check(l.ks_cons_run(self._h, rank, world, ctypes.byref(o), ctypes.c_void_p(out_ptr), 1, ctypes.byref(ms)))
         return None, ms.value
 
     def needed_sims(self, records, world=1, all_sims=False):  # noqa: D401
         """Simulations whose NewNodeClaims[0] requirements the decision output needs (in order)."""
         l = _cons_lib()
-        buf = ctypes.create_string_buffer(bytes(records), len(records))
+        buf = _records_buffer(records)
         cap = 64
         while True:
             out = (ctypes.c_int32 * cap)()
@@ -271,7 +293,7 @@ class Consolidator:
         fetch = fetch or self.claim_requirements
         table = b"".join(fetch(s) for s in need)
         tbuf = ctypes.create_string_buffer(table, max(len(table), 4))
-        buf = ctypes.create_string_buffer(bytes(records), len(records))
+        buf = _records_buffer(records)
         js = ctypes.c_void_p()
         flags = (1 if all_sims else 0) | (2 if candidates else 0)
         if clock is None:
@@ -300,7 +322,7 @@ class Consolidator:
         return list(out)
 
     def alg_bytes(self, records, world=1):
-        buf = ctypes.create_string_buffer(bytes(records), len(records))
+        buf = _records_buffer(records)
         return _cons_lib().ks_cons_records_alg_bytes(self._h, ctypes.cast(buf, ctypes.c_void_p), world)
 
     def consolidate(self, all_sims=False, device=-1, clock=None):

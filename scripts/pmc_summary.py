@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Summarise a scripts/profile.sh run: per-launch kernel stats + PMC counters for one kernel.
 
-Usage: scripts/pmc_summary.py <tag> [kernel_substring] [traffic_name]   (reads gpurun_out/prof_<tag>_*)
-Writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.txt and profiles/traffic_<traffic_name>.json.
+Usage: scripts/pmc_summary.py <tag> [kernel_substring] [traffic_name] [min_grid] [max_grid]   (reads gpurun_out/prof_<tag>_*)
+Writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_<traffic_name>_pmc.txt and profiles/traffic_<traffic_name>.json.
+min_grid: only launches with at least that many work-items (a consolidation pass, not its one-simulation
+validation launches of the same kernel).
 HBM bytes follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB; on gfx950
 FETCH_SIZE reports half the bytes of a coalesced read, so it is doubled.
 """
@@ -20,11 +22,14 @@ def main():
     tag = sys.argv[1]
     kname = sys.argv[2] if len(sys.argv) > 2 else "k_solve"
     tname = sys.argv[3] if len(sys.argv) > 3 else "c2"
+    min_grid = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    max_grid = int(sys.argv[5]) if len(sys.argv) > 5 else 1 << 62
     out = os.path.join(ROOT, "gpurun_out")
     prof = os.path.join(ROOT, "profiles")
     shutil.copy(os.path.join(out, "prof_%s_trace" % tag, "run_kernel_stats.csv"),
                 os.path.join(prof, "%s_kernel_stats.csv" % tag))
-    lines = ["PMC per launch of %s (averaged over the profiled launches)" % kname]
+    lines = ["PMC per launch of %s (averaged over the profiled launches%s)" % (
+        kname, ", grid >= %d" % min_grid if min_grid else "")]
     vals = {}
     agg = collections.defaultdict(list)
     for grp in ("fetch", "write", "sq", "cfetch", "cwrite"):
@@ -32,7 +37,7 @@ def main():
         if not os.path.exists(path):
             continue
         for r in csv.DictReader(open(path)):
-            if kname in r["Kernel_Name"]:
+            if kname in r["Kernel_Name"] and min_grid <= int(r["Grid_Size"]) <= max_grid:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, v in sorted(agg.items()):
         vals[k] = sum(v) / len(v)
@@ -48,7 +53,7 @@ def main():
         lines.append("SQ_WAIT_ANY / SQ_WAVE_CYCLES = %.3f ; SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES = %.3f" % (
             vals.get("SQ_WAIT_ANY", 0) / vals["SQ_WAVE_CYCLES"], vals.get("SQ_ACTIVE_INST_ANY", 0) / vals["SQ_WAVE_CYCLES"]))
     txt = "\n".join(lines) + "\n"
-    with open(os.path.join(prof, "%s_pmc.txt" % tag), "w") as f:
+    with open(os.path.join(prof, "%s_%s_pmc.txt" % (tag, tname)), "w") as f:
         f.write(txt)
     print(txt)
 
