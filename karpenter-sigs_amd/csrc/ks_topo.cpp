@@ -20,8 +20,10 @@
 // namespaceSelector terms resolve against the snapshot's namespace list ("namespaces").
 #include <algorithm>
 #include <climits>
+#include <unordered_map>
 
 #include "ks_host.h"
+#include "ks_parallel.h"
 
 namespace ks {
 
@@ -97,6 +99,7 @@ void Host::buildTopology() {
     tab.n_tdom.assign(1, -1);
     return;
   }
+  PhaseTimer pt("buildTopology");
   // --- domain universe (provisioner.go:229-283)
   std::map<std::string, std::set<std::string>> dom;
   auto valuesOf = [&](const std::vector<uint32_t>& rec, int k) {  // Requirement.Values(): the raw set
@@ -123,6 +126,7 @@ void Host::buildTopology() {
       if (bit(pr, k) && rs_op(L, base.data(), k) == OP_IN) for (auto& v : valuesOf(base, k)) dom[keyNames[(size_t)k]].insert(v);
   }
 
+  pt.mark("universe");
   // --- groups
   std::set<std::string> excluded;
   if (topoExcluded) excluded = *topoExcluded;
@@ -130,19 +134,39 @@ void Host::buildTopology() {
   topoContrib.clear();
   topoInvOwner.clear();
   // (group index, domain) per counted cluster pod, resolved to value ids once the groups are final
-  std::map<std::string, std::vector<std::pair<int, std::string>>> contrib;
+  std::unordered_map<std::string, std::vector<std::pair<int, std::string>>> contrib;  // uid -> contributions (per-uid order kept)
   std::vector<TopoGroup> own, inv;
-  std::map<std::string, int> ownByHash, invByHash;
-  auto nodeRec = [&](const std::map<std::string, std::string>& labels) {
-    std::vector<uint32_t> r = emptyRec();
-    addLabels(r, labels);
-    return r;
+  std::unordered_map<std::string, int> ownByHash, invByHash;  // lookups only (creation order is kept by the vectors)
+  // every node's label record, built once (before the first node filter needs one; read-only after,
+  // so countDomains' worker threads share it)
+  std::map<std::string, std::vector<uint32_t>> nodeRecs;
+  bool nodeRecsBuilt = false;
+  auto buildNodeRecs = [&]() {
+    if (nodeRecsBuilt) return;
+    for (auto& n : nodeLabelsByName) {
+      std::vector<uint32_t> r = emptyRec();
+      addLabels(r, n.second);
+      nodeRecs.emplace(n.first, std::move(r));
+    }
+    nodeRecsBuilt = true;
   };
-  auto filterMatches = [&](const TopoGroup& g, const std::vector<uint32_t>& rec, uint64_t allow) {
+  auto nodeRec = [&](const std::string& name, const std::map<std::string, std::string>&)
+      -> const std::vector<uint32_t>& { return nodeRecs.at(name); };
+  auto filterMatches = [&](const TopoGroup& g, const std::string& name, const std::map<std::string, std::string>& labels,
+                           uint64_t allow) {
     if (g.filterNil || g.filter.empty()) return true;
+    for (auto& f : g.filter)
+      if (rs_present(f.data()) == 0) return true;  // an empty term is Compatible with every record
+    const std::vector<uint32_t>& rec = nodeRec(name, labels);
     for (auto& f : g.filter)
       if (rs_compatible(L, rec.data(), f.data(), allow)) return true;
     return false;
+  };
+  // TopologyGroup.domains starts with the universe's values of the key (NewTopologyGroup); seeded only
+  // for groups that are new (a pod whose group exists already shares it)
+  auto seedDomains = [&](TopoGroup& g) {
+    auto d = dom.find(g.key);
+    if (d != dom.end()) for (auto& v : d->second) g.domains[v] = 0;
   };
   auto makeGroup = [&](int type, const std::string& key, const PodH& p, const std::set<std::string>& ns,
                        const LabelSel& sel, int32_t maxSkew, int32_t minDomains) {
@@ -154,8 +178,6 @@ void Host::buildTopology() {
     g.sel = sel;
     g.maxSkew = maxSkew;
     g.minDomains = minDomains;
-    auto d = dom.find(key);
-    if (d != dom.end()) for (auto& v : d->second) g.domains[v] = 0;
     g.filterNil = type != TG_SPREAD;
     if (type == TG_SPREAD) {  // MakeTopologyNodeFilter (topologynodefilter.go:33-51)
       std::vector<uint32_t> sel0 = emptyRec();
@@ -174,8 +196,8 @@ void Host::buildTopology() {
     for (auto& n : ns) g.hash += n + ",";
     g.hash += "#" + sel_key(sel) + "#" + std::to_string(maxSkew) + "#";
     if (g.filterNil) g.hash += "nil";
-    for (auto& f : g.filter) {
-      for (uint32_t w : f) g.hash += std::to_string(w) + ".";
+    for (auto& f : g.filter) {  // the filter records' words, as bytes (an exact key, not a printable one)
+      g.hash.append(reinterpret_cast<const char*>(f.data()), f.size() * sizeof(uint32_t));
       g.hash += "|";
     }
     return g;
@@ -196,31 +218,46 @@ void Host::buildTopology() {
     return out;
   };
   auto countDomains = [&](TopoGroup& g, int gidx) {  // topology.go:238-291
-    for (auto& cp : clusterPods) {
-      if (!g.namespaces.count(cp.ns) || !sel_lists(g.sel, cp.labels)) continue;
-      if (cp.nodeName.empty() || cp.phase == "Failed" || cp.phase == "Succeeded" || cp.deleting) continue;
-      if (excluded.count(cp.uid)) continue;
+    if (!g.filterNil && !g.filter.empty()) buildNodeRecs();
+    // each cluster pod's domain (or none), on worker threads; counted in pod order
+    const int NC = (int)clusterPods.size();
+    std::vector<const std::string*> dsel((size_t)NC, nullptr);
+    parallel_for(NC, 1024, [&](int i) {
+      const PodH& cp = clusterPods[(size_t)i];
+      if (!g.namespaces.count(cp.ns) || !sel_lists(g.sel, cp.labels)) return;
+      if (cp.nodeName.empty() || cp.phase == "Failed" || cp.phase == "Succeeded" || cp.deleting) return;
+      if (excluded.count(cp.uid)) return;
       auto n = nodeLabelsByName.find(cp.nodeName);
-      if (n == nodeLabelsByName.end()) continue;
+      if (n == nodeLabelsByName.end()) return;
       auto l = n->second.find(g.key);
-      std::string d;
-      if (l != n->second.end()) d = l->second;
-      else if (g.key == kHostnameKey) d = n->first;
-      else continue;
-      if (!filterMatches(g, nodeRec(n->second), 0)) continue;
-      g.domains[d]++;
-      if (topoExcluded) contrib[cp.uid].push_back({gidx, d});
+      const std::string* d;
+      if (l != n->second.end()) d = &l->second;
+      else if (g.key == kHostnameKey) d = &n->first;
+      else return;
+      if (!filterMatches(g, n->first, n->second, 0)) return;
+      dsel[(size_t)i] = d;
+    });
+    for (int i = 0; i < NC; i++) {
+      if (!dsel[(size_t)i]) continue;
+      g.domains[*dsel[(size_t)i]]++;
+      if (topoExcluded) contrib[clusterPods[(size_t)i].uid].push_back({gidx, *dsel[(size_t)i]});
     }
   };
-  auto inverseAnti = [&](const PodH& p, const std::map<std::string, std::string>* labels, bool cluster) {
+  auto antiGroups = [&](const PodH& p) {
+    std::vector<TopoGroup> gs;
+    for (auto& t : p.antiRequired) gs.push_back(makeGroup(TG_ANTI, t.key, p, termNs(p, t), t.sel, INT32_MAX, -1));
+    return gs;
+  };
+  auto inverseAnti = [&](const PodH& p, std::vector<TopoGroup> gs, const std::map<std::string, std::string>* labels,
+                         bool cluster) {
     uint64_t owned = 0;  // updateInverseAntiAffinity (topology.go:207-232)
-    for (auto& t : p.antiRequired) {
-      TopoGroup g = makeGroup(TG_ANTI, t.key, p, termNs(p, t), t.sel, INT32_MAX, -1);
+    for (TopoGroup& g : gs) {
       auto it = invByHash.find(g.hash);
       int idx;
       if (it == invByHash.end()) {
         idx = (int)inv.size();
         invByHash[g.hash] = idx;
+        seedDomains(g);
         inv.push_back(g);
       } else {
         idx = it->second;
@@ -257,20 +294,35 @@ void Host::buildTopology() {
     if (cp.antiRequired.empty() || cp.nodeName.empty() || excluded.count(cp.uid)) continue;
     auto n = nodeLabelsByName.find(cp.nodeName);
     if (n == nodeLabelsByName.end()) continue;
-    inverseAnti(cp, &n->second, true);
+    inverseAnti(cp, antiGroups(cp), &n->second, true);
   }
+  pt.mark("cluster inverse anti-affinity");
+  // the groups each pod's spec implies, built on worker threads (independent per pod), then
+  // deduplicated by hash in pod order exactly as the sequential Update calls would
+  std::vector<std::vector<TopoGroup>> podAnti((size_t)P), podOwn((size_t)P);
+  std::vector<char> podHasAnti((size_t)P, 0);
+  parallel_for(P, 64, [&](int p) {
+    const std::shared_ptr<PodH>& sp = states[(size_t)p][0].spec;
+    if (!sp) return;
+    if (sp->hasAffinity && sp->hasPodAnti && (!sp->antiRequired.empty() || !sp->antiPreferred.empty())) {
+      podHasAnti[(size_t)p] = 1;
+      podAnti[(size_t)p] = antiGroups(*sp);
+    }
+    podOwn[(size_t)p] = ownedSpecGroups(*sp);
+  });
+  pt.mark("pods' groups (workers)");
   std::vector<uint64_t> invOwned(P, 0);
   for (int p = 0; p < P; p++) {  // NewTopology: Update(pod) for every pod, in order
     const std::shared_ptr<PodH>& sp = states[(size_t)p][0].spec;
     if (!sp) continue;
-    if (sp->hasAffinity && sp->hasPodAnti && (!sp->antiRequired.empty() || !sp->antiPreferred.empty()))
-      invOwned[(size_t)p] = inverseAnti(*sp, nullptr, false);
+    if (podHasAnti[(size_t)p]) invOwned[(size_t)p] = inverseAnti(*sp, std::move(podAnti[(size_t)p]), nullptr, false);
     uint64_t gown = 0;
-    for (auto& g : ownedSpecGroups(*sp)) {
+    for (auto& g : podOwn[(size_t)p]) {
       auto it = ownByHash.find(g.hash);
       int idx;
       if (it == ownByHash.end()) {
         idx = (int)own.size();
+        seedDomains(g);
         countDomains(g, idx);
         ownByHash[g.hash] = idx;
         own.push_back(g);
@@ -282,6 +334,7 @@ void Host::buildTopology() {
     }
     states[(size_t)p][0].gown = gown;
   }
+  pt.mark("pods' groups + countDomains");
   uint64_t late = 0;
   for (int p = 0; p < P; p++)
     for (size_t k = 1; k < states[(size_t)p].size(); k++) {
@@ -294,6 +347,7 @@ void Host::buildTopology() {
         if (it == ownByHash.end()) {  // created by this relaxation's Update (topology.go:102-119)
           idx = (int)own.size();
           if (idx >= 64) throw KsError(-3, "more than 64 topology groups");
+          seedDomains(g);
           countDomains(g, idx);
           g.late = true;
           ownByHash[g.hash] = idx;
@@ -306,6 +360,7 @@ void Host::buildTopology() {
       }
       st.gown = gown;
     }
+  pt.mark("relaxation states' groups");
   if (own.size() + inv.size() > 64) throw KsError(-3, "more than 64 topology groups");
   const int G1 = (int)own.size(), G = G1 + (int)inv.size();
   dims.tgLate = late;
@@ -315,13 +370,14 @@ void Host::buildTopology() {
   for (auto& g : groups)  // NewExistingNode registers every node's hostname (existingnode.go:60)
     if (g.key == kHostnameKey && !g.late)  // in the groups that exist by then
       for (auto& n : nodes) g.domains.emplace(n.hostName, 0);
-  for (int p = 0; p < P; p++) {
+  parallel_for(P, 256, [&](int p) {  // per pod, independent
     tab.pod_ginv[(size_t)p] = invOwned[(size_t)p] << G1;
     for (int g = 0; g < G; g++)
       if (groups[(size_t)g].namespaces.count(pods[(size_t)p].ns) && sel_selects(groups[(size_t)g].sel, pods[(size_t)p].labels))
         tab.pod_gsel[(size_t)p] |= 1ull << g;
-  }
+  });
 
+  pt.mark("hostnames + pod selectors");
   // --- device tables
   tab.tg_meta.assign((size_t)G * TGM_WORDS, 0);
   tab.tg_cnt0.clear();
@@ -398,6 +454,7 @@ void Host::buildTopology() {
   // domain is chosen like a NodeClaim's; k_solve decides such nodes wave-wide (node_slow).
   dims.tgUnlab = 0;
   for (size_t i = 0; i < tab.n_tdom.size() && G > 0 && N > 0; i++) dims.tgUnlab |= tab.n_tdom[i] < 0;
+  pt.mark("count tables + node domains");
   if (topoExcluded) {  // the consolidation view: what each simulation's exclusions take away
     for (auto& kv : contrib)
       for (auto& gd : kv.second) {
@@ -433,6 +490,7 @@ void Host::buildTopology() {
       dims.FSW = std::max(dims.FSW, nv);
     }
   dims.tgCntWords = (int32_t)tab.tg_cnt0.size();
+  pt.mark("consolidation contributions");
 }
 
 }  // namespace ks
