@@ -229,6 +229,7 @@ struct ks_cons {
     }
   };
   Launch L;
+  hipEvent_t ev[2] = {nullptr, nullptr};  // run_sims' timing events
   int32_t* rank = nullptr;  // global NewQueue rank of every pod
 
   int sim_of_multi(int mid) const { return multiHi - mid; }  // mid in [1, multiHi]
@@ -241,6 +242,8 @@ struct ks_cons {
     if (pb && hipGetDevice(&prev) == hipSuccess) (void)hipSetDevice(pb->device);
     free_launch();
     if (rank) (void)hipFree(rank);
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
@@ -939,30 +942,29 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
   prepare_launch(c, rank, world);
   ks_problem& pb = *c.pb;
   const int ns = (int)c.L.lsims.size();
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
-  HIPCHK(hipEventRecord(e0, pb.stream));
+  if (!c.ev[0]) {  // the pass's timing events, created once per handle
+    HIPCHK(hipEventCreate(&c.ev[0]));
+    HIPCHK(hipEventCreate(&c.ev[1]));
+  }
+  HIPCHK(hipEventRecord(c.ev[0], pb.stream));
   HIPCHK(sim_queue_sort(c.rank, c.L.lentries, c.L.lentrySim, c.L.lnent, c.L.lrbits, c.L.lsbits, c.L.lkeys, c.L.lvals, c.L.ltemp,
                         c.L.ltempBytes, c.L.lpodmap, pb.stream));
   HIPCHK(launch_sims(pb.dev, c.L.lworks, ns, c.L.lplan, pb.stream));
-  HIPCHK(hipEventRecord(e1, pb.stream));
-  HIPCHK(hipEventSynchronize(e1));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  HIPCHK(hipEventRecord(c.ev[1], pb.stream));
+  // the records follow on the same stream; one synchronisation covers both
   const size_t bytes = 4 * (size_t)c.recWords * ns, all = 4 * (size_t)c.recWords * c.per_rank(world);
   if (onDevice) {
-    HIPCHK(hipMemsetAsync(records, 0, all, pb.stream));
+    if (all > bytes) HIPCHK(hipMemsetAsync((char*)records + bytes, 0, all - bytes, pb.stream));
     if (bytes) HIPCHK(hipMemcpyAsync(records, c.L.lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
-  } else {
-    if (bytes) HIPCHK(hipMemcpyAsync(c.L.hrec, c.L.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
+  } else if (bytes) {
+    HIPCHK(hipMemcpyAsync(c.L.hrec, c.L.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
   }
   HIPCHK(hipStreamSynchronize(pb.stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, c.ev[0], c.ev[1]));
   if (!onDevice) {
     memcpy(records, c.L.hrec, bytes);
-    memset((char*)records + bytes, 0, all - bytes);
+    if (all > bytes) memset((char*)records + bytes, 0, all - bytes);
   }
   return ms;
 }
