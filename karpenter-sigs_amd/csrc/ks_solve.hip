@@ -1063,9 +1063,18 @@ struct Solver {
       // Requests only grow: the options a request no longer fits are a prefix of each resource's
       // Allocatable-ascending order beyond its threshold.
       int removed = 0, examined = 0;
+      // the smallest Allocatable left beyond each resource's threshold, all read at once: a resource whose
+      // request still fits it removes nothing and skips its ballot loop (the common step)
+      int64_t nxt[RM];
+#pragma unroll
+      for (int r = 0; r < RM; r++) {
+        if (RT == 0 && r >= d.R) break;
+        nxt[r] = nthr[r] < nIT ? tsort_a((int64_t)tb * R() + (int64_t)r * nIT + nthr[r]) : INT64_MAX;
+      }
       for (int r = 0; r < R(); r++) {
         const int64_t base = (int64_t)tb * R() + (int64_t)r * nIT;
         int k = nthr[r];
+        if (!(nxt[r] < req[r])) continue;
         while (k < nIT) {
           const int i = k + lane();
           const bool ex = i < nIT && tsort_a(base + i) < req[r];
@@ -1192,10 +1201,9 @@ struct Solver {
           m = o > m ? o : m;
         }
       }
-      if (lane() == 0) {
-        v.max[(int64_t)c * R() + r] = m;
-        if (pos >= 0) s_phead[(int64_t)pos * R() + r] = m - v.req[(int64_t)c * R() + r];
-      }
+      m = rdl64(m, 0);  // lane 0's value, stored by every lane (claim state is written wave-wide, see commit_claim)
+      v.max[(int64_t)c * R() + r] = m;
+      if (pos >= 0) s_phead[(int64_t)pos * R() + r] = m - v.req[(int64_t)c * R() + r];
     }
     if (!INL) hbm_release();
     wsync();
@@ -1208,18 +1216,27 @@ struct Solver {
     const ClaimView<INL>& v = cv<INL>();
     const int okNew = uni(s_okey[pos]) + 1;
     const bool srt = pos + 1 >= n || okNew <= uni(s_okey[pos + 1]);
-    if (lane() == 0) {
+    // Claim state is written by every lane with the same (wave-uniform) values rather than under
+    // `lane() == 0`: a lane-0-only LDS store was lost in some builds, a wave-wide one has no
+    // exec-mask region to get wrong.  Same-address stores of one value are benign.
+    const int64_t hd = uni64(s_phead[(int64_t)pos * R()]);  // (read before any lane writes)
+    int64_t heads[RM];
 #pragma unroll
-      for (int r = 0; r < RM; r++) {
-        if (RT == 0 && r >= d.R) break;
-        v.req[(int64_t)c * R() + r] = req[r];
-        v.thr[(int64_t)c * R() + r] = nthr[r];
-        s_phead[(int64_t)pos * R() + r] -= pod[r];
-      }
-      v.cnt[c] = ncnt;
-      s_okey[pos] = okNew;
-      if (hpA()) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
+    for (int r = 0; r < RM; r++) {
+      if (RT == 0 && r >= d.R) break;
+      heads[r] = r == 0 ? hd : uni64(s_phead[(int64_t)pos * R() + r]);
     }
+    wsync();
+#pragma unroll
+    for (int r = 0; r < RM; r++) {
+      if (RT == 0 && r >= d.R) break;
+      v.req[(int64_t)c * R() + r] = req[r];
+      v.thr[(int64_t)c * R() + r] = nthr[r];
+      s_phead[(int64_t)pos * R() + r] = heads[r] - pod[r];
+    }
+    v.cnt[c] = ncnt;
+    s_okey[pos] = okNew;
+    if (hpA() && lane() == 0) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
     if (keys(sflags) || (TOPO && t_mask)) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
     copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     log_commit(p, c, nlog);
@@ -1349,29 +1366,30 @@ struct Solver {
                 thr[r] = k;
               }
               const int cnt = popc_words(s_rem, d.TW);
-              if (lane() == 0) {
-                for (int r = 0; r < R(); r++) {
-                  if (inl) {
-                    lc.req[(int64_t)c * R() + r] = req[r];
-                    lc.thr[(int64_t)c * R() + r] = thr[r];
-                  } else {
-                    gc.req[(int64_t)c * R() + r] = req[r];
-                    gc.thr[(int64_t)c * R() + r] = thr[r];
-                  }
-                }
+              // wave-wide stores of uniform values (see commit_claim)
+              for (int r = 0; r < R(); r++) {
                 if (inl) {
-                  lc.tpl[c] = t;
-                  lc.cnt[c] = cnt;
+                  lc.req[(int64_t)c * R() + r] = req[r];
+                  lc.thr[(int64_t)c * R() + r] = thr[r];
                 } else {
-                  gc.cnt[c] = cnt;
+                  gc.req[(int64_t)c * R() + r] = req[r];
+                  gc.thr[(int64_t)c * R() + r] = thr[r];
                 }
+              }
+              if (inl) {
+                lc.tpl[c] = t;
+                lc.cnt[c] = cnt;
+              } else {
+                gc.cnt[c] = cnt;
+              }
+              if (lane() == 0) {
                 W.c_tpl[c] = t;
                 W.c_hp[c] = cur_hpu;
                 W.c_host[c] = hostid;
-                s_order[c] = c;
-                s_okey[c] = 1;
-                s_ptpl[c] = t;
               }
+              s_order[c] = c;
+              s_okey[c] = 1;
+              s_ptpl[c] = t;
               srt = c == 0 || uni(s_okey[c - 1]) <= 1;
               log_commit(p, c, nlog);
               hbm_release();  // c_rs / c_tpl / overflow state are read by other lanes later
