@@ -355,6 +355,7 @@ struct Solver {
   bool t_nonode = false;  // some matching group admits no domain at all: no existing node can pass
   uint64_t t_active = ~0ull;  // groups in t.topologies so far (late groups join at their relaxation)
   int64_t algbytes = 0;
+  bool rem_same = false;  // the last claim_full left the claim's options unchanged (commit skips the copy back)
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
   uint64_t cur_hpo = 0;               // its own initial entries on existing nodes (HostPortUsage.Add replaces them)
   uint64_t cur_vm = 0;                // the popped pod's PVCs of limited drivers (Solve only; SIM refuses them)
@@ -1057,8 +1058,7 @@ struct Solver {
     const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
     PHS_END(u0, 0);
     PH_BEGIN(u1);
-    copy_words(s_rem, v.rem + (int64_t)c * d.TW, d.TW);
-    wsync();
+    rem_same = false;
     if (!negR()) {
       // Requests only grow: the options a request no longer fits are a prefix of each resource's
       // Allocatable-ascending order beyond its threshold.
@@ -1066,11 +1066,22 @@ struct Solver {
       // the smallest Allocatable left beyond each resource's threshold, all read at once: a resource whose
       // request still fits it removes nothing and skips its ballot loop (the common step)
       int64_t nxt[RM];
+      bool moves = false;
 #pragma unroll
       for (int r = 0; r < RM; r++) {
         if (RT == 0 && r >= d.R) break;
         nxt[r] = nthr[r] < nIT ? tsort_a((int64_t)tb * R() + (int64_t)r * nIT + nthr[r]) : INT64_MAX;
+        moves |= nxt[r] < req[r];
       }
+      if (!changed && !moves) {  // the options stay as they are: no working copy, nothing to write back
+        algbytes += 16 * R() + 4 * R();
+        PHS_END(u1, 1);
+        rem_same = true;
+        ncnt = uni(v.cnt[c]);
+        return ncnt > 0;
+      }
+      copy_words(s_rem, v.rem + (int64_t)c * d.TW, d.TW);
+      wsync();
       for (int r = 0; r < R(); r++) {
         const int64_t base = (int64_t)tb * R() + (int64_t)r * nIT;
         int k = nthr[r];
@@ -1135,6 +1146,8 @@ struct Solver {
       PHS_END(u3, 3);
       return ncnt > 0;
     }
+    copy_words(s_rem, v.rem + (int64_t)c * d.TW, d.TW);
+    wsync();
     int cnt = 0, scanned = 0;
     if (changed) feas_masks(s_rs, t, fm_row(s, t));
     for (int base = 0; base < nIT; base += kWave) {
@@ -1238,7 +1251,7 @@ struct Solver {
     s_okey[pos] = okNew;
     if (hpA() && lane() == 0) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
     if (keys(sflags) || (TOPO && t_mask)) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
-    copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
+    if (!rem_same) copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     log_commit(p, c, nlog);
     // The max bound stays valid as the options only shrink; it is tightened lazily when a full check
     // fails.  HBM-resident claim state is re-read by other lanes: drain the stores first.
