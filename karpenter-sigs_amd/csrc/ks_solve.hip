@@ -1232,14 +1232,12 @@ struct Solver {
     // Claim state is written by every lane with the same (wave-uniform) values rather than under
     // `lane() == 0`: a lane-0-only LDS store was lost in some builds, a wave-wide one has no
     // exec-mask region to get wrong.  Same-address stores of one value are benign.
-    const int64_t hd = uni64(s_phead[(int64_t)pos * R()]);  // (read before any lane writes)
-    int64_t heads[RM];
+    int64_t heads[RM];  // (each lane reads before it writes the same words: program order keeps it)
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
-      heads[r] = r == 0 ? hd : uni64(s_phead[(int64_t)pos * R() + r]);
+      heads[r] = s_phead[(int64_t)pos * R() + r];
     }
-    wsync();
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
