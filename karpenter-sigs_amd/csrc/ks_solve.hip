@@ -187,10 +187,8 @@ __device__ __attribute__((noinline)) bool rs_add_wave(const DevLayout L, LU32 ou
         const int64_t ngt = keep && x.hg ? x.gt : 0, nlt = keep && x.hl ? x.lt : 0;
         diff |= watched && (ngt != rs_gt(out, km.bslot) || nlt != rs_lt(out, km.bslot));
         wsync();
-        if (lane() == 0) {
-          rs_set_gt(out, km.bslot, ngt);
-          rs_set_lt(out, km.bslot, nlt);
-        }
+        rs_set_gt(out, km.bslot, ngt);  // wave-wide store of uniform values (see commit_claim)
+        rs_set_lt(out, km.bslot, nlt);
       }
     } else {  // rs_copy_key
       for (int i = lane(); i < km.nw; i += kWave) out[L.HDR + km.off + i] = in[L.HDR + km.off + i];
@@ -205,12 +203,10 @@ __device__ __attribute__((noinline)) bool rs_add_wave(const DevLayout L, LU32 ou
     }
   }
   wsync();
-  if (lane() == 0) {
-    wr64(out, 0, po | pi);
-    wr64(out, 2, cm);
-    wr64(out, 4, hg);
-    wr64(out, 6, hl);
-  }
+  wr64(out, 0, po | pi);  // wave-wide store of uniform values (see commit_claim)
+  wr64(out, 2, cm);
+  wr64(out, 4, hg);
+  wr64(out, 6, hl);
   wsync();
   return wballot(diff) != 0;
 }
@@ -927,10 +923,11 @@ struct Solver {
         if (wballot(any) == 0) return FC_TOPO | ((uint32_t)g << 16);
       }
       wsync();
-      if (lane() == 0) {  // requirements.Add(domains)
-        wr64(s_trs1, 0, 1ull << k);
-        rs_add(L, rs, s_trs1);
-      }
+      // requirements.Add(domains), run by every lane in lockstep on the same LDS words (wave-wide stores
+      // of uniform values, see commit_claim)
+      wr64(s_trs1, 0, 1ull << k);
+      wsync();
+      rs_add(L, rs, s_trs1);
       wsync();
     }
     // Compatible(nodeRequirements, topologyRequirements, AllowUndefinedWellKnownLabels)
@@ -1469,7 +1466,8 @@ struct Solver {
         wsync();
       }
     }
-    if (lane() == 0) { s_okey[to] = k0; s_order[to] = v0; }
+    s_okey[to] = k0;  // wave-wide store of uniform values (see commit_claim)
+    s_order[to] = v0;
     wsync();
   }
   // First i in [from, n) with key[i] < key[i-1] (a descent), or n.
