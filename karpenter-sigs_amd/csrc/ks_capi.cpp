@@ -2,6 +2,7 @@
 // workspace, kernel launch and reconstruction of scheduling.Results (scheduler.go:102-106).
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <memory>
@@ -24,7 +25,7 @@ namespace {
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
       log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, n_vm, n_vc, tg_cnt,
-      tg_ccnt, tg_cpos, fail_rs, total;
+      tg_ccnt, tg_cpos, fail_rs, log_hg, tg_act, total;
   int32_t ccs;  // tg_ccnt row stride
 };
 
@@ -64,6 +65,8 @@ WorkLayout work_layout(const KsDims& d) {
   w.tg_ccnt = a.add(4 * (size_t)std::max(d.G, 1) * (d.G ? K + 1 : 1));
   w.tg_cpos = a.add(4 * (size_t)std::max(d.G, 1));
   w.fail_rs = a.add(d.G ? 4 * (size_t)P * std::max(d.NTPL, 1) * d.FSW : 4);
+  w.log_hg = a.add(d.G ? 8 * P : 8);
+  w.tg_act = a.add(4 * (size_t)std::max(d.G, 1));
   w.total = a.total;
   return w;
 }
@@ -101,6 +104,8 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.tg_ccnt = (int32_t*)(base + w.tg_ccnt);
   k.tg_cpos = (int32_t*)(base + w.tg_cpos);
   k.fail_rs = (uint32_t*)(base + w.fail_rs);
+  k.log_hg = (uint64_t*)(base + w.log_hg);
+  k.tg_act = (int32_t*)(base + w.tg_act);
   k.ccs = w.ccs;
   return k;
 }
@@ -326,6 +331,44 @@ void ks_upload(ks_problem* pb) {
   D.fk_tpl = (const int32_t*)(b + o_fkt);
 }
 
+// A hostname-keyed group's domains at an unsatisfiable-topology failure (topology.go:167), rebuilt from the
+// Solve's commit log: NewTopology's counts (tg_cnt0: existing nodes registered by NewExistingNode,
+// existingnode.go:60, and countDomains' cluster pods), plus one per commit the device logged as counted in
+// the group (log_hg) before the failure (`seq` commits) -- on an existing node its hostname, on a NodeClaim
+// its hostname-placeholder -- plus every placeholder NewNodeClaim registered (nodeclaim.go:48-50, one per
+// ordinal up to the failing attempt's `ord`; a late group only sees those made after it was created,
+// `act`).  Recording registers a domain.  Entries "name:count" in Go's sorted map-key order.
+static std::string hostnameCounts(const Host& h, int g, int seq, int64_t ord, int32_t act,
+                                  const std::vector<uint64_t>& loghg, const std::vector<int32_t>& logt,
+                                  const std::vector<int32_t>& chost) {
+  const KsDims& d = h.dims;
+  const int32_t* gm = &h.tab.tg_meta[(size_t)g * TGM_WORDS];
+  const int k = gm[TGM_KEY], nv = gm[TGM_NV];
+  if (seq < 0 || seq > (int)logt.size() || (size_t)seq > loghg.size())
+    throw KsError(KS_ERR_INTERNAL, "hostname topology failure outside the commit log");
+  std::vector<int32_t> cnt(h.tab.tg_cnt0.begin() + gm[TGM_CNT], h.tab.tg_cnt0.begin() + gm[TGM_CNT] + nv);
+  std::map<int64_t, int32_t> ph;  // placeholder ordinal -> count
+  for (int64_t o = std::max<int64_t>(h.hostnameSeed, act) + 1; o <= ord; o++) ph[o] = 0;
+  for (int i = 0; i < seq; i++) {
+    if (!((loghg[(size_t)i] >> g) & 1ull)) continue;
+    if (logt[(size_t)i] >= 0) {
+      ph[chost[(size_t)logt[(size_t)i]]] += 1;
+    } else {
+      const int v = h.tab.n_tdom[(size_t)g * d.N + (size_t)(-logt[(size_t)i] - 1)];
+      if (v < 0 || v >= nv) throw KsError(KS_ERR_INTERNAL, "hostname record on a node without a hostname domain");
+      cnt[(size_t)v] = cnt[(size_t)v] < 0 ? 1 : cnt[(size_t)v] + 1;
+    }
+  }
+  std::vector<std::pair<std::string, int32_t>> e;
+  for (int v = 0; v < nv; v++)
+    if (cnt[(size_t)v] >= 0) e.push_back({h.values[(size_t)k][(size_t)v], cnt[(size_t)v]});
+  for (auto& kv : ph) e.push_back({h.placeholder(kv.first), kv.second});
+  std::sort(e.begin(), e.end());
+  std::string o;
+  for (size_t i = 0; i < e.size(); i++) o += (i ? " " : "") + e[i].first + ":" + std::to_string(e[i].second);
+  return o;
+}
+
 // Rebuild Results from the replica-0 workspace.
 static ks_results* collect(ks_problem* pb, const KsWork& W) {
   Host& h = pb->host;
@@ -358,6 +401,8 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
   dl(fhost, W.fail_host, (size_t)d.P * std::max(d.NTPL, 1), st);
   HIPCHK(hipStreamSynchronize(st));
   std::vector<uint32_t> frs;  // topology failure snapshots, only when some pod failed on one
+  std::vector<uint64_t> loghg;
+  std::vector<int32_t> tgact;
   if (d.G) {
     bool need = false;
     for (int p = 0; p < d.P && !need; p++) {
@@ -369,6 +414,8 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     }
     if (need) {
       dl(frs, W.fail_rs, (size_t)d.P * d.NTPL * d.FSW, st);
+      dl(loghg, W.log_hg, nl, st);
+      dl(tgact, W.tg_act, d.G, st);
       HIPCHK(hipStreamSynchronize(st));
     }
   }
@@ -567,16 +614,19 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
           const int32_t* gm = &h.tab.tg_meta[(size_t)g * TGM_WORDS];
           const int k = gm[TGM_KEY], nv = gm[TGM_NV];
           const uint32_t* fr = &frs[((size_t)p * d.NTPL + t) * d.FSW];
+          // fmt %v of TopologyGroup.domains (map[string]int32): the registered domains in name order
           std::string counts = "map[";
-          if (!gm[TGM_HOST]) {  // registered domains in name order with their counts at the failure
+          if (!gm[TGM_HOST]) {  // the device snapshot of the counts at the failure (-1: not registered)
             bool first = true;
             for (int v = 0; v < nv; v++)
-              if ((int32_t)fr[v] >= 0) {  // -1: not registered
+              if ((int32_t)fr[v] >= 0) {
                 counts += (first ? "" : " ") + h.values[(size_t)k][(size_t)v] + ":" + std::to_string((int32_t)fr[v]);
                 first = false;
               }
+          } else {
+            counts += hostnameCounts(h, g, (int)fr[0], host, tgact[(size_t)g], loghg, logt, chost);
           }
-          counts += "]";  // hostname groups: the per-placeholder counts are not snapshotted
+          counts += "]";
           std::vector<uint32_t> nr(h.tab.tpl_rs.begin() + (size_t)t * d.RSW, h.tab.tpl_rs.begin() + (size_t)(t + 1) * d.RSW);
           rs_add(h.L, nr.data(), ps.rsAll.data());
           auto dom = [&](const uint32_t* rec) {

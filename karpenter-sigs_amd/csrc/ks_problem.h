@@ -225,7 +225,10 @@ struct KsWork {
   int32_t KS_G* tg_cnt;     // topology domain counts (copy of tg_cnt0)
   int32_t KS_G* tg_cpos;    // [G] NodeClaims whose placeholder domain has a positive count
   int32_t KS_G* tg_ccnt;    // [G][Kcap] counts of the NodeClaims' hostname-placeholder domains
-  uint32_t KS_G* fail_rs;   // [P][NTPL][FSW] FC_TOPO_COMPAT: requirements; FC_TOPO: the group's counts + registered bits
+  uint32_t KS_G* fail_rs;   // [P][NTPL][FSW] FC_TOPO_COMPAT: requirements; FC_TOPO: the group's counts (-1: unregistered),
+                            // or for a hostname group the commit-log length at the failure (the host replays log_hg)
+  uint64_t KS_G* log_hg;    // [P] TOPO Solve: per commit, the hostname groups Topology.Record counted it in
+  int32_t KS_G* tg_act;     // [G] TOPO Solve: NewNodeClaim ordinal counter when a late group was created
   // consolidation simulations only (k_solve<.., SIM=true>): this simulation's view of the shared
   // cluster problem (helpers.go:73-127 — candidates removed, their pods added to the pending ones)
   const int32_t KS_G* pod_map;  // [P] local -> global pod, in NewQueue order (k_sim_keys + sort)

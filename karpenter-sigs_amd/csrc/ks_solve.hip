@@ -114,6 +114,8 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
       for (int64_t i = gtid; i < d.tgCntWords; i += gsz) W.tg_cnt[i] = D.tg_cnt0[i];
       for (int64_t i = gtid; i < (int64_t)d.G * (d.Kcap + 1); i += gsz) W.tg_ccnt[i] = 0;
       for (int64_t i = gtid; i < d.G; i += gsz) W.tg_cpos[i] = 0;
+      for (int64_t i = gtid; i < d.G; i += gsz) W.tg_act[i] = 0;
+      for (int64_t i = gtid; i < d.P; i += gsz) W.log_hg[i] = 0;
     }
     for (int64_t i = gtid; i < d.P; i += gsz) {
       W.queue[i] = qorder[i];
@@ -216,9 +218,11 @@ __device__ __attribute__((noinline)) bool rs_add_wave(const DevLayout L, LU32 ou
 // per key, the positions whose IT lacks the key (only shared keys are checked), those holding a value X
 // admits, and -- when X's operator is NotIn / DoesNotExist -- those whose IT says DoesNotExist (both
 // negative).  Every lane of the wave calls it with the same X, t and keys (ballots over X's values).
+// dnePass: pass the DoesNotExist positions unconditionally (k_feasibility's factorised rows: whether
+// they pass depends on the operator of the whole record, which feas_masks tests per step).
 template <class PX>
 __device__ __forceinline__ uint32_t fk_intersects_word(const KsDev& D, const DevLayout& L, PX X, int t, int wc,
-                                                       uint64_t keys) {
+                                                       uint64_t keys, bool dnePass = false) {
   const uint32_t KS_G* F = D.fk_words;
   const KsDims& d = D.d;
   const int TW = d.TW;
@@ -229,7 +233,7 @@ __device__ __forceinline__ uint32_t fk_intersects_word(const KsDev& D, const Dev
     const KeyMeta km = L.keys[k];
     uint32_t acc = F[base + wc];  // positions whose IT lacks the key
     const int op = rs_op(L, X, k);
-    if (op == OP_NOTIN || op == OP_DNE) acc |= F[base + TW + wc];
+    if (dnePass || op == OP_NOTIN || op == OP_DNE) acc |= F[base + TW + wc];
     if (!bit(rs_compl(X), k)) {  // X In: the positions holding one of its values
       for (int i = 0; i < km.nw; i++) {
         uint32_t x = X[L.HDR + km.off + i];
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(64) void k_feasibility(KsDev D) {
   for (int w0 = 0; w0 < d.TW; w0 += kWave) {
     const int w = w0 + lane();
     const int wc = w < d.TW ? w : d.TW - 1;
-    const uint32_t v = fk_intersects_word(D, L, X, t, wc, kx) & fk_intersects_word(D, L, T, t, wc, kt);
+    const uint32_t v = fk_intersects_word(D, L, X, t, wc, kx, true) & fk_intersects_word(D, L, T, t, wc, kt, true);
     if (w < d.TW) D.st_fm[(int64_t)row * d.TW + w] = v;
   }
 }
@@ -436,20 +440,32 @@ struct Solver {
   // fmrow: k_feasibility's row for (the popped pod's state, t) -- the keys no instance type constrains
   // with more than one value, already intersected for the template and the state -- when X is the
   // template's or a claim's requirements plus that state's (Compatible with it) and nothing else: per
-  // such key the test factorises (an IT's single value is admitted by X = A + B iff by A and by B; its
-  // DoesNotExist passes iff both are negative, which Compatible implies), and the claim's options already
-  // satisfy A's part.  Only the multi-valued keys are evaluated here then.
+  // such key the test factorises for the value positions (an IT's single value is admitted by X = A + B
+  // iff by A and by B), and the claim's options already satisfy A's part.  An IT's DoesNotExist does not
+  // factorise (Exists + NotIn is NotIn, which it intersects, requirements.go:248-252): the row passes
+  // those positions and they are tested here against X's operator.  Only the multi-valued keys are
+  // evaluated in full then.
   __device__ __forceinline__ void feas_masks(LU32 X, int t, const uint32_t KS_G* fmrow = nullptr) {
     const uint32_t KS_G* F = D.fk_words;
     const int TW = d.TW;
     const int ball = D.fk_tpl[3 * t], birr = D.fk_tpl[3 * t + 1], boff = D.fk_tpl[3 * t + 2];
     const uint64_t keysX = rs_present(X) & d.itKeys & (fmrow ? d.fkMulti : ~0ull);
+    uint64_t keysDne = 0;  // fmrow: X's single-valued IT keys whose operator is In / Exists
+    if (fmrow)
+      for (uint64_t m = rs_present(X) & d.itKeys & ~d.fkMulti; m; m &= m - 1) {
+        const int op = rs_op(L, X, ctz64(m));
+        if (op != OP_NOTIN && op != OP_DNE) keysDne |= m & (~m + 1);
+      }
     const int nz = L.keys[d.zoneKey].nv, nc = L.keys[d.ctKey].nv;
     for (int w0 = 0; w0 < TW; w0 += kWave) {
       const int w = w0 + lane();
       const int wc = w < TW ? w : TW - 1;
       uint32_t ic = F[ball + wc] & fk_intersects_word(D, L, X, t, wc, keysX);
-      if (fmrow) ic &= fmrow[wc];
+      if (fmrow) {
+        ic &= fmrow[wc];
+        // the row passes DoesNotExist positions; they intersect X iff X's operator is negative there
+        for (uint64_t m = keysDne; m; m &= m - 1) ic &= ~F[D.fk_key_off[t * d.NK + ctz64(m)] + TW + wc];
+      }
       uint32_t of = 0;
       for (int c0 = 0; c0 < nc; c0 += kWave) {
         const uint64_t cm0 = wballot(c0 + lane() < nc && rs_member(L, X, d.ctKey, c0 + lane()));
@@ -942,9 +958,12 @@ struct Solver {
   // the node's own label value (the strict Compatible admitted nothing else; ks_topo.cpp refuses
   // the one input where a pod's NotIn could stand in for a missing label), so the node's domain
   // table replaces the scan over F's value words.
+  // Solve (not SIM): returns the hostname groups it counted the pod in (the commit's log_hg entry, which
+  // the host replays to print a hostname group's counts in an unsatisfiable-topology message).
   template <class PR>
-  __device__ __forceinline__ void topo_record(PR F, int claim, int node, uint64_t allow) {
+  __device__ __forceinline__ uint64_t topo_record(PR F, int claim, int node, uint64_t allow) {
     hbm_release();
+    uint64_t hg = 0;
     const uint64_t owned = d.G1 >= 64 ? ~0ull : ((1ull << d.G1) - 1);
     const uint64_t pres = rs_present(F), compl_ = rs_compl(F);
     for (uint64_t m = (t_sel & owned & t_active) | t_inv; m; m &= m - 1) {
@@ -958,10 +977,13 @@ struct Solver {
         if (!rdl(match, 0)) continue;
       }
       if (node >= 0) {
+        int rec = 0;
         if (lane() == 0) {
           const int v = D.n_tdom[(int64_t)g * d.N + node];
           if (v >= 0) tcnt_inc(tg(g, TGM_CNT) + v);  // recording registers the domain
+          rec = v >= 0;
         }
+        if (!SIM && tg(g, TGM_HOST) && rdl(rec, 0)) hg |= 1ull << g;
         continue;
       }
       const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
@@ -973,8 +995,10 @@ struct Solver {
         for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off);
         if (bit(compl_, k) || tot != 1) continue;
       }
+      bool any = false;
       for (int w = lane(); w < km.nw; w += kWave) {  // anti-affinity: every domain of the requirement
         uint32_t x = F[L.HDR + km.off + w];
+        any = any || x != 0;
         while (x) {
           const int v = w * 32 + __builtin_ctz(x);
           x &= x - 1;
@@ -990,18 +1014,25 @@ struct Solver {
           }
         }
       }
+      if (!SIM && tg(g, TGM_HOST) && wballot(any)) hg |= 1ull << g;
     }
     hbm_release();
     wsync();
+    return hg;
+  }
+  // the commit at log position i was counted in the hostname groups hg (Solve only)
+  __device__ __forceinline__ void log_hgroups(int i, uint64_t hg) const {
+    if (!SIM && hg && lane() == 0) W.log_hg[i] = hg;
   }
 
   // Topology.Update creating the late groups `m` (topology.go:102-119), wave-wide: the NodeClaims made so
   // far registered their placeholders before these groups existed (NewNodeClaim's Register only reaches
   // t.topologies), so their placeholder domains start unregistered.
-  __device__ __forceinline__ void topo_activate(uint64_t m, int nclaims) {
+  __device__ __forceinline__ void topo_activate(uint64_t m, int nclaims, int hostCtr) {
     for (; m; m &= m - 1) {
       const int g = ctz64(m);
       for (int c = lane(); c < nclaims; c += kWave) W.tg_ccnt[(int64_t)g * W.ccs + c] = -1;
+      if (!SIM && lane() == 0) W.tg_act[g] = hostCtr;  // placeholders up to this ordinal were never registered
     }
     hbm_release();
     wsync();
@@ -1253,8 +1284,8 @@ struct Solver {
     if (keys(sflags) || !INL || hpA()) hbm_release();
     wsync();
     if (TOPO && (t_sel | t_inv)) {  // Topology.Record on the claim's final requirements (nodeclaim.go:121)
-      if (keys(sflags) || t_mask) topo_record(s_rs, c, -1, d.allowWK);
-      else topo_record(W.c_rs + (int64_t)c * d.RSW, c, -1, d.allowWK);
+      if (keys(sflags) || t_mask) log_hgroups(nlog - 1, topo_record(s_rs, c, -1, d.allowWK));
+      else log_hgroups(nlog - 1, topo_record(W.c_rs + (int64_t)c * d.RSW, c, -1, d.allowWK));
     }
     algbytes += 24 * R() + 4 * d.TW + 8;
     return srt;
@@ -1313,6 +1344,8 @@ struct Solver {
                 const int g = (int)(tc >> 16) & 0xff, nv = tg(g, TGM_NV);
                 if (!tg(g, TGM_HOST))  // the counts (-1: unregistered), for the message (FSW fits them)
                   for (int v = lane(); v < nv; v += kWave) W.fail_rs[slot + v] = (uint32_t)tcnt(g, v);
+                else if (lane() == 0)  // hostname: the commits so far; the host replays their log_hg entries
+                  W.fail_rs[slot] = (uint32_t)nlog;
               }
             }
           }
@@ -1402,7 +1435,7 @@ struct Solver {
               log_commit(p, c, nlog);
               hbm_release();  // c_rs / c_tpl / overflow state are read by other lanes later
               wsync();
-              if (TOPO && (t_sel | t_inv)) topo_record(s_rs, c, -1, d.allowWK);
+              if (TOPO && (t_sel | t_inv)) log_hgroups(nlog - 1, topo_record(s_rs, c, -1, d.allowWK));
               if (inl) recompute_max<true>(c, s_rem, t, c);
               else recompute_max<false>(c, s_rem, t, c);
               if (pool >= 0) {  // subtractMax (scheduler.go:347-362)
@@ -2063,7 +2096,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           } else if (S.keys(sflags) && lane() == owner) {
             rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, S.s_pin);
           }
-          if (TOPO && (S.t_sel | S.t_inv)) S.topo_record(S.node_rs(j), -1, j, 0);  // existingnode.go:121
+          if (TOPO && (S.t_sel | S.t_inv)) S.log_hgroups(nlog, S.topo_record(S.node_rs(j), -1, j, 0));  // existingnode.go:121
           S.log_commit(p, -(j + 1), nlog);
           PH_END(t7, 7);
           S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
@@ -2117,9 +2150,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         }
         if (TOPO && slowj) {
           S.node_store_rs(j, nrs);
-          if (S.t_sel | S.t_inv) S.topo_record(S.s_rs, -1, -1, 0);  // existingnode.go:121
+          if (S.t_sel | S.t_inv) S.log_hgroups(nlog, S.topo_record(S.s_rs, -1, -1, 0));  // existingnode.go:121
         } else if (TOPO && (S.t_sel | S.t_inv)) {
-          S.topo_record(S.node_rs(j), -1, j, 0);  // existingnode.go:121
+          S.log_hgroups(nlog, S.topo_record(S.node_rs(j), -1, j, 0));  // existingnode.go:121
         }
         S.log_commit(p, -(j + 1), nlog);
         PH_END(t7, 7);
@@ -2205,7 +2238,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (TOPO && relaxed && d.tgLate) {  // Topology.Update (scheduler.go:160-170): groups the new state creates
       const uint64_t fresh = D.st_gown[s + 1] & ~S.t_active;
       if (fresh) {
-        S.topo_activate(fresh, nclaims);
+        S.topo_activate(fresh, nclaims, hostCtr);
         S.t_active |= fresh;
       }
     }

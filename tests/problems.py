@@ -304,11 +304,24 @@ def add_namespaces(rng, pods, cluster):
     return [{"name": n, "labels": lab} for n, lab in NAMESPACES]
 
 
+def special_nsr(rng):
+    """A term on the fake instance types' 'special' key, the one key some instance types hold as
+    DoesNotExist (fake/instancetype.go: small types): Exists + NotIn is NotIn, which a DoesNotExist
+    instance type intersects (requirements.go:248-252), so the factorised feasibility rows must not
+    decide those positions from one side alone."""
+    op = _pick(rng, ["In", "NotIn", "NotIn", "Exists", "Exists", "DoesNotExist"])
+    e = {"key": "special", "operator": op}
+    if op in ("In", "NotIn"):
+        e["values"] = ["optional"]
+    return e
+
+
 def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False, topology=False,
-                   affinity=False, volumes=False, namespaces=False, same_pod_ports=False, or_terms=False):
+                   affinity=False, volumes=False, namespaces=False, same_pod_ports=False, or_terms=False,
+                   special=False):
     """same_pod_ports: existing nodes' HostPortUsage also holds entries keyed by pods being scheduled
     (their own ports, or others), the case HostPortUsage.Conflicts skips and Add replaces
-    (hostportusage.go:70-85)."""
+    (hostportusage.go:70-85).  special: NodePool and pod terms on the 'special' key (special_nsr)."""
     rng = np.random.default_rng(seed)
     its = random_its(rng, n_its)
     n_templates = int(rng.integers(1, 4)) if n_templates is None else n_templates
@@ -316,6 +329,8 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
     for t in range(n_templates):
         name = "pool-%d" % t
         reqs = [random_nsr(rng, allow_custom=False) for _ in range(int(rng.integers(0, 2)))]
+        if special and rng.random() < 0.7:
+            reqs.append(special_nsr(rng))
         taints = []
         if rng.random() < 0.35:
             taints.append({"key": "dedicated", "value": _pick(rng, TEAMS), "effect": "NoSchedule"})
@@ -365,6 +380,15 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
             d["spec"]["nodeSelector"] = {synth.ARCH: _pick(rng, ARCHS)}
         daemons.append(d)
     pods = [random_pod(rng, i) for i in range(n_pods)]
+    if special:
+        for p in pods:
+            if rng.random() < 0.45:
+                e = special_nsr(rng)
+                na = p["spec"].setdefault("affinity", {}).setdefault("nodeAffinity", {})
+                req = na.setdefault("requiredDuringSchedulingIgnoredDuringExecution",
+                                    {"nodeSelectorTerms": [{"matchExpressions": []}]})
+                for term in req["nodeSelectorTerms"]:
+                    term.setdefault("matchExpressions", []).append(dict(e))
     if host_ports:
         for p in pods:
             if rng.random() < 0.4:
@@ -397,6 +421,37 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
         "pods": pods,
         "clusterPods": cluster,
     }
+
+
+def hostname_failure_problem(seed, n_pods=150, n_nodes=8):
+    """Pods whose hostname-keyed pod affinity no domain can satisfy, so Topology.AddRequirements fails
+    with "unsatisfiable topology constraint ... (counts = map[...])" and prints every registered
+    hostname domain with its count (topology.go:167): existing nodes (NewExistingNode registers them),
+    every hostname-placeholder NewNodeClaim registered so far, and the counts this Solve recorded.
+    Kinds: affinity to an app no pod carries ("ghost"), and affinity to an app that runs on the existing
+    nodes while a hostname NotIn excludes every existing node (the target's pods then sit only on
+    excluded domains until one lands on a NodeClaim)."""
+    snap = random_problem(seed, n_pods=n_pods, n_nodes=n_nodes, topology=True, affinity=True)
+    rng = np.random.default_rng(seed + 7919)
+    names = [n["name"] for n in snap["stateNodes"]]
+    for p in snap["pods"]:
+        u = rng.random()
+        if u >= 0.35:
+            continue
+        aff = p["spec"].setdefault("affinity", {})
+        if u < 0.15:
+            target = "ghost"
+        else:
+            target = "a%d" % int(rng.integers(5))
+            if p["metadata"]["labels"]["app"] == target:
+                continue
+            na = aff.setdefault("nodeAffinity", {})
+            na["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": [{"matchExpressions": [
+                {"key": synth.HOSTNAME, "operator": "NotIn", "values": list(names) or ["nowhere"]}]}]}
+        aff["podAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"labelSelector": {"matchLabels": {"app": target}}, "topologyKey": synth.HOSTNAME}]}
+        p["spec"].pop("topologySpreadConstraints", None)
+    return snap
 
 
 def canonical(results):
