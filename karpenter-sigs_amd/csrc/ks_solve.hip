@@ -34,6 +34,9 @@
 #ifndef KS_TU
 #define KS_TU 0
 #endif
+#ifndef KS_RUN_MIN  // shortest run of identical pods the simulation fast path places in one step
+#define KS_RUN_MIN 3
+#endif
 
 #include "ks_gosort.h"
 #include "ks_problem.h"
@@ -81,6 +84,40 @@ __device__ __forceinline__ T ld_sc1(const T KS_G* p) {  // L1-bypassing load of 
 }
 __device__ __forceinline__ uint32_t lds_and(LU32 p, uint32_t v) {  // ds_and_rtn_b32
   return __hip_atomic_fetch_and(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+// Wave-wide inclusive scans (sum / max) over the 64 lanes: DPP row_shr within each 16-lane row, then the
+// rows' totals carried across by readlane.
+__device__ __forceinline__ int wscan_add(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = r0 + __builtin_amdgcn_readlane(v, 31);
+  const int r2 = r1 + __builtin_amdgcn_readlane(v, 47), l = lane();
+  return v + (l >= 48 ? r2 : l >= 32 ? r1 : l >= 16 ? r0 : 0);
+}
+__device__ __forceinline__ int wscan_max(int v) {  // values >= -1
+  auto mx = [](int a, int b) { return a > b ? a : b; };
+  v = mx(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
+  v = mx(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
+  v = mx(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));
+  v = mx(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));
+  const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = mx(r0, __builtin_amdgcn_readlane(v, 31));
+  const int r2 = mx(r1, __builtin_amdgcn_readlane(v, 47)), l = lane();
+  return mx(v, l >= 48 ? r2 : l >= 32 ? r1 : l >= 16 ? r0 : -1);
+}
+// How many more pods requesting `req` of a resource fit a node with `free` of it, capped at m (<= 64):
+// floor(free / req) from a float estimate (error < 1e-4 below m + 2) corrected exactly by one int64
+// multiply.  free < 0 (INT64_MIN marks a node that never fits) takes none.
+__device__ __forceinline__ int run_cap(int64_t free, int64_t req, float rq, int m) {
+  if (req == 0) return free >= 0 ? m : 0;
+  if (free < req) return 0;
+  const float q = (float)free * rq;
+  if (q >= (float)(m + 2)) return m;
+  int qi = (int)q;
+  if ((int64_t)qi * req > free) qi--;
+  else if ((int64_t)(qi + 1) * req <= free) qi++;
+  return qi < m ? qi : m;
 }
 
 #ifdef KS_PHASE_STATS
@@ -348,6 +385,7 @@ struct Solver {
   LU32 s_trs1;          // [RSW] one group's domains as a single-key record
   LI32 s_tcs;           // [tgSmall] counts of the small-key groups (the count table's LDS-resident prefix)
   LU32 s_tcd;           // SIM: dirty bits over count words [tgSmall, tgCntWords): set once W.tg_cnt holds the word
+  LI32 s_bnode;         // LEAN SIM: [64] run placement: the node taking the run's pod at each offset (first of a node's pods)
   uint64_t t_mask = 0;  // groups matching the popped pod (owned in its state | inverse groups selecting it)
   uint64_t t_sel = 0;   // groups whose selector selects the popped pod
   uint64_t t_inv = 0;   // inverse groups the popped pod owns
@@ -414,6 +452,26 @@ struct Solver {
       W.log_pod[nlog - kWave + lane()] = lg_p;
       W.log_tgt[nlog - kWave + lane()] = lg_t;
     }
+  }
+  // Commit-log entries for `n` (<= 64) placements at once: lane t holds entry nlog + t (pod, target).
+  __device__ __forceinline__ void log_batch(int n, int pod_t, int tgt_t, int& nlog) {
+    const int b0 = nlog & (kWave - 1);
+    const int src = (lane() - b0) & (kWave - 1);  // the entry this lane buffers: nlog + src
+    const int pv = __shfl(pod_t, src), tv = __shfl(tgt_t, src);
+    const bool mine = src < n;
+    if (mine && lane() >= b0) {
+      lg_p = pv;
+      lg_t = tv;
+    }
+    if (b0 + n >= kWave) {  // the buffered block is complete: store it, then buffer the wrapped entries
+      W.log_pod[nlog - b0 + lane()] = lg_p;
+      W.log_tgt[nlog - b0 + lane()] = lg_t;
+      if (mine && lane() < b0) {
+        lg_p = pv;
+        lg_t = tv;
+      }
+    }
+    nlog += n;
   }
   __device__ __forceinline__ void log_flush(int nlog) {
     const int k = nlog & (kWave - 1);
@@ -1792,6 +1850,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   S.s_tcs = (LI32)take(d.G ? 4 * (size_t)d.tgSmall : 0);
   const int NWC = SIM && d.G ? (d.tgCntWords - d.tgSmall + 31) >> 5 : 0;
   S.s_tcd = (LU32)take(4 * (size_t)NWC);
+  S.s_bnode = (LI32)take(SIM && LEAN ? 4 * (size_t)kWave : 0);
   for (int i = lane(); i < (d.G ? d.tgSmall : 0); i += kWave) S.s_tcs[i] = D.tg_cnt0[i];
   for (int i = lane(); i < NWC; i += kWave) S.s_tcd[i] = 0;
   for (int i = lane(); i < d.G * TGM_WORDS; i += kWave) S.s_tgm[i] = D.tg_meta[i];
@@ -1912,6 +1971,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
   }
+  bool winUnusable = false;  // some register-window node is NF_UNUSABLE (a run's placements check it)
+  if constexpr (NW > 0)
+    if (d.N > 0)
+#pragma unroll
+      for (int k = 0; k < NW; k++) winUnusable |= wballot(wnf[k] & NF_UNUSABLE) != 0;
   int nclaims = 0, nlog = 0, hostCtr = SIM ? 0 : d.hostnameSeed;
   bool allSched = true;  // SIM: AllNonPendingPodsScheduled so far (pods placed on unusable nodes)
   int nrs = 0;           // SIM: compact node-requirement slots in use
@@ -1962,6 +2026,84 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           int64_t fp[RM];
 #pragma unroll
           for (int r = 0; r < RM; r++) fp[r] = rdl64(w.req[r], wi);
+          // A run of identical pods (same requests and tolerations, none stale when it is popped): pod after
+          // pod, first-fit fills the window's nodes in order, each taking as many as fit (min over resources
+          // of floor(free / request)), so the whole run is placed in one step -- per node its capacity for
+          // the run, an exclusive scan over the node order, and each pod's node from a max-scan.
+          {
+            bool inrun = false;
+            if (lane() >= wi && lane() < wn) {
+              bool same = w.tol0 == ft0 && w.tol1 == ft1;
+#pragma unroll
+              for (int r = 0; r < RM; r++) same &= w.req[r] == fp[r];
+              const uint32_t qx = (uint32_t)(qlen - (lane() - wi));
+              inrun = same && !((uint32_t)(w.ll >> 32) == epoch && (uint32_t)w.ll == qx);
+            }
+            const uint64_t nr = wballot(!inrun) & (~0ull << wi);
+            const int m = (nr ? ctz64(nr) : kWave) - wi;
+            if (m >= KS_RUN_MIN) {
+              float rq[RM];
+#pragma unroll
+              for (int r = 0; r < RM; r++) rq[r] = fp[r] > 0 ? 1.0f / (float)fp[r] : 0.f;
+              int tk[NWA], pre[NWA];
+              int base = 0;
+#pragma unroll
+              for (int k = 0; k < NW; k++) {
+                tk[k] = 0;
+                pre[k] = 0;
+                if (base < m) {
+                  const bool tol = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
+                  int cap = tol ? m : 0;
+#pragma unroll
+                  for (int r = 0; r < RM; r++) {
+                    const int c = run_cap(wav[k][r], fp[r], rq[r], m);
+                    cap = c < cap ? c : cap;
+                  }
+                  const int incl = wscan_add(cap);
+                  const int p0 = base + incl - cap, room = m - p0;
+                  tk[k] = room <= 0 ? 0 : (cap < room ? cap : room);
+                  pre[k] = p0;
+                  base += rdl(incl, kWave - 1);
+                }
+              }
+              const int placed = base < m ? base : m;
+              if (placed == 0) break;  // pod wi fits no window node: the general step
+              S.s_bnode[lane()] = -1;
+              wsync();
+#pragma unroll
+              for (int k = 0; k < NW; k++)
+                if (tk[k] > 0) {
+                  S.s_bnode[pre[k]] = k * kWave + lane();
+#pragma unroll
+                  for (int r = 0; r < RM; r++) wav[k][r] -= (int64_t)tk[k] * fp[r];
+                }
+              wsync();
+              const int nt = wscan_max(lane() < placed ? S.s_bnode[lane()] : -1);  // node of the run's pod `lane`
+              const int src = wi + lane() < kWave ? wi + lane() : kWave - 1;
+              const int fpod_t = __shfl(w.p, src);
+              if (winUnusable) {  // AllNonPendingPodsScheduled: a non-provisionable pod on an unusable node
+                int nf = 0;
+#pragma unroll
+                for (int k = 0; k < NW; k++) {
+                  const int v = __shfl(wnf[k], nt & (kWave - 1));
+                  if ((nt >> 6) == k) nf = v;
+                }
+                const int pf_t = __shfl(w.pf, src);
+                if (wballot(lane() < placed && (nf & NF_UNUSABLE) && !(pf_t & PF_PROVISIONABLE))) allSched = false;
+              }
+              const int st_t = __shfl(w.st, src);
+              if (lane() < placed && st_t == ST_FAILED) W.pod_status[fpod_t] = ST_SCHEDULED;
+              S.log_batch(placed, fpod_t, -(nt + 1), nlog);
+              S.algbytes += (int64_t)rdl(wscan_add(lane() < placed ? nt + 1 : 0), kWave - 1) * (16 * R + 16);
+              qhead += placed;
+              if (qhead >= P) qhead -= P;
+              qlen -= placed;
+              pops += placed;
+              wi += placed;
+              if (placed < m) break;  // the next pod of the run fits no window node
+              continue;
+            }
+          }
           int kj = -1;
           uint64_t mj = 0;
 #pragma unroll
