@@ -187,6 +187,19 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
         n1, secs1 = bridge.time_cons_sims(snap, max(n_sims // (4 * args.cpu_threads), 8), 1)
         cpu1 = _baseline(n1 / secs1, "cands/s", 1, "first %d single-node simulations of the same cluster "
                          "(sequential, as the reference's single goroutine runs them)" % n1, secs1)
+    # Strong-scaling evidence on one GPU: the pass sharded as `world` ranks would run it (s % world == rank),
+    # each shard's launch timed alone; a world-rank pass is bounded below by its slowest shard's kernel.
+    shards = None
+    if world == 1 and not args.no_shards:
+        shards = {}
+        for w in (2, 4, 8):
+            per = []
+            for r in range(w):
+                c.run(r, w, device=local)  # the shard's launch plan
+                per.append(min(c.run(r, w, device=local)[1] for _ in range(3)))
+            shards[str(w)] = {"max_kernel_ms": round(max(per), 4), "mean_kernel_ms": round(sum(per) / w, 4),
+                              "max_over_world1_kernel": round(max(per) / k_ms, 3)}
+        c.run(0, 1, device=local)  # restore the whole-pass plan
     # Validation.IsValid + ValidateCommand (validation.go:68-180) of the command the controller would run
     # (multi-node first): one re-simulation on the GPU, timed after the passes (its own launch)
     final = doc["multi"]["command"] if doc["multi"]["command"]["action"] != "no-op" else doc["single"]["command"]
@@ -222,6 +235,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
         "cpu_baseline": cpu,
         "cpu_baseline_1thread": cpu1,
         "validation": validation,
+        **({"shards_on_one_gpu": shards} if shards else {}),
     }
 
 
@@ -291,6 +305,7 @@ def main():
     ap.add_argument("--only-solve", default="", help="profiling: run only this Solve line (c2, c3, c4)")
     ap.add_argument("--cons-nodes", type=int, default=5000, help="C5 cluster size (20 pods per node)")
     ap.add_argument("--cons-steps", type=int, default=20)
+    ap.add_argument("--no-shards", action="store_true", help="skip the per-shard kernel timing (world 2/4/8 on one GPU)")
     ap.add_argument("--cpu-sims", type=int, default=2400, help="oracle consolidation sample (simulations)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--c3-cpu-pods", type=int, default=2000, help="oracle C3 sample (pods)")

@@ -775,6 +775,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   // A Solve that outgrows the default plan's NodeClaim capacity runs again with the wide plan; the
   // caller pays both launches, so the reported times are their sums (the re-plan is remembered).
   float ms = 0, setup = 0, fms = 0;
+  int feasLaunches = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     HIPCHK(hipEventRecord(e0, pb->stream));
     HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp,
@@ -784,7 +785,10 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
     float a = 0, b = 0, f = 0;
     HIPCHK(hipEventElapsedTime(&a, e0, e1));
     HIPCHK(hipEventElapsedTime(&b, e0, em));
-    if (pb->dev.d.fmOn) HIPCHK(hipEventElapsedTime(&f, ef[0], ef[1]));
+    if (pb->dev.d.fmOn) {
+      HIPCHK(hipEventElapsedTime(&f, ef[0], ef[1]));
+      feasLaunches++;
+    }
     ms += a;
     setup += b;
     fms += f;
@@ -820,7 +824,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   r->kernel_ms = ms;
   r->solve_ms = ms - setup;
   r->feas_ms = fms;
-  r->feas_bytes = pb->dev.d.fmOn ? pb->fmBytes : 0;
+  r->feas_bytes = pb->dev.d.fmOn ? pb->fmBytes * feasLaunches : 0;  // bytes of every launch feas_ms sums
   *out = r;
   return KS_OK;
   API_CATCH

@@ -826,6 +826,15 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
       ksjson::quote(o, h.reqsString(rsOf(sim), before.at(sim) + r[RF_HOST]));
       o += "}";
     }
+    // the simulation's own computeConsolidation outcome: action, the replacement's options after
+    // filterByPrice and (multi-node) after filterOutSameType
+    static const char* sact[] = {"no-op", "delete", "replace", "error"};
+    o += std::string(",\"action\":\"") + sact[r[RF_ACTION]] + "\"";
+    if (r[RF_ACTION] == CA_REPLACE) {
+      o += ",\"priceOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR + d.TW));
+      if (c.sims[(size_t)sim].multi)
+        o += ",\"sameTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR + 2 * d.TW));
+    }
     return o + "}";
   };
   // commandJSON: action, candidates, replacement (multi: filterOutSameType's options)

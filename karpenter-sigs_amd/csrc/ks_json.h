@@ -6,6 +6,9 @@
 // stateNodes, clusterPods) are split at element boundaries by a skip scan and their elements parsed by
 // worker threads (ks_parallel.h), each into its own slot.
 #pragma once
+#include <mutex>
+#include <deque>
+#include <condition_variable>
 #include <algorithm>
 #include <cctype>
 #include <cstdint>
@@ -201,6 +204,13 @@ class Parser {
       // exactly sized buffer: no growth reallocations
       static thread_local std::vector<Object::Entry> stack;
       const size_t base = stack.size();
+      struct Cut {  // an exception from any nested value leaves this thread's stack at `base`
+        std::vector<Object::Entry>& s;
+        size_t b;
+        ~Cut() {
+          if (s.size() > b) s.resize(b);
+        }
+      } cut{stack, base};
       for (;;) {
         ws();
         if (p_ >= end_ || *p_ != '"') fail("expected key");
@@ -213,7 +223,6 @@ class Parser {
         ws();
         if (p_ < end_ && *p_ == ',') { ++p_; continue; }
         if (p_ < end_ && *p_ == '}') { ++p_; break; }
-        stack.resize(base);
         fail("expected ',' or '}'");
       }
       v.o->e.reserve(stack.size() - base);
@@ -315,12 +324,53 @@ class Parser {
 
 inline Value parse(const std::string& s) { return Parser(s.data(), s.size()).parse(); }
 
-// Destroy a (large) document on a detached thread: its ~millions of frees leave the caller's critical
-// path (ks_problem_create / ks_cons_create return while the snapshot DOM is still being released).
-inline void release_async(Value&& v) {
-  auto* p = new Value(std::move(v));
-  std::thread([p]() { delete p; }).detach();
+// Destroy (large) documents on one long-lived worker thread: their ~millions of frees leave the caller's
+// critical path (ks_problem_create / ks_cons_create return while the snapshot DOM is still being
+// released).  The worker drains its queue and is joined when the library is unloaded (static destructor),
+// so no free races process exit.
+class Reaper {
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Value*> q_;
+  bool stop_ = false;
+  std::thread th_;
+  void run() {
+    for (;;) {
+      Value* p;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        p = q_.front();
+        q_.pop_front();
+      }
+      delete p;
+    }
+  }
+
+ public:
+  void push(Value* p) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      if (!th_.joinable()) th_ = std::thread([this] { run(); });
+      q_.push_back(p);
+    }
+    cv_.notify_one();
+  }
+  ~Reaper() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_one();
+    if (th_.joinable()) th_.join();
+  }
+};
+inline Reaper& reaper() {
+  static Reaper r;
+  return r;
 }
+inline void release_async(Value&& v) { reaper().push(new Value(std::move(v))); }
 
 // ---- writer helpers -------------------------------------------------------------------------
 inline void quote(std::string& out, const std::string& s) {

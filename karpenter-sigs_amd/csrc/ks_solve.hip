@@ -37,6 +37,9 @@
 #ifndef KS_RUN_MIN  // shortest run of identical pods the simulation fast path places in one step
 #define KS_RUN_MIN 3
 #endif
+#ifndef KS_CLAIM_RUNS  // LEAN Solve: runs of identical pods placed on one NodeClaim in one step
+#define KS_CLAIM_RUNS 1
+#endif
 
 #include "ks_gosort.h"
 #include "ks_problem.h"
@@ -1349,6 +1352,76 @@ struct Solver {
     return srt;
   }
 
+  // --- runs of identical resource-only pods on one NodeClaim (LEAN Solve) -------------------------
+  // After a pod lands on the claim at sorted position `pos` and s.newNodeClaims stays non-decreasing, an
+  // identical next pod meets the same sort (nothing to reorder), the same rejections before `pos` (those
+  // claims and the existing nodes did not change) and lands on this claim again while it accepts -- as
+  // long as the claim's count stays <= the next position's.  The pods one claim takes that way: at most
+  // M (the run, and that count bound), and at most as many as its best remaining option still fits:
+  // max over the options of min over resources of floor((Allocatable - requests) / pod).
+  template <bool INL>
+  __device__ __forceinline__ int claim_run_cap(int c, const int64_t* pod, int M) const {
+    const ClaimView<INL>& v = cv<INL>();
+    const int t = uni(v.tpl[c]);
+    const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
+    float rq[RM];
+    int64_t rc[RM];
+#pragma unroll
+    for (int r = 0; r < RM; r++) {
+      if (RT == 0 && r >= d.R) break;
+      rq[r] = pod[r] > 0 ? 1.0f / (float)pod[r] : 0.f;
+      rc[r] = v.req[(int64_t)c * R() + r];
+    }
+    int best = 0;
+    for (int q0 = 0; q0 < nIT; q0 += kWave) {
+      const int q = q0 + lane();
+      if (q < nIT && ((v.rem[(int64_t)c * d.TW + (q >> 5)] >> (q & 31)) & 1u)) {
+        int cap = M;
+#pragma unroll
+        for (int r = 0; r < RM; r++) {
+          if (RT == 0 && r >= d.R) break;
+          const int x = run_cap(alloc_pos(tb + q, r) - rc[r], pod[r], rq[r], M);
+          cap = x < cap ? x : cap;
+        }
+        best = cap > best ? cap : best;
+      }
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+      const int o = __shfl_xor(best, off);
+      best = o > best ? o : best;
+    }
+    return uni(best);
+  }
+  // Commit of k identical pods (podk = k x pod, claim_full already applied to it) to claim c at sorted
+  // position pos: commit_claim's stores with the count advanced by k.  Returns whether s.newNodeClaims
+  // is still non-decreasing.
+  template <bool INL>
+  __device__ __forceinline__ bool commit_bulk(int c, int pos, int n, int k, const int64_t* podk, const int64_t* req,
+                                              const int* nthr, int ncnt) {
+    const ClaimView<INL>& v = cv<INL>();
+    const int okNew = uni(s_okey[pos]) + k;
+    const bool srt = pos + 1 >= n || okNew <= uni(s_okey[pos + 1]);
+    int64_t heads[RM];
+#pragma unroll
+    for (int r = 0; r < RM; r++) {
+      if (RT == 0 && r >= d.R) break;
+      heads[r] = s_phead[(int64_t)pos * R() + r];
+    }
+#pragma unroll
+    for (int r = 0; r < RM; r++) {  // wave-wide stores of uniform values (see commit_claim)
+      if (RT == 0 && r >= d.R) break;
+      v.req[(int64_t)c * R() + r] = req[r];
+      v.thr[(int64_t)c * R() + r] = nthr[r];
+      s_phead[(int64_t)pos * R() + r] = heads[r] - podk[r];
+    }
+    v.cnt[c] = ncnt;
+    s_okey[pos] = okNew;
+    if (!rem_same) copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
+    if (!INL) hbm_release();
+    wsync();
+    return srt;
+  }
+
   // --- new NodeClaim from each template in order (scheduler.go:258-283) -----------------------
   // Returns 1 placed, 0 failed (fail codes recorded), 2 no templates (add() returns nil), -1 cap.
   __device__ __forceinline__ int try_templates(int p, int s, int sflags, uint32_t toltpl, const int64_t* pod,
@@ -2155,6 +2228,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     qhead = qhead + 1 == P ? 0 : qhead + 1;
     qlen--;
     if (++pops > popCap) { err = KE_ITER_CAP; break; }
+    const int64_t abPop = S.algbytes;  // (claim runs: one pod's algorithmic bytes)
     const int s = rdl(w.s, wi);
     const int sflags = rdl(w.flags, wi);
     const uint32_t toltpl = (uint32_t)rdl((int)w.toltpl, wi);
@@ -2337,6 +2411,49 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             srt = U(inl ? S.template commit_claim<true>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog)
                          : S.template commit_claim<false>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog));
             placed = true;
+            if constexpr (LEAN && !SIM && KS_CLAIM_RUNS) {
+              // the identical pods that follow land here too (claim_run_cap): placed in one step
+              if (srt && wi < wn) {
+                bool inrun = false;
+                if (lane() >= wi && lane() < wn) {
+                  bool same = (uint32_t)w.toltpl == toltpl && w.tol0 == tol0 && w.tol1 == tol1;
+#pragma unroll
+                  for (int r = 0; r < RM; r++) {
+                    if (RT == 0 && r >= R) break;
+                    same &= w.req[r] == pod[r];
+                  }
+                  const uint32_t qx = (uint32_t)(qlen - (lane() - wi));
+                  inrun = same && !((uint32_t)(w.ll >> 32) == epoch && (uint32_t)w.ll == qx);
+                }
+                const uint64_t nr = wballot(!inrun) & (~0ull << wi);
+                const int m = (nr ? ctz64(nr) : kWave) - wi;
+                if (m > 0) {
+                  const int cj = uni(S.s_okey[jj]);
+                  const int nx = jj + 1 < nclaims ? uni(S.s_okey[jj + 1]) : 0x3fffffff;
+                  const int M = m < nx - cj + 1 ? m : nx - cj + 1;
+                  const int k = inl ? S.template claim_run_cap<true>(c, pod, M) : S.template claim_run_cap<false>(c, pod, M);
+                  if (k > 0) {
+                    int64_t podk[RM];
+#pragma unroll
+                    for (int r = 0; r < RM; r++) podk[r] = (int64_t)k * pod[r];
+                    const int64_t ab0 = S.algbytes;
+                    int kcnt = 0;
+                    if (inl) (void)S.template claim_full<true>(c, s, sflags, podk, req, nthr, kcnt);
+                    else (void)S.template claim_full<false>(c, s, sflags, podk, req, nthr, kcnt);
+                    srt = inl ? S.template commit_bulk<true>(c, jj, nclaims, k, podk, req, nthr, kcnt)
+                              : S.template commit_bulk<false>(c, jj, nclaims, k, podk, req, nthr, kcnt);
+                    S.algbytes = ab0 + (int64_t)k * (ab0 - abPop);  // each pod scanned as the first one did
+                    const int src = wi + lane() < kWave ? wi + lane() : kWave - 1;
+                    S.log_batch(k, __shfl(w.p, src), c, nlog);
+                    qhead += k;
+                    if (qhead >= P) qhead -= P;
+                    qlen -= k;
+                    pops += k;
+                    wi += k;
+                  }
+                }
+              }
+            }
           } else {
             // the quick bound was stale: tighten it to the exact max over the current options
             fullFails++;

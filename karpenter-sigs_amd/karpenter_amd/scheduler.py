@@ -13,8 +13,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # KS_LIB_VARIANT=stats loads the diagnostic build with per-phase cycle counters; =asan the ASan + UBSan
-# build of the host translation units (make -C karpenter-sigs_amd asan; scripts/asan_cpu_suite.sh).
-_VARIANTS = {"stats": "libkarpenter_amd_stats.so", "asan": "libkarpenter_amd_asan.so"}
+# build of the host translation units (make -C karpenter-sigs_amd asan; scripts/asan_cpu_suite.sh); =tsan
+# their ThreadSanitizer build (scripts/tsan_cpu_suite.sh).
+_VARIANTS = {"stats": "libkarpenter_amd_stats.so", "asan": "libkarpenter_amd_asan.so", "tsan": "libkarpenter_amd_tsan.so"}
 _VARIANT = os.environ.get("KS_LIB_VARIANT", "")
 _LIB_PATH = os.path.join(_HERE, _VARIANTS.get(_VARIANT, "libkarpenter_amd_%s.so" % _VARIANT if _VARIANT else "libkarpenter_amd.so"))
 _lib = None
@@ -95,7 +96,8 @@ def _encode(snapshot):
 def _records_buffer(records):
     """A ctypes buffer over gathered records: a run's own buffer (the memoryview run() returns) as is,
     anything else bytes-like copied once."""
-    if isinstance(records, memoryview) and isinstance(records.obj, ctypes.Array):
+    if (isinstance(records, memoryview) and isinstance(records.obj, ctypes.Array)
+            and records.nbytes == ctypes.sizeof(records.obj)):  # the whole buffer, not a slice of it
         return records.obj
     return ctypes.create_string_buffer(bytes(records), len(records))
 
@@ -245,8 +247,12 @@ class Consolidator:
 
     def run(self, rank=0, world=1, device=-1, out_ptr=None):
         """Run this rank's simulations.  out_ptr: device pointer for records_per_rank*record_bytes
-        bytes (e.g. a torch tensor's data_ptr()); None returns the records as host bytes.
-        Returns (records bytes or None, kernel ms)."""
+        bytes (e.g. a torch tensor's data_ptr()); None returns the records in host memory.
+        Returns (records or None, kernel ms).
+
+        The host records are a memoryview over one buffer per handle that every run() of the handle
+        overwrites (no copy per pass): a caller keeping one pass's records across the next run() must copy
+        them (bytes(records))."""
         l = _cons_lib()
         o = _Opts(device, 1, 1, 0, 0)
         ms = ctypes.c_double()

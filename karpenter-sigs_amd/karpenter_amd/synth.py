@@ -356,13 +356,15 @@ def config5(n_nodes=5000, pods_per_node=20, seed=4205):
 C3_ZONES = ["test-zone-1", "test-zone-2", "test-zone-3", "test-zone-4"]
 
 
-def config4(n_pods=10000, n_nodes=2000, seed=4204, n_apps=20):
+def config4(n_pods=10000, n_nodes=2000, seed=4204, n_apps=20, limits=None, ghost_frac=0.0):
     """C4 (BASELINE.json configs[3]): pending pods with zonal + hostname topology spread and pod
     anti-affinity onto existing initialized nodes.  fake.InstanceTypes(400) offered in 4 zones x
     {spot, on-demand}; `n_nodes` nodes (8-32 cpu, unique hostnames, zones round-robin) 50-80 %
     utilised by bound cluster pods that carry the same app labels, so countDomains seeds every
     group.  `n_apps` apps as label selectors: the first half zonal spread maxSkew 1, the next 30 %
-    hostname spread maxSkew 1, the rest required hostname anti-affinity."""
+    hostname spread maxSkew 1, the rest required hostname anti-affinity.
+    limits: NodePool limits (the pool is then also listed in nodePools); ghost_frac: that share of the
+    pods carries required hostname pod affinity to an app no pod runs (unsatisfiable topology)."""
     rng = np.random.default_rng(seed)
     its = []
     for i in range(400):
@@ -370,7 +372,7 @@ def config4(n_pods=10000, n_nodes=2000, seed=4204, n_apps=20):
         offers = [{"capacityType": ct, "zone": z, "price": price * (0.5 if ct == "spot" else 1.0), "available": True}
                   for z in C3_ZONES for ct in ("spot", "on-demand")]
         its.append(fake_instance_type("fake-it-%d" % i, i + 1, 2 * (i + 1), pods=10 * (i + 1), offerings=offers))
-    pool = node_pool("default")
+    pool = node_pool("default", limits=limits)
     apps = ["app-%02d" % a for a in range(n_apps)]
     n_zone, n_host = n_apps // 2, (n_apps * 3) // 10
 
@@ -425,13 +427,17 @@ def config4(n_pods=10000, n_nodes=2000, seed=4204, n_apps=20):
         a = int(rng.integers(n_apps))
         p = pod(i, cpu=CPU_CHOICES[rng.integers(5)], mem=MEM_CHOICES[rng.integers(6)], labels={"app": apps[a]})
         p["spec"].update(app_spec(a))
+        if ghost_frac and rng.random() < ghost_frac:
+            p["spec"].pop("topologySpreadConstraints", None)
+            p["spec"]["affinity"] = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": {"matchLabels": {"app": "ghost"}}, "topologyKey": HOSTNAME}]}}
         pods.append(p)
     return {
         "wellKnownLabels": FAKE_WELL_KNOWN,
         "instanceTypes": its,
         "instanceTypesByNodePool": {"default": list(range(400))},
         "nodeClaimTemplates": [pool],
-        "nodePools": [],
+        "nodePools": [pool] if limits else [],
         "stateNodes": nodes,
         "daemonSetPods": [],
         "pods": pods,

@@ -29,6 +29,9 @@ def lib():
         l.oref_consolidate_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_double)]
         l.oref_consolidate_json.restype = ctypes.c_int
+        l.oref_consolidate_json_threads.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                                    ctypes.POINTER(ctypes.c_double)]
+        l.oref_consolidate_json_threads.restype = ctypes.c_int
         l.oref_consolidate_clock_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                                   ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]
         l.oref_consolidate_clock_json.restype = ctypes.c_int
@@ -73,15 +76,20 @@ def time_solve(snapshot, reps):
     return secs.value
 
 
-def consolidate(snapshot, all_sims=False, with_stats=False):
+def consolidate(snapshot, all_sims=False, with_stats=False, threads=1):
     """Oracle multi-node then single-node consolidation over a cluster snapshot; returns (doc, seconds)
     (with_stats: (doc, seconds, stats), stats = {"algBytesRef": SURVEY §8d bytes over the simulations run}).
-    all_sims: simulate every candidate / prefix (what the GPU computes) and report each outcome."""
+    all_sims: simulate every candidate / prefix (what the GPU computes) and report each outcome.
+    threads > 1 (with all_sims): the simulations are precomputed on that many host threads."""
     l = lib()
     s = snapshot if isinstance(snapshot, str) else json.dumps(snapshot)
     out = ctypes.c_void_p()
     secs = ctypes.c_double()
-    if l.oref_consolidate_json(s.encode(), 1 if all_sims else 0, ctypes.byref(out), ctypes.byref(secs)) != 0:
+    if all_sims and threads > 1:
+        rc = l.oref_consolidate_json_threads(s.encode(), int(threads), ctypes.byref(out), ctypes.byref(secs))
+    else:
+        rc = l.oref_consolidate_json(s.encode(), 1 if all_sims else 0, ctypes.byref(out), ctypes.byref(secs))
+    if rc != 0:
         raise RuntimeError("oracle: " + l.oref_last_error().decode())
     doc = json.loads(_take(out))
     stats = doc.pop("stats", {})

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cctype>
 #include <chrono>
+#include <atomic>
 #include <thread>
 #include <cmath>
 #include <limits>
@@ -1710,6 +1711,23 @@ int oref_consolidate_json(const char* snapshot, int all_sims, char** out, double
     oref::ConsProblem cp = oref::parseConsProblem(root);
     auto t0 = std::chrono::steady_clock::now();
     std::string r = oref::consolidateJSON(cp, all_sims != 0);
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (out) *out = dupstr(r);
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// consolidate_json(all_sims=1) with the simulations precomputed on `threads` host threads (checker speed-up
+// for the full-size digests; consolidation.inc precompute).
+int oref_consolidate_json_threads(const char* snapshot, int threads, char** out, double* seconds) {
+  try {
+    ojson::Value root = ojson::parse(snapshot);
+    oref::ConsProblem cp = oref::parseConsProblem(root);
+    auto t0 = std::chrono::steady_clock::now();
+    std::string r = oref::consolidateJSON(cp, true, nullptr, threads);
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (out) *out = dupstr(r);
     return 0;

@@ -12,7 +12,18 @@ The GPU box has no reference and the oracle needs minutes at these sizes (C3 20k
   C4  10k pods onto 2k existing nodes, zonal + hostname spread and hostname anti-affinity
   C5  5k-node / 100k-pod cluster: every multi-node prefix simulation firstNConsolidationOption can
       probe (multinodeconsolidation.go:87-137) and every single-node simulation
-      (singlenodeconsolidation.go:42-88), with the chosen commands
+      (singlenodeconsolidation.go:42-88), with the chosen commands and each simulation's own
+      computeConsolidation outcome (action, filterByPrice / filterOutSameType options)
+Decision-exercising variants (the BASELINE shapes above are decision-degenerate: every C5 simulation
+deletes, C4 places every pod on an existing node):
+  C4X 10k pods onto 500 existing nodes: most pods overflow to NodeClaims under zonal / hostname spread
+      and hostname anti-affinity; 3 % carry hostname pod affinity no domain satisfies (PodErrors that
+      print the registered hostname domains and counts, topology.go:167)
+  C5R 5k nodes of 4-16 cpu, 30 pods each, half spot: single-node simulations mostly need one
+      NodeClaim (filterByPrice, the spot->spot refusal and the [spot, on-demand] narrowing,
+      consolidation.go:113-194), multi-node prefixes need 1-3 (filterOutSameType)
+  C5T the bench's consolidation_topology cluster: C5 with its pods in 20 apps (zonal / hostname spread,
+      pod affinity, anti-affinity), every bound pod in clusterPods
 
 Per config: one digest of the whole canonical Results document (json.dumps with sorted keys and no
 whitespace) and one digest per NewNodeClaim / existing node / simulation, so a mismatch names the
@@ -56,7 +67,12 @@ def cons_digest(doc):
             "multi": {"command": sha(doc["multi"]["command"]), "sims": [sha(s) for s in doc["multi"]["sims"]]},
             "single": {"command": sha(doc["single"]["command"]), "sims": [sha(s) for s in doc["single"]["sims"]]},
             "summary": {"multi": doc["multi"]["command"]["action"], "single": doc["single"]["command"]["action"],
-                        "candidates": len(doc["candidates"])}}
+                        "candidates": len(doc["candidates"]),
+                        "singleActions": _actions(doc["single"]["sims"]), "multiActions": _actions(doc["multi"]["sims"])}}
+
+
+def _actions(sims):
+    return {a: sum(1 for s in sims if s["action"] == a) for a in ("delete", "replace", "no-op", "error")}
 
 
 CONFIGS = {
@@ -65,7 +81,11 @@ CONFIGS = {
     "C3": lambda: synth.config3(20000),
     "C4": lambda: synth.config4(10000, 2000),
     "C5": lambda: synth.config5(5000),
+    "C4X": lambda: synth.config4(10000, 500, seed=4208, ghost_frac=0.03),
+    "C5R": lambda: synth.cluster_snapshot(5000, 30, 400, seed=4207, it_range=(3, 16), spot_frac=0.5),
+    "C5T": lambda: synth.cluster_snapshot(5000, 20, 400, seed=4205, topology=20),
 }
+CONS = ("C5", "C5R", "C5T")
 
 
 def main(names):
@@ -75,8 +95,8 @@ def main(names):
     for name in names:
         t = time.time()
         snap = json.dumps(CONFIGS[name]())
-        if name == "C5":
-            doc, secs, stats = bridge.consolidate(snap, all_sims=True, with_stats=True)
+        if name in CONS:  # the simulations on every host thread (bridge.consolidate threads)
+            doc, secs, stats = bridge.consolidate(snap, all_sims=True, with_stats=True, threads=os.cpu_count() or 1)
             out[name] = cons_digest(doc)
         else:
             res, secs = bridge.solve(snap)

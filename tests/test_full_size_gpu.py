@@ -7,8 +7,11 @@ container by tests/golden/make_full_size_digests.py, where the oracle needs minu
   C3  20k pods, 800 instance types x 8 offerings, selectors / affinity / taints
   C4  10k pods onto 2k existing nodes, zonal + hostname spread, anti-affinity
   C5  consolidation over the 5k-node / 100k-pod cluster: every multi-node prefix and single-node
-      simulation with its outcome, and both commands (multinodeconsolidation.go:87-137,
-      singlenodeconsolidation.go:42-88)
+      simulation with its outcome and its own computeConsolidation command, and both commands
+      (multinodeconsolidation.go:87-137, singlenodeconsolidation.go:42-88)
+Decision-exercising variants (make_full_size_digests.py): C4X (NodeClaims under topology and
+unsatisfiable hostname affinity PodErrors), C5R (Replace / NoOp: filterByPrice, spot rules,
+filterOutSameType on a 5k-node cluster), C5T (the bench's consolidation-with-topology cluster).
 
 A digest mismatch names the first differing NewNodeClaim / simulation."""
 import hashlib
@@ -68,10 +71,20 @@ def test_c4_10k_pods_onto_2k_nodes_topology():
     _check_solve("C4")
 
 
-def test_c5_every_consolidation_simulation():
+def test_c4x_overflow_to_nodeclaims_and_hostname_errors():
+    want = DIGESTS["C4X"]["counts"]
+    assert want["newNodeClaims"] > 0 and want["podErrors"] > 0
+    _check_solve("C4X")
+
+
+@pytest.mark.parametrize("name", ["C5", "C5R", "C5T"])
+def test_c5_every_consolidation_simulation(name):
     m = _mfd()
-    want = DIGESTS["C5"]
-    doc = Consolidator(_snapshot("C5")).consolidate(all_sims=True)
+    want = DIGESTS[name]
+    if name == "C5R":  # the decisions this variant exists for
+        acts = want["summary"]["singleActions"]
+        assert acts["replace"] > 0 and acts["no-op"] > 0 and acts["delete"] > 0
+    doc = Consolidator(_snapshot(name)).consolidate(all_sims=True)
     doc.pop("kernel_ms")
     got = m.cons_digest(doc)
     assert got["summary"] == want["summary"], (got["summary"], want["summary"])
