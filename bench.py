@@ -375,6 +375,14 @@ def main():
         algb.append(r.algorithmic_bytes)
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    # the same Solves with the Results copied back and read through the structured accessors (what the
+    # drop-in caller does: ks_solve + ks_results_* in INTEGRATION.md's cgo shim, no JSON)
+    barrier_sync()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        sch.solve_structured(device=local)
+    barrier_sync()
+    structured_ms = (time.perf_counter() - t1) * 1000.0 / args.steps
     if dist is not None:
         import torch
 
@@ -448,6 +456,9 @@ def main():
         # snapshot; e2e = create + one Solve with its results copied back and rendered
         "create_ms": round(create_ms, 3),
         "full_solve_ms": round(full_ms, 3),
+        # a Solve with its Results read through the structured accessors, per step, and that rate
+        "structured_solve_ms": round(structured_ms, 3),
+        "structured_pods_per_s": round(args.pods * world / (structured_ms / 1000.0), 1),
         "e2e_pods_per_s": round(args.pods / ((create_ms + full_ms) / 1000.0), 1),
         "roofline": _roofline("k_solve", k_ms, bytes_per_launch, ref, "c2", extra={
             "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3),

@@ -168,6 +168,9 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
 int ks_cons_validate(ks_cons* c, const char* command_json, size_t len, const ks_solve_opts* opts, char** json_out);
 /* Diagnostics: the 24 solve counters of simulation `sim` in the last ks_cons_run of this handle. */
 int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out24);
+/* The same for up to n counters (26 in this build: + runs of identical pods, pods they placed); returns the
+ * number copied or a negative error. */
+int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n);
 /* Algorithmic bytes the gathered simulations scanned, summed from their records. */
 double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world);
 

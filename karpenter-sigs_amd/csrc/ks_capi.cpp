@@ -396,10 +396,15 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
   dl(logp, W.log_pod, nl, st);
   dl(logt, W.log_tgt, nl, st);
   dl(status, W.pod_status, d.P, st);
-  dl(fstate, W.pod_fstate, d.P, st);
-  dl(fcode, W.fail_code, (size_t)d.P * std::max(d.NTPL, 1), st);
-  dl(fhost, W.fail_host, (size_t)d.P * std::max(d.NTPL, 1), st);
   HIPCHK(hipStreamSynchronize(st));
+  bool anyFailed = false;  // (the failure tables are read only for pods whose last attempt failed)
+  for (int p = 0; p < d.P && !anyFailed; p++) anyFailed = status[(size_t)p] == ST_FAILED;
+  if (anyFailed) {
+    dl(fstate, W.pod_fstate, d.P, st);
+    dl(fcode, W.fail_code, (size_t)d.P * std::max(d.NTPL, 1), st);
+    dl(fhost, W.fail_host, (size_t)d.P * std::max(d.NTPL, 1), st);
+    HIPCHK(hipStreamSynchronize(st));
+  }
   std::vector<uint32_t> frs;  // topology failure snapshots, only when some pod failed on one
   std::vector<uint64_t> loghg;
   std::vector<int32_t> tgact;
@@ -437,18 +442,36 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     const Host::Tpl& tp = h.tpls[cl.tpl];
     for (int pos = 0; pos < (int)tp.its.size(); pos++)
       if ((crem[(size_t)c * d.TW + (pos >> 5)] >> (pos & 31)) & 1u) cl.its.push_back(tp.its[pos]);
-    // requests = Merge(daemon, RequestsForPods(pod_1), ...) replayed in commit order
-    QList req = tp.daemon;
-    for (int p : cl.pods)
-      for (auto& kv : h.pods[p].requests) req[kv.first].add(kv.second);
-    for (auto& kv : req) {
-      int r = h.resId.at(kv.first);
-      if (h.toDev(r, kv.second) != creq[(size_t)c * d.R + r])
-        throw KsError(KS_ERR_INTERNAL, "device requests diverge from the replayed Merge for " + kv.first + " (claim " +
-                                           std::to_string(c) + " at position " + std::to_string(k) + " of " +
+    // requests = Merge(daemon, RequestsForPods(pod_1), ...) replayed in commit order (resources.go:53-63),
+    // in the exact device units: Quantity.Add adopts the addend's format while the sum is zero
+    int64_t sum[kMaxR];
+    uint8_t fmt[kMaxR];
+    uint32_t present = h.tab.tpl_rmask[(size_t)cl.tpl];
+    for (int r = 0; r < d.R; r++) {
+      sum[r] = h.tab.tpl_daemon[(size_t)cl.tpl * d.R + r];
+      fmt[r] = h.tab.tpl_rfmt[(size_t)cl.tpl * d.R + r];
+    }
+    for (int p : cl.pods) {
+      const uint32_t m = h.tab.pod_rmask[(size_t)p];
+      present |= m;
+      for (uint32_t b = m; b; b &= b - 1) {
+        const int r = __builtin_ctz(b);
+        if (sum[r] == 0) fmt[r] = h.tab.pod_rfmt[(size_t)p * d.R + r];
+        sum[r] += h.tab.pod_req[(size_t)p * d.R + r];
+      }
+    }
+    QList req;
+    for (int r = 0; r < d.R; r++) {
+      if (!((present >> r) & 1u)) continue;
+      if (sum[r] != creq[(size_t)c * d.R + r])
+        throw KsError(KS_ERR_INTERNAL, "device requests diverge from the replayed Merge for " + h.resNames[(size_t)r] +
+                                           " (claim " + std::to_string(c) + " at position " + std::to_string(k) + " of " +
                                            std::to_string(nc) + ": device " + std::to_string(creq[(size_t)c * d.R + r]) +
-                                           ", replay " + std::to_string(h.toDev(r, kv.second)) + " over " +
+                                           ", replay " + std::to_string(sum[r]) + " over " +
                                            std::to_string(cl.pods.size()) + " pods)");
+      Qty q = h.fromDev(r, sum[r]);
+      q.f = (QFmt)fmt[r];
+      req.emplace_hint(req.end(), h.resNames[(size_t)r], q);  // resource ids are in name order
     }
     const uint32_t* rec = &crs[(size_t)c * d.RSW];
     std::string j = "{\"nodePoolName\":";
@@ -854,8 +877,9 @@ int ks_results_json(const ks_results* r, char** json_out) {
   static const char* names[] = {"nclaims", "ncommits", "hostnameCounter", "error", "pops", "algBytes",
                                 "sorts", "sortsWithDescent", "claimFull", "claimQuickFail", "windows",
                                 "cycPop", "cycNodes", "cycSort", "cycQuick", "cycFull", "cycCommit", "cycTemplates",
-                                "cycTotal", "cycNodeCommit", "cycFullRs", "cycFullThr", "cycFullMasks", "cycFullApply"};
-  for (int i = 0; i < 24; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
+                                "cycTotal", "cycNodeCommit", "cycFullRs", "cycFullThr", "cycFullMasks", "cycFullApply",
+                                "runs", "runPods"};
+  for (int i = 0; i < CT_NCOUNTERS; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
   o += "}}";
   *json_out = strdup(o.c_str());
   return KS_OK;

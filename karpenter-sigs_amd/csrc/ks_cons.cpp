@@ -1232,13 +1232,16 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
 
 // Diagnostics: the solve counters (ks_problem.h Counter) of the last run's simulation `sim` (this
 // rank's launch; with the KS_PHASE_STATS build they include per-phase cycles).
-int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out) {
+int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out) { return ks_cons_sim_counters_n(c, sim, out, CT_ABI) < 0 ? -1 : 0; }
+
+int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n) {
   API_TRY
-  if (!c || !out) throw KsError(KS_ERR_ARG, "bad argument");
+  if (!c || !out || n < 0) throw KsError(KS_ERR_ARG, "bad argument");
+  n = std::min(n, (int)CT_NCOUNTERS);
   for (size_t k = 0; k < c->L.lsims.size(); k++)
     if (c->L.lsims[k] == sim) {
-      HIPCHK(hipMemcpy(out, c->L.lhost[k].counters, 8 * CT_NCOUNTERS, hipMemcpyDeviceToHost));
-      return KS_OK;
+      HIPCHK(hipMemcpy(out, c->L.lhost[k].counters, 8 * (size_t)n, hipMemcpyDeviceToHost));
+      return n;
     }
   throw KsError(KS_ERR_ARG, "simulation not in this rank's launch");
   API_CATCH

@@ -756,6 +756,14 @@ void Host::build(const Value& root) {
     for (int r = 0; r < R; r++) out[r] = 0;
     for (auto& kv : q) out[resId.at(kv.first)] = toDev(resId.at(kv.first), kv.second);
   };
+  auto qmeta = [&](const QList& q, uint32_t& mask, uint8_t* fmt) {  // names present + formats
+    mask = 0;
+    for (auto& kv : q) {
+      const int r = resId.at(kv.first);
+      mask |= 1u << r;
+      fmt[r] = (uint8_t)kv.second.f;
+    }
+  };
 
   // --- taints universe
   auto internTaint = [&](const TaintH& t) {
@@ -803,6 +811,8 @@ void Host::build(const Value& root) {
   tab.tpl_rs.assign((size_t)std::max(NT, 1) * dims.RSW, 0);
   tab.tpl_taint.assign((size_t)std::max(NT, 1) * 2, 0);
   tab.tpl_daemon.assign((size_t)std::max(NT, 1) * R, 0);
+  tab.tpl_rmask.assign((size_t)std::max(NT, 1), 0);
+  tab.tpl_rfmt.assign((size_t)std::max(NT, 1) * R, 0);
   tab.tpl_it_beg.assign(NT + 1, 0);
   tab.tpl_pool.assign(std::max(NT, 1), -1);
   int maxIts = 0;
@@ -843,6 +853,7 @@ void Host::build(const Value& root) {
     tp.daemon = overhead;
     if (!resId.count("pods")) throw KsError(-5, "pods resource missing");
     vec(overhead, &tab.tpl_daemon[(size_t)t * R]);
+    qmeta(overhead, tab.tpl_rmask[(size_t)t], &tab.tpl_rfmt[(size_t)t * R]);
     for (int i : tp.its) tab.tpl_its.push_back(i);
     tab.tpl_it_beg[t + 1] = (int)tab.tpl_its.size();
     maxIts = std::max(maxIts, (int)tp.its.size());
@@ -1126,6 +1137,8 @@ void Host::build(const Value& root) {
   int P = (int)pods.size();
   dims.P = P;
   tab.pod_req.assign((size_t)std::max(P, 1) * R, 0);
+  tab.pod_rmask.assign((size_t)std::max(P, 1), 0);
+  tab.pod_rfmt.assign((size_t)std::max(P, 1) * R, 0);
   tab.pod_sortkey.assign((size_t)std::max(P, 1) * 4, 0);
   tab.pod_state0.assign(std::max(P, 1), 0);
   tab.pod_nstate.assign(std::max(P, 1), 0);
@@ -1162,6 +1175,7 @@ void Host::build(const Value& root) {
   parallel_for(P, 128, [&](int i) {
     PodH& p = pods[i];
     vec(p.requests, &tab.pod_req[(size_t)i * R]);
+    qmeta(p.requests, tab.pod_rmask[(size_t)i], &tab.pod_rfmt[(size_t)i * R]);
     int64_t cpu = cpuR >= 0 ? tab.pod_req[(size_t)i * R + cpuR] : 0;
     int64_t mem = memR >= 0 ? tab.pod_req[(size_t)i * R + memR] : 0;
     int64_t* k4 = &tab.pod_sortkey[(size_t)i * 4];

@@ -198,6 +198,10 @@ struct Host {
     std::vector<uint64_t> tpl_taint, st_tol, n_taint;
     std::vector<int32_t> tsort_pos, it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,
         st_flags;
+    // the Quantity side of each request list (results replay of Merge, resources.go:53-63, in integers):
+    // which resources the list names and each entry's format ([P][R] / [NTPL][R])
+    std::vector<uint32_t> pod_rmask, tpl_rmask;
+    std::vector<uint8_t> pod_rfmt, tpl_rfmt;
     // feasibility tables (k_solve feas_masks)
     std::vector<uint32_t> fk_words;
     std::vector<int32_t> fk_key_off;  // [NTPL][NK] block of key k in template t, -1: no table

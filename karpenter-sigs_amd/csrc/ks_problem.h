@@ -255,7 +255,10 @@ enum Counter {
   CT_CYC_POP, CT_CYC_NODES, CT_CYC_SORT, CT_CYC_QUICK, CT_CYC_FULL, CT_CYC_COMMIT, CT_CYC_TPL, CT_CYC_TOTAL,
   CT_CYC_NCOMMIT,  // existing-node commit (inside CT_CYC_NODES)
   CT_CYC_SUB,      // [4] claim_full sub-phases (inside CT_CYC_FULL): requirements, thresholds, masks, apply
-  CT_NCOUNTERS = 24
+  CT_ABI = 24,     // counters ks_cons_sim_counters hands out (include/karpenter_amd.h)
+  CT_RUNS = 24,    // runs of identical pods placed in one step (simulation fast path; Solve NodeClaim runs)
+  CT_RUN_PODS,     // pods those runs placed
+  CT_NCOUNTERS = 26
 };
 enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3 };
 

@@ -2057,7 +2057,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   uint32_t epoch = 1;
   int qhead = 0, qlen = P;
   int wn = 0, wi = 0;  // window size / next index
-  int64_t pops = 0, sorts = 0, slow = 0, windows = 0, fulls = 0, fullFails = 0;
+  int64_t pops = 0, sorts = 0, slow = 0, windows = 0, fulls = 0, fullFails = 0, runs = 0, runPods = 0;
   // Every pop either places a pod, relaxes it, or marks it stale; the reference's queue can cycle
   // O(P^2) in adversarial inputs, far beyond any realistic batch.  Bound it so a logic error ends the
   // kernel with KE_ITER_CAP instead of hanging the device.
@@ -2173,6 +2173,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
               qlen -= placed;
               pops += placed;
               wi += placed;
+              runs++;
+              runPods += placed;
               if (placed < m) break;  // the next pod of the run fits no window node
               continue;
             }
@@ -2450,6 +2452,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                     qlen -= k;
                     pops += k;
                     wi += k;
+                    runs++;
+                    runPods += k;
                   }
                 }
               }
@@ -2526,6 +2530,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     W.counters[CT_CLAIM_FULL] = fulls;
     W.counters[CT_CLAIM_QUICK_FAIL] = fullFails;
     W.counters[CT_WINDOWS] = windows;
+    W.counters[CT_RUNS] = runs;
+    W.counters[CT_RUN_PODS] = runPods;
 #ifdef KS_PHASE_STATS
     for (int i = 0; i < 7; i++) W.counters[CT_CYC_POP + i] = (int64_t)cyc[i];
     W.counters[CT_CYC_TOTAL] = (int64_t)(__builtin_amdgcn_s_memtime() - tstart);

@@ -141,6 +141,84 @@ class Results:
         return d
 
 
+class _Requirement(ctypes.Structure):  # ks_requirement
+    _fields_ = [("key", ctypes.c_char_p), ("op", ctypes.c_char_p), ("n_values", ctypes.c_int),
+                ("values", ctypes.POINTER(ctypes.c_char_p)), ("has_gt", ctypes.c_int), ("has_lt", ctypes.c_int),
+                ("gt", ctypes.c_int64), ("lt", ctypes.c_int64)]
+
+
+_accessors_bound = False
+
+
+def _bind_accessors(l):
+    global _accessors_bound
+    if _accessors_bound:
+        return
+    vp, ip = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)
+    i32pp = ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))
+    strpp = ctypes.POINTER(ctypes.POINTER(ctypes.c_char_p))
+    l.ks_results_num_new_nodeclaims.argtypes = [vp]
+    l.ks_results_nodeclaim.argtypes = [vp, ctypes.c_int, ip, i32pp, ip, i32pp, ip]
+    l.ks_results_nodeclaim_requests.argtypes = [vp, ctypes.c_int, ip, strpp, strpp]
+    l.ks_results_nodeclaim_requirements.argtypes = [vp, ctypes.c_int, ip, ctypes.POINTER(ctypes.POINTER(_Requirement))]
+    l.ks_results_num_existing_nodes.argtypes = [vp]
+    l.ks_results_existing_node.argtypes = [vp, ctypes.c_int, ip, i32pp, ip]
+    l.ks_results_num_pod_errors.argtypes = [vp]
+    l.ks_results_pod_error.argtypes = [vp, ctypes.c_int, ip, ctypes.POINTER(ctypes.c_char_p)]
+    _accessors_bound = True
+
+
+class StructuredResults:
+    """Results read through the C-ABI's structured accessors (what the cgo shim in INTEGRATION.md does):
+    new_nodeclaims = [{template, pods, instance_types (indices), requests {name: quantity},
+    requirements [(key, op, values, gt, lt)]}], existing_nodes = [(state node index, pods)],
+    pod_errors = {pod index: message}."""
+
+    def __init__(self, claims, nodes, errors, kernel_ms, solve_kernel_ms):
+        self.new_nodeclaims = claims
+        self.existing_nodes = nodes
+        self.pod_errors = errors
+        self.kernel_ms = kernel_ms
+        self.solve_kernel_ms = solve_kernel_ms
+
+
+def _read_structured(l, r):
+    import numpy as np
+
+    _bind_accessors(l)
+    tpl, n1, n2 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    a1, a2 = ctypes.POINTER(ctypes.c_int32)(), ctypes.POINTER(ctypes.c_int32)()
+    claims = []
+    for i in range(l.ks_results_num_new_nodeclaims(r)):
+        _check(l.ks_results_nodeclaim(r, i, ctypes.byref(tpl), ctypes.byref(a1), ctypes.byref(n1), ctypes.byref(a2),
+                                      ctypes.byref(n2)))
+        pods = np.ctypeslib.as_array(a1, (n1.value,)).copy() if n1.value else np.zeros(0, np.int32)
+        its = np.ctypeslib.as_array(a2, (n2.value,)).copy() if n2.value else np.zeros(0, np.int32)
+        names, qtys = ctypes.POINTER(ctypes.c_char_p)(), ctypes.POINTER(ctypes.c_char_p)()
+        _check(l.ks_results_nodeclaim_requests(r, i, ctypes.byref(n1), ctypes.byref(names), ctypes.byref(qtys)))
+        requests = {names[k].decode(): qtys[k].decode() for k in range(n1.value)}
+        rq = ctypes.POINTER(_Requirement)()
+        _check(l.ks_results_nodeclaim_requirements(r, i, ctypes.byref(n1), ctypes.byref(rq)))
+        reqs = []
+        for k in range(n1.value):
+            x = rq[k]
+            reqs.append((x.key.decode(), x.op.decode(), [x.values[v].decode() for v in range(x.n_values)],
+                         x.gt if x.has_gt else None, x.lt if x.has_lt else None))
+        claims.append({"template": tpl.value, "pods": pods, "instance_types": its, "requests": requests,
+                       "requirements": reqs})
+    nodes = []
+    for i in range(l.ks_results_num_existing_nodes(r)):
+        _check(l.ks_results_existing_node(r, i, ctypes.byref(n2), ctypes.byref(a1), ctypes.byref(n1)))
+        pods = np.ctypeslib.as_array(a1, (n1.value,)).copy() if n1.value else np.zeros(0, np.int32)
+        nodes.append((n2.value, pods))
+    errors = {}
+    msg = ctypes.c_char_p()
+    for i in range(l.ks_results_num_pod_errors(r)):
+        _check(l.ks_results_pod_error(r, i, ctypes.byref(n1), ctypes.byref(msg)))
+        errors[n1.value] = msg.value.decode()
+    return claims, nodes, errors
+
+
 class Scheduler:
     """NewScheduler(...) on the GPU: the snapshot is encoded once and stays resident in HBM."""
 
@@ -173,6 +251,19 @@ class Scheduler:
         finally:
             lib().ks_results_free(r)
 
+    def solve_structured(self, device=-1, simulation_mode=True):
+        """Solve(ctx, pods) with the Results read through the structured accessors (no JSON): the drop-in
+        caller's full return path (INTEGRATION.md's cgo shim)."""
+        l = lib()
+        o = _Opts(device, 1 if simulation_mode else 0, 1, 0, 0)
+        r = ctypes.c_void_p()
+        _check(l.ks_solve(self._h, ctypes.byref(o), ctypes.byref(r)))
+        try:
+            claims, nodes, errors = _read_structured(l, r)
+            return StructuredResults(claims, nodes, errors, l.ks_results_kernel_ms(r), l.ks_results_solve_kernel_ms(r))
+        finally:
+            l.ks_results_free(r)
+
     def close(self):
         if self._h:
             lib().ks_problem_free(self._h)
@@ -204,6 +295,7 @@ def _cons_lib():
         l.ks_cons_claim_requirements.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
         l.ks_cons_validate.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_Opts), ctypes.POINTER(vp)]
         l.ks_cons_sim_counters.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+        l.ks_cons_sim_counters_n.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
         l.ks_cons_records_alg_bytes.argtypes = [vp, vp, ctypes.c_int]
         l.ks_cons_records_alg_bytes.restype = ctypes.c_double
         l._cons_ready = True
@@ -323,9 +415,11 @@ class Consolidator:
 
     def sim_counters(self, sim):
         """Solve counters of simulation `sim` from the last run (ks_problem.h Counter order)."""
-        out = (ctypes.c_int64 * 24)()
-        _check(_cons_lib().ks_cons_sim_counters(self._h, sim, out))
-        return list(out)
+        out = (ctypes.c_int64 * 26)()
+        n = _cons_lib().ks_cons_sim_counters_n(self._h, sim, out, 26)
+        if n < 0:
+            _check(n)
+        return list(out)[:n]
 
     def alg_bytes(self, records, world=1):
         buf = _records_buffer(records)
