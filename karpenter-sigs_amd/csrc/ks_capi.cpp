@@ -203,6 +203,14 @@ void ks_upload(ks_problem* pb) {
   size_t o_st = put(t.st_tol.data(), t.st_tol.size() * 8);
   size_t o_sf = put(t.st_flags.data(), t.st_flags.size() * 4);
   size_t o_stt = put(t.st_toltpl.data(), t.st_toltpl.size() * 4);
+  std::vector<uint64_t> ps0((size_t)std::max(h.dims.P, 1) * 3, 0);
+  for (int p = 0; p < h.dims.P; p++) {
+    const int s0 = t.pod_state0[(size_t)p];
+    ps0[(size_t)p * 3] = t.st_tol[(size_t)s0 * 2];
+    ps0[(size_t)p * 3 + 1] = t.st_tol[(size_t)s0 * 2 + 1];
+    ps0[(size_t)p * 3 + 2] = ((uint64_t)t.st_toltpl[(size_t)s0] << 32) | (uint32_t)t.st_flags[(size_t)s0];
+  }
+  size_t o_ps0i = put(ps0.data(), ps0.size() * 8);
   size_t o_na = put(t.n_avail.data(), t.n_avail.size() * 8);
   size_t o_nr = put(t.n_req0.data(), t.n_req0.size() * 8);
   size_t o_nrs = put(t.n_rs0.data(), t.n_rs0.size() * 4);
@@ -295,6 +303,7 @@ void ks_upload(ks_problem* pb) {
   D.pool_mask = (const uint32_t*)(b + o_pm);
   D.pod_req = (const int64_t*)(b + o_preq);
   D.pod_state0 = (const int32_t*)(b + o_ps0);
+  D.pod_s0 = (const uint64_t*)(b + o_ps0i);
   D.pod_nstate = (const int32_t*)(b + o_pns);
   D.pod_uid = (const int32_t*)(b + o_pu);
   D.pod_sortkey = (const int64_t*)(b + o_psk);

@@ -218,6 +218,7 @@ struct ks_cons {
     void* ltemp = nullptr;
     size_t ltempBytes = 0;
     int lnent = 0, lrbits = 0, lsbits = 0;
+    bool lsorted = false;  // lpodmap holds every simulation's NewQueue order (a plan's pods never change)
     Plan lplan{};
     std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
     void release() {
@@ -956,8 +957,13 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
     HIPCHK(hipEventCreate(&c.ev[1]));
   }
   HIPCHK(hipEventRecord(c.ev[0], pb.stream));
-  HIPCHK(sim_queue_sort(c.rank, c.L.lentries, c.L.lentrySim, c.L.lnent, c.L.lrbits, c.L.lsbits, c.L.lkeys, c.L.lvals, c.L.ltemp,
-                        c.L.ltempBytes, c.L.lpodmap, pb.stream));
+  // NewQueue per simulation (queue.go:37-44): the plan's pod lists and the global rank are fixed for the
+  // handle, and the kernel only reads pod_map, so one sort per plan serves every pass
+  if (!c.L.lsorted) {
+    HIPCHK(sim_queue_sort(c.rank, c.L.lentries, c.L.lentrySim, c.L.lnent, c.L.lrbits, c.L.lsbits, c.L.lkeys, c.L.lvals,
+                          c.L.ltemp, c.L.ltempBytes, c.L.lpodmap, pb.stream));
+    c.L.lsorted = true;
+  }
   HIPCHK(launch_sims(pb.dev, c.L.lworks, ns, c.L.lplan, pb.stream));
   HIPCHK(hipEventRecord(c.ev[1], pb.stream));
   // the records follow on the same stream; one synchronisation covers both

@@ -120,6 +120,8 @@ struct KsDev {
   const int32_t KS_G* pod_nstate;  // [P]
   const int32_t KS_G* pod_uid;     // [P] interned UID (queue staleness key, queue.go:54-69)
   const int64_t KS_G* pod_sortkey; // [P][4] cpu, memory, creation second, uid rank (queue.go:83-112)
+  const uint64_t KS_G* pod_s0;     // [P][3] the pod's first relaxation state: st_tol[0..1], st_toltpl << 32 | st_flags
+                                   // (queue window refills before any Queue.Push read these, one level fewer)
   // relaxation states (preferences.go:38-147 applied 0..n times)
   const uint32_t KS_G* st_rs;      // [S][RSW] NewPodRequirements
   const uint64_t KS_G* st_tol;     // [S][2] tolerated-taint masks

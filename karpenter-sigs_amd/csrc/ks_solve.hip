@@ -127,10 +127,12 @@ __device__ __forceinline__ int run_cap(int64_t free, int64_t req, float rq, int 
 #define PH_BEGIN(v) uint64_t v = __builtin_amdgcn_s_memtime()
 #define PH_END(v, slot) cyc[slot] += __builtin_amdgcn_s_memtime() - v
 #define PHS_END(v, slot) scyc[slot] += __builtin_amdgcn_s_memtime() - v  // sub-phases (Solver member)
+#define SPHS_END(o, v, slot) o.scyc[slot] += __builtin_amdgcn_s_memtime() - v  // (from k_solve)
 #else
 #define PH_BEGIN(v)
 #define PH_END(v, slot)
 #define PHS_END(v, slot)
+#define SPHS_END(o, v, slot)
 #endif
 
 // ------------------------------------------------------------------------------------------------
@@ -1837,23 +1839,39 @@ struct Solver {
   }
 
   // --- 64-pod queue window: one gather per 64 pops, one entry per lane ------------------------
-  __device__ __forceinline__ void refill(Window<RT>& w, int qhead, int qlen, int P, bool pushed) {
+  // ident: no pod was pushed back yet in this Solve, so every pod is in its first relaxation state, its
+  // staleness word is 0, a simulation's pending status is untouched and its queue is still the identity:
+  // the window reads the pods' first-state copies (pod_s0) instead of going through W.pod_state and the
+  // state tables (one dependent memory level fewer per refill).
+  __device__ __forceinline__ void refill(Window<RT>& w, int qhead, int qlen, int P, bool pushed, bool ident) {
     if (pushed) hbm_release();  // queue pushes / relaxation states / staleness words have landed
     const int n = qlen < kWave ? qlen : kWave;
     if (lane() < n) {
       int pos = qhead + lane();
       if (pos >= P) pos -= P;
-      w.p = ld_sc1(W.queue + pos);
+      w.p = SIM && ident ? pos : ld_sc1(W.queue + pos);
       w.g = SIM ? W.pod_map[w.p] : w.p;
       w.uid = SIM ? w.p : D.pod_uid[w.p];  // simulations reject duplicate UIDs: local index == UID
-      w.s = ld_sc1(W.pod_state + w.p);
-      w.ll = ld_sc1(W.last_len + w.uid);
-      w.flags = D.st_flags[w.s];
+      if (ident) {
+        w.s = D.pod_state0[w.g];
+        w.ll = 0;
+        const uint64_t KS_G* s0 = D.pod_s0 + 3 * (int64_t)w.g;
+        w.tol0 = s0[0];
+        w.tol1 = s0[1];
+        const uint64_t tf = s0[2];
+        w.toltpl = (int)(uint32_t)(tf >> 32);
+        w.flags = (int)(uint32_t)tf;
+        w.st = ST_PENDING;
+      } else {
+        w.s = ld_sc1(W.pod_state + w.p);
+        w.ll = ld_sc1(W.last_len + w.uid);
+        w.flags = D.st_flags[w.s];
+        w.st = SIM ? ld_sc1(W.pod_status + w.p) : 0;
+        w.toltpl = D.st_toltpl[w.s];
+        w.tol0 = D.st_tol[2 * w.s];
+        w.tol1 = D.st_tol[2 * w.s + 1];
+      }
       w.pf = SIM ? D.pod_flags[w.g] : 0;
-      w.st = SIM ? ld_sc1(W.pod_status + w.p) : 0;
-      w.toltpl = D.st_toltpl[w.s];
-      w.tol0 = D.st_tol[2 * w.s];
-      w.tol1 = D.st_tol[2 * w.s + 1];
       w.hpc = D.pod_hpc[w.g];
       w.hpu = D.pod_hpu[w.g];
       w.hpo = D.pod_hpo[w.g];
@@ -2054,6 +2072,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   int nrs = 0;           // SIM: compact node-requirement slots in use
   bool srt = true;      // s.newNodeClaims non-decreasing in len(Pods)
   bool pushed = false;  // a failed pod was pushed back since the last window refill
+  bool ident = true;    // no pod was pushed back yet (refill reads the pods' first states directly)
   uint32_t epoch = 1;
   int qhead = 0, qlen = P;
   int wn = 0, wi = 0;  // window size / next index
@@ -2080,7 +2099,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (qlen <= 0) break;
     PH_BEGIN(t0);
     if (wi == wn) {
-      S.refill(w, qhead, qlen, P, pushed);
+      PH_BEGIN(tr);
+      S.refill(w, qhead, qlen, P, pushed, ident);
+      if (FREEW) SPHS_END(S, tr, 0);  // simulation fast path (stats build): window refills
       pushed = false;
       wn = qlen < kWave ? qlen : kWave;
       wi = 0;
@@ -2115,6 +2136,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             const uint64_t nr = wballot(!inrun) & (~0ull << wi);
             const int m = (nr ? ctz64(nr) : kWave) - wi;
             if (m >= KS_RUN_MIN) {
+              PH_BEGIN(tb);
               float rq[RM];
 #pragma unroll
               for (int r = 0; r < RM; r++) rq[r] = fp[r] > 0 ? 1.0f / (float)fp[r] : 0.f;
@@ -2175,6 +2197,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
               wi += placed;
               runs++;
               runPods += placed;
+              SPHS_END(S, tb, 1);  // (stats build): runs placed in one step
               if (placed < m) break;  // the next pod of the run fits no window node
               continue;
             }
@@ -2510,6 +2533,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (lane() == 0) W.queue[tail] = p;
     qlen++;
     pushed = true;
+    ident = false;
     if (!relaxed && lane() == 0) W.last_len[uid] = ((uint64_t)epoch << 32) | (uint32_t)qlen;
   }
   S.log_flush(nlog);

@@ -38,8 +38,9 @@ print("sum of all simulations' cycles / max = %.1f (the pass cannot be shorter t
       % (sum(tot) / mx))
 for cyc, s, d in rows[:12]:
     pops = max(d["pops"], 1)
-    print("sim %5d: cyc %9d (%.2f of max) pops %5d runs %4d (%5d pods) windows %3d | pop %.0f nodes %.0f (commit %.0f) claims %.0f tpl %.0f per pod" % (
-        s, cyc, cyc / mx, d["pops"], d.get("runs", 0), d.get("runPods", 0), d["windows"], d["cycPop"] / pops,
+    print("sim %5d: cyc %9d (%.2f of max) pops %5d runs %4d (%5d pods, %.0f cyc) windows %3d (%.0f cyc) | pop %.0f nodes %.0f (commit %.0f) claims %.0f tpl %.0f per pod" % (
+        s, cyc, cyc / mx, d["pops"], d.get("runs", 0), d.get("runPods", 0), d["cycFullThr"], d["windows"], d["cycFullRs"],
+        d["cycPop"] / pops,
         d["cycNodes"] / pops, d["cycNodeCommit"] / pops,
         (d["cycQuick"] + d["cycFull"] + d["cycCommit"] + d["cycSort"]) / pops, d["cycTpl"] / pops))
 # the multi-node prefix simulations are the first 100 (largest first)
