@@ -102,6 +102,11 @@ double ks_results_solve_kernel_ms(const ks_results* r);
  * algorithmic bytes; 0 when the problem has no pod label requirements (the kernel is not launched). */
 double ks_results_feasibility_ms(const ks_results* r);
 double ks_results_feasibility_bytes(const ks_results* r);
+/* k_feasibility_nodes (the static pod-state x existing-node rows: taints + strict Compatible,
+ * existingnode.go:64-124) inside this Solve: HIP-event time and algorithmic bytes; 0 when not launched
+ * (no pod label requirements or no existing nodes). */
+double ks_results_node_feasibility_ms(const ks_results* r);
+double ks_results_node_feasibility_bytes(const ks_results* r);
 /* Algorithmic bytes the solve scanned (SURVEY.md §8d formula, counted by the kernel). */
 double ks_results_algorithmic_bytes(const ks_results* r);
 

@@ -159,7 +159,7 @@ struct ks_results {
   std::vector<Claim> claims;
   std::vector<ENode> nodes;
   std::vector<std::pair<int32_t, std::string>> errors;
-  double kernel_ms = 0, solve_ms = 0, algbytes = 0, feas_ms = 0, feas_bytes = 0;
+  double kernel_ms = 0, solve_ms = 0, algbytes = 0, feas_ms = 0, feas_bytes = 0, feasn_ms = 0, feasn_bytes = 0;
   std::vector<int64_t> counters;
 };
 
@@ -238,6 +238,17 @@ void ks_upload(ks_problem* pb) {
   size_t o_fkw = put(t.fk_words.data(), t.fk_words.size() * 4);
   size_t o_fkk = put(t.fk_key_off.data(), t.fk_key_off.size() * 4);
   size_t o_fkt = put(t.fk_tpl.data(), t.fk_tpl.size() * 4);
+  // k_feasibility_nodes rows: one per relaxation state with label requirements (the others' strict
+  // Compatible is trivially true, their node test is the taint mask alone)
+  std::vector<int32_t> fnrow((size_t)std::max(h.dims.S, 1), -1), fnState;
+  for (int s = 0; s < h.dims.S; s++)
+    if (t.st_flags[(size_t)s] & SF_HAS_KEYS) {
+      fnrow[(size_t)s] = (int32_t)fnState.size();
+      fnState.push_back(s);
+    }
+  if (fnState.empty()) fnState.push_back(0);
+  size_t o_fnr = put(fnrow.data(), fnrow.size() * 4);
+  size_t o_fns = put(fnState.data(), fnState.size() * 4);
   HIPCHK(hipMalloc(&pb->dbuf, a.total));
   std::vector<char> staging(a.total, 0);
   for (auto& it : items)
@@ -271,15 +282,41 @@ void ks_upload(ks_problem* pb) {
       }
       return w;
     };
-    double tplW = 0;
-    for (int tt = 0; tt < h.dims.NTPL; tt++) tplW += tableWords(&t.tpl_rs[(size_t)tt * h.dims.RSW]);
+    // (a row whose state does not tolerate the template's taints is written as zeros without reads)
+    std::vector<double> tplW((size_t)h.dims.NTPL);
+    for (int tt = 0; tt < h.dims.NTPL; tt++) tplW[(size_t)tt] = tableWords(&t.tpl_rs[(size_t)tt * h.dims.RSW]);
     for (int s = 0; s < h.dims.S; s++) {
       const double sw = tableWords(&t.st_rs[(size_t)s * h.dims.RSW]);
-      pb->fmBytes += 4.0 * h.dims.TW * (h.dims.NTPL * (1 + sw) + tplW) + 4.0 * 2 * h.dims.HDR * h.dims.NTPL;
+      for (int tt = 0; tt < h.dims.NTPL; tt++)
+        pb->fmBytes += ((t.st_toltpl[(size_t)s] >> tt) & 1u)
+                           ? 4.0 * h.dims.TW * (1 + sw + tplW[(size_t)tt]) + 4.0 * 2 * h.dims.HDR + 4.0
+                           : 4.0 * h.dims.TW + 4.0;
     }
   }
   if (h.dims.fmOn) HIPCHK(hipMalloc(&pb->fmbuf, fmBytes));
   D.st_fm = (uint32_t*)pb->fmbuf;
+  // k_feasibility_nodes: FNR rows of ceil(N/32) words (skipped above 512 MiB: the node scan then runs the
+  // strict Compatible per step).  Algorithmic bytes per launch: per (row, node) the node's taints, record
+  // header and the words of the keys the state's record holds; per row the state's record and tolerations;
+  // the rows written.
+  const int FNR = fnrow.empty() ? 0 : (int)std::count_if(fnrow.begin(), fnrow.end(), [](int32_t x) { return x >= 0; });
+  const size_t NWN = ((size_t)h.dims.N + 31) / 32;
+  const size_t fnBytes = 4 * (size_t)FNR * NWN;
+  h.dims.FNR = FNR;
+  h.dims.fnOn = FNR > 0 && h.dims.N > 0 && fnBytes <= ((size_t)1 << 29) && !getenv("KS_NO_NODE_ROWS");
+  pb->fnBytes = 0;
+  if (h.dims.fnOn) {
+    for (int i = 0; i < FNR; i++) {
+      const uint32_t* X = &t.st_rs[(size_t)fnState[(size_t)i] * h.dims.RSW];
+      double kw = 0;
+      for (uint64_t m = rs_present(X); m; m &= m - 1) kw += h.keys[(size_t)__builtin_ctzll(m)].nw;
+      pb->fnBytes += (double)h.dims.N * (16.0 + 4.0 * (8 + kw)) + 4.0 * h.dims.RSW + 16.0 + 4.0 * NWN;
+    }
+    HIPCHK(hipMalloc(&pb->fnbuf, fnBytes));
+  }
+  D.st_fn = (uint32_t*)pb->fnbuf;
+  D.st_fnrow = (const int32_t*)(b + o_fnr);
+  D.fn_state = (const int32_t*)(b + o_fns);
   D.d = h.dims;
   D.keys = (const KeyMeta*)(b + o_keys);
   D.wordValid = (const uint32_t*)(b + o_wv);
@@ -798,17 +835,17 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
     pb->wreps = reps;
   }
   KsWork w0 = work_ptrs((char*)pb->wbuf, wl);
-  hipEvent_t e0, em, e1, ef[2];
+  hipEvent_t e0, em, e1, ef[4];
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&em));
   HIPCHK(hipEventCreate(&e1));
-  HIPCHK(hipEventCreate(&ef[0]));
-  HIPCHK(hipEventCreate(&ef[1]));
+  for (auto& e : ef) HIPCHK(hipEventCreate(&e));
   // A Solve that outgrows the default plan's NodeClaim capacity runs again with the wide plan; the
   // caller pays both launches, so the reported times are their sums (the re-plan is remembered).
-  float ms = 0, setup = 0, fms = 0;
-  int feasLaunches = 0;
+  float ms = 0, setup = 0, fms = 0, fnms = 0;
+  int feasLaunches = 0, attempts = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
+    attempts++;
     HIPCHK(hipEventRecord(e0, pb->stream));
     HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp,
                         pb->stempBytes, pb->stream, em, pb->hqorder, ef));
@@ -820,6 +857,11 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
     if (pb->dev.d.fmOn) {
       HIPCHK(hipEventElapsedTime(&f, ef[0], ef[1]));
       feasLaunches++;
+    }
+    if (pb->dev.d.fnOn) {
+      float fn = 0;
+      HIPCHK(hipEventElapsedTime(&fn, ef[2], ef[3]));
+      fnms += fn;
     }
     ms += a;
     setup += b;
@@ -837,8 +879,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(em);
   (void)hipEventDestroy(e1);
-  (void)hipEventDestroy(ef[0]);
-  (void)hipEventDestroy(ef[1]);
+  for (auto& e : ef) (void)hipEventDestroy(e);
   ks_results* r;
   if (opts && opts->timing_only) {
     r = new ks_results();
@@ -857,6 +898,8 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   r->solve_ms = ms - setup;
   r->feas_ms = fms;
   r->feas_bytes = pb->dev.d.fmOn ? pb->fmBytes * feasLaunches : 0;  // bytes of every launch feas_ms sums
+  r->feasn_ms = fnms;
+  r->feasn_bytes = pb->dev.d.fnOn ? pb->fnBytes * attempts : 0;  // one k_feasibility_nodes per launch
   *out = r;
   return KS_OK;
   API_CATCH
@@ -941,6 +984,8 @@ double ks_results_kernel_ms(const ks_results* r) { return r->kernel_ms; }
 double ks_results_solve_kernel_ms(const ks_results* r) { return r->solve_ms; }
 double ks_results_feasibility_ms(const ks_results* r) { return r->feas_ms; }
 double ks_results_feasibility_bytes(const ks_results* r) { return r->feas_bytes; }
+double ks_results_node_feasibility_ms(const ks_results* r) { return r->feasn_ms; }
+double ks_results_node_feasibility_bytes(const ks_results* r) { return r->feasn_bytes; }
 double ks_results_algorithmic_bytes(const ks_results* r) { return r->algbytes; }
 
 }  // extern "C"

@@ -77,6 +77,8 @@ struct KsDims {
   int32_t fmOn;            // st_fm is computed (k_feasibility) and k_solve reads it
   int32_t lean;            // none of host ports, limited volumes, pod label requirements, shared UIDs,
                            // negative requests, topology: k_solve's LEAN instantiation applies
+  int32_t fnOn;            // st_fn is computed (k_feasibility_nodes) and k_solve reads it
+  int32_t FNR;             // rows of st_fn: the relaxation states with label requirements
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
@@ -85,6 +87,7 @@ struct Plan {
   int32_t KL;      // claims [0, KL) keep template/requests/max/options in LDS, the rest in HBM
   int32_t talloc;  // 1: template instance-type Allocatable tables are LDS-resident
   int32_t tsort;   // 1: the sorted Allocatable lists (tsort_*) are LDS-resident
+  int32_t tcl;     // topology count words [0, tcl) are LDS-resident (>= KsDims::tgSmall)
   uint64_t lds;    // dynamic LDS bytes
 };
 
@@ -163,6 +166,13 @@ struct KsDev {
   // Intersects both the template's and the state's requirements on every key no instance type constrains
   // with more than one value (fkMulti excluded); [S][NTPL][TW]
   uint32_t KS_G* st_fm;
+  // k_feasibility_nodes's output: per relaxation state with label requirements (st_fnrow[s] = its row, -1
+  // for the others; fn_state[row] = s), one bit per existing node: Taints.Tolerates(node taints) AND the
+  // strict Requirements.Compatible(node labels, pod requirements) of ExistingNode.Add (existingnode.go:
+  // 64-124), on the nodes' initial records; [FNR][ceil(N/32)]
+  const int32_t KS_G* st_fnrow;
+  const int32_t KS_G* fn_state;
+  uint32_t KS_G* st_fn;
 };
 
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };

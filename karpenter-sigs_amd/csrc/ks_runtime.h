@@ -49,6 +49,8 @@ struct ks_problem {
   void* dbuf = nullptr;
   void* fmbuf = nullptr;  // k_feasibility rows (KsDev::st_fm)
   double fmBytes = 0;     // k_feasibility's algorithmic bytes per launch
+  void* fnbuf = nullptr;  // k_feasibility_nodes rows (KsDev::st_fn)
+  double fnBytes = 0;     // k_feasibility_nodes's algorithmic bytes per launch
   void* wbuf = nullptr;
   size_t wbytes = 0;
   ks::KsWork* works_dev = nullptr;
@@ -72,6 +74,7 @@ struct ks_problem {
     if (hqorder) (void)hipFree(hqorder);
     if (dbuf) (void)hipFree(dbuf);
     if (fmbuf) (void)hipFree(fmbuf);
+    if (fnbuf) (void)hipFree(fnbuf);
     if (wbuf) (void)hipFree(wbuf);
     if (works_dev) (void)hipFree(works_dev);
     if (stream) (void)hipStreamDestroy(stream);

@@ -37,6 +37,15 @@
 #ifndef KS_RUN_MIN  // shortest run of identical pods the simulation fast path places in one step
 #define KS_RUN_MIN 3
 #endif
+#ifndef KS_NODE_K  // existing nodes per lane per step of the first-fit scan beyond the register window
+#define KS_NODE_K 2
+#endif
+#ifndef KS_TOPO_WINDOW_BATCH  // register window + topology: every window node's topology loads issued at once
+#define KS_TOPO_WINDOW_BATCH 0
+#endif
+#ifndef KS_TOPO_NODE_SERIAL  // the topology node test one node at a time (see topo_node_stateK)
+#define KS_TOPO_NODE_SERIAL 1
+#endif
 #ifndef KS_CLAIM_RUNS  // LEAN Solve: runs of identical pods placed on one NodeClaim in one step
 #define KS_CLAIM_RUNS 1
 #endif
@@ -55,7 +64,7 @@ using GI64 = int64_t KS_G*;
 using GU32 = uint32_t KS_G*;
 using DevLayout = ReqLayoutT<const KeyMeta KS_L*, const uint32_t KS_G*, const int64_t KS_G*>;
 
-__device__ __forceinline__ int lane() { return (int)threadIdx.x; }
+__device__ __forceinline__ int lane() { return (int)threadIdx.x & (kWave - 1); }
 __device__ __forceinline__ uint64_t wballot(bool p) { return __ballot(p ? 1 : 0); }
 __device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -304,16 +313,69 @@ __device__ __forceinline__ uint32_t fk_intersects_word(const KsDev& D, const Dev
 }
 
 #if KS_TU == 0
+// Requirements.Intersects(IT, X) for word wc, as fk_intersects_word, evaluated by a group of GW lanes (GW = 32:
+// the two halves of the wave work on different rows, each with its own X, t and key set; the complement
+// branches ballot over the group's lanes only).
+template <int GW, class PX>
+__device__ __forceinline__ uint32_t fk_intersects_word_g(const KsDev& D, const DevLayout& L, PX X, int t, int wc,
+                                                         uint64_t keys) {
+  const uint32_t KS_G* F = D.fk_words;
+  const KsDims& d = D.d;
+  const int TW = d.TW;
+  const int sub = lane() & (GW - 1), sh = GW == 64 ? 0 : (lane() & 32);
+  auto gballot = [&](bool p) -> uint64_t {
+    const uint64_t b = wballot(p);
+    return GW == 64 ? b : (uint64_t)(uint32_t)(b >> sh);
+  };
+  uint32_t ic = ~0u;
+  for (uint64_t m = keys; m; m &= m - 1) {
+    const int k = ctz64(m);
+    const int base = D.fk_key_off[t * d.NK + k];
+    const KeyMeta km = L.keys[k];
+    uint32_t acc = F[base + wc] | F[base + TW + wc];  // lacks the key; DoesNotExist (passed, see feas_masks)
+    if (!bit(rs_compl(X), k)) {  // X In: the positions holding one of its values
+      for (int i = 0; i < km.nw; i++) {
+        uint32_t x = X[L.HDR + km.off + i];
+        while (x) {
+          const int v = i * 32 + __builtin_ctz(x);
+          x &= x - 1;
+          acc |= F[base + (3 + v) * TW + wc];
+        }
+      }
+    } else if (!bit(d.fkMulti, k)) {  // complement, one value per IT: In positions minus the values X excludes
+      uint32_t sbt = 0;
+      for (int v0 = 0; v0 < km.nv; v0 += GW) {
+        uint64_t out = gballot(v0 + sub < km.nv && !rs_member(L, X, k, v0 + sub));
+        for (; out; out &= out - 1) sbt |= F[base + (3 + v0 + ctz64(out)) * TW + wc];
+      }
+      acc |= F[base + 2 * TW + wc] & ~sbt;
+    } else {  // complement over multi-valued ITs: the values X admits
+      for (int v0 = 0; v0 < km.nv; v0 += GW) {
+        uint64_t in = gballot(v0 + sub < km.nv && rs_member(L, X, k, v0 + sub));
+        for (; in; in &= in - 1) acc |= F[base + (3 + v0 + ctz64(in)) * TW + wc];
+      }
+    }
+    ic &= acc;
+  }
+  return ic;
+}
+
 // k_feasibility (north_star "feasibility matrix"): the static part of the pod x
-// instance-type feasibility, one wavefront per (relaxation state, template) row, lanes over the words of
-// the template's position bitset.  Row = Intersects(IT, template) AND Intersects(IT, state) on the keys
-// no instance type constrains with more than one value (nodeclaim.go:225-260; requirements.go:241-258).
-// k_solve ANDs the row where it would otherwise re-evaluate those keys per step (feas_masks).
-// HBM-bound: reads the state's and template's records and the template's position tables, writes TW words.
-__global__ __launch_bounds__(64) void k_feasibility(KsDev D) {
+// instance-type feasibility per (relaxation state, template) row, over the words of the template's position
+// bitset.  Row = Tolerates(template taints) AND Intersects(IT, template) AND Intersects(IT, state) on the keys
+// no instance type constrains with more than one value (nodeclaim.go:68-71,225-260; requirements.go:241-258).
+// k_solve ANDs the row where it would otherwise re-evaluate those keys per step (feas_masks); it tests the
+// template's taints before it reads a row (try_templates, claim_quick), so an intolerant row is all zero and
+// costs no reads.  HBM-bound: reads the state's and template's records and the template's position tables,
+// writes TW words per row.
+// Persistent 256-lane blocks: the key table is staged once per block, and each wave walks rows with a
+// grid stride.  A row of TW <= 32 words takes half a wave (two rows per wave step), so lanes are not idle
+// for the narrow template lists (C3: TW = 25).
+template <int GW>
+__global__ __launch_bounds__(256) void k_feasibility(KsDev D) {
   const KsDims& d = D.d;
   __shared__ __attribute__((aligned(16))) uint32_t s_kraw[64 * sizeof(KeyMeta) / 4];
-  for (int i = lane(); i < d.NK * (int)(sizeof(KeyMeta) / 4); i += kWave) s_kraw[i] = ((const uint32_t KS_G*)D.keys)[i];
+  for (int i = threadIdx.x; i < d.NK * (int)(sizeof(KeyMeta) / 4); i += blockDim.x) s_kraw[i] = ((const uint32_t KS_G*)D.keys)[i];
   __syncthreads();
   DevLayout L;
   L.nkeys = d.NK;
@@ -325,17 +387,71 @@ __global__ __launch_bounds__(64) void k_feasibility(KsDev D) {
   L.wordValid = D.wordValid;
   L.vIsInt = D.vIsInt;
   L.vInt = D.vInt;
-  const int row = blockIdx.x, s = row / d.NTPL, t = row - s * d.NTPL;
-  const uint32_t KS_G* X = D.st_rs + (int64_t)s * d.RSW;
-  const uint32_t KS_G* T = D.tpl_rs + (int64_t)t * d.RSW;
+  constexpr int RPW = 64 / GW;  // rows per wave step
+  const int rows = d.S * d.NTPL;
+  const int wave = (int)(threadIdx.x >> 6), half = GW == 64 ? 0 : (lane() >> 5), sub = lane() & (GW - 1);
   const uint64_t km = d.itKeys & ~d.fkMulti;
-  const uint64_t kx = rs_present(X) & km, kt = rs_present(T) & km;
-  for (int w0 = 0; w0 < d.TW; w0 += kWave) {
-    const int w = w0 + lane();
-    const int wc = w < d.TW ? w : d.TW - 1;
-    const uint32_t v = fk_intersects_word(D, L, X, t, wc, kx, true) & fk_intersects_word(D, L, T, t, wc, kt, true);
-    if (w < d.TW) D.st_fm[(int64_t)row * d.TW + w] = v;
+  for (int r0 = (blockIdx.x * 4 + wave) * RPW; r0 < rows; r0 += gridDim.x * 4 * RPW) {
+    const int row = r0 + half;
+    const bool live = row < rows;
+    const int rr = live ? row : rows - 1;
+    const int s = rr / d.NTPL, t = rr - s * d.NTPL;
+    uint32_t KS_G* out = D.st_fm + (int64_t)rr * d.TW;
+    if (!((D.st_toltpl[s] >> t) & 1u)) {  // the state does not tolerate the template's taints
+      for (int w = sub; w < d.TW; w += GW)
+        if (live) out[w] = 0;
+      continue;
+    }
+    const uint32_t KS_G* X = D.st_rs + (int64_t)s * d.RSW;
+    const uint32_t KS_G* T = D.tpl_rs + (int64_t)t * d.RSW;
+    const uint64_t kx = rs_present(X) & km, kt = rs_present(T) & km;
+    for (int w0 = 0; w0 < d.TW; w0 += GW) {
+      const int w = w0 + sub;
+      const int wc = w < d.TW ? w : d.TW - 1;
+      const uint32_t v = fk_intersects_word_g<GW>(D, L, X, t, wc, kx) & fk_intersects_word_g<GW>(D, L, T, t, wc, kt);
+      if (live && w < d.TW) out[w] = v;
+    }
   }
+}
+// k_feasibility_nodes (north_star "feasibility matrix", the existing-node side): per relaxation state with
+// label requirements and per existing node, Taints.Tolerates AND the strict Requirements.Compatible of
+// ExistingNode.Add (existingnode.go:64-124; taints.go:38-50; requirements.go:163-174) on the node's
+// initial labels.  Both inputs are static for the whole Solve / pass, so k_solve's node scan reads one
+// bit instead of re-running Compatible per (pod, node) step -- until a commit narrows a node's own
+// requirements (existingnode.go:118), after which that node is tested exactly again.
+// One thread per (row, node): a block of 256 nodes of one row; lanes evaluate their node against the same
+// state record (uniform key loop), a ballot packs 64 node bits, lanes 0 and 32 store one word each.
+__global__ __launch_bounds__(256) void k_feasibility_nodes(KsDev D, int nbx) {
+  const KsDims& d = D.d;
+  __shared__ __attribute__((aligned(16))) uint32_t s_kraw[64 * sizeof(KeyMeta) / 4];
+  for (int i = threadIdx.x; i < d.NK * (int)(sizeof(KeyMeta) / 4); i += blockDim.x) s_kraw[i] = ((const uint32_t KS_G*)D.keys)[i];
+  __syncthreads();
+  DevLayout L;
+  L.nkeys = d.NK;
+  L.W = d.W;
+  L.NB = d.NB;
+  L.HDR = d.HDR;
+  L.RSW = d.RSW;
+  L.keys = (const KeyMeta KS_L*)s_kraw;
+  L.wordValid = D.wordValid;
+  L.vIsInt = D.vIsInt;
+  L.vInt = D.vInt;
+  const int row = blockIdx.x / nbx, bx = blockIdx.x - row * nbx;
+  const int s = D.fn_state[row];
+  const uint32_t KS_G* X = D.st_rs + (int64_t)s * d.RSW;
+  const uint64_t t0 = D.st_tol[2 * s], t1 = D.st_tol[2 * s + 1];
+  const int NWN = (d.N + 31) >> 5;
+  const int n = bx * 256 + (int)threadIdx.x;  // a wave's 64 nodes start at a multiple of 64
+  bool ok = false;
+  if (n < d.N) {
+    const uint64_t KS_G* tp = D.n_taint + 2 * (int64_t)n;
+    ok = ((tp[0] & ~t0) | (tp[1] & ~t1)) == 0 && rs_compatible(L, D.n_rs0 + (int64_t)n * d.RSW, X, 0);
+  }
+  const uint64_t b = wballot(ok);
+  const int w = (n - lane()) >> 5;  // this wave's first word
+  uint32_t KS_G* out = D.st_fn + (int64_t)row * NWN;
+  if (lane() == 0 && w < NWN) out[w] = (uint32_t)b;
+  if (lane() == 32 && w + 1 < NWN) out[w + 1] = (uint32_t)(b >> 32);
 }
 #endif
 
@@ -382,19 +498,22 @@ struct Solver {
   LU32 s_firr;          // [TW+2] feas_masks: irregular positions (exact per-position check)
   LU32 s_rmv;           // SIM: [ceil(N/32)] nodes removed by the simulation (the candidates)
   LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose requests live in a W.n_req slot
-  LU32 s_tchr;          // SIM: [ceil(N/32)] nodes whose requirements live in a W.n_rs slot
+  LU32 s_tchr;          // SIM: [ceil(N/32)] nodes whose requirements live in a W.n_rs slot; Solve (d.fnOn): nodes
+                        // whose requirements a commit narrowed (k_feasibility_nodes's bits no longer apply)
   LU32 s_tvol;          // SIM: [ceil(N/32)] nodes whose volume usage lives in W.n_vm / W.n_vc
   LI32 s_tgm;           // [G][TGM_WORDS] topology group metadata
   LI32 s_tmin;          // [G] domainMinCount of the popped pod, per spread group
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
   LU32 s_trs1;          // [RSW] one group's domains as a single-key record
-  LI32 s_tcs;           // [tgSmall] counts of the small-key groups (the count table's LDS-resident prefix)
+  LI32 s_tcs;           // [pl.tcl] the count table's LDS-resident prefix: the small-key groups (a Solve: the
+                        // whole table when it fits, make_plan)
   LU32 s_tcd;           // SIM: dirty bits over count words [tgSmall, tgCntWords): set once W.tg_cnt holds the word
   LI32 s_bnode;         // LEAN SIM: [64] run placement: the node taking the run's pod at each offset (first of a node's pods)
   uint64_t t_mask = 0;  // groups matching the popped pod (owned in its state | inverse groups selecting it)
   uint64_t t_sel = 0;   // groups whose selector selects the popped pod
   uint64_t t_inv = 0;   // inverse groups the popped pod owns
   int t_s = 0;          // the popped pod's relaxation state
+  const uint32_t KS_G* fnp = nullptr;  // k_feasibility_nodes's row of the popped pod's state (null: none)
   bool t_nonode = false;  // some matching group admits no domain at all: no existing node can pass
   uint64_t t_active = ~0ull;  // groups in t.topologies so far (late groups join at their relaxation)
   int64_t algbytes = 0;
@@ -602,90 +721,84 @@ struct Solver {
   }
   // Lane (n & 63) is the only lane that ever reads or writes node n's mutable state.
   __device__ __forceinline__ bool tbit(LU32 m, int n) const { return (m[n >> 5] >> (n & 31)) & 1u; }
-  // Existing-node check for two nodes per lane (positions n and n + 64 of the first-fit order):
-  // every load of both is issued before any test, so a 128-node step of the scan costs one memory
-  // round trip.  Out-of-range positions are clamped for the loads and masked.  nf: NodeFlag bits.
-  // sl0 / sl1: the node passed every check but lacks the label of a matching group's key, so only the
-  // wave-cooperative node_slow can decide it (ok is false then).
-  __device__ __forceinline__ void node_ok2(int n0, int s, int sflags, const int64_t* pod, uint64_t tol0,
-                                           uint64_t tol1, bool& ok0, bool& ok1, int& nf0, int& nf1,
-                                           int64_t* q0, int64_t* q1, bool& sl0, bool& sl1) const {
-    const int n1 = n0 + kWave;
-    const int c0 = n0 < d.N ? n0 : d.N - 1, c1 = n1 < d.N ? n1 : d.N - 1;
-    const bool own0 = !SIM || tbit(s_tch, c0), own1 = !SIM || tbit(s_tch, c1);
-    const uint64_t KS_G* t0p = D.n_taint + 2 * c0;
-    const uint64_t KS_G* t1p = D.n_taint + 2 * c1;
-    const int64_t KS_G* a0p = D.n_avail + (int64_t)c0 * R();
-    const int64_t KS_G* a1p = D.n_avail + (int64_t)c1 * R();
-    const int64_t KS_G* q0p = (own0 ? W.n_req : D.n_req0) + (int64_t)c0 * R();
-    const int64_t KS_G* q1p = (own1 ? W.n_req : D.n_req0) + (int64_t)c1 * R();
-    const uint64_t x0 = t0p[0], y0 = t0p[1], x1 = t1p[0], y1 = t1p[1];
-    int64_t a0[RM], a1[RM];
+  // Existing-node check for KN nodes per lane (positions n, n + 64, ... of the first-fit order): every
+  // load of all of them is issued before any test, so a (KN * 64)-node step of the scan costs one memory
+  // round trip (two with topology: the nodes' domains, then their counts).  Out-of-range positions are
+  // clamped for the loads and masked.  nf: NodeFlag bits.  sl[i]: the node passed every check but lacks
+  // the label of a matching group's key, so only the wave-cooperative node_slow can decide it (ok is
+  // false then).
+  template <int KN>
+  __device__ __forceinline__ void node_okK(int n0, int sflags, const int64_t* pod, uint64_t tol0, uint64_t tol1,
+                                           bool* ok, int* nf, int64_t (*q)[RM], bool* sl) const {
+    int c[KN];
+    uint64_t tx[KN], ty[KN], h[KN];
+    int64_t a[KN][RM];
 #pragma unroll
-    for (int r = 0; r < RM; r++) {
-      if (RT == 0 && r >= d.R) break;
-      a0[r] = a0p[r];
-      a1[r] = a1p[r];
-      q0[r] = q0p[r];
-      q1[r] = q1p[r];
-    }
-    nf0 = SIM ? D.n_flags[c0] : 0;
-    nf1 = SIM ? D.n_flags[c1] : 0;
-    uint64_t h0 = 0, h1 = 0;
-    if (hpA()) {  // HostPortUsage.Conflicts (hostportusage.go:74-85)
-      h0 = own0 ? W.n_hp[c0] : D.n_hp0[c0];
-      h1 = own1 ? W.n_hp[c1] : D.n_hp0[c1];
-    }
-    ok0 = (n0 < d.N) & (((x0 & ~tol0) | (y0 & ~tol1)) == 0) & ((h0 & cur_hpc) == 0);  // Taints.Tolerates
-    ok1 = (n1 < d.N) & (((x1 & ~tol0) | (y1 & ~tol1)) == 0) & ((h1 & cur_hpc) == 0);
-    if (SIM) {  // the simulation removed these candidates
-      ok0 &= !tbit(s_rmv, c0);
-      ok1 &= !tbit(s_rmv, c1);
+    for (int i = 0; i < KN; i++) {
+      const int n = n0 + i * kWave;
+      c[i] = n < d.N ? n : d.N - 1;
+      const bool own = !SIM || tbit(s_tch, c[i]);
+      const uint64_t KS_G* tp = D.n_taint + 2 * c[i];
+      const int64_t KS_G* ap = D.n_avail + (int64_t)c[i] * R();
+      const int64_t KS_G* qp = (own ? W.n_req : D.n_req0) + (int64_t)c[i] * R();
+      tx[i] = tp[0];
+      ty[i] = tp[1];
+#pragma unroll
+      for (int r = 0; r < RM; r++) {
+        if (RT == 0 && r >= d.R) break;
+        a[i][r] = ap[r];
+        q[i][r] = qp[r];
+      }
+      nf[i] = SIM ? D.n_flags[c[i]] : 0;
+      h[i] = 0;
+      if (hpA()) h[i] = own ? W.n_hp[c[i]] : D.n_hp0[c[i]];  // HostPortUsage.Conflicts (hostportusage.go:74-85)
     }
 #pragma unroll
-    for (int r = 0; r < RM; r++) {  // Fits(requests + pod, Available())
-      if (RT == 0 && r >= d.R) break;
-      ok0 &= (a0[r] >= 0) & (q0[r] + pod[r] <= a0[r]);
-      ok1 &= (a1[r] >= 0) & (q1[r] + pod[r] <= a1[r]);
-    }
-    if (volA() && cur_vm) {
-      if (ok0) ok0 = vol_ok(c0);
-      if (ok1) ok1 = vol_ok(c1);
-    }
-    if (keys(sflags)) {  // strict Compatible: no AllowUndefinedWellKnownLabels
-      if (ok0) ok0 = rs_compatible(L, node_rs(c0), s_pin, 0);
-      if (ok1) ok1 = rs_compatible(L, node_rs(c1), s_pin, 0);
-    }
-    sl0 = sl1 = false;
-    if (TOPO && t_mask) {  // topology (existingnode.go:106-114)
-      if (ok0) {
-        const int t = topo_node_state(c0);
-        ok0 = t == 1;
-        sl0 = t == 2;
+    for (int i = 0; i < KN; i++) {
+      ok[i] = (n0 + i * kWave < d.N) & (((tx[i] & ~tol0) | (ty[i] & ~tol1)) == 0) & ((h[i] & cur_hpc) == 0);  // Taints.Tolerates
+      if (SIM) ok[i] &= !tbit(s_rmv, c[i]);  // the simulation removed these candidates
+#pragma unroll
+      for (int r = 0; r < RM; r++) {  // Fits(requests + pod, Available())
+        if (RT == 0 && r >= d.R) break;
+        ok[i] &= (a[i][r] >= 0) & (q[i][r] + pod[r] <= a[i][r]);
       }
-      if (ok1) {
-        const int t = topo_node_state(c1);
-        ok1 = t == 1;
-        sl1 = t == 2;
-      }
+      if (volA() && cur_vm && ok[i]) ok[i] = vol_ok(c[i]);
+      if (keys(sflags) && ok[i]) ok[i] = node_compat(c[i]);  // strict Compatible
+      sl[i] = false;
     }
+    if (TOPO && t_mask) topo_node_stateK<KN>(c, ok, sl);  // topology (existingnode.go:106-114)
   }
   __device__ __forceinline__ const uint32_t KS_G* node_rs(int n) const {
     if (!SIM) return W.n_rs + (int64_t)n * d.RSW;
     return tbit(s_tchr, n) ? W.n_rs + (int64_t)W.n_slot[n] * d.RSW : D.n_rs0 + (int64_t)n * d.RSW;
+  }
+  // ExistingNode.Add's strict Compatible(node requirements, pod requirements) (existingnode.go:97-104) for
+  // node n: k_feasibility_nodes's bit while the node keeps its initial record (that bit also ANDs the
+  // taint test the caller already applied), else the exact test on the node's current record.
+  __device__ __forceinline__ bool node_compat(int n) const {
+    if (fnp && !tbit(s_tchr, n)) return (fnp[n >> 5] >> (n & 31)) & 1u;
+    return rs_compatible(L, node_rs(n), s_pin, 0);
+  }
+  // Solve (d.fnOn): node j's requirements were narrowed by a commit; its row bit no longer applies.
+  __device__ __forceinline__ void node_rs_changed(int j) const {
+    if (!SIM && d.fnOn)
+      __hip_atomic_fetch_or(s_tchr + (j >> 5), 1u << (j & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   }
   // Solve: commit of a pod to node j by its owner lane.
   __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod) {
     for (int r = 0; r < R(); r++) W.n_req[(int64_t)j * R() + r] += pod[r];
     if (hpA()) W.n_hp[j] = (W.n_hp[j] & ~cur_hpo) | cur_hpu;  // HostPortUsage.Add (hostportusage.go:70-72)
     if (volA() && cur_vm) vol_commit(j);
-    if (keys(sflags)) rs_add(L, W.n_rs + (int64_t)j * d.RSW, s_pin);
+    if (keys(sflags)) {
+      rs_add(L, W.n_rs + (int64_t)j * d.RSW, s_pin);
+      node_rs_changed(j);
+    }
   }
   // SIM: copy-on-write commit (wave-uniform).  W.n_req is indexed by node but only the nodes a pod
   // landed on are ever written (s_tch marks them), so a fresh simulation needs no initialisation.
   // Requirements are copied only when a pod with label requirements lands, into the next compact
   // slot of W.n_rs (wave-cooperatively, through LDS).
-  // `q`: the owner lane's requests of node j as node_ok2 loaded them (no reload before the store).
+  // `q`: the owner lane's requests of node j as node_okK loaded them (no reload before the store).
   // regReq: node j sits in the register window (its requests are updated there, not in HBM).
   __device__ __forceinline__ void sim_node_commit(int j, int s, int sflags, const int64_t* pod, const int64_t* q,
                                                   int& nrs, bool regReq) {
@@ -732,7 +845,7 @@ struct Solver {
   // holds a full copy (k_init); a simulation reads the shared NewTopology counts until it first writes a
   // word (copy-on-write, s_tcd), so no simulation copies the table.
   __device__ __forceinline__ int tcnt_at(int off) const {
-    if (off < d.tgSmall) return s_tcs[off];
+    if (off < pl.tcl) return s_tcs[off];
     if constexpr (SIM) {
       const int b = off - d.tgSmall;
       const int own = ld_sc1(W.tg_cnt + off), shared = D.tg_cnt0[off];
@@ -746,7 +859,7 @@ struct Solver {
   __device__ __forceinline__ void tcnt_inc(int off) const {
     const int c = tcnt_at(off);
     const int n = c < 0 ? 1 : c + 1;
-    if (off < d.tgSmall) {
+    if (off < pl.tcl) {
       s_tcs[off] = n;
       return;
     }
@@ -830,11 +943,14 @@ struct Solver {
     }
     wsync();
   }
-  // ExistingNode.Add's topology step for node n (one lane): the node's single domain of each
-  // matching group must be the one TopologyGroup.Get returns (existingnode.go:106-114).
-  // Returns 0 (fails), 1 (passes) or 2 (every labelled group passes, but the node lacks the label of
-  // some group's key: its domain then comes from the requirements it accumulated, node_slow decides).
-  __device__ __forceinline__ int topo_node_state(int n) const {
+  // ExistingNode.Add's topology step for nodes c[0..KN) (one lane each): a node's single domain of each
+  // matching group must be the one TopologyGroup.Get returns (existingnode.go:106-114).  Nodes with ok[i]
+  // false stay failed.  sl[i]: every labelled group passes, but the node lacks the label of some group's
+  // key (its domain then comes from the requirements it accumulated; node_slow decides).  The groups go
+  // in chunks of TGC: all KN * TGC domains are loaded, then all their counts, then tested, so a chunk
+  // costs two memory round trips however many nodes and groups it covers.
+  // The per-node form (KS_TOPO_NODE_SERIAL): 0 fails, 1 passes, 2 decided by node_slow.
+  __device__ __forceinline__ int topo_node_state1(int n) const {
     int st = 1;
     for (uint64_t m = t_mask; m; m &= m - 1) {
       const int g = ctz64(m);
@@ -858,6 +974,69 @@ struct Solver {
     }
     return st;
   }
+  template <int KN>
+  __device__ __forceinline__ void topo_node_stateK(const int* c, bool* ok, bool* sl) const {
+#if KS_TOPO_NODE_SERIAL
+#pragma unroll
+    for (int i = 0; i < KN; i++) {
+      const int st = ok[i] ? topo_node_state1(c[i]) : 0;
+      ok[i] = st == 1;
+      sl[i] = st == 2;
+    }
+    return;
+#endif
+    constexpr int TGC = 4;
+    int st[KN];  // 0 fails, 1 passes, 2 decided by node_slow
+#pragma unroll
+    for (int i = 0; i < KN; i++) st[i] = ok[i] ? 1 : 0;
+    for (uint64_t m = t_mask; m;) {
+      int gs[TGC];
+#pragma unroll
+      for (int j = 0; j < TGC; j++) {
+        gs[j] = m ? ctz64(m) : -1;
+        m &= m - 1;
+      }
+      int v[TGC][KN], cn[TGC][KN];
+#pragma unroll
+      for (int j = 0; j < TGC; j++)
+#pragma unroll
+        for (int i = 0; i < KN; i++) v[j][i] = gs[j] >= 0 ? D.n_tdom[(int64_t)gs[j] * d.N + c[i]] : 0;
+#pragma unroll
+      for (int j = 0; j < TGC; j++)
+#pragma unroll
+        for (int i = 0; i < KN; i++) cn[j][i] = (gs[j] >= 0 && v[j][i] >= 0) ? tcnt(gs[j], v[j][i]) : 0;
+#pragma unroll
+      for (int j = 0; j < TGC; j++) {
+        if (gs[j] < 0) break;
+        const int g = gs[j], type = tg(g, TGM_TYPE);
+        const bool self = (t_sel >> g) & 1ull;
+#pragma unroll
+        for (int i = 0; i < KN; i++) {
+          if (v[j][i] < 0) {
+            if (st[i] == 1) st[i] = 2;
+            continue;
+          }
+          const int cc = cn[j][i];
+          bool pass;
+          if (cc < 0) {
+            pass = false;  // unregistered: Get never returns it
+          } else if (type == TG_SPREAD) {
+            pass = (int64_t)cc + (int)self - s_tmin[g] <= tg(g, TGM_SKEW);
+          } else if (type == TG_AFFINITY) {  // a selected pod's domain, or the bootstrap for a self-selecting pod
+            pass = tpod_has(g, v[j][i]) && (s_tmin[g] ? cc != 0 : self);
+          } else {
+            pass = cc == 0 && tpod_has(g, v[j][i]);
+          }
+          if (!pass) st[i] = 0;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < KN; i++) {
+      ok[i] = st[i] == 1;
+      sl[i] = st[i] == 2;
+    }
+  }
   // ExistingNode.Add's requirement and topology steps for node j, wave-wide, for a node lacking the
   // label of a matching group's key (existingnode.go:91-115): nodeRequirements = the node's requirements
   // + the pod's, then AddRequirements picks the domains over nodeRequirements.Get(key) exactly as for a
@@ -877,6 +1056,7 @@ struct Solver {
     wsync();
     if (!SIM) {
       copy_words(W.n_rs + (int64_t)j * d.RSW, s_rs, d.RSW);
+      if (lane() == 0) node_rs_changed(j);
     } else {
       const int owner = j & (kWave - 1);
       const bool rsfresh = !tbit(s_tchr, j);
@@ -1932,17 +2112,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int NWN = (d.N + 31) >> 5;
   S.s_rmv = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tch = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
-  S.s_tchr = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
+  S.s_tchr = (LU32)take(SIM || d.fnOn ? 4 * (size_t)NWN : 0);
   S.s_tvol = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
   S.s_tgm = (LI32)take(4 * (size_t)d.G * TGM_WORDS);
   S.s_tmin = (LI32)take(4 * (size_t)d.G);
   S.s_trs0 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
   S.s_trs1 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
-  S.s_tcs = (LI32)take(d.G ? 4 * (size_t)d.tgSmall : 0);
+  S.s_tcs = (LI32)take(d.G ? 4 * (size_t)pl.tcl : 0);
   const int NWC = SIM && d.G ? (d.tgCntWords - d.tgSmall + 31) >> 5 : 0;
   S.s_tcd = (LU32)take(4 * (size_t)NWC);
   S.s_bnode = (LI32)take(SIM && LEAN ? 4 * (size_t)kWave : 0);
-  for (int i = lane(); i < (d.G ? d.tgSmall : 0); i += kWave) S.s_tcs[i] = D.tg_cnt0[i];
+  for (int i = lane(); i < (d.G ? pl.tcl : 0); i += kWave) S.s_tcs[i] = D.tg_cnt0[i];
   for (int i = lane(); i < NWC; i += kWave) S.s_tcd[i] = 0;
   for (int i = lane(); i < d.G * TGM_WORDS; i += kWave) S.s_tgm[i] = D.tg_meta[i];
   S.gc.tpl = W.c_tpl;
@@ -1956,6 +2136,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   for (int i = lane(); i <= d.NTPL; i += kWave) S.s_tbeg[i] = D.tpl_it_beg[i];
   for (int i = lane(); i < d.NPOOL * R; i += kWave) S.s_pool[i] = SIM ? W.pool0[i] : D.pool_rem0[i];
   const int P = SIM ? W.P : d.P;
+  if (!SIM && d.fnOn)
+    for (int i = lane(); i < NWN; i += kWave) S.s_tchr[i] = 0;
   if constexpr (SIM) {
     // the simulation's fresh Scheduler state (what k_init does for plain Solves): NewQueue order is
     // the local order (pod_map is sorted), nothing placed, no staleness marks
@@ -2266,6 +2448,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (S.volA()) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
     if (S.keys(sflags)) {  // the state's record, read by every check of this pop
       S.copy_words(S.s_pin, D.st_rs + (int64_t)s * d.RSW, d.RSW);
+      S.fnp = d.fnOn ? D.st_fn + (int64_t)uni(D.st_fnrow[s]) * ((d.N + 31) >> 5) : nullptr;
       wsync();
     }
     if (TOPO) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
@@ -2283,11 +2466,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const bool skipNodes = TOPO && S.t_nonode && !d.tgUnlab;
     int scanFrom = 0;
     if constexpr (NW > 0) {
-      // (problems with unlabelled nodes scan every node through node_ok2, which handles them)
+      // (problems with unlabelled nodes scan every node through node_okK, which handles them)
       if (d.N > 0 && !skipNodes && !(TOPO && d.tgUnlab)) {
         int kj = -1;
         uint64_t mj = 0;
         asm volatile("; KS_MARK window_begin");
+        if (KS_TOPO_WINDOW_BATCH && TOPO && S.t_mask) {  // every node is labelled here: all window nodes' topology loads at once
+          bool okw[NWA], slw[NWA];
+          int cw[NWA];
+#pragma unroll
+          for (int k = 0; k < NW; k++) {
+            const int n = k * kWave + lane();
+            cw[k] = n < d.N ? n : d.N - 1;
+            bool ok = (((wtx[k] & ~tol0) | (wty[k] & ~tol1)) == 0) & (n < d.N);
+            if (SIM) ok &= !S.tbit(S.s_rmv, cw[k]);
+#pragma unroll
+            for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
+            ok &= (whp[k] & S.cur_hpc) == 0;
+            if (S.volA() && S.cur_vm && ok) ok = S.vol_ok(cw[k]);
+            if (S.keys(sflags) && ok) ok = S.node_compat(cw[k]);
+            okw[k] = ok;
+          }
+          S.template topo_node_stateK<NWA>(cw, okw, slw);
+#pragma unroll
+          for (int k = 0; k < NW; k++) {
+            const uint64_t m = wballot(okw[k]);
+            if (m) {
+              kj = k;
+              mj = m;
+              break;
+            }
+          }
+        } else {
 #pragma unroll
         for (int k = 0; k < NW; k++) {
           const int n = k * kWave + lane();
@@ -2303,14 +2513,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           }
           ok &= (whp[k] & S.cur_hpc) == 0;
           if (S.volA() && S.cur_vm && ok) ok = S.vol_ok(n);
-          if (S.keys(sflags) && ok) ok = rs_compatible(S.L, S.node_rs(n), S.s_pin, 0);
-          if (TOPO && S.t_mask && ok) ok = S.topo_node_state(n) == 1;  // every node is labelled here
+          if (S.keys(sflags) && ok) ok = S.node_compat(n);
+          if (TOPO && !KS_TOPO_WINDOW_BATCH && S.t_mask && ok) {  // every node is labelled here
+            int cn = n < d.N ? n : d.N - 1;
+            bool sl;
+            S.template topo_node_stateK<1>(&cn, &ok, &sl);
+          }
           const uint64_t m = wballot(ok);
           if (m) {
             kj = k;
             mj = m;
             break;
           }
+        }
         }
         asm volatile("; KS_MARK window_end");
         if (U(kj >= 0)) {
@@ -2336,6 +2551,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             if ((rdl(nfv, owner) & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
           } else if (S.keys(sflags) && lane() == owner) {
             rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, S.s_pin);
+            S.node_rs_changed(j);
           }
           if (TOPO && (S.t_sel | S.t_inv)) S.log_hgroups(nlog, S.topo_record(S.node_rs(j), -1, j, 0));  // existingnode.go:121
           S.log_commit(p, -(j + 1), nlog);
@@ -2348,23 +2564,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         scanFrom = NW * kWave;
       }
     }
-    for (int base = skipNodes ? d.N : scanFrom; U(base < d.N && !placed); base += 2 * kWave) {
-      bool ok0, ok1, sl0, sl1;
-      int nf0, nf1;
-      int64_t q0[RM], q1[RM];
-      S.node_ok2(base + lane(), s, sflags, pod, tol0, tol1, ok0, ok1, nf0, nf1, q0, q1, sl0, sl1);
-      uint64_t m0 = wballot(ok0), m1 = wballot(ok1);
+    for (int base = skipNodes ? d.N : scanFrom; U(base < d.N && !placed); base += KS_NODE_K * kWave) {
+      constexpr int KN = KS_NODE_K;
+      bool ok[KN], sl[KN];
+      int nf[KN];
+      int64_t q[KN][RM];
+      S.template node_okK<KN>(base + lane(), sflags, pod, tol0, tol1, ok, nf, q, sl);
+      uint64_t mk[KN];
+#pragma unroll
+      for (int i = 0; i < KN; i++) mk[i] = wballot(ok[i]);
       int j = -1;
       bool slowj = false;
-      if (m0 | m1) j = m0 ? base + ctz64(m0) : base + kWave + ctz64(m1);
+#pragma unroll
+      for (int i = KN - 1; i >= 0; i--)
+        if (mk[i]) j = base + i * kWave + ctz64(mk[i]);
       if (TOPO && d.tgUnlab) {  // unlabelled nodes before the first fast fit are decided wave-wide, in order
-        uint64_t s0 = wballot(sl0), s1 = wballot(sl1);
-        for (int half = 0; half < 2 && !slowj; half++) {
-          uint64_t sm = half ? s1 : s0;
-          const uint64_t fm = half ? m1 : m0;
-          if (fm) sm &= (fm & (~fm + 1)) - 1;  // only those before the half's first fast fit
+#pragma unroll
+        for (int i = 0; i < KN; i++) {
+          if (slowj) break;
+          uint64_t sm = wballot(sl[i]);
+          const uint64_t fm = mk[i];
+          if (fm) sm &= (fm & (~fm + 1)) - 1;  // only those before this block's first fast fit
           for (; sm && !slowj; sm &= sm - 1) {
-            const int jj = base + half * kWave + ctz64(sm);
+            const int jj = base + i * kWave + ctz64(sm);
             if (S.node_slow(jj, s, sflags)) {
               j = jj;
               slowj = true;
@@ -2375,17 +2597,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
       j = UI(j);
       if (j >= 0) {
-        const bool hi = j - base >= kWave;
+        const int hi = (j - base) >> 6;  // the block of the step holding node j
         S.algbytes += (int64_t)(j - base + 1) * (16 * R + 16);
         PH_BEGIN(t7);
         const int fl = slowj ? (sflags & ~SF_HAS_KEYS) : sflags;  // node_slow's record replaces rs_add
         if constexpr (SIM) {
           int64_t qs[RM];
+          int nfs = 0;
 #pragma unroll
-          for (int r = 0; r < RM; r++) qs[r] = hi ? q1[r] : q0[r];
+          for (int i = 0; i < KN; i++)
+            if (i == hi) {
+              nfs = nf[i];
+#pragma unroll
+              for (int r = 0; r < RM; r++) qs[r] = q[i][r];
+            }
           S.sim_node_commit(j, s, fl, pod, qs, nrs, false);
-          const int nf = rdl(hi ? nf1 : nf0, j & (kWave - 1));
-          if ((nf & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
+          const int nfj = rdl(nfs, j & (kWave - 1));
+          if ((nfj & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
         } else if (lane() == (j & (kWave - 1))) {
           S.node_commit(j, s, fl, pod);  // the owner lane of node j
         }
@@ -2399,7 +2627,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         PH_END(t7, 7);
         placed = true;
       } else {
-        S.algbytes += (int64_t)min(2 * kWave, d.N - base) * (16 * R + 16);
+        S.algbytes += (int64_t)min(KN * kWave, d.N - base) * (16 * R + 16);
       }
     }
     PH_END(t1, 1);
@@ -2620,9 +2848,9 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
                        2 * r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 +
-                       (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
+                       (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : d.fnOn ? r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
                        (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) +
-                                  r16(4 * (size_t)d.tgSmall) + (sim ? r16(4 * (size_t)((d.tgCntWords - d.tgSmall + 31) / 32)) : 0)
+                                  (sim ? r16(4 * (size_t)((d.tgCntWords - d.tgSmall + 31) / 32)) : 0)
                               : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)
   const size_t clmB = 16 + 16 * R + 4 * TW + 4 * R;      // tpl, cnt, req, max, rem, thr (+ rounding)
@@ -2630,6 +2858,13 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   const size_t tallocB = r16(8 * tot * R);
   const size_t tsortB = r16(8 * tot * R) + r16(4 * tot * R);
   size_t avail = budget > fixed + slack ? budget - fixed - slack : 0;
+  // The topology count table's LDS-resident prefix: the small-key groups; a Solve also keeps the
+  // hostname groups there when the whole table takes at most a quarter of what is left (a simulation's
+  // hostname counts are copy-on-write over the shared HBM table instead).
+  pl.tcl = d.G ? d.tgSmall : 0;
+  if (d.G && !sim && 4 * (size_t)d.tgCntWords <= avail / 4) pl.tcl = d.tgCntWords;
+  const size_t tclB = r16(4 * (size_t)pl.tcl);
+  avail = avail > tclB ? avail - tclB : 0;
   // The threshold filter needs the sorted lists only without negative requests.
   const size_t tablesB = tallocB + (d.negReq ? 0 : tsortB);
   pl.talloc = (!wideKO && tablesB + 64 * (posB + clmB) <= avail) ? 1 : 0;
@@ -2648,9 +2883,25 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   }
   pl.KO = (int)ko;
   pl.KL = (int)kl;
-  pl.lds = fixed + 3 * r16(4 * ko) + r16(8 * ko * R) + 2 * r16(4 * kl) + 2 * r16(8 * kl * R) + r16(4 * kl * TW) +
+  pl.lds = fixed + tclB + 3 * r16(4 * ko) + r16(8 * ko * R) + 2 * r16(4 * kl) + 2 * r16(8 * kl * R) + r16(4 * kl * TW) +
            r16(4 * kl * R) + (pl.tsort ? tsortB : 0) + (pl.talloc ? tallocB : 0);
   return pl;
+}
+
+void launch_feasibility(const KsDev& D, hipStream_t st) {
+  const int rows = D.d.S * D.d.NTPL;
+  if (D.d.TW <= 32) {  // two rows per wave step
+    const int blocks = std::min(2048, (rows + 7) / 8);
+    hipLaunchKernelGGL(k_feasibility<32>, dim3(blocks), dim3(256), 0, st, D);
+  } else {
+    const int blocks = std::min(2048, (rows + 3) / 4);
+    hipLaunchKernelGGL(k_feasibility<64>, dim3(blocks), dim3(256), 0, st, D);
+  }
+}
+
+void launch_feasibility_nodes(const KsDev& D, hipStream_t st) {
+  const int nbx = (D.d.N + 255) / 256;
+  hipLaunchKernelGGL(k_feasibility_nodes, dim3(D.d.FNR * nbx), dim3(256), 0, st, D, nbx);
 }
 
 hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
@@ -2670,8 +2921,13 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
   }
   if (D.d.fmOn) {
     if (feas) (void)hipEventRecord(feas[0], st);
-    hipLaunchKernelGGL(k_feasibility, dim3(D.d.S * D.d.NTPL), dim3(kWave), 0, st, D);
+    launch_feasibility(D, st);
     if (feas) (void)hipEventRecord(feas[1], st);
+  }
+  if (D.d.fnOn) {
+    if (feas) (void)hipEventRecord(feas[2], st);
+    launch_feasibility_nodes(D, st);
+    if (feas) (void)hipEventRecord(feas[3], st);
   }
   hipLaunchKernelGGL(k_init, dim3(512), dim3(256), 0, st, D, works_dev, nrep,
                      fixed_order ? fixed_order : (const int32_t*)qorder);
@@ -2684,7 +2940,8 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st) {
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
   if (nsims <= 0) return hipSuccess;
-  if (D.d.fmOn) hipLaunchKernelGGL(k_feasibility, dim3(D.d.S * D.d.NTPL), dim3(kWave), 0, st, D);
+  if (D.d.fmOn) launch_feasibility(D, st);
+  if (D.d.fnOn) launch_feasibility_nodes(D, st);
   return (D.d.G ? launch_sims_topo : launch_sims_plain)(D, works_dev, nsims, pl, st);
 }
 #endif

@@ -70,6 +70,10 @@ def lib():
     l.ks_results_feasibility_ms.restype = ctypes.c_double
     l.ks_results_feasibility_bytes.argtypes = [vp]
     l.ks_results_feasibility_bytes.restype = ctypes.c_double
+    l.ks_results_node_feasibility_ms.argtypes = [vp]
+    l.ks_results_node_feasibility_ms.restype = ctypes.c_double
+    l.ks_results_node_feasibility_bytes.argtypes = [vp]
+    l.ks_results_node_feasibility_bytes.restype = ctypes.c_double
     l.ks_cluster_state.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
     l.ks_free.argtypes = [vp]
     l.ks_last_error.restype = ctypes.c_char_p
@@ -134,6 +138,8 @@ class Results:
         self.algorithmic_bytes = alg_bytes
         self.feasibility_ms = 0.0     # k_feasibility inside this Solve (0: not launched)
         self.feasibility_bytes = 0.0  # its algorithmic bytes
+        self.node_feasibility_ms = 0.0     # k_feasibility_nodes inside this Solve (0: not launched)
+        self.node_feasibility_bytes = 0.0  # its algorithmic bytes
 
     def canonical(self):
         d = dict(self.doc)
@@ -247,6 +253,8 @@ class Scheduler:
                               lib().ks_results_solve_kernel_ms(r))
             out.feasibility_ms = lib().ks_results_feasibility_ms(r)
             out.feasibility_bytes = lib().ks_results_feasibility_bytes(r)
+            out.node_feasibility_ms = lib().ks_results_node_feasibility_ms(r)
+            out.node_feasibility_bytes = lib().ks_results_node_feasibility_bytes(r)
             return out
         finally:
             lib().ks_results_free(r)
