@@ -9,6 +9,19 @@
 #include <cstdlib>
 #include <vector>
 
+#ifndef REPRO_NOBREAK
+#define REPRO_NOBREAK 0
+#endif
+#ifndef REPRO_SELECT
+#define REPRO_SELECT 0
+#endif
+#ifndef REPRO_TAG
+#define REPRO_TAG "default"
+#endif
+#ifndef REPRO_KN
+#define REPRO_KN 4
+#endif
+
 constexpr int G = 8, NV = 256, N = 256, TRIALS = 4096;
 enum { TG_SPREAD = 0, TG_AFFINITY = 1, TG_ANTI = 2 };
 
@@ -63,11 +76,26 @@ __device__ __forceinline__ void batched(const In& x, const int* dom, const int* 
       for (int i = 0; i < KN; i++) cn[j][i] = (gs[j] >= 0 && v[j][i] >= 0) ? cnt[gs[j] * NV + v[j][i]] : 0;
 #pragma unroll
     for (int j = 0; j < TGC; j++) {
+#if REPRO_NOBREAK
+      if (gs[j] >= 0) {
+#else
       if (gs[j] < 0) break;
+      {
+#endif
       const int g = gs[j], type = x.type[g];
       const bool self = (x.t_sel >> g) & 1ull;
 #pragma unroll
       for (int i = 0; i < KN; i++) {
+#if REPRO_SELECT
+        const int cc = cn[j][i];
+        const bool hv = has[g * NV + (v[j][i] < 0 ? 0 : v[j][i])] != 0;
+        const bool sp = (long long)cc + (int)self - x.tmin[g] <= x.skew[g];
+        const bool af = hv && (x.tmin[g] ? cc != 0 : self);
+        const bool an = cc == 0 && hv;
+        const bool pass = cc >= 0 && (type == TG_SPREAD ? sp : type == TG_AFFINITY ? af : an);
+        const bool unl = v[j][i] < 0;
+        st[i] = unl ? (st[i] == 1 ? 2 : st[i]) : (pass ? st[i] : 0);
+#else
         if (v[j][i] < 0) {
           if (st[i] == 1) st[i] = 2;
           continue;
@@ -79,6 +107,8 @@ __device__ __forceinline__ void batched(const In& x, const int* dom, const int* 
         else if (type == TG_AFFINITY) pass = has[g * NV + v[j][i]] && (x.tmin[g] ? cc != 0 : self);
         else pass = cc == 0 && has[g * NV + v[j][i]];
         if (!pass) st[i] = 0;
+#endif
+      }
       }
     }
   }
@@ -96,9 +126,9 @@ __global__ __launch_bounds__(64) void k(const In* ins, const int* dom, const int
   int s1[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) s1[i] = st[i] ? serial1(x, dom, cnt, has, c[i]) : 0;
-  batched<4>(x, dom, cnt, has, c, st);
+  batched<REPRO_KN>(x, dom, cnt, has, c, st);
 #pragma unroll
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < REPRO_KN; i++)
     if (st[i] != s1[i]) atomicAdd(bad, 1);
 }
 
@@ -135,7 +165,7 @@ int main() {
   hipLaunchKernelGGL(k, dim3(TRIALS), dim3(64), 0, 0, dIns, dDom, dCnt, dHas, dBad);
   int bad = -1;
   hipMemcpy(&bad, dBad, 4, hipMemcpyDeviceToHost);
-  printf("topo_batch_repro: %d of %d (lane, node) decisions differ between the batched and serial forms\n", bad,
+  printf("topo_batch_repro[%s]: %d of %d (lane, node) decisions differ between the batched and serial forms\n", REPRO_TAG, bad,
          TRIALS * 64 * 4);
   return 0;
 }
