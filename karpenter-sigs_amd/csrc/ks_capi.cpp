@@ -415,6 +415,72 @@ static std::string hostnameCounts(const Host& h, int g, int seq, int64_t ord, in
   return o;
 }
 
+// Host replay of the device's bookkeeping before any result is rendered (a lost or stale device store turns
+// into a loud KS_ERR_INTERNAL, never a wrong Results): the commit log places each pod at most once (a Solve
+// records ST_FAILED per failed attempt and nothing on success, so the status is not cross-checked here); the
+// claim order is a permutation; every NodeClaim holds pods and options, its options are
+// positions of its template's list whose Allocatable fits the claim's requests (the device's Fits,
+// nodeclaim.go:225-260); every existing node's requests (its daemon remainder plus the pods placed there)
+// fit its Available (existingnode.go:78-83).  The claims' requests are replayed against the Merge below.
+static void replay_check(const Host& h, int nc, int nl, const std::vector<int32_t>& order,
+                         const std::vector<int32_t>& ctpl, const std::vector<int64_t>& creq,
+                         const std::vector<uint32_t>& crem, const std::vector<int32_t>& logp,
+                         const std::vector<int32_t>& logt) {
+  const KsDims& d = h.dims;
+  auto fail = [](const std::string& m) { throw KsError(KS_ERR_INTERNAL, "device state check: " + m); };
+  std::vector<char> placed((size_t)d.P, 0);
+  std::vector<int32_t> claimCount((size_t)nc, 0);
+  std::vector<int64_t> nodeReq(h.tab.n_req0);
+  for (int i = 0; i < nl; i++) {
+    const int p = logp[(size_t)i], t = logt[(size_t)i];
+    if (p < 0 || p >= d.P) fail("commit log pod index " + std::to_string(p) + " out of range");
+    if (placed[(size_t)p]++) fail("pod " + std::to_string(p) + " placed twice");
+    if (t >= 0) {
+      if (t >= nc) fail("commit log claim " + std::to_string(t) + " beyond " + std::to_string(nc));
+      claimCount[(size_t)t]++;
+    } else {
+      const int n = -t - 1;
+      if (n >= d.N) fail("commit log node " + std::to_string(n) + " out of range");
+      for (int r = 0; r < d.R; r++) nodeReq[(size_t)n * d.R + r] += h.tab.pod_req[(size_t)p * d.R + r];
+    }
+  }
+  for (int n = 0; n < d.N; n++)
+    for (int r = 0; r < d.R; r++) {
+      const int64_t q = nodeReq[(size_t)n * d.R + r], a = h.tab.n_avail[(size_t)n * d.R + r];
+      if (q != h.tab.n_req0[(size_t)n * d.R + r] && !(a >= 0 && q <= a))
+        fail("node " + std::to_string(n) + " over its Available for " + h.resNames[(size_t)r]);
+    }
+  std::vector<char> seen((size_t)nc, 0);
+  for (int k = 0; k < nc; k++) {
+    const int c = order[(size_t)k];
+    if (c < 0 || c >= nc || seen[(size_t)c]++) fail("NodeClaim order is not a permutation");
+  }
+  for (int c = 0; c < nc; c++) {
+    const int t = ctpl[(size_t)c];
+    if (t < 0 || t >= d.NTPL) fail("NodeClaim " + std::to_string(c) + " template out of range");
+    if (claimCount[(size_t)c] == 0) fail("NodeClaim " + std::to_string(c) + " holds no pod");
+    const int nIT = (int)h.tpls[(size_t)t].its.size();
+    int opts = 0;
+    for (int w = 0; w < d.TW; w++) {
+      const int lo = w * 32;
+      const uint32_t valid = nIT >= lo + 32 ? ~0u : nIT > lo ? (1u << (nIT - lo)) - 1u : 0u;
+      if (crem[(size_t)c * d.TW + w] & ~valid) fail("NodeClaim " + std::to_string(c) + " has options beyond its template's list");
+      for (uint32_t m = crem[(size_t)c * d.TW + w]; m; m &= m - 1) {
+        const int pos = lo + __builtin_ctz(m);
+        opts++;
+        const int it = h.tab.tpl_its[(size_t)h.tab.tpl_it_beg[(size_t)t] + pos];
+        for (int r = 0; r < d.R; r++) {
+          const int64_t a = h.tab.it_alloc[(size_t)it * d.R + r];
+          if (!(a >= 0 && creq[(size_t)c * d.R + r] <= a))
+            fail("NodeClaim " + std::to_string(c) + " keeps option " + h.its[(size_t)it].name + " its requests exceed (" +
+                 h.resNames[(size_t)r] + ")");
+        }
+      }
+    }
+    if (opts == 0) fail("NodeClaim " + std::to_string(c) + " has no instance type option");
+  }
+}
+
 // Rebuild Results from the replica-0 workspace.
 static ks_results* collect(ks_problem* pb, const KsWork& W) {
   Host& h = pb->host;
@@ -471,6 +537,7 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     }
   }
 
+  replay_check(h, nc, nl, order, ctpl, creq, crem, logp, logt);
   auto* res = new ks_results();
   res->counters = ctr;
   res->algbytes = (double)ctr[CT_ALGBYTES];

@@ -798,6 +798,37 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
     if (rec((int)s)[RF_ERROR] != KE_OK)
       throw KsError(rec((int)s)[RF_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
                     "simulation " + std::to_string(s) + " reported kernel error " + std::to_string(rec((int)s)[RF_ERROR]));
+  // Record invariants (a lost or stale device store becomes a loud error, not a wrong decision): the action
+  // agrees with the NodeClaim count (computeConsolidation, consolidation.go:113-194: Delete = none, Replace =
+  // exactly one); NewNodeClaims[0]'s options lie in its template's list and number RF_NOPT; filterByPrice's
+  // and filterOutSameType's outputs are subsets of their inputs.
+  for (size_t s = 0; s < c.sims.size(); s++) {
+    const int32_t* r = rec((int)s);
+    auto bad = [&](const char* what) {
+      throw KsError(KS_ERR_INTERNAL, "simulation " + std::to_string(s) + " record check: " + what);
+    };
+    if (r[RF_ACTION] < CA_NOOP || r[RF_ACTION] > CA_ERROR) bad("action out of range");
+    if (r[RF_NCLAIMS] < 0 || r[RF_HOSTINCR] < r[RF_NCLAIMS]) bad("NodeClaim counts");
+    if (r[RF_ACTION] == CA_DELETE && r[RF_NCLAIMS] != 0) bad("Delete with NodeClaims");
+    if (r[RF_ACTION] == CA_REPLACE && r[RF_NCLAIMS] != 1) bad("Replace without exactly one NodeClaim");
+    if (r[RF_NCLAIMS] == 0) continue;
+    if (r[RF_TPL] < 0 || r[RF_TPL] >= d.NTPL) bad("template out of range");
+    const int nIT = (int)h.tpls[(size_t)r[RF_TPL]].its.size();
+    const uint32_t* o = (const uint32_t*)r + RF_HDR;
+    int nopt = 0, nprice = 0, nsame = 0;
+    for (int w = 0; w < d.TW; w++) {
+      const int lo = w * 32;
+      const uint32_t valid = nIT >= lo + 32 ? ~0u : nIT > lo ? (1u << (nIT - lo)) - 1u : 0u;
+      if (o[w] & ~valid) bad("options beyond the template's list");
+      if (o[d.TW + w] & ~o[w]) bad("filterByPrice output not a subset of the options");
+      if (o[2 * d.TW + w] & ~o[d.TW + w]) bad("filterOutSameType output not a subset of filterByPrice's");
+      nopt += __builtin_popcount(o[w]);
+      nprice += __builtin_popcount(o[d.TW + w]);
+      nsame += __builtin_popcount(o[2 * d.TW + w]);
+    }
+    if (nopt != r[RF_NOPT] || nopt == 0) bad("option count");
+    if (nprice != r[RF_NPRICE] || nsame != r[RF_NSAME]) bad("price-filter counts");
+  }
   const int n = c.nPass;
   int64_t counter = c.hostnameSeed;
   std::map<int, int64_t> before;  // sim -> hostname counter before it ran

@@ -1005,29 +1005,24 @@ struct Solver {
       for (int j = 0; j < TGC; j++)
 #pragma unroll
         for (int i = 0; i < KN; i++) cn[j][i] = (gs[j] >= 0 && v[j][i] >= 0) ? tcnt(gs[j], v[j][i]) : 0;
+      // Branch-free per node: the per-lane `continue` / if-else form of this update is miscompiled at -O1
+      // and above for KN > 1 (scripts/repro/topo_batch_repro.hip reproduces it standalone).
 #pragma unroll
       for (int j = 0; j < TGC; j++) {
         if (gs[j] < 0) break;
-        const int g = gs[j], type = tg(g, TGM_TYPE);
-        const bool self = (t_sel >> g) & 1ull;
+        const int g = gs[j], type = tg(g, TGM_TYPE), tmin = s_tmin[g], skew = tg(g, TGM_SKEW);
+        const int self = (int)((t_sel >> g) & 1ull);
 #pragma unroll
         for (int i = 0; i < KN; i++) {
-          if (v[j][i] < 0) {
-            if (st[i] == 1) st[i] = 2;
-            continue;
-          }
-          const int cc = cn[j][i];
-          bool pass;
-          if (cc < 0) {
-            pass = false;  // unregistered: Get never returns it
-          } else if (type == TG_SPREAD) {
-            pass = (int64_t)cc + (int)self - s_tmin[g] <= tg(g, TGM_SKEW);
-          } else if (type == TG_AFFINITY) {  // a selected pod's domain, or the bootstrap for a self-selecting pod
-            pass = tpod_has(g, v[j][i]) && (s_tmin[g] ? cc != 0 : self);
-          } else {
-            pass = cc == 0 && tpod_has(g, v[j][i]);
-          }
-          if (!pass) st[i] = 0;
+          const int vv = v[j][i], cc = cn[j][i];
+          const bool unl = vv < 0;
+          const bool has = tpod_has(g, unl ? 0 : vv);
+          const bool sp = (int64_t)cc + self - tmin <= skew;
+          const bool af = has && (tmin ? cc != 0 : self != 0);
+          const bool an = cc == 0 && has;
+          const bool pass = cc >= 0 && (type == TG_SPREAD ? sp : type == TG_AFFINITY ? af : an);
+          const int s0 = st[i];
+          st[i] = unl ? (s0 == 1 ? 2 : s0) : (pass ? s0 : 0);
         }
       }
     }
