@@ -105,6 +105,20 @@ def _create(cls, snap_json):
     return h, (time.perf_counter() - t) * 1000.0
 
 
+def _create_binary(h, cls):
+    """(save_ms, create_binary_ms, snapshot bytes): the handle rebuilt from its binary snapshot (the second of
+    two loads, like _create), i.e. what a caller that keeps the encoded problem pays instead of create_ms."""
+    t = time.perf_counter()
+    blob = h.save()
+    save_ms = (time.perf_counter() - t) * 1000.0
+    cls.from_binary(blob).close()
+    t = time.perf_counter()
+    x = cls.from_binary(blob)
+    load_ms = (time.perf_counter() - t) * 1000.0
+    x.close()
+    return save_ms, load_ms, len(blob)
+
+
 def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0):
     """C5 (BASELINE.json configs[4]): one consolidation pass = every candidate-deletion simulation of
     a 5k-node / 100k-pod cluster (5000 single-node + 100 multi-node prefix sims), sharded over the
@@ -119,6 +133,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
     snap = json.dumps(synth.config5(args.cons_nodes) if not topology else
                       synth.cluster_snapshot(args.cons_nodes, 20, 400, seed=4205, topology=topology))
     c, create_ms = _create(Consolidator, snap)
+    save_ms, create_bin_ms, snap_bytes = _create_binary(c, Consolidator)
     per, rb = c.records_per_rank(world), c.record_bytes
     dev = "cuda:%d" % local
     out = gathered = None
@@ -225,6 +240,11 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
         # ks_cons_create: parse + NewCandidate + encode + upload of the cluster snapshot (once per pass in
         # the reference's terms); e2e = a fresh snapshot every pass: create + first pass (plan + run + decide)
         "create_ms": round(create_ms, 3),
+        # the same handle from its binary snapshot (ks_cons_create_binary: no JSON parse, no NewCandidate,
+        # no encode; upload + queue ranks), and what writing that snapshot cost (ks_cons_save)
+        "create_binary_ms": round(create_bin_ms, 3),
+        "save_ms": round(save_ms, 3),
+        "snapshot_bytes": snap_bytes,
         "first_pass_ms": round(first_ms, 3),
         "e2e_cands_per_s": round(c.num_sims / ((create_ms + first_ms) / 1000.0), 1),
         "decision": {"multi": [doc["multi"]["command"]["action"], len(doc["multi"]["command"]["candidates"])],
@@ -354,6 +374,7 @@ def main():
     snap = synth.config2(args.pods) if args.its == 400 else synth.benchmark_snapshot(args.pods, args.its, 42, False)
     snap_json = json.dumps(snap)
     sch, create_ms = _create(Scheduler, snap_json)
+    save_ms, create_bin_ms, snap_bytes = _create_binary(sch, Scheduler)
 
     # one full solve (results copied back and rendered) to verify the result shape outside the timed region
     t = time.perf_counter()
@@ -455,6 +476,7 @@ def main():
         # the drop-in caller's cost (never `value`): ks_problem_create = parse + encode + upload of the
         # snapshot; e2e = create + one Solve with its results copied back and rendered
         "create_ms": round(create_ms, 3),
+        "create_binary_ms": round(create_bin_ms, 3),  # Scheduler.from_binary(save()): upload only
         "full_solve_ms": round(full_ms, 3),
         # a Solve with its Results read through the structured accessors, per step, and that rate
         "structured_solve_ms": round(structured_ms, 3),

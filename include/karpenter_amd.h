@@ -51,6 +51,16 @@ typedef struct ks_solve_opts {
 int ks_problem_create(const char* snapshot_json, size_t len, ks_problem** out);
 void ks_problem_free(ks_problem* p);
 
+/* Binary snapshot of an encoded problem (the whole host model NewScheduler built: universes, tables, pods,
+ * relaxation chains, topology): ks_problem_save writes it (free with ks_free); ks_problem_create_binary
+ * rebuilds the problem from it and uploads it, skipping the JSON parse and the encode.  A snapshot is tied to
+ * the library build that wrote it (a blob from another build is refused with KS_ERR_PARSE). */
+int ks_problem_save(const ks_problem* p, void** buf, size_t* len);
+int ks_problem_create_binary(const void* buf, size_t len, ks_problem** out);
+/* Host-only (no device): encode snapshot_json, save it, load the bytes and save again; KS_OK when the two
+ * byte strings are identical.  *bytes: the snapshot size. */
+int ks_snapshot_check(const char* snapshot_json, size_t len, size_t* bytes);
+
 /* Host-only encode of a snapshot (no device needed): returns JSON with the universe sizes (keys,
  * value words, resources, instance types, relaxation states).  Diagnostics / CPU tests. */
 int ks_problem_inspect(const char* snapshot_json, size_t len, char** dims_json);
@@ -120,6 +130,10 @@ double ks_results_algorithmic_bytes(const ks_results* r);
  * 42-88); each ends in the computeConsolidation decision (consolidation.go:113-194) on the GPU. */
 typedef struct ks_cons ks_cons;
 int ks_cons_create(const char* snapshot_json, size_t len, ks_cons** out);
+/* Binary snapshot of a consolidation handle (host model + candidates in disruption-cost order + the
+ * simulation plan), as for ks_problem_save / ks_problem_create_binary. */
+int ks_cons_save(const ks_cons* c, void** buf, size_t* len);
+int ks_cons_create_binary(const void* buf, size_t len, ks_cons** out);
 /* Host-only (no device): JSON {candidates:[{name, disruptionCost, pods}], sims, multiPrefixes, recordBytes}. */
 int ks_cons_inspect(const char* snapshot_json, size_t len, char** out_json);
 void ks_cons_free(ks_cons* c);

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/karpenter_amd.h"
+#include "ks_archive.h"
 #include "ks_host.h"
 #include "ks_runtime.h"
 
@@ -249,11 +250,13 @@ void ks_upload(ks_problem* pb) {
   if (fnState.empty()) fnState.push_back(0);
   size_t o_fnr = put(fnrow.data(), fnrow.size() * 4);
   size_t o_fns = put(fnState.data(), fnState.size() * 4);
+  // one allocation, zeroed on the device (padding and empty tables), each table copied from its host vector
+  // (no host staging image of the whole problem)
   HIPCHK(hipMalloc(&pb->dbuf, a.total));
-  std::vector<char> staging(a.total, 0);
+  HIPCHK(hipMemsetAsync(pb->dbuf, 0, a.total, pb->stream));
   for (auto& it : items)
-    if (it.bytes) memcpy(staging.data() + it.off, it.src, it.bytes);
-  HIPCHK(hipMemcpy(pb->dbuf, staging.data(), a.total, hipMemcpyHostToDevice));
+    if (it.bytes) HIPCHK(hipMemcpyAsync((char*)pb->dbuf + it.off, it.src, it.bytes, hipMemcpyHostToDevice, pb->stream));
+  HIPCHK(hipStreamSynchronize(pb->stream));
   char* b = (char*)pb->dbuf;
   KsDev& D = pb->dev;
   // k_feasibility's output: one row of TW words per (relaxation state, template), rewritten by every
@@ -806,6 +809,25 @@ int ks_device_count(void) {
   return n;
 }
 
+// The device half of NewScheduler for an encoded host model: upload, queue-sort workspaces, the host's
+// NewQueue order when pods tie.
+static void problem_device_init(ks_problem* pb) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw KsError(KS_ERR_HIP, "no HIP device visible");
+  HIPCHK(hipGetDevice(&pb->device));
+  HIPCHK(hipStreamCreateWithFlags(&pb->stream, hipStreamNonBlocking));
+  ks_upload(pb);
+  size_t np = std::max(pb->host.dims.P, 1);
+  HIPCHK(hipMalloc(&pb->skeys, 2 * np * sizeof(uint64_t)));
+  HIPCHK(hipMalloc(&pb->svals, 2 * np * sizeof(int32_t)));
+  pb->stempBytes = std::max<size_t>(queue_sort_temp_bytes((int)np), 256);
+  HIPCHK(hipMalloc(&pb->stemp, pb->stempBytes));
+  if (!pb->host.hostQueue.empty()) {
+    HIPCHK(hipMalloc(&pb->hqorder, 4 * np));
+    HIPCHK(hipMemcpy(pb->hqorder, pb->host.hostQueue.data(), 4 * pb->host.hostQueue.size(), hipMemcpyHostToDevice));
+  }
+}
+
 int ks_problem_create(const char* json, size_t len, ks_problem** out) {
   API_TRY
   if (!json || !out) throw KsError(KS_ERR_ARG, "null argument");
@@ -813,23 +835,96 @@ int ks_problem_create(const char* json, size_t len, ks_problem** out) {
   std::unique_ptr<ks_problem> pb(new ks_problem());
   pb->host.build(root);
   ksjson::release_async(std::move(root));
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw KsError(KS_ERR_HIP, "no HIP device visible");
-  HIPCHK(hipGetDevice(&pb->device));
-  HIPCHK(hipStreamCreateWithFlags(&pb->stream, hipStreamNonBlocking));
-  ks_upload(pb.get());
-  {
-    size_t n = std::max(pb->host.dims.P, 1);
-    HIPCHK(hipMalloc(&pb->skeys, 2 * n * sizeof(uint64_t)));
-    HIPCHK(hipMalloc(&pb->svals, 2 * n * sizeof(int32_t)));
-    pb->stempBytes = std::max<size_t>(queue_sort_temp_bytes((int)n), 256);
-    HIPCHK(hipMalloc(&pb->stemp, pb->stempBytes));
-    if (!pb->host.hostQueue.empty()) {
-      HIPCHK(hipMalloc(&pb->hqorder, 4 * n));
-      HIPCHK(hipMemcpy(pb->hqorder, pb->host.hostQueue.data(), 4 * pb->host.hostQueue.size(), hipMemcpyHostToDevice));
-    }
-  }
+  problem_device_init(pb.get());
   *out = pb.release();
+  return KS_OK;
+  API_CATCH
+}
+
+// --- binary snapshot (ks_archive.h, ks_snapshot.cpp) ----------------------------------------------------
+extern "C++" {
+namespace {
+constexpr char kProblemMagic[8] = {'K', 'S', 'P', 'R', 'O', 'B', '0', '1'};
+}  // namespace
+
+void snapshot_header(ArOut& a, const char magic[8]) {
+  a.raw(magic, 8);
+  uint32_t v[4] = {1u, (uint32_t)sizeof(KsDims), (uint32_t)sizeof(KeyMeta), (uint32_t)sizeof(Host)};
+  a.raw(v, sizeof(v));
+}
+void snapshot_check_header(ArIn& a, const char magic[8]) {
+  char m[8];
+  uint32_t v[4];
+  a.raw(m, 8);
+  a.raw(v, sizeof(v));
+  if (memcmp(m, magic, 8) != 0) throw KsError(KS_ERR_PARSE, "not a binary snapshot of this kind");
+  if (v[0] != 1u || v[1] != sizeof(KsDims) || v[2] != sizeof(KeyMeta) || v[3] != sizeof(Host))
+    throw KsError(KS_ERR_PARSE, "binary snapshot from another build of the library");
+}
+char* snapshot_bytes(const std::string& s) {
+  char* b = (char*)malloc(std::max<size_t>(s.size(), 1));
+  if (!b) throw KsError(KS_ERR_CAPACITY, "out of host memory");
+  memcpy(b, s.data(), s.size());
+  return b;
+}
+}  // extern "C++"
+
+int ks_problem_save(const ks_problem* p, void** buf, size_t* len) {
+  API_TRY
+  if (!p || !buf || !len) throw KsError(KS_ERR_ARG, "null argument");
+  ArOut a;
+  snapshot_header(a, kProblemMagic);
+  host_save(a, const_cast<Host&>(p->host));
+  *buf = snapshot_bytes(a.buf);
+  *len = a.buf.size();
+  return KS_OK;
+  API_CATCH
+}
+
+int ks_problem_create_binary(const void* buf, size_t len, ks_problem** out) {
+  API_TRY
+  if (!buf || !out) throw KsError(KS_ERR_ARG, "null argument");
+  std::unique_ptr<ks_problem> pb(new ks_problem());
+  try {
+    ArIn a{(const char*)buf, (const char*)buf + len};
+    snapshot_check_header(a, kProblemMagic);
+    host_load(a, pb->host);
+    if (a.p != a.end) throw KsError(KS_ERR_PARSE, "binary snapshot has trailing bytes");
+  } catch (const ArchiveError& e) {
+    throw KsError(KS_ERR_PARSE, e.what());
+  }
+  problem_device_init(pb.get());
+  *out = pb.release();
+  return KS_OK;
+  API_CATCH
+}
+
+// Host-only check of the snapshot format: encode the snapshot, save it, load the bytes into a fresh model and
+// save that again; the two byte strings must be identical (*bytes: the snapshot size).
+int ks_snapshot_check(const char* json, size_t len, size_t* bytes) {
+  API_TRY
+  if (!json) throw KsError(KS_ERR_ARG, "null argument");
+  PhaseTimer pt("ks_snapshot_check");
+  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  Host h;
+  h.build(root);
+  pt.mark("parse + encode");
+  ArOut a;
+  host_save(a, h);
+  pt.mark("save");
+  Host g;
+  try {
+    ArIn in{a.buf.data(), a.buf.data() + a.buf.size()};
+    host_load(in, g);
+    pt.mark("load");
+    if (in.p != in.end) throw KsError(KS_ERR_INTERNAL, "snapshot reload left bytes");
+  } catch (const ArchiveError& e) {
+    throw KsError(KS_ERR_INTERNAL, e.what());
+  }
+  ArOut b;
+  host_save(b, g);
+  if (bytes) *bytes = a.buf.size();
+  if (a.buf != b.buf) throw KsError(KS_ERR_INTERNAL, "snapshot save -> load -> save is not the identity");
   return KS_OK;
   API_CATCH
 }

@@ -30,6 +30,7 @@
 
 #include "../../include/karpenter_amd.h"
 #include "ks_gosort.h"
+#include "ks_archive.h"
 #include "ks_host.h"
 #include "ks_runtime.h"
 
@@ -240,7 +241,9 @@ struct ks_cons {
   void free_launch() { L.release(); }
   ~ks_cons() {
     int prev = -1;
-    if (pb && hipGetDevice(&prev) == hipSuccess) (void)hipSetDevice(pb->device);
+    // (a handle whose load failed before device init has device -1: nothing to select, and hipSetDevice(-1)
+    // would leave a sticky error for the caller's next launch)
+    if (pb && pb->device >= 0 && hipGetDevice(&prev) == hipSuccess) (void)hipSetDevice(pb->device);
     free_launch();
     if (rank) (void)hipFree(rank);
     for (hipEvent_t e : ev)
@@ -1093,19 +1096,16 @@ std::string validate_json(ks_cons& c, const Value& cmd) {
 
 extern "C" {
 
-int ks_cons_create(const char* json, size_t len, ks_cons** out) {
-  API_TRY
-  if (!json || !out) throw KsError(KS_ERR_ARG, "null argument");
-  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
-  std::unique_ptr<ks_cons> c(new ks_cons());
-  build_cons(*c, root);
-  ksjson::release_async(std::move(root));
+// The device half of a consolidation handle: upload + every pod's global NewQueue rank.
+static void cons_device_init(ks_cons* c, PhaseTimer& pt) {
   ks_problem& pb = *c->pb;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw KsError(KS_ERR_HIP, "no HIP device visible");
   HIPCHK(hipGetDevice(&pb.device));
   HIPCHK(hipStreamCreateWithFlags(&pb.stream, hipStreamNonBlocking));
+  pt.mark("device + stream");
   ks_upload(&pb);
+  pt.mark("upload");
   // global NewQueue rank of every pod (each simulation's queue is this order restricted to its pods)
   const int P = pb.host.dims.P;
   const size_t np = std::max(P, 1);
@@ -1120,6 +1120,69 @@ int ks_cons_create(const char* json, size_t len, ks_cons** out) {
   HIPCHK(rank_from_order(order, c->rank, P, pb.stream));
   HIPCHK(hipStreamSynchronize(pb.stream));
   (void)hipFree(order);
+  pt.mark("queue rank");
+}
+
+int ks_cons_create(const char* json, size_t len, ks_cons** out) {
+  API_TRY
+  if (!json || !out) throw KsError(KS_ERR_ARG, "null argument");
+  PhaseTimer pt("ks_cons_create");
+  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  pt.mark("json parse");
+  std::unique_ptr<ks_cons> c(new ks_cons());
+  build_cons(*c, root);
+  ksjson::release_async(std::move(root));
+  pt.mark("build_cons");
+  cons_device_init(c.get(), pt);
+  *out = c.release();
+  return KS_OK;
+  API_CATCH
+}
+
+// --- binary snapshot of a consolidation handle: the host model + candidates + simulation plan ----------
+extern "C++" {
+namespace ks {
+template <class A> void io(A& a, ks_cons::Cand& x) { io_all(a, x.node, x.name, x.pool, x.ct, x.zone, x.it, x.cost, x.pods); }
+template <class A> void io(A& a, ks_cons::Sim& x) { io_all(a, x.cands, x.multi); }
+}  // namespace ks
+namespace {
+constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '1'};
+template <class A> void cons_io(A& a, ks_cons& c) {
+  io_all(a, c.cands, c.nPass, c.sims, c.multiHi, c.pending, c.deleting, c.nominated, c.hostnameSeed, c.recWords);
+}
+}  // namespace
+}  // extern "C++"
+
+int ks_cons_save(const ks_cons* c, void** buf, size_t* len) {
+  API_TRY
+  if (!c || !buf || !len) throw KsError(KS_ERR_ARG, "null argument");
+  ArOut a;
+  snapshot_header(a, kConsMagic);
+  host_save(a, c->pb->host);
+  cons_io(a, const_cast<ks_cons&>(*c));
+  *buf = snapshot_bytes(a.buf);
+  *len = a.buf.size();
+  return KS_OK;
+  API_CATCH
+}
+
+int ks_cons_create_binary(const void* buf, size_t len, ks_cons** out) {
+  API_TRY
+  if (!buf || !out) throw KsError(KS_ERR_ARG, "null argument");
+  PhaseTimer pt("ks_cons_create_binary");
+  std::unique_ptr<ks_cons> c(new ks_cons());
+  c->pb.reset(new ks_problem());
+  try {
+    ArIn a{(const char*)buf, (const char*)buf + len};
+    snapshot_check_header(a, kConsMagic);
+    host_load(a, c->pb->host);
+    cons_io(a, *c);
+    if (a.p != a.end) throw KsError(KS_ERR_PARSE, "binary snapshot has trailing bytes");
+  } catch (const ArchiveError& e) {
+    throw KsError(KS_ERR_PARSE, e.what());
+  }
+  pt.mark("load");
+  cons_device_init(c.get(), pt);
   *out = c.release();
   return KS_OK;
   API_CATCH

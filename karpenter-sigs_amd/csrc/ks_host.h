@@ -247,6 +247,12 @@ struct PhaseTimer {
   }
 };
 
+// Binary snapshot of the host model (ks_snapshot.cpp, ks_archive.h)
+struct ArOut;
+struct ArIn;
+void host_save(ArOut& a, Host& h);
+void host_load(ArIn& a, Host& h);
+
 std::string qlist_json(const QList& l);  // resources.String (pretty.Concise)
 std::string go_quote(const std::string& s);
 std::string normalize_key(const std::string& k);

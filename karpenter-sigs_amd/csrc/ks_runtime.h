@@ -94,6 +94,7 @@ struct DeviceGuard {
                                     std::to_string(dev) + ")");
     HIPCHK(hipGetDevice(&prev));
     if (prev != dev) HIPCHK(hipSetDevice(dev));
+    (void)hipGetLastError();  // clear a sticky error of an unrelated earlier call: the launches check it
   }
   ~DeviceGuard() {
     if (prev >= 0) (void)hipSetDevice(prev);
@@ -105,6 +106,12 @@ struct DeviceGuard {
 
 // Upload the host tables to one HBM allocation and point pb->dev at them.
 void ks_upload(ks_problem* pb);
+
+// Binary snapshots (ks_capi.cpp): a magic, the format version and the sizes of the shared structs.
+namespace ks { struct ArOut; struct ArIn; }
+void snapshot_header(ks::ArOut& a, const char magic[8]);
+void snapshot_check_header(ks::ArIn& a, const char magic[8]);
+char* snapshot_bytes(const std::string& s);
 
 #define API_TRY try {
 #define API_CATCH                                  \

@@ -76,6 +76,11 @@ def lib():
     l.ks_results_node_feasibility_bytes.restype = ctypes.c_double
     l.ks_cluster_state.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
     l.ks_free.argtypes = [vp]
+    l.ks_problem_save.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+    l.ks_problem_create_binary.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
+    l.ks_snapshot_check.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+    l.ks_cons_save.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+    l.ks_cons_create_binary.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
     l.ks_last_error.restype = ctypes.c_char_p
     l.ks_build_info.restype = ctypes.c_char_p
     _lib = l
@@ -225,14 +230,44 @@ def _read_structured(l, r):
     return claims, nodes, errors
 
 
-class Scheduler:
-    """NewScheduler(...) on the GPU: the snapshot is encoded once and stays resident in HBM."""
+def _take_bytes(fn, handle):
+    buf, n = ctypes.c_void_p(), ctypes.c_size_t()
+    _check(fn(handle, ctypes.byref(buf), ctypes.byref(n)))
+    try:
+        return ctypes.string_at(buf, n.value)
+    finally:
+        lib().ks_free(buf)
 
-    def __init__(self, snapshot):
-        b = _encode(snapshot)
+
+def snapshot_check(snapshot):
+    """Host-only: encode, save, load, save again; raises unless the two snapshots are byte-identical.
+    Returns the snapshot size in bytes."""
+    b = _encode(snapshot)
+    n = ctypes.c_size_t()
+    _check(lib().ks_snapshot_check(b, len(b), ctypes.byref(n)))
+    return n.value
+
+
+class Scheduler:
+    """NewScheduler(...) on the GPU: the snapshot is encoded once and stays resident in HBM.
+    Scheduler.from_binary(blob) rebuilds one from save()'s binary snapshot (no JSON parse, no encode)."""
+
+    def __init__(self, snapshot, _binary=None):
         h = ctypes.c_void_p()
-        _check(lib().ks_problem_create(b, len(b), ctypes.byref(h)))
+        if _binary is not None:
+            _check(lib().ks_problem_create_binary(_binary, len(_binary), ctypes.byref(h)))
+        else:
+            b = _encode(snapshot)
+            _check(lib().ks_problem_create(b, len(b), ctypes.byref(h)))
         self._h = h
+
+    @classmethod
+    def from_binary(cls, blob):
+        return cls(None, _binary=bytes(blob))
+
+    def save(self):
+        """The binary snapshot of the encoded problem (bytes)."""
+        return _take_bytes(lib().ks_problem_save, self._h)
 
     def solve(self, replicas=1, device=-1, simulation_mode=True, timing_only=False, lds_budget=0):
         """Solve(ctx, pods) with fresh scheduler state; replicas>1 runs that many independent copies
@@ -331,16 +366,27 @@ class Consolidator:
     runs on the GPU with its computeConsolidation decision; `decide` replays the reference's
     sequential choice.  Sharding: rank r of `world` runs simulations s with s % world == r."""
 
-    def __init__(self, snapshot):
+    def __init__(self, snapshot, _binary=None):
         l = _cons_lib()
-        b = _encode(snapshot)
         h = ctypes.c_void_p()
-        _check(l.ks_cons_create(b, len(b), ctypes.byref(h)))
+        if _binary is not None:
+            _check(l.ks_cons_create_binary(_binary, len(_binary), ctypes.byref(h)))
+        else:
+            b = _encode(snapshot)
+            _check(l.ks_cons_create(b, len(b), ctypes.byref(h)))
         self._h = h
         self.num_candidates = l.ks_cons_num_candidates(h)
         self.num_sims = l.ks_cons_num_sims(h)
         self.record_bytes = l.ks_cons_record_bytes(h)
         self.requirement_words = l.ks_cons_requirement_words(h)
+
+    @classmethod
+    def from_binary(cls, blob):
+        """A handle from save()'s binary snapshot (host model + candidates + simulation plan)."""
+        return cls(None, _binary=bytes(blob))
+
+    def save(self):
+        return _take_bytes(_cons_lib().ks_cons_save, self._h)
 
     def records_per_rank(self, world=1):
         return _cons_lib().ks_cons_records_per_rank(self._h, world)
