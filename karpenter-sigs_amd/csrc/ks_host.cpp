@@ -409,6 +409,10 @@ void Host::addNSR(std::vector<uint32_t>& rec, const std::string& key0, const std
 void Host::addLabels(std::vector<uint32_t>& rec, const std::map<std::string, std::string>& labels) const {
   for (auto& kv : labels) addNSR(rec, kv.first, "In", {kv.second});
 }
+void Host::addNodeLabels(std::vector<uint32_t>& rec, const std::map<std::string, std::string>& labels) const {
+  for (auto& kv : labels)
+    if (keyId.count(normalize_key(kv.first))) addNSR(rec, kv.first, "In", {kv.second});
+}
 
 // newPodRequirements (requirements.go:64-100).  Sorting the preferred terms mutates the pod, as
 // the reference's sort.Slice does.
@@ -631,7 +635,7 @@ void Host::build(const Value& root) {
     for (auto& o : it.offers) { intern(kZone, o.first); intern(kCT, o.second); }
   }
   for (auto& t : tpls) { visitNSR(t.reqs); visitLabels(t.labels); }
-  for (auto& n : nodes) { visitLabels(n.labels); intern(kHostname, n.hostName); }
+  for (auto& n : nodes) intern(kHostname, n.hostName);  // (node labels below: only the keys something mentions)
   for (auto& p : pods) visitPod(p);
   for (auto& p : daemons) visitPod(p);
   // topology keys and the domains the cluster's nodes contribute (countDomains, updateInverseAffinities)
@@ -656,6 +660,16 @@ void Host::build(const Value& root) {
       }
     }
   }
+  // An existing node's labels enter its requirement record only for keys some requirement, template label or
+  // topology key mentions: ExistingNode.Add's strict Compatible(node, pod) (existingnode.go:97-104,
+  // requirements.go:163-174) reads the node's value of a key only when the pod names it, the daemon overhead
+  // test likewise, and a node's record is never rendered.  So the label keys only nodes carry (a production
+  // node has dozens) do not count against the 64-key universe and cost no record words.
+  for (auto& n : nodes)
+    for (auto& kv : n.labels) {
+      const std::string k = normalize_key(kv.first);
+      if (keyId.count(k)) intern(k, kv.second);
+    }
   for (auto& kv : valueSet_[kHostname])
     if (kv.rfind("hostname-placeholder-", 0) == 0)
       throw KsError(-2, "input names a hostname-placeholder value (reserved for new NodeClaims)");
@@ -1073,7 +1087,7 @@ void Host::build(const Value& root) {
     tab.n_flags[i] = (!n.initialized || !n.ready) ? NF_UNUSABLE : 0;
     tab.n_hp0[i] = hpMask(n.hostPorts);
     std::vector<uint32_t> lab = emptyRec();
-    addLabels(lab, n.labels);
+    addNodeLabels(lab, n.labels);  // the keys of the universe only (see the universe build)
     QList dreq;
     int nd = 0;
     for (size_t d = 0; d < daemons.size(); d++) {

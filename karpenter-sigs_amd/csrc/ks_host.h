@@ -216,6 +216,8 @@ struct Host {
   void addNSR(std::vector<uint32_t>& rec, const std::string& key, const std::string& op,
               const std::vector<std::string>& vals) const;
   void addLabels(std::vector<uint32_t>& rec, const std::map<std::string, std::string>& labels) const;
+  // an existing node's labels, restricted to the universe's keys (node-only keys are not interned: build)
+  void addNodeLabels(std::vector<uint32_t>& rec, const std::map<std::string, std::string>& labels) const;
   std::vector<uint32_t> podRequirements(PodH& p, bool all) const;
   uint64_t tolMask(const std::vector<TolH>& tols, uint64_t out[2]) const;
   int64_t toDev(int r, const Qty& q) const;

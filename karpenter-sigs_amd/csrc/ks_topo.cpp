@@ -145,7 +145,7 @@ void Host::buildTopology() {
     if (nodeRecsBuilt) return;
     for (auto& n : nodeLabelsByName) {
       std::vector<uint32_t> r = emptyRec();
-      addLabels(r, n.second);
+      addNodeLabels(r, n.second);  // (the filter terms name only universe keys)
       nodeRecs.emplace(n.first, std::move(r));
     }
     nodeRecsBuilt = true;
