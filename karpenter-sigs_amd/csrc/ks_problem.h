@@ -270,7 +270,8 @@ enum Counter {
   CT_ABI = 24,     // counters ks_cons_sim_counters hands out (include/karpenter_amd.h)
   CT_RUNS = 24,    // runs of identical pods placed in one step (simulation fast path; Solve NodeClaim runs)
   CT_RUN_PODS,     // pods those runs placed
-  CT_NCOUNTERS = 26
+  CT_SORT_EXACT,   // claim re-sorts that ran the lane-0 pdqsort (not the wave-parallel partialInsertionSort)
+  CT_NCOUNTERS = 27
 };
 enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3 };
 

@@ -43,6 +43,9 @@
 #ifndef KS_TOPO_WINDOW_BATCH  // register window + topology: every window node's topology loads issued at once
 #define KS_TOPO_WINDOW_BATCH 0
 #endif
+#ifndef KS_SORT_LANE0  // 1: the claim re-sort's exact pdqsort on lane 0 (the round-2 form)
+#define KS_SORT_LANE0 0
+#endif
 #ifndef KS_TOPO_NODE_SERIAL  // the topology node test one node at a time (see topo_node_stateK)
 #define KS_TOPO_NODE_SERIAL 1
 #endif
@@ -1824,26 +1827,28 @@ struct Solver {
   // steps finds the next descent by ballot, swaps the pair, then moves the smaller entry left past
   // every greater one and the greater entry right past every smaller one.  Returns its result and
   // widens [tlo, thi] to the positions it moved.
-  __device__ __forceinline__ bool pis_wave(int n, int& tlo, int& thi) {
-    int i = 1;
+  __device__ __forceinline__ bool pis_wave(int a, int b, int& tlo, int& thi) {
+    int i = a + 1;
     for (int step = 0; step < 5; step++) {
-      i = pis_descent(i, n);
-      if (i == n) return true;
-      if (n < 50) return false;
+      i = pis_descent(i, b);
+      if (i == b) return true;
+      if (b - a < 50) return false;
       const int x = uni(s_okey[i]), y = uni(s_okey[i - 1]);  // after the swap: x at i-1, y at i
-      int p = i - 1;  // x passes the entries q < i-1 with x < key[q]
-      for (int hi = i - 1; hi > 0; hi -= kWave) {
-        const int q = hi - 1 - lane();
-        const uint64_t m = wballot(q >= 0 && !(x < s_okey[q]));
-        if (m) { p = hi - ctz64(m); break; }
-        p = hi - kWave > 0 ? hi - kWave : 0;
+      int p = i - 1;  // x passes the entries q < i-1 with x < key[q] (Go's loop runs down to index 1,
+      if (i - a >= 2) {  // not to a, once the pair is at least two past a)
+        for (int hi = i - 1; hi > 0; hi -= kWave) {
+          const int q = hi - 1 - lane();
+          const uint64_t m = wballot(q >= 0 && !(x < s_okey[q]));
+          if (m) { p = hi - ctz64(m); break; }
+          p = hi - kWave > 0 ? hi - kWave : 0;
+        }
       }
       int r = i;  // y passes the entries q > i with key[q] < y
-      for (int lo = i + 1; lo < n; lo += kWave) {
+      for (int lo = i + 1; lo < b; lo += kWave) {
         const int q = lo + lane();
-        const uint64_t m = wballot(q < n && !(s_okey[q] < y));
+        const uint64_t m = wballot(q < b && !(s_okey[q] < y));
         if (m) { r = lo + ctz64(m) - 1; break; }
-        r = lo + kWave - 1 < n - 1 ? lo + kWave - 1 : n - 1;
+        r = lo + kWave - 1 < b - 1 ? lo + kWave - 1 : b - 1;
       }
       pis_move(i, p);  // x (at i before the swap) to p; y moves from i-1 to i with the shifted run
       pis_move(i, r);  // y to r
@@ -1852,7 +1857,195 @@ struct Solver {
     }
     return false;
   }
-  __device__ __forceinline__ void sort_claims(int n) {
+
+  // --- the rest of pdqsort_func, wave-parallel and swap-for-swap equal to Go's (ks_gosort.h) -------
+  // Exchange of two uniform positions (wave-wide stores of uniform values).
+  __device__ __forceinline__ void w_swap(int i, int j) {
+    const int ki = uni(s_okey[i]), kj = uni(s_okey[j]), vi = uni(s_order[i]), vj = uni(s_order[j]);
+    wsync();
+    s_okey[i] = kj;
+    s_order[i] = vj;
+    wsync();
+    s_okey[j] = ki;
+    s_order[j] = vi;
+    wsync();
+  }
+  // Entries of [a, b) whose key is below `pk` (below_or_eq: at most `pk`).
+  __device__ __forceinline__ int w_count(int a, int b, int pk, bool below_or_eq) const {
+    int c = 0;
+    for (int base = a; base < b; base += kWave) {
+      const int p = base + lane();
+      const int k = p < b ? s_okey[p] : 0;
+      c += __popcll(wballot(p < b && (below_or_eq ? k <= pk : k < pk)));
+    }
+    return c;
+  }
+  // A Hoare pass (partition_func / partitionEqual_func) whose boundary `m` is known up front: its i scan
+  // stops on the left region's entries [l0, m) of the wrong side, its j scan on the right region's
+  // [m, r1), and it exchanges the k-th from the left with the k-th from the right, for every k (the two
+  // counts are equal, and the scans cross exactly at the boundary).  `eq` selects partitionEqual's
+  // predicates (wrong on the left: key > pk) over partition's (key >= pk).  Returns the exchange count.
+  __device__ int w_hoare(int l0, int m, int r1, int pk, bool eq) {
+    int lb = l0, rb = r1, lbase = 0, rtop = 0, swaps = 0;
+    uint64_t mL = 0, mR = 0;
+    for (;;) {
+      if (mL == 0) {
+        if (lb >= m) break;
+        const int p = lb + lane();
+        const int k = p < m ? s_okey[p] : 0;
+        mL = wballot(p < m && (eq ? k > pk : k >= pk));
+        lbase = lb;
+        lb += kWave;
+        continue;
+      }
+      if (mR == 0) {
+        if (rb <= m) break;
+        const int p = rb - 1 - lane();  // bit t <-> position rtop - t: ascending bits walk down from r1
+        const int k = p >= m ? s_okey[p] : 0;
+        mR = wballot(p >= m && (eq ? k <= pk : k < pk));
+        rtop = rb - 1;
+        rb -= kWave;
+        continue;
+      }
+      const int nL = __popcll(mL), nR = __popcll(mR), np = nL < nR ? nL : nR;
+      const uint64_t below = (1ull << lane()) - 1ull;
+      const bool inL = (mL >> lane()) & 1ull, inR = (mR >> lane()) & 1ull;
+      const int rkL = __popcll(mL & below), rkR = __popcll(mR & below);
+      // ds_permute pushes every lane's position to its rank (a bijection over the 64 lanes)
+      const int dL = inL ? rkL : nL + (lane() - rkL), dR = inR ? rkR : nR + (lane() - rkR);
+      const int posL = __builtin_amdgcn_ds_permute(dL * 4, lbase + lane());
+      const int posR = __builtin_amdgcn_ds_permute(dR * 4, rtop - lane());
+      if (lane() < np) {  // disjoint positions: the lanes' exchanges do not overlap
+        const int kl = s_okey[posL], vl = s_order[posL], kr = s_okey[posR], vr = s_order[posR];
+        s_okey[posL] = kr;
+        s_order[posL] = vr;
+        s_okey[posR] = kl;
+        s_order[posR] = vl;
+      }
+      wsync();
+      for (int t = 0; t < np; t++) {
+        mL &= mL - 1;
+        mR &= mR - 1;
+      }
+      swaps += np;
+    }
+    return swaps;
+  }
+  // partition_func: returns the new pivot position; `already` = no exchange was needed.
+  __device__ __forceinline__ int w_partition(int a, int b, int pivot, bool& already) {
+    w_swap(a, pivot);
+    const int pk = uni(s_okey[a]);
+    const int j = a + w_count(a + 1, b, pk, false);
+    already = w_hoare(a + 1, j + 1, b, pk, false) == 0;
+    w_swap(j, a);
+    return j;
+  }
+  // partitionEqual_func: returns the first position past the entries equal to the pivot.
+  __device__ __forceinline__ int w_partition_equal(int a, int b, int pivot) {
+    w_swap(a, pivot);
+    const int pk = uni(s_okey[a]);
+    const int m = a + 1 + w_count(a + 1, b, pk, true);
+    w_hoare(a + 1, m, b, pk, true);
+    return m;
+  }
+  __device__ __forceinline__ void w_reverse(int a, int b) {
+    const int h = (b - a) / 2;
+    for (int base = 0; base < h; base += kWave) {
+      const int t = base + lane();
+      if (t < h) {
+        const int i = a + t, j = b - 1 - t;
+        const int ki = s_okey[i], vi = s_order[i], kj = s_okey[j], vj = s_order[j];
+        s_okey[i] = kj;
+        s_order[i] = vj;
+        s_okey[j] = ki;
+        s_order[j] = vi;
+      }
+    }
+    wsync();
+  }
+  // GoSortExactT::run with the whole wave: frames live one per lane (lane k = stack slot k), the
+  // partitions, reversals and partialInsertionSorts run wave-parallel; insertionSort (<= 12 entries),
+  // heapSort (the depth limit), breakPatterns and choosePivot stay on lane 0.  resumePivot as in run().
+  __device__ void w_pdqsort(int n, int resumePivot) {
+    int fa = 0, fb = 0, fl = 0, ff = 0;  // this lane's stack slot: a, b, limit, flags (wb | wp << 1)
+    int sp = 0;
+    {
+      const bool me = lane() == 0;
+      fa = me ? 0 : fa;
+      fb = me ? n : fb;
+      fl = me ? GoSortT<LI32>::bitsLen((uint32_t)n) : fl;
+      ff = me ? 3 : ff;
+      sp = 1;
+    }
+    bool resume = resumePivot >= 0;
+    int dummy_lo = 0, dummy_hi = 0;
+    while (sp > 0) {
+      sp--;
+      int a = rdl(fa, sp), b = rdl(fb, sp), limit = rdl(fl, sp);
+      const int flags = rdl(ff, sp);
+      bool wasBalanced = flags & 1, wasPartitioned = (flags >> 1) & 1;
+      for (;;) {
+        const int length = b - a;
+        int pivot;
+        if (resume) {
+          resume = false;
+          pivot = resumePivot;
+        } else {
+          if (length <= 12 || limit == 0) {
+            if (lane() == 0) {
+              GoSortT<LI32> g{s_okey, s_order};
+              if (length <= 12) g.insertionSort(a, b);
+              else g.heapSort(a, b);
+            }
+            wsync();
+            break;
+          }
+          int hint = 0, pv = 0;
+          if (lane() == 0) {
+            GoSortT<LI32> g{s_okey, s_order};
+            if (!wasBalanced) g.breakPatterns(a, b);
+            pv = g.choosePivot(a, b, hint);
+          }
+          wsync();
+          if (!wasBalanced) limit--;
+          hint = rdl(hint, 0);
+          pivot = rdl(pv, 0);
+          if (hint == 2) {
+            w_reverse(a, b);
+            pivot = (b - 1) - (pivot - a);
+            hint = 1;
+          }
+          if (wasBalanced && wasPartitioned && hint == 1 && pis_wave(a, b, dummy_lo, dummy_hi)) break;
+        }
+        if (a > 0 && ub(!(s_okey[a - 1] < s_okey[pivot]))) {
+          a = w_partition_equal(a, b, pivot);
+          continue;
+        }
+        bool already = false;
+        const int mid = w_partition(a, b, pivot, already);
+        wasPartitioned = already;
+        const int leftLen = mid - a, rightLen = b - mid, thr = length / 8;
+        if (sp + 2 > kWave) return;  // unreachable: depth <= 2*log2(n) + 2
+        int c0a, c0b, c1a, c1b;
+        if (leftLen < rightLen) {
+          wasBalanced = leftLen >= thr;
+          c0a = mid + 1; c0b = b; c1a = a; c1b = mid;  // continuation, then the recursive call
+        } else {
+          wasBalanced = rightLen >= thr;
+          c0a = a; c0b = mid; c1a = mid + 1; c1b = b;
+        }
+        const bool m0 = lane() == sp, m1 = lane() == sp + 1;
+        fa = m0 ? c0a : (m1 ? c1a : fa);
+        fb = m0 ? c0b : (m1 ? c1b : fb);
+        fl = (m0 || m1) ? limit : fl;
+        ff = m0 ? ((int)wasBalanced | ((int)wasPartitioned << 1)) : (m1 ? 3 : ff);
+        sp += 2;
+        break;
+      }
+    }
+  }
+  // Returns true when lane 0 ran the exact pdqsort (the wave-parallel fast path did not finish it).
+  __device__ __forceinline__ bool sort_claims(int n) {
     int tlo = n, thi = -1, pivot = -1;
     bool done = false;
     if (n > 12) {  // pdqsort_func's top-level frame: choosePivot (reads only), then partialInsertionSort
@@ -1865,14 +2058,18 @@ struct Solver {
       pv = rdl(pv, 0);
       if (hint == 1) {
         pivot = pv;
-        done = pis_wave(n, tlo, thi);
+        done = pis_wave(0, n, tlo, thi);
       }
     }
     if (!done) {
+#if KS_SORT_LANE0
       if (lane() == 0) {
         GoSortExactT<LI32> g{GoSortT<LI32>{s_okey, s_order}};
         g.run(n, pivot);
       }
+#else
+      w_pdqsort(n, pivot);
+#endif
       tlo = 0;
       thi = n - 1;
     }
@@ -1888,6 +2085,7 @@ struct Solver {
     }
     wsync();
     algbytes += (int64_t)(thi - tlo + 1) * (8 + 16 * R());
+    return !done;
   }
 
   // --- consolidation decision for this simulation (SIM epilogue) -------------------------------
@@ -2253,7 +2451,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   uint32_t epoch = 1;
   int qhead = 0, qlen = P;
   int wn = 0, wi = 0;  // window size / next index
-  int64_t pops = 0, sorts = 0, slow = 0, windows = 0, fulls = 0, fullFails = 0, runs = 0, runPods = 0;
+  int64_t pops = 0, sorts = 0, slow = 0, exact = 0, windows = 0, fulls = 0, fullFails = 0, runs = 0, runPods = 0;
   // Every pop either places a pod, relaxes it, or marks it stale; the reference's queue can cycle
   // O(P^2) in adversarial inputs, far beyond any realistic batch.  Bound it so a logic error ends the
   // kernel with KE_ITER_CAP instead of hanging the device.
@@ -2631,7 +2829,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       PH_BEGIN(t2);
       sorts++;
       if (!U(srt)) {
-        S.sort_claims(nclaims);
+        exact += S.sort_claims(nclaims);
         slow++;
         srt = true;
       }
@@ -2779,6 +2977,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     W.counters[CT_WINDOWS] = windows;
     W.counters[CT_RUNS] = runs;
     W.counters[CT_RUN_PODS] = runPods;
+    W.counters[CT_SORT_EXACT] = exact;
 #ifdef KS_PHASE_STATS
     for (int i = 0; i < 7; i++) W.counters[CT_CYC_POP + i] = (int64_t)cyc[i];
     W.counters[CT_CYC_TOTAL] = (int64_t)(__builtin_amdgcn_s_memtime() - tstart);

@@ -70,11 +70,13 @@ def test_config3_selectors_affinity_taints():
 
 def test_config3_long_claim_sorts():
     """C3 at 4000 pods: ~200 NodeClaims, so the per-placement sort.Slice (scheduler.go:247) runs the
-    wave-parallel partialInsertionSort on long arrays, and falls back to the serial pdqsort resume."""
+    wave-parallel partialInsertionSort on long arrays, and the wave-parallel exact pdqsort (partition,
+    partitionEqual, reversal, recursion) when choosePivot's samples straddle a descent."""
     want, got = _solve_both(synth.config3(4000))
     d = _diff(want, got)
     assert d is None, d
     assert got.stats["sortsWithDescent"] > 100
+    assert got.stats["sortsExact"] > 0
 
 
 def test_config1_benchmark_scheduling_2000():
