@@ -1814,14 +1814,56 @@ struct Solver {
     s_order[to] = v0;
     wsync();
   }
-  // First i in [from, n) with key[i] < key[i-1] (a descent), or n.
+  // First i in [from, n) with key[i] < key[i-1] (a descent), or n.  Four chunks per round trip: the
+  // scan usually runs to the end of the array (proving it sorted), so it is latency-bound.
   __device__ __forceinline__ int pis_descent(int from, int n) const {
-    for (int base = from; base < n; base += kWave) {
-      const int i = base + lane();
-      const uint64_t m = wballot(i < n && s_okey[i] < s_okey[i - 1]);
-      if (m) return base + ctz64(m);
+    for (int base = from; base < n; base += 4 * kWave) {
+      uint64_t m[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = base + u * kWave + lane();
+        const int k1 = i < n ? s_okey[i] : 0, k0 = i < n ? s_okey[i - 1] : 0;
+        m[u] = wballot(k1 < k0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (m[u]) return base + u * kWave + ctz64(m[u]);
     }
     return n;
+  }
+  // choosePivot_func (zsortfunc.go): the wave reads the (up to) nine samples at once, lane t sample t,
+  // and the medians run on scalars; same pivot and hint as GoSortT::choosePivot.
+  __device__ __forceinline__ int w_choose_pivot(int a, int b, int& hint) const {
+    const int l = b - a;
+    int i = a + l / 4, j = a + l / 4 * 2, k = a + l / 4 * 3, swaps = 0;
+    if (l >= 8) {
+      const int t = lane() < 9 ? lane() : 0, g = t / 3;
+      const int pos = (g == 0 ? i : g == 1 ? j : k) + (t % 3) - 1;
+      const int key = s_okey[pos];
+      int ik[9], kk[9];
+#pragma unroll
+      for (int u = 0; u < 9; u++) {
+        ik[u] = (u / 3 == 0 ? i : u / 3 == 1 ? j : k) + (u % 3) - 1;
+        kk[u] = rdl(key, u);
+      }
+      auto median = [&](int ia, int ka, int ib, int kb, int ic, int kc, int& km) {
+        if (kb < ka) { swaps++; int t0 = ia; ia = ib; ib = t0; t0 = ka; ka = kb; kb = t0; }
+        if (kc < kb) { swaps++; int t0 = ib; ib = ic; ic = t0; t0 = kb; kb = kc; kc = t0; }
+        if (kb < ka) { swaps++; int t0 = ia; ia = ib; ib = t0; t0 = ka; ka = kb; kb = t0; }
+        km = kb;
+        return ib;
+      };
+      int ki = kk[1], kj = kk[4], kq = kk[7];
+      if (l >= 50) {
+        i = median(ik[0], kk[0], ik[1], kk[1], ik[2], kk[2], ki);
+        j = median(ik[3], kk[3], ik[4], kk[4], ik[5], kk[5], kj);
+        k = median(ik[6], kk[6], ik[7], kk[7], ik[8], kk[8], kq);
+      }
+      int km = 0;
+      j = median(i, ki, j, kj, k, kq, km);
+    }
+    hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+    return j;
   }
   // partialInsertionSort_func(data, 0, n) of Go 1.21 (zsortfunc.go), wave-parallel: each of its <= 5
   // steps finds the next descent by ballot, swaps the pair, then moves the smaller entry left past
@@ -2000,16 +2042,16 @@ struct Solver {
             wsync();
             break;
           }
-          int hint = 0, pv = 0;
-          if (lane() == 0) {
-            GoSortT<LI32> g{s_okey, s_order};
-            if (!wasBalanced) g.breakPatterns(a, b);
-            pv = g.choosePivot(a, b, hint);
+          if (!wasBalanced) {
+            if (lane() == 0) {
+              GoSortT<LI32> g{s_okey, s_order};
+              g.breakPatterns(a, b);
+            }
+            wsync();
+            limit--;
           }
-          wsync();
-          if (!wasBalanced) limit--;
-          hint = rdl(hint, 0);
-          pivot = rdl(pv, 0);
+          int hint = 0;
+          pivot = w_choose_pivot(a, b, hint);
           if (hint == 2) {
             w_reverse(a, b);
             pivot = (b - 1) - (pivot - a);
@@ -2049,13 +2091,8 @@ struct Solver {
     int tlo = n, thi = -1, pivot = -1;
     bool done = false;
     if (n > 12) {  // pdqsort_func's top-level frame: choosePivot (reads only), then partialInsertionSort
-      int hint = 0, pv = -1;
-      if (lane() == 0) {
-        GoSortT<LI32> g{s_okey, s_order};
-        pv = g.choosePivot(0, n, hint);
-      }
-      hint = rdl(hint, 0);
-      pv = rdl(pv, 0);
+      int hint = 0;
+      const int pv = w_choose_pivot(0, n, hint);
       if (hint == 1) {
         pivot = pv;
         done = pis_wave(0, n, tlo, thi);
