@@ -60,6 +60,13 @@ int ks_problem_create_binary(const void* buf, size_t len, ks_problem** out);
 /* Host-only (no device): encode snapshot_json, save it, load the bytes and save again; KS_OK when the two
  * byte strings are identical.  *bytes: the snapshot size. */
 int ks_snapshot_check(const char* snapshot_json, size_t len, size_t* bytes);
+/* Host-only (no device): the binary snapshot of snapshot_json, as ks_problem_save would write it for a
+ * problem created from that JSON (free with ks_free), e.g. to convert fixtures offline. */
+int ks_problem_encode_binary(const char* snapshot_json, size_t len, void** buf, size_t* blen);
+/* Host-only (no device): the load-time checks of ks_problem_create_binary (header, lengths backed by bytes,
+ * offset tables, every table against the dims and every stored index against its table): KS_OK, or
+ * KS_ERR_PARSE for a truncated, foreign or internally inconsistent blob. */
+int ks_problem_check_binary(const void* buf, size_t len);
 
 /* Host-only encode of a snapshot (no device needed): returns JSON with the universe sizes (keys,
  * value words, resources, instance types, relaxation states).  Diagnostics / CPU tests. */
@@ -187,8 +194,9 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
 int ks_cons_validate(ks_cons* c, const char* command_json, size_t len, const ks_solve_opts* opts, char** json_out);
 /* Diagnostics: the 24 solve counters of simulation `sim` in the last ks_cons_run of this handle. */
 int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out24);
-/* The same for up to n counters (26 in this build: + runs of identical pods, pods they placed); returns the
- * number copied or a negative error. */
+/* The same for up to n counters (27 in this build: + runs of identical pods, pods they placed, exact claim
+ * re-sorts); n larger than the build's count copies that count. Returns the number copied or a negative
+ * KS_ERR_* code. */
 int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n);
 /* Algorithmic bytes the gathered simulations scanned, summed from their records. */
 double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world);

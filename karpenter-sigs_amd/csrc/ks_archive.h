@@ -37,6 +37,11 @@ struct ArIn {
     std::memcpy(dst, p, n);
     p += n;
   }
+  // A length read from the blob must be backed by at least `n` more bytes before anything is allocated for
+  // it: a corrupt length is then a parse error, not a multi-GB allocation.
+  void need(uint64_t n) const {
+    if ((uint64_t)(end - p) < n) throw ArchiveError("binary snapshot length exceeds the remaining bytes");
+  }
 };
 
 template <class A, class T>
@@ -56,6 +61,7 @@ void io(A& a, std::string& s) {
   uint64_t n = s.size();
   io_len(a, n);
   if constexpr (A::reading) {
+    a.need(n);
     s.resize(n);
     if (n) a.raw(&s[0], n);
   } else if (n) {
@@ -67,7 +73,12 @@ template <class A, class T>
 void io(A& a, std::vector<T>& v) {
   uint64_t n = v.size();
   io_len(a, n);
-  if constexpr (A::reading) v.resize(n);
+  if constexpr (A::reading) {
+    // every element takes at least one byte (raw elements exactly sizeof(T))
+    constexpr bool raw = std::is_trivially_copyable<T>::value && !std::is_same<T, bool>::value;
+    a.need(raw ? n * sizeof(T) : n);
+    v.resize(n);
+  }
   if constexpr (std::is_trivially_copyable<T>::value && !std::is_same<T, bool>::value) {
     if (n) {
       if constexpr (A::reading) a.raw(v.data(), n * sizeof(T));

@@ -929,6 +929,41 @@ int ks_snapshot_check(const char* json, size_t len, size_t* bytes) {
   API_CATCH
 }
 
+// Host-only: the binary snapshot of a JSON problem without creating a handle (no device), e.g. to convert
+// fixtures offline on a machine without a GPU; ks_problem_create_binary accepts the bytes.
+int ks_problem_encode_binary(const char* json, size_t len, void** buf, size_t* blen) {
+  API_TRY
+  if (!json || !buf || !blen) throw KsError(KS_ERR_ARG, "null argument");
+  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  Host h;
+  h.build(root);
+  ArOut a;
+  snapshot_header(a, kProblemMagic);
+  host_save(a, h);
+  *buf = snapshot_bytes(a.buf);
+  *blen = a.buf.size();
+  return KS_OK;
+  API_CATCH
+}
+
+// Host-only: load and validate a problem snapshot (the checks ks_problem_create_binary runs before any upload):
+// KS_OK, or KS_ERR_PARSE for a truncated, foreign or internally inconsistent blob.
+int ks_problem_check_binary(const void* buf, size_t len) {
+  API_TRY
+  if (!buf) throw KsError(KS_ERR_ARG, "null argument");
+  Host h;
+  try {
+    ArIn a{(const char*)buf, (const char*)buf + len};
+    snapshot_check_header(a, kProblemMagic);
+    host_load(a, h);
+    if (a.p != a.end) throw KsError(KS_ERR_PARSE, "binary snapshot has trailing bytes");
+  } catch (const ArchiveError& e) {
+    throw KsError(KS_ERR_PARSE, e.what());
+  }
+  return KS_OK;
+  API_CATCH
+}
+
 // Host-only encode (no device): layout sizes for diagnostics and CPU tests.
 int ks_problem_inspect(const char* json, size_t len, char** out) {
   API_TRY

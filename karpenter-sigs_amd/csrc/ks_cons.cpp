@@ -1150,6 +1150,26 @@ constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '1'};
 template <class A> void cons_io(A& a, ks_cons& c) {
   io_all(a, c.cands, c.nPass, c.sims, c.multiHi, c.pending, c.deleting, c.nominated, c.hostnameSeed, c.recWords);
 }
+// The loaded plan's indices must lie inside the loaded model (host_check covers the model itself).
+void cons_check(const ks_cons& c) {
+  const Host& h = c.pb->host;
+  auto bad = [](const char* what) { throw ArchiveError(std::string("binary snapshot: inconsistent ") + what); };
+  const int P = h.dims.P, N = h.dims.N, NC = (int)c.cands.size();
+  if (c.nPass < 0 || c.nPass > NC || c.multiHi < 0 || c.multiHi > c.nPass) bad("candidate counts");
+  if (c.recWords != rec_words(h.dims.TW)) bad("record width");
+  if ((int)c.sims.size() != c.multiHi + c.nPass) bad("simulation plan");
+  for (auto& cd : c.cands) {
+    if (cd.node < 0 || cd.node >= N || cd.it >= h.dims.T) bad("candidate node");
+    for (int p : cd.pods)
+      if (p < 0 || p >= P) bad("candidate pod");
+  }
+  for (auto& s : c.sims)
+    for (int ci : s.cands)
+      if (ci < 0 || ci >= c.nPass) bad("simulation candidate");
+  for (const std::vector<int>* v : {&c.pending, &c.deleting})
+    for (int p : *v)
+      if (p < 0 || p >= P) bad("pending / deleting pod");
+}
 }  // namespace
 }  // extern "C++"
 
@@ -1178,6 +1198,7 @@ int ks_cons_create_binary(const void* buf, size_t len, ks_cons** out) {
     host_load(a, c->pb->host);
     cons_io(a, *c);
     if (a.p != a.end) throw KsError(KS_ERR_PARSE, "binary snapshot has trailing bytes");
+    cons_check(*c);
   } catch (const ArchiveError& e) {
     throw KsError(KS_ERR_PARSE, e.what());
   }
@@ -1332,7 +1353,10 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
 
 // Diagnostics: the solve counters (ks_problem.h Counter) of the last run's simulation `sim` (this
 // rank's launch; with the KS_PHASE_STATS build they include per-phase cycles).
-int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out) { return ks_cons_sim_counters_n(c, sim, out, CT_ABI) < 0 ? -1 : 0; }
+int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out) {
+  const int r = ks_cons_sim_counters_n(c, sim, out, CT_ABI);
+  return r < 0 ? r : KS_OK;  // the specific KS_ERR_* code (ARG / HIP / ...), as every entry point returns it
+}
 
 int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n) {
   API_TRY

@@ -53,6 +53,7 @@ void io_rows(A& a, std::vector<uint32_t>& v, uint64_t width) {
   const uint64_t rows = n / width;
   std::vector<uint64_t> nz((rows + 63) / 64, 0);
   if constexpr (A::reading) {
+    a.need(8 * ((rows + 63) / 64));  // the bitmap must be there before the table is allocated
     io(a, nz);
     if (nz.size() != (rows + 63) / 64) throw ArchiveError("binary snapshot: row bitmap size");
     v.assign(n, 0);
@@ -90,14 +91,22 @@ template <class A, class T>
 void io_par(A& a, std::vector<T>& v) {
   uint64_t n = v.size();
   io_len(a, n);
+  if constexpr (A::reading) {
+    a.need(8 * (n + 1));  // the offset table itself
+    if (n > (uint64_t)INT32_MAX) throw ArchiveError("binary snapshot: too many elements");
+  }
   std::vector<uint64_t> off(n + 1, 0);
   if constexpr (A::reading) {
-    v.resize(n);
     io(a, off);
-    if (off.size() != n + 1 || off[n] > (uint64_t)(a.end - a.p)) throw ArchiveError("binary snapshot offsets out of range");
+    if (off.size() != n + 1 || off[0] != 0 || off[n] > (uint64_t)(a.end - a.p))
+      throw ArchiveError("binary snapshot offsets out of range");
+    // the whole table is checked before any element is decoded: every element's byte range lies inside
+    // [0, off[n]], so no decode (on a worker thread) can read past the caller's buffer
+    for (uint64_t i = 0; i < n; i++)
+      if (off[i] > off[i + 1]) throw ArchiveError("binary snapshot offsets out of order");
+    v.resize(n);
     const char* base = a.p;
     parallel_for((int)n, 64, [&](int i) {
-      if (off[(size_t)i] > off[(size_t)i + 1]) throw ArchiveError("binary snapshot offsets out of order");
       ArIn sub{base + off[(size_t)i], base + off[(size_t)i + 1]};
       io(sub, v[(size_t)i]);
       if (sub.p != sub.end) throw ArchiveError("binary snapshot element size mismatch");
@@ -113,6 +122,122 @@ void io_par(A& a, std::vector<T>& v) {
     for (uint64_t i = 0; i < n; i++) off[i + 1] = off[i] + parts[i].size();
     io(a, off);
     for (auto& p : parts) a.raw(p.data(), p.size());
+  }
+}
+
+// A loaded model must be internally consistent before anything reads it by its dims: every table at
+// least as long as the dims say the host and the kernels index it (ks_capi.cpp problem_device_init, the
+// k_* kernels), every stored index inside the table it points into.  A blob that is complete but corrupt
+// (a flipped dims field, a shortened table) is refused here as a parse error instead of being read out of
+// bounds on the host or the device.
+void host_check(const Host& h) {
+  const KsDims& d = h.dims;
+  auto bad = [](const char* what) { throw ArchiveError(std::string("binary snapshot: inconsistent ") + what); };
+  auto need = [&](size_t have, int64_t want, const char* what) {
+    if (want < 0 || (int64_t)have < want) bad(what);
+  };
+  if (d.R < 1 || d.R > kMaxR || d.NK < 0 || d.NK > 64 || d.NTPL < 0 || d.NTPL > kMaxTpl || d.T < 0 || d.N < 0 ||
+      d.P < 0 || d.S < 1 || d.NU < 1 || d.NPOOL < 0 || d.VD < 0 || d.VD > kMaxVD || d.TW < 1 || d.G < 0 ||
+      d.G1 < 0 || d.G1 > d.G || d.Kcap < 1)
+    bad("dims");
+  if (d.HDR != 8 + 4 * d.NB || d.RSW < d.HDR + d.W || d.W < 0 || d.NB < 0) bad("record layout");
+  if ((int)h.keys.size() != d.NK || (int)h.keyNames.size() != d.NK || (int)h.values.size() != d.NK) bad("key tables");
+  need(h.wordValid.size(), d.W, "wordValid");
+  need(h.vIsInt.size(), d.W, "vIsInt");
+  for (const KeyMeta& km : h.keys) {
+    if (km.off < 0 || km.nw < 0 || km.off + km.nw > d.W || km.nv < 0 || km.nv > 32 * km.nw) bad("key layout");
+    if (km.bslot >= d.NB) bad("key bound slot");
+    if (km.vint >= 0 && (size_t)km.vint + (size_t)km.nv > h.vInt.size()) bad("key int table");
+  }
+  for (int k : {d.zoneKey, d.ctKey})
+    if (k < 0 || k >= d.NK) bad("zone / capacity-type key");
+  if ((int)h.tpls.size() != d.NTPL || (int)h.its.size() != d.T || (int)h.nodes.size() != d.N ||
+      (int)h.pods.size() != d.P || (int)h.states.size() != d.P || (int)h.pools.size() != d.NPOOL ||
+      (int)h.groups.size() != d.G)
+    bad("object counts");
+  const Host::Tables& t = h.tab;
+  const int64_t R = d.R, RSW = d.RSW, T = d.T, N1 = std::max(d.N, 1), P1 = std::max(d.P, 1), S = d.S;
+  const int64_t NT1 = std::max(d.NTPL, 1), NP1 = std::max(d.NPOOL, 1), VD1 = std::max(d.VD, 1);
+  need(t.it_alloc.size(), T * R, "it_alloc");
+  need(t.it_cap.size(), T * R, "it_cap");
+  need(t.it_rs.size(), T * RSW, "it_rs");
+  need(t.it_off_beg.size(), T + 1, "it_off_beg");
+  need(t.tpl_rs.size(), NT1 * RSW, "tpl_rs");
+  need(t.tpl_taint.size(), NT1 * 2, "tpl_taint");
+  need(t.tpl_daemon.size(), NT1 * R, "tpl_daemon");
+  need(t.tpl_rmask.size(), NT1, "tpl_rmask");
+  need(t.tpl_rfmt.size(), NT1 * R, "tpl_rfmt");
+  need(t.tpl_it_beg.size(), (int64_t)d.NTPL + 1, "tpl_it_beg");
+  need(t.tpl_pool.size(), NT1, "tpl_pool");
+  need(t.pool_rem0.size(), NP1 * R, "pool_rem0");
+  need(t.pool_mask.size(), NP1, "pool_mask");
+  need(t.pod_req.size(), P1 * R, "pod_req");
+  need(t.pod_rfmt.size(), P1 * R, "pod_rfmt");
+  need(t.pod_sortkey.size(), P1 * 4, "pod_sortkey");
+  for (auto* v : {&t.pod_state0, &t.pod_nstate, &t.pod_uid, &t.pod_flags}) need(v->size(), P1, "per-pod table");
+  for (auto* v : {&t.pod_hpc, &t.pod_hpu, &t.pod_hpo, &t.pod_vm}) need(v->size(), P1, "per-pod mask");
+  need(t.pod_rmask.size(), P1, "pod_rmask");
+  need(t.st_rs.size(), S * RSW, "st_rs");
+  need(t.st_tol.size(), S * 2, "st_tol");
+  need(t.st_flags.size(), S, "st_flags");
+  need(t.st_toltpl.size(), S, "st_toltpl");
+  need(t.st_gown.size(), S, "st_gown");
+  need(t.n_avail.size(), N1 * R, "n_avail");
+  need(t.n_req0.size(), N1 * R, "n_req0");
+  need(t.n_rs0.size(), N1 * RSW, "n_rs0");
+  need(t.n_taint.size(), N1 * 2, "n_taint");
+  need(t.n_flags.size(), N1, "n_flags");
+  need(t.n_hp0.size(), N1, "n_hp0");
+  need(t.n_vm0.size(), N1, "n_vm0");
+  need(t.n_vc0.size(), N1 * VD1, "n_vc0");
+  need(t.n_vlim.size(), N1 * VD1, "n_vlim");
+  need(t.vol_dm.size(), VD1, "vol_dm");
+  need(t.pod_gsel.size(), P1, "pod_gsel");
+  need(t.pod_ginv.size(), P1, "pod_ginv");
+  // CSR tables and the indices the kernels follow
+  auto mono = [&](const std::vector<int32_t>& v, size_t n, int64_t hi, const char* what) {
+    if (v[0] != 0) bad(what);
+    for (size_t i = 0; i < n; i++)
+      if (v[i] > v[i + 1]) bad(what);
+    if (v[n] > hi) bad(what);
+  };
+  mono(t.it_off_beg, (size_t)T, (int64_t)std::min({t.off_zone.size(), t.off_ct.size(), t.off_price.size()}), "offerings");
+  mono(t.tpl_it_beg, (size_t)d.NTPL, (int64_t)t.tpl_its.size(), "template instance-type lists");
+  if (t.tpl_it_beg[(size_t)d.NTPL] != d.totalTplIts) bad("totalTplIts");
+  for (int i = 0; i < d.NTPL; i++) {
+    const int n = t.tpl_it_beg[(size_t)i + 1] - t.tpl_it_beg[(size_t)i];
+    if (n > d.maxTplIts || (d.maxTplIts + 31) / 32 > d.TW) bad("template list width");
+    if (t.tpl_pool[(size_t)i] >= d.NPOOL) bad("template pool");
+  }
+  for (int32_t x : t.tpl_its)
+    if (x < 0 || x >= d.T) bad("template instance type");
+  need(t.tsort_alloc.size(), (int64_t)std::max(d.totalTplIts, 1) * R, "tsort_alloc");
+  need(t.tsort_pos.size(), (int64_t)std::max(d.totalTplIts, 1) * R, "tsort_pos");
+  for (int64_t p = 0; p < d.P; p++) {
+    const int64_t s0 = t.pod_state0[(size_t)p], ns = t.pod_nstate[(size_t)p];
+    if (s0 < 0 || ns < 1 || s0 + ns > S || ns != (int64_t)h.states[(size_t)p].size()) bad("relaxation states");
+    if (t.pod_uid[(size_t)p] < 0 || t.pod_uid[(size_t)p] >= d.NU) bad("pod uid");
+  }
+  if (!h.hostQueue.empty()) {
+    if ((int)h.hostQueue.size() != d.P) bad("host queue");
+    for (int32_t x : h.hostQueue)
+      if (x < 0 || x >= d.P) bad("host queue entry");
+  }
+  // topology
+  if (d.G) {
+    need(t.tg_meta.size(), (int64_t)d.G * TGM_WORDS, "tg_meta");
+    need(t.n_tdom.size(), (int64_t)d.G * N1, "n_tdom");
+    need(t.st_rss.size(), S * RSW, "st_rss");
+    if (d.tgCntWords != (int32_t)t.tg_cnt0.size() || d.tgSmall < 0 || d.tgSmall > d.tgCntWords) bad("count table");
+    for (int g = 0; g < d.G; g++) {
+      const int32_t* m = &t.tg_meta[(size_t)g * TGM_WORDS];
+      if (m[TGM_KEY] < 0 || m[TGM_KEY] >= d.NK || m[TGM_NV] < 0 || m[TGM_NV] > h.keys[(size_t)m[TGM_KEY]].nv ||
+          m[TGM_CNT] < 0 || (int64_t)m[TGM_CNT] + std::max(m[TGM_NV], 1) > d.tgCntWords || m[TGM_FBEG] < 0 ||
+          m[TGM_FBEG] > m[TGM_FEND] || (int64_t)m[TGM_FEND] * RSW > (int64_t)t.tg_frs.size())
+        bad("topology group");
+    }
+    for (int32_t v : t.n_tdom)
+      if (v < -1 || v >= std::max(d.tgMaxNv, 1) + 1) bad("node domain");
   }
 }
 
@@ -162,6 +287,7 @@ template <class A> void host_io(A& a, Host& h) {
     h.L.vInt = h.vInt.data();
     h.topoExcluded = nullptr;
     h.preParsedPods = nullptr;
+    host_check(h);
   }
 }
 

@@ -79,6 +79,9 @@ def lib():
     l.ks_problem_save.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
     l.ks_problem_create_binary.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
     l.ks_snapshot_check.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+    l.ks_problem_encode_binary.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp),
+                                           ctypes.POINTER(ctypes.c_size_t)]
+    l.ks_problem_check_binary.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
     l.ks_cons_save.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
     l.ks_cons_create_binary.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
     l.ks_last_error.restype = ctypes.c_char_p
@@ -246,6 +249,23 @@ def snapshot_check(snapshot):
     n = ctypes.c_size_t()
     _check(lib().ks_snapshot_check(b, len(b), ctypes.byref(n)))
     return n.value
+
+
+def encode_binary(snapshot):
+    """Host-only: the binary snapshot of a JSON problem (what Scheduler(snapshot).save() returns), no device."""
+    b = _encode(snapshot)
+    buf, n = ctypes.c_void_p(), ctypes.c_size_t()
+    _check(lib().ks_problem_encode_binary(b, len(b), ctypes.byref(buf), ctypes.byref(n)))
+    try:
+        return ctypes.string_at(buf, n.value)
+    finally:
+        lib().ks_free(buf)
+
+
+def check_binary(blob):
+    """Host-only: ks_problem_create_binary's load-time checks; raises KsError (KS_ERR_PARSE) on a bad blob."""
+    blob = bytes(blob)
+    _check(lib().ks_problem_check_binary(blob, len(blob)))
 
 
 class Scheduler:
@@ -469,8 +489,8 @@ class Consolidator:
 
     def sim_counters(self, sim):
         """Solve counters of simulation `sim` from the last run (ks_problem.h Counter order)."""
-        out = (ctypes.c_int64 * 26)()
-        n = _cons_lib().ks_cons_sim_counters_n(self._h, sim, out, 26)
+        out = (ctypes.c_int64 * 64)()  # the library copies min(64, its counter count) and returns that count
+        n = _cons_lib().ks_cons_sim_counters_n(self._h, sim, out, 64)
         if n < 0:
             _check(n)
         return list(out)[:n]

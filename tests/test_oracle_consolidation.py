@@ -45,3 +45,29 @@ def test_all_sims_mode_same_commands():
     assert a["multi"]["command"] == b["multi"]["command"]
     assert a["single"]["command"] == b["single"]["command"]
     assert len(b["single"]["sims"]) == 24
+
+
+@pytest.mark.parametrize("kind,seed", [("c5t", 11), ("c5t", 12), ("c5r", 13), ("c5r", 14)])
+def test_threaded_precompute_equals_sequential(kind, seed):
+    """the full-size digests come from the oracle's threaded precompute, which starts
+    every simulation's hostname-placeholder counter at hostnameSeed instead of the reference's running
+    global counter (nodeclaim.go:44-48).  On C5T-shaped clusters (hostname spread, hostname and zonal
+    anti-affinity, pod affinity) and C5R-shaped ones (Replace / NoOp, spot), the threaded mode must give the
+    sequential all-sims mode's simulation outcomes and commands exactly."""
+    from karpenter_amd import synth
+    if kind == "c5t":
+        snap = synth.cluster_snapshot(40, 10, n_its=60, seed=seed, topology=8 + seed % 3, n_pending=2)
+    else:
+        snap = synth.cluster_snapshot(40, 12, n_its=60, seed=seed, it_range=(3, 16), spot_frac=0.5, n_pending=2)
+    s = json.dumps(snap)
+    seq, _ = bridge.consolidate(s, all_sims=True, threads=1)
+    thr, _ = bridge.consolidate(s, all_sims=True, threads=4)
+    assert thr["multi"]["command"] == seq["multi"]["command"]
+    assert thr["single"]["command"] == seq["single"]["command"]
+    for method in ("multi", "single"):
+        a, b = seq[method].get("sims"), thr[method].get("sims")
+        assert a is not None and len(a) == len(b)
+        assert b == a
+    # the clusters exercise decisions, not only deletes
+    actions = {x["action"] for x in seq["single"]["sims"]} | {x["action"] for x in seq["multi"]["sims"]}
+    assert len(actions) >= 2, actions

@@ -6,11 +6,15 @@ encodes (topology, host ports, volumes, limits, taints, the consolidation cluste
 foreign blob is refused.  GPU: a problem / handle rebuilt from its snapshot gives the Results / decisions of
 the one built from JSON, and both equal the oracle."""
 import json
+import struct
 
 import pytest
 
 import problems
-from karpenter_amd import Consolidator, KsError, Scheduler, snapshot_check, synth
+
+KS_ERR_PARSE = -1
+from karpenter_amd import (Consolidator, KsError, Scheduler, check_binary, encode_binary, inspect, snapshot_check,
+                           synth)
 from oracle import bridge
 
 CPU_CASES = ([("random", s) for s in range(6)] + [("topology", s) for s in range(40, 44)] +
@@ -81,3 +85,84 @@ def test_consolidation_from_binary_snapshot(seed, topo):
     assert gb == want
     with pytest.raises(KsError):
         Consolidator.from_binary(b"KSPROB01" + blob[8:])  # a problem's magic on a handle's bytes
+
+
+def _u64s(blob, at, n):
+    return list(struct.unpack_from("<%dQ" % n, blob, at))
+
+
+def _pods_offsets(blob, n_pods, first_name):
+    """Byte position of the pods' io_par offsets: element count n_pods, the offset vector (its length n_pods + 1,
+    then the offsets from 0), then the elements, the first of which starts with the first pod's name (a
+    length-prefixed string)."""
+    pat = struct.pack("<QQQ", n_pods, n_pods + 1, 0)
+    name = struct.pack("<Q", len(first_name)) + first_name.encode()
+    at = blob.find(pat)
+    while at >= 0:
+        data = at + 8 * (n_pods + 3)
+        off = _u64s(blob, at + 16, n_pods + 1)
+        if (all(off[i] <= off[i + 1] for i in range(n_pods)) and off[-1] <= len(blob) - data and
+                blob[data:data + len(name)] == name):
+            return at + 16
+        at = blob.find(pat, at + 1)
+    raise AssertionError("pods offset table not found")
+
+
+def _dims_at(blob, info):
+    """Byte position of the serialized KsDims (its leading int32 fields are known from inspect())."""
+    nb = info["NB"]
+    pre = struct.pack("<13i", info["R"], info["keys"], info["W"], nb, 8 + 4 * nb, info["RSW"], info["T"],
+                      info["templates"], info["pools"], info["nodes"], info["pods"], info["states"], info["uids"])
+    at = blob.find(pre)
+    assert at >= 0 and blob.find(pre, at + 1) < 0
+    return at
+
+
+@pytest.mark.parametrize("kind,arg", [("random", 1), ("topology", 41), ("c3", 300)])
+def test_binary_snapshot_rejects_corrupt_blobs(kind, arg):
+    """a complete but corrupt blob is a parse error, never an out-of-bounds read: an offset table
+    whose element ends past the table's end, dims fields that disagree with the tables, oversized lengths."""
+    snap = _snap(kind, arg)
+    blob = encode_binary(json.dumps(snap))
+    check_binary(blob)  # the untouched blob loads
+    info = inspect(json.dumps(snap))
+    P = info["pods"]
+    # element 0's end offset far past the table's end (off[n] itself unchanged): rejected before any decode
+    at = _pods_offsets(blob, P, snap["pods"][0]["metadata"]["name"])
+    bad = bytearray(blob)
+    struct.pack_into("<Q", bad, at + 8, _u64s(blob, at, P + 1)[-1] + 4096)
+    with pytest.raises(KsError) as e:
+        check_binary(bad)
+    assert e.value.code == KS_ERR_PARSE
+    # dims fields flipped: more pods / instance types / resources than the tables hold
+    d = _dims_at(blob, info)
+    for field, delta in ((10, 1000), (6, 64), (0, 1), (5, 2)):
+        bad = bytearray(blob)
+        v = struct.unpack_from("<i", bad, d + 4 * field)[0]
+        struct.pack_into("<i", bad, d + 4 * field, v + delta)
+        with pytest.raises(KsError) as e:
+            check_binary(bad)
+        assert e.value.code == KS_ERR_PARSE, field
+    # a length field claiming 2^33 elements is refused without allocating them
+    bad = bytearray(blob)
+    struct.pack_into("<Q", bad, at - 16, 1 << 33)
+    with pytest.raises(KsError) as e:
+        check_binary(bad)
+    assert e.value.code == KS_ERR_PARSE
+    # truncation anywhere past the header
+    for cut in (30, len(blob) // 3, len(blob) - 1):
+        with pytest.raises(KsError):
+            check_binary(blob[:cut])
+
+
+@pytest.mark.gpu
+def test_create_binary_rejects_flipped_dims():
+    snap = problems.random_problem(2)
+    s = json.dumps(snap)
+    blob = Scheduler(s).save()
+    d = _dims_at(blob, inspect(s))
+    bad = bytearray(blob)
+    struct.pack_into("<i", bad, d + 40, struct.unpack_from("<i", bad, d + 40)[0] + 1000)  # P
+    with pytest.raises(KsError) as e:
+        Scheduler.from_binary(bytes(bad))
+    assert e.value.code == KS_ERR_PARSE
