@@ -269,7 +269,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
         "decision": {"multi": [doc["multi"]["command"]["action"], len(doc["multi"]["command"]["candidates"])],
                      "single": [doc["single"]["command"]["action"], doc["single"]["command"]["candidates"]]},
         "roofline": _roofline("k_solve<SIM%s>" % (", TOPO" if topology else ""), k_ms, algb, ref,
-                              "cons_c5" if not topology else "cons_c5t", per_gpu_div=world,
+                              "c5" if not topology else "c5t", per_gpu_div=world,
                               extra={"kernel_ms_max_rank": round(kmax, 3)}),
         "cpu_baseline": cpu,
         "cpu_baseline_1thread": cpu1,
