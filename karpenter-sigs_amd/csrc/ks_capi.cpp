@@ -66,7 +66,7 @@ WorkLayout work_layout(const KsDims& d) {
   w.tg_ccnt = a.add(4 * (size_t)std::max(d.G, 1) * (d.G ? K + 1 : 1));
   w.tg_cpos = a.add(4 * (size_t)std::max(d.G, 1));
   w.fail_rs = a.add(d.G ? 4 * (size_t)P * std::max(d.NTPL, 1) * d.FSW : 4);
-  w.log_hg = a.add(d.G ? 8 * P : 8);
+  w.log_hg = a.add(d.G ? 8 * P * (size_t)d.GMW : 8);
   w.tg_act = a.add(4 * (size_t)std::max(d.G, 1));
   w.total = a.total;
   return w;
@@ -234,6 +234,7 @@ void ks_upload(ks_problem* pb) {
   size_t o_sgo = put(t.st_gown.data(), t.st_gown.size() * 8);
   size_t o_pgs = put(t.pod_gsel.data(), t.pod_gsel.size() * 8);
   size_t o_pgi = put(t.pod_ginv.data(), t.pod_ginv.size() * 8);
+  size_t o_tgl = put(t.tg_late.data(), t.tg_late.size() * 8);
   size_t o_srs = put(t.st_rss.data(), t.st_rss.size() * 4);
   size_t o_ntd = put(t.n_tdom.data(), t.n_tdom.size() * 4);
   size_t o_fkw = put(t.fk_words.data(), t.fk_words.size() * 4);
@@ -373,6 +374,7 @@ void ks_upload(ks_problem* pb) {
   D.st_gown = (const uint64_t*)(b + o_sgo);
   D.pod_gsel = (const uint64_t*)(b + o_pgs);
   D.pod_ginv = (const uint64_t*)(b + o_pgi);
+  D.tg_late = (const uint64_t*)(b + o_tgl);
   D.st_rss = (const uint32_t*)(b + o_srs);
   D.n_tdom = (const int32_t*)(b + o_ntd);
   D.fk_words = (const uint32_t*)(b + o_fkw);
@@ -393,13 +395,13 @@ static std::string hostnameCounts(const Host& h, int g, int seq, int64_t ord, in
   const KsDims& d = h.dims;
   const int32_t* gm = &h.tab.tg_meta[(size_t)g * TGM_WORDS];
   const int k = gm[TGM_KEY], nv = gm[TGM_NV];
-  if (seq < 0 || seq > (int)logt.size() || (size_t)seq > loghg.size())
+  if (seq < 0 || seq > (int)logt.size() || (size_t)seq * d.GMW > loghg.size())
     throw KsError(KS_ERR_INTERNAL, "hostname topology failure outside the commit log");
   std::vector<int32_t> cnt(h.tab.tg_cnt0.begin() + gm[TGM_CNT], h.tab.tg_cnt0.begin() + gm[TGM_CNT] + nv);
   std::map<int64_t, int32_t> ph;  // placeholder ordinal -> count
   for (int64_t o = std::max<int64_t>(h.hostnameSeed, act) + 1; o <= ord; o++) ph[o] = 0;
   for (int i = 0; i < seq; i++) {
-    if (!((loghg[(size_t)i] >> g) & 1ull)) continue;
+    if (!gtest(loghg, (size_t)i, d.GMW, g)) continue;
     if (logt[(size_t)i] >= 0) {
       ph[chost[(size_t)logt[(size_t)i]]] += 1;
     } else {
@@ -534,7 +536,7 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     }
     if (need) {
       dl(frs, W.fail_rs, (size_t)d.P * d.NTPL * d.FSW, st);
-      dl(loghg, W.log_hg, nl, st);
+      dl(loghg, W.log_hg, (size_t)nl * d.GMW, st);
       dl(tgact, W.tg_act, d.G, st);
       HIPCHK(hipStreamSynchronize(st));
     }
@@ -749,7 +751,7 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
           break;
         }
         case FC_TOPO: {  // Topology.AddRequirements (topology.go:160-165)
-          const int g = (int)(code >> 16) & 0xff;
+          const int g = (int)(code >> 16) & 0xffff;
           const int32_t* gm = &h.tab.tg_meta[(size_t)g * TGM_WORDS];
           const int k = gm[TGM_KEY], nv = gm[TGM_NV];
           const uint32_t* fr = &frs[((size_t)p * d.NTPL + t) * d.FSW];
@@ -978,7 +980,9 @@ int ks_problem_inspect(const char* json, size_t len, char** out) {
   kv("pools", d.NPOOL); kv("nodes", d.N); kv("pods", d.P); kv("states", d.S); kv("uids", d.NU); kv("TW", d.TW);
   kv("Kcap", d.Kcap); kv("taints", (long long)h.taints.size()); kv("G", d.G); kv("G1", d.G1);
   kv("hostQueue", h.hostQueue.empty() ? 0 : 1); kv("hostPorts", (long long)h.hostPortUniverse.size());
-  kv("lateGroups", __builtin_popcountll(d.tgLate)); kv("unlabelledNodes", d.tgUnlab);
+  long long nlate = 0;
+  for (uint64_t x : h.tab.tg_late) nlate += __builtin_popcountll(x);
+  kv("lateGroups", nlate); kv("groupWords", d.GMW); kv("unlabelledNodes", d.tgUnlab);
   // LDS plans (ks_solve.hip make_plan) at the default and a few reduced budgets
   o += ",\"plans\":{";
   const size_t budgets[] = {160 * 1024 - 256, 6000, 9000, 14000, 24000, 40000};

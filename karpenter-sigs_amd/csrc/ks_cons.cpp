@@ -482,7 +482,7 @@ bool offering_price(const Host::IT& it, const std::string& ct, const std::string
 // (existingnode.go:60).  Returns (tg_cnt offset, (pods removed << 1) | unregister-if-zero) pairs,
 // one per touched domain; `dead` gets the inverse groups none of whose owners is in the simulation.
 std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, const std::vector<int>& simPods,
-                                  uint64_t& dead) {
+                                  std::vector<uint64_t>& dead) {
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
   const int hostKey = h.keyId.count("kubernetes.io/hostname") ? h.keyId.at("kubernetes.io/hostname") : -1;
@@ -498,7 +498,7 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
         for (auto& gv : ct->second) dec[gv]++;
       auto io = h.topoInvOwner.find(uid);
       if (io != h.topoInvOwner.end())
-        for (uint64_t m = io->second; m; m &= m - 1) ownersGone[(size_t)__builtin_ctzll(m)]++;
+        for (int32_t g : io->second) ownersGone[(size_t)g]++;
     }
     auto hv = hostKey >= 0 ? h.valueId[(size_t)hostKey].find(h.nodes[(size_t)k.node].hostName)
                            : h.valueId[0].end();
@@ -522,11 +522,13 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
     out.push_back(h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_CNT] + v);
     out.push_back((e.second << 1) | (keep ? 0 : 1));
   }
-  uint64_t simOwn = 0;  // inverse groups a simulation pod owns (Topology.Update, topology.go:91-122)
-  for (int p : simPods) simOwn |= h.tab.pod_ginv[(size_t)p];
-  dead = 0;
+  // inverse groups a simulation pod owns (Topology.Update, topology.go:91-122)
+  std::vector<uint64_t> simOwn((size_t)d.GMW, 0);
+  for (int p : simPods)
+    for (int w = 0; w < d.GMW; w++) simOwn[(size_t)w] |= h.tab.pod_ginv[(size_t)p * d.GMW + w];
+  dead.assign((size_t)d.GMW, 0);
   for (int g = d.G1; g < d.G; g++)
-    if (h.topoInvOwners[(size_t)g] - ownersGone[(size_t)g] <= 0 && !((simOwn >> g) & 1ull)) dead |= 1ull << g;
+    if (h.topoInvOwners[(size_t)g] - ownersGone[(size_t)g] <= 0 && !gtest(simOwn, 0, d.GMW, g)) gset(dead, 0, d.GMW, g);
   return out;
 }
 
@@ -552,13 +554,13 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   struct Off {
     size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
         last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price, n_hp,
-        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, n_vm, n_vc;
+        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, tdead, n_vm, n_vc;
   };
   std::vector<Off> offs(ns);
   std::vector<int> simP(ns), entBeg(ns + 1, 0);
   std::vector<int32_t> entries, entrySim;
   std::vector<std::vector<int32_t>> tdel(ns);
-  std::vector<uint64_t> tdead(ns, 0);
+  std::vector<std::vector<uint64_t>> tdead(ns);
   std::vector<std::vector<int>> simPods(ns);
   int maxP = 1;
   for (int k = 0; k < ns; k++) {
@@ -613,6 +615,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       o.tg_cpos = a.add(4 * (size_t)d.G);
       tdel[k] = sim_topology(c, sm, simPods[k], tdead[k]);
       o.tdel = ai.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
+      o.tdead = ai.add(8 * (size_t)d.GMW);
     }
   }
   c.L.lnent = (int)entries.size();
@@ -744,7 +747,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       memcpy(stage.data() + o.tdel, tdel[k].data(), 4 * tdel[k].size());
       w.tdel = (const int32_t*)(ibase + o.tdel);
       w.ntdel = (int32_t)(tdel[k].size() / 2);
-      w.tdead = tdead[k];
+      memcpy(stage.data() + o.tdead, tdead[k].data(), 8 * tdead[k].size());
+      w.tdead = (const uint64_t*)(ibase + o.tdead);
     }
     works[k] = w;
   }
@@ -1249,7 +1253,8 @@ int ks_cons_inspect(const char* json, size_t len, char** out) {
   }
   o += "],\"sims\":" + std::to_string(c.sims.size()) + ",\"multiPrefixes\":" + std::to_string(c.multiHi) +
        ",\"recordBytes\":" + std::to_string(4 * c.recWords) + ",\"pods\":" + std::to_string(c.pb->host.dims.P) +
-       ",\"nodes\":" + std::to_string(c.pb->host.dims.N) + "}";
+       ",\"nodes\":" + std::to_string(c.pb->host.dims.N) + ",\"groups\":" + std::to_string(c.pb->host.dims.G) +
+       ",\"groupsOwned\":" + std::to_string(c.pb->host.dims.G1) + "}";
   *out = strdup(o.c_str());
   return KS_OK;
   API_CATCH

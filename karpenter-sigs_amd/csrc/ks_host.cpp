@@ -1314,7 +1314,7 @@ void Host::build(const Value& root) {
   tab.st_tol.assign((size_t)dims.S * 2, 0);
   tab.st_flags.assign(dims.S, 0);
   tab.st_toltpl.assign(dims.S, 0);
-  tab.st_gown.assign(dims.S, 0);
+  tab.st_gown.assign((size_t)dims.S * dims.GMW, 0);
   tab.st_rss.assign(groups.empty() ? 1 : (size_t)dims.S * dims.RSW, 0);
   int s = 0;
   for (auto& chain : states)
@@ -1330,7 +1330,7 @@ void Host::build(const Value& root) {
         if (((tab.tpl_taint[(size_t)t * 2] & ~m[0]) | (tab.tpl_taint[(size_t)t * 2 + 1] & ~m[1])) == 0) tt |= 1u << t;
       tab.st_toltpl[s] = tt;
       if (!groups.empty()) {
-        tab.st_gown[s] = st.gown;
+        for (int32_t g : st.gown) gset(tab.st_gown, (size_t)s, dims.GMW, g);
         std::copy(st.rsStrict.begin(), st.rsStrict.end(), tab.st_rss.begin() + (size_t)s * dims.RSW);
       }
       tab.st_flags[s] = (st.hasPreferred ? SF_HAS_PREFERRED : 0) | ((pres & itKeys) ? SF_TOUCHES_IT_KEYS : 0) |

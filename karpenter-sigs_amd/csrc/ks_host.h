@@ -80,7 +80,7 @@ struct PodState {  // one point of the relaxation chain
   std::vector<uint32_t> rsAll, rsStrict;
   bool hasPreferred = false;
   std::vector<TolH> tols;
-  uint64_t gown = 0;  // topology groups the pod owns in this state (Topology.Update, topology.go:91-122)
+  std::vector<int32_t> gown;  // topology groups the pod owns in this state (Topology.Update, topology.go:91-122)
   std::shared_ptr<PodH> spec;  // the (relaxed) pod spec of this state, kept for topology pods only
 };
 
@@ -165,7 +165,7 @@ struct Host {
   const std::set<std::string>* topoExcluded = nullptr;
   std::vector<PodH>* preParsedPods = nullptr;  // set: the snapshot's "pods" already parsed (moved in by build)
   std::map<std::string, std::vector<std::pair<int, int>>> topoContrib;  // cluster pod UID -> (group, value) counted
-  std::map<std::string, uint64_t> topoInvOwner;                         // cluster pod UID -> inverse groups it owns
+  std::map<std::string, std::vector<int32_t>> topoInvOwner;             // cluster pod UID -> inverse groups it owns
   std::vector<int> topoInvOwners;                                       // per group: owning cluster pods
   std::vector<std::vector<char>> topoUniverse;                          // per group, per value: in the domain universe
   std::set<int> topoHostActive;                                         // hostname value ids of the nodes (Register)
@@ -191,7 +191,8 @@ struct Host {
     std::vector<int32_t> tg_meta;   // [G][TGM_WORDS]
     std::vector<int32_t> tg_cnt0;   // counts per (group, value) at NewScheduler time
     std::vector<uint32_t> tg_frs;   // node-filter requirement records
-    std::vector<uint64_t> st_gown, pod_gsel, pod_ginv;
+    std::vector<uint64_t> st_gown, pod_gsel, pod_ginv;  // [S][GMW], [P][GMW], [P][GMW] group sets
+    std::vector<uint64_t> tg_late;                      // [GMW] groups a relaxation creates mid-Solve
     std::vector<uint32_t> st_rss;   // [S][RSW] strict pod requirements (NewStrictPodRequirements)
     std::vector<int32_t> n_tdom;    // [G][N] value index of the node's label for the group's key (-1: none)
     std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask, st_toltpl;
@@ -250,6 +251,12 @@ struct PhaseTimer {
 };
 
 // Binary snapshot of the host model (ks_snapshot.cpp, ks_archive.h)
+// Topology-group sets as GMW-word bitsets (ks_problem.h): set bit g of row `row`; test it.
+inline void gset(std::vector<uint64_t>& v, size_t row, int gmw, int g) { v[row * (size_t)gmw + (size_t)(g >> 6)] |= 1ull << (g & 63); }
+inline bool gtest(const std::vector<uint64_t>& v, size_t row, int gmw, int g) {
+  return (v[row * (size_t)gmw + (size_t)(g >> 6)] >> (g & 63)) & 1ull;
+}
+
 struct ArOut;
 struct ArIn;
 void host_save(ArOut& a, Host& h);

@@ -38,7 +38,7 @@ enum FailCode : uint32_t {
   FC_HOSTPORT = 3,  // checking host port usage
   FC_COMPAT = 4,    // incompatible requirements
   FC_NO_IT = 5,     // no instance type satisfied resources ... (flags in bits 8..13)
-  FC_TOPO = 6,      // unsatisfiable topology constraint (group in bits 16..23)
+  FC_TOPO = 6,      // unsatisfiable topology constraint (group in bits 16..31)
   FC_TOPO_COMPAT = 7,  // the topology requirements are incompatible with the NodeClaim's (record in fail_rs)
   FC_RS_SNAP = 1u << 15,  // FC_NO_IT: the claim's requirements (topology included) are in fail_rs
 };
@@ -72,7 +72,8 @@ struct KsDims {
   int32_t volAny;          // some pending pod mounts a PVC of a driver an existing node limits
   int32_t VD;              // limited drivers (<= kMaxVD); vol_dm[VD] partitions the pods' PVC universe
   int32_t tgUnlab;         // some existing node lacks the label of a topology group's key (k_solve node_slow)
-  uint64_t tgLate;         // groups a relaxed state creates mid-Solve: inactive until that relaxation
+  int32_t GMW;             // 64-bit words of a topology-group set (st_gown, pod_gsel, pod_ginv, tg_late, log_hg):
+                           // ceil(G / 64), at least 1
   uint64_t fkMulti;        // keys some instance type constrains with more than one value (feas_masks)
   int32_t fmOn;            // st_fm is computed (k_feasibility) and k_solve reads it
   int32_t lean;            // none of host ports, limited volumes, pod label requirements, shared UIDs,
@@ -153,9 +154,11 @@ struct KsDev {
   const int32_t KS_G* tg_meta;     // [G][TGM_WORDS]
   const int32_t KS_G* tg_cnt0;     // per group: domain counts over its key's values, -1 = not registered (NewTopology state)
   const uint32_t KS_G* tg_frs;     // node-filter requirement records (spread groups)
-  const uint64_t KS_G* st_gown;    // [S] groups the pod owns in the state
-  const uint64_t KS_G* pod_gsel;   // [P] groups whose selector selects the pod
-  const uint64_t KS_G* pod_ginv;   // [P] inverse groups the pod owns
+  // group sets are GMW-word bitsets (bit g of word g / 64); one word covers every problem with <= 64 groups
+  const uint64_t KS_G* st_gown;    // [S][GMW] groups the pod owns in the state
+  const uint64_t KS_G* pod_gsel;   // [P][GMW] groups whose selector selects the pod
+  const uint64_t KS_G* pod_ginv;   // [P][GMW] inverse groups the pod owns
+  const uint64_t KS_G* tg_late;    // [GMW] groups a relaxed state creates mid-Solve: inactive until that relaxation
   const uint32_t KS_G* st_rss;     // [S][RSW] strict pod requirements (podDomains)
   const int32_t KS_G* n_tdom;      // [G][N] value of the node's label for the group's key, -1 none
   // feasibility tables (ks_host.cpp; k_solve feas_masks): per template, position bitsets per (key, value)
@@ -239,7 +242,7 @@ struct KsWork {
   int32_t KS_G* tg_ccnt;    // [G][Kcap] counts of the NodeClaims' hostname-placeholder domains
   uint32_t KS_G* fail_rs;   // [P][NTPL][FSW] FC_TOPO_COMPAT: requirements; FC_TOPO: the group's counts (-1: unregistered),
                             // or for a hostname group the commit-log length at the failure (the host replays log_hg)
-  uint64_t KS_G* log_hg;    // [P] TOPO Solve: per commit, the hostname groups Topology.Record counted it in
+  uint64_t KS_G* log_hg;    // [P][GMW] TOPO Solve: per commit, the hostname groups Topology.Record counted it in
   int32_t KS_G* tg_act;     // [G] TOPO Solve: NewNodeClaim ordinal counter when a late group was created
   // consolidation simulations only (k_solve<.., SIM=true>): this simulation's view of the shared
   // cluster problem (helpers.go:73-127 — candidates removed, their pods added to the pending ones)
@@ -257,7 +260,7 @@ struct KsWork {
   // SIM topology: NewTopology's counts with this simulation's pods excluded (topology.go:61-85)
   const int32_t KS_G* tdel;     // [ntdel][2]: tg_cnt offset, (pods removed << 1) | unregister-if-zero
   int32_t ntdel;
-  uint64_t tdead;               // inverse groups none of whose owners exist in this simulation
+  const uint64_t KS_G* tdead;   // [GMW] inverse groups none of whose owners exist in this simulation
 };
 
 enum Counter {

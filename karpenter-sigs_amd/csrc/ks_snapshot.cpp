@@ -78,7 +78,7 @@ template <class A> void io_tables(A& a, Host::Tables& t, uint64_t rsw) {
          t.n_vlim, t.tg_meta, t.tg_cnt0, t.tg_frs, t.st_gown, t.pod_gsel, t.pod_ginv, t.n_tdom, t.it_rs, t.tpl_rs, t.n_rs0,
          t.pool_mask, t.st_toltpl, t.tpl_taint, t.st_tol, t.n_taint, t.tsort_pos, t.it_off_beg, t.off_zone, t.off_ct,
          t.tpl_it_beg, t.tpl_its, t.tpl_pool, t.pod_state0, t.pod_nstate, t.pod_uid, t.st_flags, t.pod_rmask, t.tpl_rmask,
-         t.pod_rfmt, t.tpl_rfmt, t.fk_words, t.fk_key_off, t.fk_tpl);
+         t.pod_rfmt, t.tpl_rfmt, t.fk_words, t.fk_key_off, t.fk_tpl, t.tg_late);
   // (st_rss is one word when the problem has no topology groups)
   io_rows(a, t.st_rs, rsw);
   io_rows(a, t.st_rss, t.st_rss.size() < rsw && !A::reading ? t.st_rss.size() : rsw);
@@ -181,7 +181,9 @@ void host_check(const Host& h) {
   need(t.st_tol.size(), S * 2, "st_tol");
   need(t.st_flags.size(), S, "st_flags");
   need(t.st_toltpl.size(), S, "st_toltpl");
-  need(t.st_gown.size(), S, "st_gown");
+  if (d.GMW < 1 || d.GMW < (d.G + 63) / 64) bad("group set width");
+  need(t.st_gown.size(), S * d.GMW, "st_gown");
+  need(t.tg_late.size(), d.GMW, "tg_late");
   need(t.n_avail.size(), N1 * R, "n_avail");
   need(t.n_req0.size(), N1 * R, "n_req0");
   need(t.n_rs0.size(), N1 * RSW, "n_rs0");
@@ -192,8 +194,8 @@ void host_check(const Host& h) {
   need(t.n_vc0.size(), N1 * VD1, "n_vc0");
   need(t.n_vlim.size(), N1 * VD1, "n_vlim");
   need(t.vol_dm.size(), VD1, "vol_dm");
-  need(t.pod_gsel.size(), P1, "pod_gsel");
-  need(t.pod_ginv.size(), P1, "pod_ginv");
+  need(t.pod_gsel.size(), P1 * d.GMW, "pod_gsel");
+  need(t.pod_ginv.size(), P1 * d.GMW, "pod_ginv");
   // CSR tables and the indices the kernels follow
   auto mono = [&](const std::vector<int32_t>& v, size_t n, int64_t hi, const char* what) {
     if (v[0] != 0) bad(what);
@@ -294,13 +296,13 @@ template <class A> void host_io(A& a, Host& h) {
 // Layout guards: adding a member to one of these types changes its size and stops the build here until the
 // member is listed above (sizes of this toolchain's libstdc++, x86-64).
 static_assert(sizeof(PodH) == 640, "PodH changed: update io(PodH) in ks_snapshot.cpp");
-static_assert(sizeof(Host::Tables) == 1344, "Host::Tables changed: update io(Host::Tables)");
+static_assert(sizeof(Host::Tables) == 1368, "Host::Tables changed: update io(Host::Tables)");
 static_assert(sizeof(Host::Node) == 456, "Host::Node changed: update io(Host::Node)");
 static_assert(sizeof(Host::Tpl) == 280, "Host::Tpl changed: update io(Host::Tpl)");
 static_assert(sizeof(Host::IT) == 224, "Host::IT changed: update io(Host::IT)");
 static_assert(sizeof(TopoGroup) == 256, "TopoGroup changed: update io(TopoGroup)");
-static_assert(sizeof(PodState) == 104, "PodState changed: update io(PodState)");
-static_assert(sizeof(Host) == 2848, "Host changed: update host_io");
+static_assert(sizeof(PodState) == 120, "PodState changed: update io(PodState)");
+static_assert(sizeof(Host) == 2864, "Host changed: update host_io");
 static_assert(sizeof(HostPortH) == 88 && sizeof(AffTerm) == 128 && sizeof(SpreadC) == 104 && sizeof(LabelSel) == 32,
               "a pod-spec type changed: update its io()");
 

@@ -40,14 +40,8 @@
 #ifndef KS_NODE_K  // existing nodes per lane per step of the first-fit scan beyond the register window
 #define KS_NODE_K 2
 #endif
-#ifndef KS_TOPO_WINDOW_BATCH  // register window + topology: every window node's topology loads issued at once
-#define KS_TOPO_WINDOW_BATCH 0
-#endif
 #ifndef KS_SORT_LANE0  // 1: the claim re-sort's exact pdqsort on lane 0 (the round-2 form)
 #define KS_SORT_LANE0 0
-#endif
-#ifndef KS_TOPO_NODE_SERIAL  // the topology node test one node at a time (see topo_node_stateK)
-#define KS_TOPO_NODE_SERIAL 1
 #endif
 #ifndef KS_CLAIM_RUNS  // LEAN Solve: runs of identical pods placed on one NodeClaim in one step
 #define KS_CLAIM_RUNS 1
@@ -62,10 +56,13 @@ namespace ks {
 using LI32 = int32_t KS_L*;
 using LI64 = int64_t KS_L*;
 using LU32 = uint32_t KS_L*;
+using LU64 = uint64_t KS_L*;
 using GI32 = int32_t KS_G*;
 using GI64 = int64_t KS_G*;
 using GU32 = uint32_t KS_G*;
 using DevLayout = ReqLayoutT<const KeyMeta KS_L*, const uint32_t KS_G*, const int64_t KS_G*>;
+// Topology-group sets of the popped pod kept in LDS beyond word 0 (Solver::s_gw rows)
+enum GroupSet : int { GS_MASK = 0, GS_SEL, GS_INV, GS_ACT, GS_N };
 
 __device__ __forceinline__ int lane() { return (int)threadIdx.x & (kWave - 1); }
 __device__ __forceinline__ uint64_t wballot(bool p) { return __ballot(p ? 1 : 0); }
@@ -169,7 +166,7 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
       for (int64_t i = gtid; i < (int64_t)d.G * (d.Kcap + 1); i += gsz) W.tg_ccnt[i] = 0;
       for (int64_t i = gtid; i < d.G; i += gsz) W.tg_cpos[i] = 0;
       for (int64_t i = gtid; i < d.G; i += gsz) W.tg_act[i] = 0;
-      for (int64_t i = gtid; i < d.P; i += gsz) W.log_hg[i] = 0;
+      for (int64_t i = gtid; i < (int64_t)d.P * d.GMW; i += gsz) W.log_hg[i] = 0;
     }
     for (int64_t i = gtid; i < d.P; i += gsz) {
       W.queue[i] = qorder[i];
@@ -512,13 +509,18 @@ struct Solver {
                         // whole table when it fits, make_plan)
   LU32 s_tcd;           // SIM: dirty bits over count words [tgSmall, tgCntWords): set once W.tg_cnt holds the word
   LI32 s_bnode;         // LEAN SIM: [64] run placement: the node taking the run's pod at each offset (first of a node's pods)
-  uint64_t t_mask = 0;  // groups matching the popped pod (owned in its state | inverse groups selecting it)
-  uint64_t t_sel = 0;   // groups whose selector selects the popped pod
-  uint64_t t_inv = 0;   // inverse groups the popped pod owns
+  // Topology-group sets are GMW-word bitsets (ks_problem.h).  Word 0 lives in a register (it is the whole set
+  // whenever a problem has <= 64 groups); words 1.. live in LDS, s_gw[set * GMW + w] (sets GS_*).
+  LU64 s_gw;            // [GS_N][GMW] when GMW > 1
+  uint64_t t_mask = 0;  // groups matching the popped pod (owned in its state | inverse groups selecting it), word 0
+  uint64_t t_sel = 0;   // groups whose selector selects the popped pod, word 0
+  uint64_t t_inv = 0;   // inverse groups the popped pod owns, word 0
+  bool t_any = false;   // t_mask is not empty (any word)
+  bool t_rec = false;   // t_sel | t_inv is not empty (any word): Topology.Record has groups to visit
   int t_s = 0;          // the popped pod's relaxation state
   const uint32_t KS_G* fnp = nullptr;  // k_feasibility_nodes's row of the popped pod's state (null: none)
   bool t_nonode = false;  // some matching group admits no domain at all: no existing node can pass
-  uint64_t t_active = ~0ull;  // groups in t.topologies so far (late groups join at their relaxation)
+  uint64_t t_active = ~0ull;  // groups in t.topologies so far (late groups join at their relaxation), word 0
   int64_t algbytes = 0;
   bool rem_same = false;  // the last claim_full left the claim's options unchanged (commit skips the copy back)
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
@@ -674,7 +676,7 @@ struct Solver {
   // k_feasibility's row for (state s, template t), or null where it does not apply: not computed, or
   // topology requirements were added to the record (they are not part of the row).
   __device__ __forceinline__ const uint32_t KS_G* fm_row(int s, int t) const {
-    if (KS_FM_OFF || !d.fmOn || (TOPO && t_mask)) return nullptr;
+    if (KS_FM_OFF || !d.fmOn || (TOPO && t_any)) return nullptr;
     return D.st_fm + ((int64_t)s * d.NTPL + t) * d.TW;
   }
   __device__ __forceinline__ bool fbit(LU32 m, int pos) const { return (m[pos >> 5] >> (pos & 31)) & 1u; }
@@ -769,7 +771,7 @@ struct Solver {
       if (keys(sflags) && ok[i]) ok[i] = node_compat(c[i]);  // strict Compatible
       sl[i] = false;
     }
-    if (TOPO && t_mask) topo_node_stateK<KN>(c, ok, sl);  // topology (existingnode.go:106-114)
+    if (TOPO && t_any) topo_node_stateK<KN>(c, ok, sl);  // topology (existingnode.go:106-114)
   }
   __device__ __forceinline__ const uint32_t KS_G* node_rs(int n) const {
     if (!SIM) return W.n_rs + (int64_t)n * d.RSW;
@@ -880,159 +882,143 @@ struct Solver {
   // inverse groups whose selector selects the pod), domainMinCount per spread group (:192-213) and,
   // per affinity group, whether some domain the pod allows already holds a selected pod (:215-221;
   // for hostname keys that includes NodeClaim placeholders, counted in tg_cpos).
+  // Word w of the set {0, ..., n-1}.
+  __device__ __forceinline__ static uint64_t bits_below(int n, int w) {
+    const int k = n - 64 * w;
+    return k >= 64 ? ~0ull : k <= 0 ? 0ull : ((1ull << k) - 1ull);
+  }
+  // Word w of group set `set` (GS_*); r0: the set's register word 0.
+  __device__ __forceinline__ uint64_t gword(int set, int w, uint64_t r0) const {
+    return w == 0 ? r0 : (uint64_t)uni64((int64_t)s_gw[set * d.GMW + w]);
+  }
+  __device__ __forceinline__ bool sel_has(int g) const {  // the popped pod is selected by group g
+    return ((gword(GS_SEL, g >> 6, t_sel) >> (g & 63)) & 1ull) != 0;
+  }
   __device__ __forceinline__ void topo_pop(int s, int gpod) {
     t_s = s;
-    t_sel = D.pod_gsel[gpod];
-    t_inv = D.pod_ginv[gpod];
-    const uint64_t all = d.G >= 64 ? ~0ull : ((1ull << d.G) - 1);
-    const uint64_t owned = d.G1 >= 64 ? ~0ull : ((1ull << d.G1) - 1);
-    t_mask = D.st_gown[s] | (t_sel & all & ~owned);
-    if (SIM) t_mask &= ~W.tdead;
-    t_nonode = false;
-    for (uint64_t m = t_mask; m; m &= m - 1) {
-      const int g = ctz64(m);
-      if (tg(g, TGM_TYPE) == TG_AFFINITY) {
-        const int nv = tg(g, TGM_NV);
-        bool pos = false, reg = false;
-        for (int v = lane(); v < nv && !pos; v += kWave) {
-          const int c = tcnt(g, v);
-          const bool has = c >= 0 && tpod_has(g, v);
-          pos = has && c > 0;
-          reg = reg || has;
-        }
-        if (lane() == 0 && tg(g, TGM_HOST) && tpod_has(g, nv) && ld_sc1(W.tg_cpos + g) > 0) pos = true;
-        const bool any = wballot(pos) != 0;
-        if (lane() == 0) s_tmin[g] = any ? 1 : 0;
-        // topo_node_ok's test for this group over every domain: with a selected pod somewhere the
-        // node's domain must hold one; otherwise only a self-selecting pod passes (a registered domain)
-        if (!tg(g, TGM_HOST) && !any && !(((t_sel >> g) & 1ull) && wballot(reg))) t_nonode = true;
-        continue;
+    const int GMW = d.GMW;
+    const uint64_t KS_G* sel = D.pod_gsel + (int64_t)gpod * GMW;
+    const uint64_t KS_G* inv = D.pod_ginv + (int64_t)gpod * GMW;
+    const uint64_t KS_G* own = D.st_gown + (int64_t)s * GMW;
+    t_sel = sel[0];
+    t_inv = inv[0];
+    t_mask = own[0] | (t_sel & bits_below(d.G, 0) & ~bits_below(d.G1, 0));
+    if (SIM) t_mask &= ~W.tdead[0];
+    bool anyM = t_mask != 0, anyR = (t_sel | t_inv) != 0;
+    if (GMW > 1) {  // words 1.. (more than 64 groups), one lane each, into LDS
+      bool m = false, r = false;
+      for (int w = 1 + lane(); w < GMW; w += kWave) {
+        const uint64_t sw = sel[w], iw = inv[w];
+        uint64_t mw = own[w] | (sw & bits_below(d.G, w) & ~bits_below(d.G1, w));
+        if (SIM) mw &= ~W.tdead[w];
+        s_gw[GS_SEL * GMW + w] = sw;
+        s_gw[GS_INV * GMW + w] = iw;
+        s_gw[GS_MASK * GMW + w] = mw;
+        m = m || mw != 0;
+        r = r || (sw | iw) != 0;
       }
-      if (tg(g, TGM_TYPE) == TG_ANTI) {  // topo_node_ok: the node's domain must hold no selected pod
-        if (!tg(g, TGM_HOST)) {
-          const int nv = tg(g, TGM_NV);
-          bool ok = false;
-          for (int v = lane(); v < nv && !ok; v += kWave) ok = tcnt(g, v) == 0 && tpod_has(g, v);
-          if (!wballot(ok)) t_nonode = true;
-        }
-        continue;
-      }
-      if (tg(g, TGM_TYPE) != TG_SPREAD) continue;
-      int mn = 0x7fffffff, num = 0;
-      if (!tg(g, TGM_HOST)) {  // hostname groups always have a min of 0
-        const int nv = tg(g, TGM_NV);
-        int lo = 0x7fffffff;  // smallest registered count (any domain): topo_node_ok's best case
-        for (int v = lane(); v < nv; v += kWave) {
-          const int c = tcnt(g, v);
-          if (c >= 0) lo = c < lo ? c : lo;
-          if (c >= 0 && tpod_has(g, v)) {
-            num++;
-            mn = c < mn ? c : mn;
-          }
-        }
-        for (int off = 32; off >= 1; off >>= 1) {
-          const int o = __shfl_xor(mn, off), l = __shfl_xor(lo, off);
-          mn = o < mn ? o : mn;
-          lo = l < lo ? l : lo;
-          num += __shfl_xor(num, off);
-        }
-        if (tg(g, TGM_MIND) >= 0 && num < tg(g, TGM_MIND)) mn = 0;
-        const int self = (int)((t_sel >> g) & 1ull);
-        if (lo == 0x7fffffff || (int64_t)lo + self - mn > tg(g, TGM_SKEW)) t_nonode = true;
-      } else {
-        mn = 0;
-      }
-      if (lane() == 0) s_tmin[g] = mn;
+      anyM = anyM || wballot(m) != 0;
+      anyR = anyR || wballot(r) != 0;
+      wsync();
     }
+    t_any = anyM;
+    t_rec = anyR;
+    t_nonode = false;
+    for (int w = 0; w < GMW; w++)
+      for (uint64_t m = gword(GS_MASK, w, t_mask); m; m &= m - 1) {
+        const int g = 64 * w + ctz64(m);
+        if (tg(g, TGM_TYPE) == TG_AFFINITY) {
+          const int nv = tg(g, TGM_NV);
+          bool pos = false, reg = false;
+          for (int v = lane(); v < nv && !pos; v += kWave) {
+            const int c = tcnt(g, v);
+            const bool has = c >= 0 && tpod_has(g, v);
+            pos = has && c > 0;
+            reg = reg || has;
+          }
+          if (lane() == 0 && tg(g, TGM_HOST) && tpod_has(g, nv) && ld_sc1(W.tg_cpos + g) > 0) pos = true;
+          const bool any = wballot(pos) != 0;
+          s_tmin[g] = any ? 1 : 0;  // wave-wide store of a uniform value
+          // topo_node_ok's test for this group over every domain: with a selected pod somewhere the
+          // node's domain must hold one; otherwise only a self-selecting pod passes (a registered domain)
+          if (!tg(g, TGM_HOST) && !any && !(sel_has(g) && wballot(reg))) t_nonode = true;
+          continue;
+        }
+        if (tg(g, TGM_TYPE) == TG_ANTI) {  // topo_node_ok: the node's domain must hold no selected pod
+          if (!tg(g, TGM_HOST)) {
+            const int nv = tg(g, TGM_NV);
+            bool ok = false;
+            for (int v = lane(); v < nv && !ok; v += kWave) ok = tcnt(g, v) == 0 && tpod_has(g, v);
+            if (!wballot(ok)) t_nonode = true;
+          }
+          continue;
+        }
+        if (tg(g, TGM_TYPE) != TG_SPREAD) continue;
+        int mn = 0x7fffffff, num = 0;
+        if (!tg(g, TGM_HOST)) {  // hostname groups always have a min of 0
+          const int nv = tg(g, TGM_NV);
+          int lo = 0x7fffffff;  // smallest registered count (any domain): topo_node_ok's best case
+          for (int v = lane(); v < nv; v += kWave) {
+            const int c = tcnt(g, v);
+            if (c >= 0) lo = c < lo ? c : lo;
+            if (c >= 0 && tpod_has(g, v)) {
+              num++;
+              mn = c < mn ? c : mn;
+            }
+          }
+          for (int off = 32; off >= 1; off >>= 1) {
+            const int o = __shfl_xor(mn, off), l = __shfl_xor(lo, off);
+            mn = o < mn ? o : mn;
+            lo = l < lo ? l : lo;
+            num += __shfl_xor(num, off);
+          }
+          if (tg(g, TGM_MIND) >= 0 && num < tg(g, TGM_MIND)) mn = 0;
+          const int self = sel_has(g) ? 1 : 0;
+          if (lo == 0x7fffffff || (int64_t)lo + self - mn > tg(g, TGM_SKEW)) t_nonode = true;
+        } else {
+          mn = 0;
+        }
+        s_tmin[g] = mn;  // wave-wide store of a uniform value (mn is reduced over the wave)
+      }
     wsync();
   }
-  // ExistingNode.Add's topology step for nodes c[0..KN) (one lane each): a node's single domain of each
-  // matching group must be the one TopologyGroup.Get returns (existingnode.go:106-114).  Nodes with ok[i]
-  // false stay failed.  sl[i]: every labelled group passes, but the node lacks the label of some group's
-  // key (its domain then comes from the requirements it accumulated; node_slow decides).  The groups go
-  // in chunks of TGC: all KN * TGC domains are loaded, then all their counts, then tested, so a chunk
-  // costs two memory round trips however many nodes and groups it covers.
-  // The per-node form (KS_TOPO_NODE_SERIAL): 0 fails, 1 passes, 2 decided by node_slow.
+  // ExistingNode.Add's topology step for node n (one lane each): a node's single domain of each matching group
+  // must be the one TopologyGroup.Get returns (existingnode.go:106-114).  0 fails, 1 passes, 2: every labelled
+  // group passes, but the node lacks the label of some group's key (its domain then comes from the
+  // requirements it accumulated; node_slow decides).  (A batched form -- all nodes' and groups' loads issued
+  // before any test -- measured slower, DESIGN §3, and is not kept.)
   __device__ __forceinline__ int topo_node_state1(int n) const {
     int st = 1;
-    for (uint64_t m = t_mask; m; m &= m - 1) {
-      const int g = ctz64(m);
-      const int v = D.n_tdom[(int64_t)g * d.N + n];
-      if (v < 0) {
-        st = 2;
-        continue;
+    for (int w = 0; w < d.GMW; w++)
+      for (uint64_t m = gword(GS_MASK, w, t_mask); m; m &= m - 1) {
+        const int g = 64 * w + ctz64(m);
+        const int v = D.n_tdom[(int64_t)g * d.N + n];
+        if (v < 0) {
+          st = 2;
+          continue;
+        }
+        const int c = tcnt(g, v);
+        if (c < 0) return 0;  // unregistered: Get never returns it
+        const int type = tg(g, TGM_TYPE);
+        if (type == TG_SPREAD) {
+          const int self = sel_has(g) ? 1 : 0;
+          if ((int64_t)c + self - s_tmin[g] > tg(g, TGM_SKEW)) return 0;
+        } else if (type == TG_AFFINITY) {  // a selected pod's domain, or the bootstrap for a self-selecting pod
+          if (!tpod_has(g, v)) return 0;
+          if (s_tmin[g] ? c == 0 : !sel_has(g)) return 0;
+        } else if (c != 0 || !tpod_has(g, v)) {
+          return 0;
+        }
       }
-      const int c = tcnt(g, v);
-      if (c < 0) return 0;  // unregistered: Get never returns it
-      const int type = tg(g, TGM_TYPE);
-      if (type == TG_SPREAD) {
-        const int self = (int)((t_sel >> g) & 1ull);
-        if ((int64_t)c + self - s_tmin[g] > tg(g, TGM_SKEW)) return 0;
-      } else if (type == TG_AFFINITY) {  // a selected pod's domain, or the bootstrap for a self-selecting pod
-        if (!tpod_has(g, v)) return 0;
-        if (s_tmin[g] ? c == 0 : !((t_sel >> g) & 1ull)) return 0;
-      } else if (c != 0 || !tpod_has(g, v)) {
-        return 0;
-      }
-    }
     return st;
   }
   template <int KN>
   __device__ __forceinline__ void topo_node_stateK(const int* c, bool* ok, bool* sl) const {
-#if KS_TOPO_NODE_SERIAL
 #pragma unroll
     for (int i = 0; i < KN; i++) {
       const int st = ok[i] ? topo_node_state1(c[i]) : 0;
       ok[i] = st == 1;
       sl[i] = st == 2;
-    }
-    return;
-#endif
-    constexpr int TGC = 4;
-    int st[KN];  // 0 fails, 1 passes, 2 decided by node_slow
-#pragma unroll
-    for (int i = 0; i < KN; i++) st[i] = ok[i] ? 1 : 0;
-    for (uint64_t m = t_mask; m;) {
-      int gs[TGC];
-#pragma unroll
-      for (int j = 0; j < TGC; j++) {
-        gs[j] = m ? ctz64(m) : -1;
-        m &= m - 1;
-      }
-      int v[TGC][KN], cn[TGC][KN];
-#pragma unroll
-      for (int j = 0; j < TGC; j++)
-#pragma unroll
-        for (int i = 0; i < KN; i++) v[j][i] = gs[j] >= 0 ? D.n_tdom[(int64_t)gs[j] * d.N + c[i]] : 0;
-#pragma unroll
-      for (int j = 0; j < TGC; j++)
-#pragma unroll
-        for (int i = 0; i < KN; i++) cn[j][i] = (gs[j] >= 0 && v[j][i] >= 0) ? tcnt(gs[j], v[j][i]) : 0;
-      // Branch-free per node: the per-lane `continue` / if-else form of this update is miscompiled at -O1
-      // and above for KN > 1 (scripts/repro/topo_batch_repro.hip reproduces it standalone).
-#pragma unroll
-      for (int j = 0; j < TGC; j++) {
-        if (gs[j] < 0) break;
-        const int g = gs[j], type = tg(g, TGM_TYPE), tmin = s_tmin[g], skew = tg(g, TGM_SKEW);
-        const int self = (int)((t_sel >> g) & 1ull);
-#pragma unroll
-        for (int i = 0; i < KN; i++) {
-          const int vv = v[j][i], cc = cn[j][i];
-          const bool unl = vv < 0;
-          const bool has = tpod_has(g, unl ? 0 : vv);
-          const bool sp = (int64_t)cc + self - tmin <= skew;
-          const bool af = has && (tmin ? cc != 0 : self != 0);
-          const bool an = cc == 0 && has;
-          const bool pass = cc >= 0 && (type == TG_SPREAD ? sp : type == TG_AFFINITY ? af : an);
-          const int s0 = st[i];
-          st[i] = unl ? (s0 == 1 ? 2 : s0) : (pass ? s0 : 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < KN; i++) {
-      ok[i] = st[i] == 1;
-      sl[i] = st[i] == 2;
     }
   }
   // ExistingNode.Add's requirement and topology steps for node j, wave-wide, for a node lacking the
@@ -1080,8 +1066,9 @@ struct Solver {
   __device__ __forceinline__ uint32_t topo_apply(LU32 rs, int claim, uint64_t allow) {
     copy_words(s_trs0, rs, d.RSW);
     wsync();
-    for (uint64_t m = t_mask; m; m &= m - 1) {
-      const int g = ctz64(m);
+    for (int w = 0; w < d.GMW; w++)
+    for (uint64_t m = gword(GS_MASK, w, t_mask); m; m &= m - 1) {
+      const int g = 64 * w + ctz64(m);
       const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
       const bool host = tg(g, TGM_HOST) != 0;
       const KeyMeta km = L.keys[k];
@@ -1105,7 +1092,7 @@ struct Solver {
         }
       };
       if (tg(g, TGM_TYPE) == TG_SPREAD) {  // nextDomainTopologySpread: smallest count, then smallest name
-        const int self = (int)((t_sel >> g) & 1ull), mn = s_tmin[g], skew = tg(g, TGM_SKEW);
+        const int self = sel_has(g) ? 1 : 0, mn = s_tmin[g], skew = tg(g, TGM_SKEW);
         uint64_t best = ~0ull;
         scan(true, [&](int v) {
           const bool nodeHas = rs_member(L, s_trs0, k, v);
@@ -1126,7 +1113,7 @@ struct Solver {
         const int bv = (int)(uint32_t)best;
         if (lane() == 0) s_trs1[L.HDR + km.off + (bv >> 5)] = 1u << (bv & 31);
       } else if (tg(g, TGM_TYPE) == TG_AFFINITY) {  // nextDomainAffinity
-        const bool self = (t_sel >> g) & 1ull;
+        const bool self = sel_has(g);
         if (s_tmin[g]) {  // the domains already holding a selected pod (other placeholders drop out in Add)
           scan(true, [&](int v) {
             const int c = v < nv ? tcnt(g, v) : tccnt(g, claim);
@@ -1199,83 +1186,93 @@ struct Solver {
   // the node's own label value (the strict Compatible admitted nothing else; ks_topo.cpp refuses
   // the one input where a pod's NotIn could stand in for a missing label), so the node's domain
   // table replaces the scan over F's value words.
-  // Solve (not SIM): returns the hostname groups it counted the pod in (the commit's log_hg entry, which
-  // the host replays to print a hostname group's counts in an unsatisfiable-topology message).
+  // Solve (not SIM): logAt >= 0 is the commit's log position; its log_hg entry gets the hostname groups Topology.Record
+  // counted the pod in (the host replays them to print a hostname group's counts in an unsatisfiable-topology
+  // message).
   template <class PR>
-  __device__ __forceinline__ uint64_t topo_record(PR F, int claim, int node, uint64_t allow) {
+  __device__ __forceinline__ void topo_record(PR F, int claim, int node, uint64_t allow, int logAt) {
     hbm_release();
-    uint64_t hg = 0;
-    const uint64_t owned = d.G1 >= 64 ? ~0ull : ((1ull << d.G1) - 1);
+    const int GMW = d.GMW;
     const uint64_t pres = rs_present(F), compl_ = rs_compl(F);
-    for (uint64_t m = (t_sel & owned & t_active) | t_inv; m; m &= m - 1) {
-      const int g = ctz64(m);
-      const bool ownedGroup = g < d.G1;
-      if (ownedGroup && tg(g, TGM_TYPE) == TG_SPREAD && tg(g, TGM_FEND) > tg(g, TGM_FBEG)) {  // nodeFilter
-        int match = 0;
-        if (lane() == 0)
-          for (int f = tg(g, TGM_FBEG); f < tg(g, TGM_FEND) && !match; f++)
-            match = rs_compatible(L, F, D.tg_frs + (int64_t)f * d.RSW, allow) ? 1 : 0;
-        if (!rdl(match, 0)) continue;
-      }
-      if (node >= 0) {
-        int rec = 0;
-        if (lane() == 0) {
-          const int v = D.n_tdom[(int64_t)g * d.N + node];
-          if (v >= 0) tcnt_inc(tg(g, TGM_CNT) + v);  // recording registers the domain
-          rec = v >= 0;
+    for (int w = 0; w < GMW; w++) {
+      uint64_t hg = 0;
+      const uint64_t sel = gword(GS_SEL, w, t_sel), inv = gword(GS_INV, w, t_inv), act = gword(GS_ACT, w, t_active);
+      for (uint64_t m = (sel & bits_below(d.G1, w) & act) | inv; m; m &= m - 1) {
+        const int g = 64 * w + ctz64(m);
+        const bool ownedGroup = g < d.G1;
+        if (ownedGroup && tg(g, TGM_TYPE) == TG_SPREAD && tg(g, TGM_FEND) > tg(g, TGM_FBEG)) {  // nodeFilter
+          int match = 0;
+          if (lane() == 0)
+            for (int f = tg(g, TGM_FBEG); f < tg(g, TGM_FEND) && !match; f++)
+              match = rs_compatible(L, F, D.tg_frs + (int64_t)f * d.RSW, allow) ? 1 : 0;
+          if (!rdl(match, 0)) continue;
         }
-        if (!SIM && tg(g, TGM_HOST) && rdl(rec, 0)) hg |= 1ull << g;
-        continue;
-      }
-      const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
-      if (!bit(pres, k)) continue;  // Get() of a missing key is Exists: no values
-      const KeyMeta km = L.keys[k];
-      if (ownedGroup && tg(g, TGM_TYPE) != TG_ANTI) {  // spread / affinity: only a collapsed domain
-        int tot = 0;
-        for (int w = lane(); w < km.nw; w += kWave) tot += __popc(F[L.HDR + km.off + w]);
-        for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off);
-        if (bit(compl_, k) || tot != 1) continue;
-      }
-      bool any = false;
-      for (int w = lane(); w < km.nw; w += kWave) {  // anti-affinity: every domain of the requirement
-        uint32_t x = F[L.HDR + km.off + w];
-        any = any || x != 0;
-        while (x) {
-          const int v = w * 32 + __builtin_ctz(x);
-          x &= x - 1;
-          if (v >= nv) {
-            if (claim >= 0) {  // -1: not registered in a late group (recording registers it)
-              const int64_t at = (int64_t)g * W.ccs + claim;
-              const int cc = W.tg_ccnt[at];
-              W.tg_ccnt[at] = cc < 0 ? 1 : cc + 1;
-              if (cc <= 0) W.tg_cpos[g] += 1;  // one more placeholder holding a counted pod
+        if (node >= 0) {
+          int rec = 0;
+          if (lane() == 0) {
+            const int v = D.n_tdom[(int64_t)g * d.N + node];
+            if (v >= 0) tcnt_inc(tg(g, TGM_CNT) + v);  // recording registers the domain
+            rec = v >= 0;
+          }
+          if (!SIM && tg(g, TGM_HOST) && rdl(rec, 0)) hg |= 1ull << (g & 63);
+          continue;
+        }
+        const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
+        if (!bit(pres, k)) continue;  // Get() of a missing key is Exists: no values
+        const KeyMeta km = L.keys[k];
+        if (ownedGroup && tg(g, TGM_TYPE) != TG_ANTI) {  // spread / affinity: only a collapsed domain
+          int tot = 0;
+          for (int wd = lane(); wd < km.nw; wd += kWave) tot += __popc(F[L.HDR + km.off + wd]);
+          for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off);
+          if (bit(compl_, k) || tot != 1) continue;
+        }
+        bool any = false;
+        for (int wd = lane(); wd < km.nw; wd += kWave) {  // anti-affinity: every domain of the requirement
+          uint32_t x = F[L.HDR + km.off + wd];
+          any = any || x != 0;
+          while (x) {
+            const int v = wd * 32 + __builtin_ctz(x);
+            x &= x - 1;
+            if (v >= nv) {
+              if (claim >= 0) {  // -1: not registered in a late group (recording registers it)
+                const int64_t at = (int64_t)g * W.ccs + claim;
+                const int cc = W.tg_ccnt[at];
+                W.tg_ccnt[at] = cc < 0 ? 1 : cc + 1;
+                if (cc <= 0) W.tg_cpos[g] += 1;  // one more placeholder holding a counted pod
+              }
+            } else {
+              tcnt_inc(tg(g, TGM_CNT) + v);
             }
-          } else {
-            tcnt_inc(tg(g, TGM_CNT) + v);
           }
         }
+        if (!SIM && tg(g, TGM_HOST) && wballot(any)) hg |= 1ull << (g & 63);
       }
-      if (!SIM && tg(g, TGM_HOST) && wballot(any)) hg |= 1ull << g;
+      if (!SIM && logAt >= 0 && hg) W.log_hg[(int64_t)logAt * GMW + w] = hg;  // wave-wide store of a uniform value
     }
     hbm_release();
     wsync();
-    return hg;
-  }
-  // the commit at log position i was counted in the hostname groups hg (Solve only)
-  __device__ __forceinline__ void log_hgroups(int i, uint64_t hg) const {
-    if (!SIM && hg && lane() == 0) W.log_hg[i] = hg;
   }
 
-  // Topology.Update creating the late groups `m` (topology.go:102-119), wave-wide: the NodeClaims made so
-  // far registered their placeholders before these groups existed (NewNodeClaim's Register only reaches
-  // t.topologies), so their placeholder domains start unregistered.
-  __device__ __forceinline__ void topo_activate(uint64_t m, int nclaims, int hostCtr) {
-    for (; m; m &= m - 1) {
-      const int g = ctz64(m);
-      for (int c = lane(); c < nclaims; c += kWave) W.tg_ccnt[(int64_t)g * W.ccs + c] = -1;
-      if (!SIM && lane() == 0) W.tg_act[g] = hostCtr;  // placeholders up to this ordinal were never registered
+  // Topology.Update for relaxation state s1 (topology.go:102-119), wave-wide: the late groups it owns that do not
+  // exist yet are created now.  The NodeClaims made so far registered their placeholders before these groups
+  // existed (NewNodeClaim's Register only reaches t.topologies), so their placeholder domains start unregistered.
+  __device__ __forceinline__ void topo_activate_state(int s1, int nclaims, int hostCtr) {
+    const int GMW = d.GMW;
+    const uint64_t KS_G* own = D.st_gown + (int64_t)s1 * GMW;
+    bool any = false;
+    for (int w = 0; w < GMW; w++) {
+      const uint64_t act = gword(GS_ACT, w, t_active), fresh = own[w] & ~act;
+      if (!fresh) continue;
+      any = true;
+      for (uint64_t m = fresh; m; m &= m - 1) {
+        const int g = 64 * w + ctz64(m);
+        for (int c = lane(); c < nclaims; c += kWave) W.tg_ccnt[(int64_t)g * W.ccs + c] = -1;
+        if (!SIM) W.tg_act[g] = hostCtr;  // placeholders up to this ordinal were never registered (uniform store)
+      }
+      if (w == 0) t_active = act | fresh;
+      else s_gw[GS_ACT * GMW + w] = act | fresh;  // wave-wide store of a uniform value
     }
-    hbm_release();
+    if (any) hbm_release();
     wsync();
   }
 
@@ -1302,13 +1299,13 @@ struct Solver {
     const ClaimView<INL>& v = cv<INL>();
     bool changed = false;
     PH_BEGIN(u0);
-    if (keys(sflags) || (TOPO && t_mask)) {
+    if (keys(sflags) || (TOPO && t_any)) {
       const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
       copy_words(s_rs, crs, d.RSW);
       wsync();
       if (keys(sflags))
         changed = rs_add_wave(L, s_rs, s_pin, (sflags & SF_TOUCHES_IT_KEYS) ? d.itKeys : 0);
-      if (TOPO && t_mask) {
+      if (TOPO && t_any) {
         if (topo_apply(s_rs, c, d.allowWK) != 0) {  // topology requirements (nodeclaim.go:92-100)
           ncnt = 0;
           return false;
@@ -1517,16 +1514,16 @@ struct Solver {
     v.cnt[c] = ncnt;
     s_okey[pos] = okNew;
     if (hpA() && lane() == 0) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
-    if (keys(sflags) || (TOPO && t_mask)) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
+    if (keys(sflags) || (TOPO && t_any)) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
     if (!rem_same) copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     log_commit(p, c, nlog);
     // The max bound stays valid as the options only shrink; it is tightened lazily when a full check
     // fails.  HBM-resident claim state is re-read by other lanes: drain the stores first.
     if (keys(sflags) || !INL || hpA()) hbm_release();
     wsync();
-    if (TOPO && (t_sel | t_inv)) {  // Topology.Record on the claim's final requirements (nodeclaim.go:121)
-      if (keys(sflags) || t_mask) log_hgroups(nlog - 1, topo_record(s_rs, c, -1, d.allowWK));
-      else log_hgroups(nlog - 1, topo_record(W.c_rs + (int64_t)c * d.RSW, c, -1, d.allowWK));
+    if (TOPO && t_rec) {  // Topology.Record on the claim's final requirements (nodeclaim.go:121)
+      if (keys(sflags) || t_any) topo_record(s_rs, c, -1, d.allowWK, nlog - 1);
+      else topo_record(W.c_rs + (int64_t)c * d.RSW, c, -1, d.allowWK, nlog - 1);
     }
     algbytes += 24 * R() + 4 * d.TW + 8;
     return srt;
@@ -1642,7 +1639,7 @@ struct Solver {
             ok = rs_compatible(L, s_rs, s_pin, d.allowWK);
             if (ok) rs_add_wave(L, s_rs, s_pin, 0);
           }
-          if (TOPO && ok && t_mask) {  // topology requirements of the fresh NodeClaim (nodeclaim.go:92-100)
+          if (TOPO && ok && t_any) {  // topology requirements of the fresh NodeClaim (nodeclaim.go:92-100)
             const uint32_t tc = topo_apply(s_rs, nclaims, d.allowWK);
             if (tc) {
               ok = false;
@@ -1652,7 +1649,7 @@ struct Solver {
               } else if (tc == FC_TOPO_COMPAT) {
                 copy_words(W.fail_rs + slot, s_rs, d.RSW);  // the topology requirements, for the message
               } else {
-                const int g = (int)(tc >> 16) & 0xff, nv = tg(g, TGM_NV);
+                const int g = (int)(tc >> 16) & 0xffff, nv = tg(g, TGM_NV);
                 if (!tg(g, TGM_HOST))  // the counts (-1: unregistered), for the message (FSW fits them)
                   for (int v = lane(); v < nv; v += kWave) W.fail_rs[slot + v] = (uint32_t)tcnt(g, v);
                 else if (lane() == 0)  // hostname: the commits so far; the host replays their log_hg entries
@@ -1697,7 +1694,7 @@ struct Solver {
             wsync();
             if (any == 0) {
               code = FC_NO_IT | (flags << 8);
-              if (!SIM && TOPO && t_mask) {  // the message prints the requirements the topology narrowed
+              if (!SIM && TOPO && t_any) {  // the message prints the requirements the topology narrowed
                 copy_words(W.fail_rs + ((int64_t)p * d.NTPL + t) * d.FSW, s_rs, d.RSW);
                 code |= FC_RS_SNAP;
               }
@@ -1746,7 +1743,7 @@ struct Solver {
               log_commit(p, c, nlog);
               hbm_release();  // c_rs / c_tpl / overflow state are read by other lanes later
               wsync();
-              if (TOPO && (t_sel | t_inv)) log_hgroups(nlog - 1, topo_record(s_rs, c, -1, d.allowWK));
+              if (TOPO && t_rec) topo_record(s_rs, c, -1, d.allowWK, nlog - 1);
               if (inl) recompute_max<true>(c, s_rem, t, c);
               else recompute_max<false>(c, s_rem, t, c);
               if (pool >= 0) {  // subtractMax (scheduler.go:347-362)
@@ -2312,7 +2309,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const KsWork KS_C& W = ((const KsWork KS_C*)works)[blockIdx.x];
   const KsDims& d = D.d;
   Solver<RT, TL, SIM, TOPO, LEAN> S(D, W, pl);
-  if (TOPO) S.t_active = ~d.tgLate;
   const int R = S.R();
   char KS_L* sp = smem;
   auto take = [&](size_t bytes) { char KS_L* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
@@ -2352,6 +2348,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int NWC = SIM && d.G ? (d.tgCntWords - d.tgSmall + 31) >> 5 : 0;
   S.s_tcd = (LU32)take(4 * (size_t)NWC);
   S.s_bnode = (LI32)take(SIM && LEAN ? 4 * (size_t)kWave : 0);
+  S.s_gw = (LU64)take(TOPO && d.G && d.GMW > 1 ? 8 * (size_t)GS_N * d.GMW : 0);
+  if constexpr (TOPO) {  // groups in t.topologies at the start: all but the late ones (topology.go:102-119)
+    S.t_active = ~D.tg_late[0];
+    for (int w = 1 + lane(); w < d.GMW; w += kWave) S.s_gw[GS_ACT * d.GMW + w] = ~D.tg_late[w];
+  }
   for (int i = lane(); i < (d.G ? pl.tcl : 0); i += kWave) S.s_tcs[i] = D.tg_cnt0[i];
   for (int i = lane(); i < NWC; i += kWave) S.s_tcd[i] = 0;
   for (int i = lane(); i < d.G * TGM_WORDS; i += kWave) S.s_tgm[i] = D.tg_meta[i];
@@ -2701,33 +2702,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         int kj = -1;
         uint64_t mj = 0;
         asm volatile("; KS_MARK window_begin");
-        if (KS_TOPO_WINDOW_BATCH && TOPO && S.t_mask) {  // every node is labelled here: all window nodes' topology loads at once
-          bool okw[NWA], slw[NWA];
-          int cw[NWA];
-#pragma unroll
-          for (int k = 0; k < NW; k++) {
-            const int n = k * kWave + lane();
-            cw[k] = n < d.N ? n : d.N - 1;
-            bool ok = (((wtx[k] & ~tol0) | (wty[k] & ~tol1)) == 0) & (n < d.N);
-            if (SIM) ok &= !S.tbit(S.s_rmv, cw[k]);
-#pragma unroll
-            for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
-            ok &= (whp[k] & S.cur_hpc) == 0;
-            if (S.volA() && S.cur_vm && ok) ok = S.vol_ok(cw[k]);
-            if (S.keys(sflags) && ok) ok = S.node_compat(cw[k]);
-            okw[k] = ok;
-          }
-          S.template topo_node_stateK<NWA>(cw, okw, slw);
-#pragma unroll
-          for (int k = 0; k < NW; k++) {
-            const uint64_t m = wballot(okw[k]);
-            if (m) {
-              kj = k;
-              mj = m;
-              break;
-            }
-          }
-        } else {
 #pragma unroll
         for (int k = 0; k < NW; k++) {
           const int n = k * kWave + lane();
@@ -2744,7 +2718,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           ok &= (whp[k] & S.cur_hpc) == 0;
           if (S.volA() && S.cur_vm && ok) ok = S.vol_ok(n);
           if (S.keys(sflags) && ok) ok = S.node_compat(n);
-          if (TOPO && !KS_TOPO_WINDOW_BATCH && S.t_mask && ok) {  // every node is labelled here
+          if (TOPO && S.t_any && ok) {  // every node is labelled here
             int cn = n < d.N ? n : d.N - 1;
             bool sl;
             S.template topo_node_stateK<1>(&cn, &ok, &sl);
@@ -2755,7 +2729,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             mj = m;
             break;
           }
-        }
         }
         asm volatile("; KS_MARK window_end");
         if (U(kj >= 0)) {
@@ -2783,7 +2756,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, S.s_pin);
             S.node_rs_changed(j);
           }
-          if (TOPO && (S.t_sel | S.t_inv)) S.log_hgroups(nlog, S.topo_record(S.node_rs(j), -1, j, 0));  // existingnode.go:121
+          if (TOPO && S.t_rec) S.topo_record(S.node_rs(j), -1, j, 0, nlog);  // existingnode.go:121
           S.log_commit(p, -(j + 1), nlog);
           PH_END(t7, 7);
           S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
@@ -2849,9 +2822,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         }
         if (TOPO && slowj) {
           S.node_store_rs(j, nrs);
-          if (S.t_sel | S.t_inv) S.log_hgroups(nlog, S.topo_record(S.s_rs, -1, -1, 0));  // existingnode.go:121
-        } else if (TOPO && (S.t_sel | S.t_inv)) {
-          S.log_hgroups(nlog, S.topo_record(S.node_rs(j), -1, j, 0));  // existingnode.go:121
+          if (S.t_rec) S.topo_record(S.s_rs, -1, -1, 0, nlog);  // existingnode.go:121
+        } else if (TOPO && S.t_rec) {
+          S.topo_record(S.node_rs(j), -1, j, 0, nlog);  // existingnode.go:121
         }
         S.log_commit(p, -(j + 1), nlog);
         PH_END(t7, 7);
@@ -2979,13 +2952,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       if (relaxed) W.pod_state[p] = s + 1;
     }
     if (relaxed) epoch++;
-    if (TOPO && relaxed && d.tgLate) {  // Topology.Update (scheduler.go:160-170): groups the new state creates
-      const uint64_t fresh = D.st_gown[s + 1] & ~S.t_active;
-      if (fresh) {
-        S.topo_activate(fresh, nclaims, hostCtr);
-        S.t_active |= fresh;
-      }
-    }
+    if (TOPO && relaxed) S.topo_activate_state(s + 1, nclaims, hostCtr);  // Topology.Update (scheduler.go:160-170)
     int tail = qhead + qlen;
     if (tail >= P) tail -= P;
     if (lane() == 0) W.queue[tail] = p;
@@ -3081,6 +3048,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
                        2 * r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 +
                        (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : d.fnOn ? r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
                        (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) +
+                                  (d.GMW > 1 ? r16(8 * (size_t)GS_N * d.GMW) : 0) +
                                   (sim ? r16(4 * (size_t)((d.tgCntWords - d.tgSmall + 31) / 32)) : 0)
                               : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)

@@ -86,8 +86,10 @@ void Host::buildTopology() {
   for (auto& cp : clusterPods) any = any || !cp.antiRequired.empty();
   if (emptyTopology) any = false;  // AddRequirements / Record see no groups; pod affinity terms are inert
   const int P = (int)pods.size(), N = (int)nodes.size(), S = dims.S;
+  dims.GMW = 1;
   tab.pod_gsel.assign(std::max(P, 1), 0);
   tab.pod_ginv.assign(std::max(P, 1), 0);
+  tab.tg_late.assign(1, 0);
   if (!any) {
     dims.G = dims.G1 = 0;
     dims.tgCntWords = 1;
@@ -250,7 +252,7 @@ void Host::buildTopology() {
   };
   auto inverseAnti = [&](const PodH& p, std::vector<TopoGroup> gs, const std::map<std::string, std::string>* labels,
                          bool cluster) {
-    uint64_t owned = 0;  // updateInverseAntiAffinity (topology.go:207-232)
+    std::vector<int32_t> owned;  // updateInverseAntiAffinity (topology.go:207-232): inverse group indices
     for (TopoGroup& g : gs) {
       auto it = invByHash.find(g.hash);
       int idx;
@@ -269,9 +271,8 @@ void Host::buildTopology() {
           if (topoExcluded) contrib[p.uid].push_back({-1 - idx, d->second});
         }
       }
-      if (idx >= 64) throw KsError(-3, "more than 64 topology groups");
-      if (cluster && topoExcluded) topoInvOwner[p.uid] |= 1ull << idx;
-      owned |= 1ull << idx;
+      if (cluster && topoExcluded) topoInvOwner[p.uid].push_back(idx);
+      owned.push_back(idx);
     }
     return owned;
   };
@@ -311,12 +312,12 @@ void Host::buildTopology() {
     podOwn[(size_t)p] = ownedSpecGroups(*sp);
   });
   pt.mark("pods' groups (workers)");
-  std::vector<uint64_t> invOwned(P, 0);
+  std::vector<std::vector<int32_t>> invOwned(P);
   for (int p = 0; p < P; p++) {  // NewTopology: Update(pod) for every pod, in order
     const std::shared_ptr<PodH>& sp = states[(size_t)p][0].spec;
     if (!sp) continue;
     if (podHasAnti[(size_t)p]) invOwned[(size_t)p] = inverseAnti(*sp, std::move(podAnti[(size_t)p]), nullptr, false);
-    uint64_t gown = 0;
+    std::vector<int32_t> gown;
     for (auto& g : podOwn[(size_t)p]) {
       auto it = ownByHash.find(g.hash);
       int idx;
@@ -329,52 +330,62 @@ void Host::buildTopology() {
       } else {
         idx = it->second;
       }
-      if (idx >= 64) throw KsError(-3, "more than 64 topology groups");
-      gown |= 1ull << idx;
+      gown.push_back(idx);
     }
-    states[(size_t)p][0].gown = gown;
+    std::sort(gown.begin(), gown.end());
+    gown.erase(std::unique(gown.begin(), gown.end()), gown.end());
+    states[(size_t)p][0].gown = std::move(gown);
   }
   pt.mark("pods' groups + countDomains");
-  uint64_t late = 0;
+  std::vector<int32_t> late;
   for (int p = 0; p < P; p++)
     for (size_t k = 1; k < states[(size_t)p].size(); k++) {
       PodState& st = states[(size_t)p][k];
       if (!st.spec) continue;
-      uint64_t gown = 0;
+      std::vector<int32_t> gown;
       for (auto& g : ownedSpecGroups(*st.spec)) {
         auto it = ownByHash.find(g.hash);
         int idx;
         if (it == ownByHash.end()) {  // created by this relaxation's Update (topology.go:102-119)
           idx = (int)own.size();
-          if (idx >= 64) throw KsError(-3, "more than 64 topology groups");
           seedDomains(g);
           countDomains(g, idx);
           g.late = true;
           ownByHash[g.hash] = idx;
           own.push_back(g);
-          late |= 1ull << idx;
+          late.push_back(idx);
         } else {
           idx = it->second;
         }
-        gown |= 1ull << idx;
+        gown.push_back(idx);
       }
-      st.gown = gown;
+      std::sort(gown.begin(), gown.end());
+      gown.erase(std::unique(gown.begin(), gown.end()), gown.end());
+      st.gown = std::move(gown);
     }
   pt.mark("relaxation states' groups");
-  if (own.size() + inv.size() > 64) throw KsError(-3, "more than 64 topology groups");
+  // Group sets are GMW-word bitsets on the device (no 64-group limit); the group index rides in bits 16..31
+  // of a topology failure code (FC_TOPO), and the group table must fit the LDS plan (make_plan refuses it
+  // with KS_ERR_CAPACITY long before this bound).
+  if (own.size() + inv.size() > 65535) throw KsError(-3, "more than 65535 topology groups");
   const int G1 = (int)own.size(), G = G1 + (int)inv.size();
-  dims.tgLate = late;
+  const int GMW = std::max(1, (G + 63) / 64);
+  dims.GMW = GMW;
+  tab.tg_late.assign((size_t)GMW, 0);
+  for (int g : late) gset(tab.tg_late, 0, GMW, g);
   groups = own;
   groups.insert(groups.end(), inv.begin(), inv.end());
   groupsOwned = G1;
   for (auto& g : groups)  // NewExistingNode registers every node's hostname (existingnode.go:60)
     if (g.key == kHostnameKey && !g.late)  // in the groups that exist by then
       for (auto& n : nodes) g.domains.emplace(n.hostName, 0);
-  parallel_for(P, 256, [&](int p) {  // per pod, independent
-    tab.pod_ginv[(size_t)p] = invOwned[(size_t)p] << G1;
+  tab.pod_gsel.assign((size_t)std::max(P, 1) * GMW, 0);
+  tab.pod_ginv.assign((size_t)std::max(P, 1) * GMW, 0);
+  parallel_for(P, 256, [&](int p) {  // per pod, independent (each writes its own row)
+    for (int i : invOwned[(size_t)p]) gset(tab.pod_ginv, (size_t)p, GMW, G1 + i);
     for (int g = 0; g < G; g++)
       if (groups[(size_t)g].namespaces.count(pods[(size_t)p].ns) && sel_selects(groups[(size_t)g].sel, pods[(size_t)p].labels))
-        tab.pod_gsel[(size_t)p] |= 1ull << g;
+        gset(tab.pod_gsel, (size_t)p, GMW, g);
   });
 
   pt.mark("hostnames + pod selectors");
@@ -461,10 +472,14 @@ void Host::buildTopology() {
         const int g = gd.first >= 0 ? gd.first : G1 + (-1 - gd.first);
         topoContrib[kv.first].push_back({g, valueId[(size_t)groups[(size_t)g].keyId].at(gd.second)});
       }
-    for (auto& kv : topoInvOwner) kv.second <<= G1;
+    for (auto& kv : topoInvOwner) {  // (a pod owning one group twice owns it once)
+      std::sort(kv.second.begin(), kv.second.end());
+      kv.second.erase(std::unique(kv.second.begin(), kv.second.end()), kv.second.end());
+      for (int32_t& i : kv.second) i += G1;
+    }
     topoInvOwners.assign((size_t)G, 0);
     for (auto& kv : topoInvOwner)
-      for (uint64_t m = kv.second; m; m &= m - 1) topoInvOwners[(size_t)__builtin_ctzll(m)]++;
+      for (int32_t g : kv.second) topoInvOwners[(size_t)g]++;
     topoHostActive.clear();
     if (keyId.count(kHostnameKey))
       for (auto& n : nodes) {

@@ -483,3 +483,67 @@ def unlabel_topology_nodes(snap, seed, frac=0.3):
         for term in req["nodeSelectorTerms"]:
             term.setdefault("matchExpressions", []).append(dict(expr))
     return snap
+
+
+def many_groups_problem(seed, n_apps=150, n_pods=600, n_nodes=30, n_its=40):
+    """A Solve whose topology has far more than 64 groups (one spread or anti-affinity group
+    per deployment is what production clusters carry): n_apps apps, each with its own zonal or hostname
+    spread (DoNotSchedule or ScheduleAnyway, maxSkew 1-3, some minDomains), some with required or preferred
+    hostname / zonal anti-affinity or pod affinity to another app; bound cluster pods of every app on the
+    existing nodes seed the counts, and some of them carry required anti-affinity (inverse groups)."""
+    rng = np.random.default_rng(seed)
+    snap = random_problem(seed, n_pods=n_pods, n_its=n_its, n_nodes=n_nodes)
+    apps = {}
+    for a in range(n_apps):
+        app = "m%d" % a
+        spec = {}
+        if rng.random() < 0.8:
+            key = _pick(rng, [synth.ZONE, synth.HOSTNAME, synth.ZONE, synth.CT])
+            c = {"topologyKey": key, "maxSkew": int(rng.integers(1, 4)), "labelSelector": {"matchLabels": {"app": app}},
+                 "whenUnsatisfiable": "ScheduleAnyway" if rng.random() < 0.2 else "DoNotSchedule"}
+            if c["whenUnsatisfiable"] == "DoNotSchedule" and key != synth.HOSTNAME and rng.random() < 0.15:
+                c["minDomains"] = int(rng.integers(2, 4))
+            spec["tsc"] = [c]
+        if rng.random() < 0.3:
+            spec["anti"] = [{"labelSelector": {"matchLabels": {"app": app}},
+                             "topologyKey": _pick(rng, [synth.HOSTNAME, synth.ZONE])}]
+        elif rng.random() < 0.2:
+            spec["antiPref"] = [{"weight": int(rng.integers(1, 100)), "podAffinityTerm": {
+                "labelSelector": {"matchLabels": {"app": app}}, "topologyKey": synth.HOSTNAME}}]
+        if rng.random() < 0.1:
+            spec["aff"] = [{"labelSelector": {"matchLabels": {"app": "m%d" % int(rng.integers(n_apps))}},
+                            "topologyKey": synth.ZONE}]
+        apps[app] = spec
+    for i, p in enumerate(snap["pods"]):
+        app = "m%d" % (i % n_apps)
+        p["metadata"]["labels"]["app"] = app
+        sp = p["spec"]
+        sp.pop("nodeSelector", None)
+        sp.pop("affinity", None)
+        spec = apps[app]
+        if "tsc" in spec:
+            sp["topologySpreadConstraints"] = spec["tsc"]
+        aff = {}
+        if "anti" in spec:
+            aff["podAntiAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": spec["anti"]}
+        if "antiPref" in spec:
+            aff["podAntiAffinity"] = {"preferredDuringSchedulingIgnoredDuringExecution": spec["antiPref"]}
+        if "aff" in spec:
+            aff["podAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": spec["aff"]}
+        if aff:
+            sp["affinity"] = aff
+    cluster = []
+    for j, n in enumerate(snap["stateNodes"]):
+        for k in range(int(rng.integers(0, 5))):
+            app = "m%d" % int(rng.integers(n_apps))
+            cp = synth.pod(200000 + 10 * j + k, cpu="100m", mem="64Mi", labels={"app": app})
+            cp["metadata"]["name"] = "bound-%d-%d" % (j, k)
+            cp["spec"]["nodeName"] = n["name"]
+            cp["status"] = {"phase": "Running"}
+            if rng.random() < 0.15:
+                cp["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                    {"labelSelector": {"matchLabels": {"app": "m%d" % int(rng.integers(n_apps))}},
+                     "topologyKey": _pick(rng, [synth.HOSTNAME, synth.ZONE])}]}}
+            cluster.append(cp)
+    snap["clusterPods"] = cluster
+    return snap
