@@ -192,6 +192,13 @@ void ks_upload(ks_problem* pb) {
   size_t o_ti = put(t.tpl_its.data(), t.tpl_its.size() * 4);
   size_t o_tp = put(t.tpl_pool.data(), t.tpl_pool.size() * 4);
   size_t o_tsa = put(t.tsort_alloc.data(), t.tsort_alloc.size() * 8);
+  // Allocatable per template position ([totalTplIts][R], position-major): what k_solve stages into LDS (TL)
+  // with one contiguous copy instead of a gather through tpl_its (every simulation's prologue does it)
+  std::vector<int64_t> tplAlloc((size_t)std::max(h.dims.totalTplIts, 1) * h.dims.R, 0);
+  for (int i = 0; i < h.dims.totalTplIts; i++)
+    for (int r = 0; r < h.dims.R; r++)
+      tplAlloc[(size_t)i * h.dims.R + r] = t.it_alloc[(size_t)t.tpl_its[(size_t)i] * h.dims.R + r];
+  size_t o_tpa = put(tplAlloc.data(), tplAlloc.size() * 8);
   size_t o_tsp = put(t.tsort_pos.data(), t.tsort_pos.size() * 4);
   size_t o_pr = put(t.pool_rem0.data(), t.pool_rem0.size() * 8);
   size_t o_pm = put(t.pool_mask.data(), t.pool_mask.size() * 4);
@@ -339,6 +346,7 @@ void ks_upload(ks_problem* pb) {
   D.tpl_its = (const int32_t*)(b + o_ti);
   D.tpl_pool = (const int32_t*)(b + o_tp);
   D.tsort_alloc = (const int64_t*)(b + o_tsa);
+  D.tpl_alloc = (const int64_t*)(b + o_tpa);
   D.tsort_pos = (const int32_t*)(b + o_tsp);
   D.pool_rem0 = (const int64_t*)(b + o_pr);
   D.pool_mask = (const uint32_t*)(b + o_pm);

@@ -214,6 +214,8 @@ struct ks_cons {
     int32_t* lentries = nullptr;
     int32_t* lentrySim = nullptr;
     int32_t* lpodmap = nullptr;
+    int32_t* lrunlen = nullptr;   // identical pods left in the run at each sorted entry (sim_run_lengths)
+    uint64_t* lrunw = nullptr;    // run-start bits, 64 entries per word
     uint64_t* lkeys = nullptr;
     int32_t* lvals = nullptr;
     void* ltemp = nullptr;
@@ -224,7 +226,7 @@ struct ks_cons {
     std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
     void release() {
       for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
-                      (void*)lkeys, (void*)lvals, ltemp})
+                      (void*)lrunlen, (void*)lrunw, (void*)lkeys, (void*)lvals, ltemp})
         if (p) (void)hipFree(p);
       if (hrec) (void)hipHostFree(hrec);
       *this = Launch{};  // stale lookups (claim requirements, counters) now fail cleanly
@@ -629,6 +631,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   HIPCHK(hipMalloc(&c.L.lentries, 4 * (size_t)std::max(c.L.lnent, 1)));
   HIPCHK(hipMalloc(&c.L.lentrySim, 4 * (size_t)std::max(c.L.lnent, 1)));
   HIPCHK(hipMalloc(&c.L.lpodmap, 4 * (size_t)std::max(c.L.lnent, 1)));
+  HIPCHK(hipMalloc(&c.L.lrunlen, 4 * (size_t)std::max(c.L.lnent, 1)));
+  HIPCHK(hipMalloc(&c.L.lrunw, 8 * (size_t)std::max((c.L.lnent + 63) / 64, 1)));
   HIPCHK(hipMalloc(&c.L.lkeys, 16 * (size_t)std::max(c.L.lnent, 1)));
   HIPCHK(hipMalloc(&c.L.lvals, 8 * (size_t)std::max(c.L.lnent, 1)));
   c.L.ltempBytes = std::max<size_t>(queue_sort_temp_bytes(std::max(c.L.lnent, 1)), 256);
@@ -728,6 +732,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     w.n_hp = (uint64_t*)(base + o.n_hp);
     w.c_hp = (uint64_t*)(base + o.c_hp);
     w.pod_map = c.L.lpodmap + entBeg[k];
+    w.run_len = c.L.lrunlen + entBeg[k];
     w.P = simP[k];
     w.nrm = (int32_t)rm.size();
     w.rm = (const int32_t*)(ibase + o.rm);
@@ -758,11 +763,13 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   if (ai.total) HIPCHK(hipMemcpy(ibase, stage.data(), ai.total, hipMemcpyHostToDevice));
   if (ns) HIPCHK(hipMemcpy(c.L.lworks, works.data(), sizeof(KsWork) * ns, hipMemcpyHostToDevice));
   c.L.lhost = works;
-  // LDS plan: a small budget per simulation so several simulations share a CU
+  // LDS plan: a small budget per simulation so several simulations share a CU.  A pass with topology is bound by
+  // its longest simulation (a multi-node prefix), not by throughput: its simulations get room for the
+  // instance-type tables in LDS (TL) at the price of fewer resident per CU.
   KsDims dd = d;
   dd.Kcap = std::max(1, std::min(maxP, 16384));
-  c.L.lplan = make_plan(dd, 40 * 1024, true);
-  if (c.L.lplan.lds > 64 * 1024 || c.L.lplan.KO < 1) c.L.lplan = make_plan(dd, 160 * 1024 - 256, true);
+  c.L.lplan = make_plan(dd, d.G ? 64 * 1024 : 40 * 1024, true);
+  if (c.L.lplan.lds > 80 * 1024 || c.L.lplan.KO < 1) c.L.lplan = make_plan(dd, 160 * 1024 - 256, true);
   if (c.L.lplan.lds > 160 * 1024 || c.L.lplan.KO < 1) throw KsError(KS_ERR_CAPACITY, "simulation state does not fit in LDS");
   c.L.lrank = rank;
   c.L.lworld = world;
@@ -1000,6 +1007,8 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
   if (!c.L.lsorted) {
     HIPCHK(sim_queue_sort(c.rank, c.L.lentries, c.L.lentrySim, c.L.lnent, c.L.lrbits, c.L.lsbits, c.L.lkeys, c.L.lvals,
                           c.L.ltemp, c.L.ltempBytes, c.L.lpodmap, pb.stream));
+    HIPCHK(sim_run_lengths(c.L.lpodmap, c.L.lentrySim, pb.dev.pod_req, pb.dev.pod_s0, pb.dev.pod_flags, pb.host.dims.R,
+                           c.L.lnent, c.L.lrunw, c.L.lrunlen, pb.stream));
     c.L.lsorted = true;
   }
   HIPCHK(launch_sims(pb.dev, c.L.lworks, ns, c.L.lplan, pb.stream));

@@ -115,6 +115,7 @@ struct KsDev {
   const int32_t KS_G* tpl_pool;    // [NTPL] limit pool or -1
   const int64_t KS_G* tsort_alloc; // [totalTplIts][R] per template, per resource: Allocatable ascending
   const int32_t KS_G* tsort_pos;   //   ... and the template position it belongs to (tb*R + r*nIT + i)
+  const int64_t KS_G* tpl_alloc;   // [totalTplIts][R] Allocatable per template position (it_alloc of tpl_its)
   // NodePool limits (remainingResources, scheduler.go:76-78,306-308)
   const int64_t KS_G* pool_rem0;   // [NPOOL][R]
   const uint32_t KS_G* pool_mask;  // [NPOOL] resource names present in the remaining ResourceList
@@ -247,6 +248,8 @@ struct KsWork {
   // consolidation simulations only (k_solve<.., SIM=true>): this simulation's view of the shared
   // cluster problem (helpers.go:73-127 — candidates removed, their pods added to the pending ones)
   const int32_t KS_G* pod_map;  // [P] local -> global pod, in NewQueue order (k_sim_keys + sort)
+  const int32_t KS_G* run_len;  // [P] identical pods (requests, tolerations, provisionable) from each queue position
+                                // to the end of their run in this simulation's NewQueue order (k_sim_runs)
   int32_t P;                    // pods in this simulation
   int32_t nrm;                  // removed (candidate) nodes
   const int32_t KS_G* rm;       // [nrm] their indices in calculateExistingNodeClaims order

@@ -103,4 +103,46 @@ hipError_t sim_queue_sort(const int32_t* rank, const int32_t* entries, const int
   return hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys + n, vals, out, n, 0, rbits + sbits, st);
 }
 
+// Runs of identical pods in every simulation's NewQueue order (the LEAN simulation fast path places a run in one
+// step while no pod has been pushed back, ks_solve.hip): entry i of the sorted CSR starts a run when it is its
+// simulation's first entry or its pod differs from the previous entry's in requests, tolerations (the pod's first
+// relaxation state) or the provisionable flag.  One bit per entry, 64 per word (one ballot per wave).
+__global__ __launch_bounds__(256) void k_sim_run_breaks(const int32_t* podmap, const int32_t* entry_sim,
+                                                        const int64_t* pod_req, const uint64_t* pod_s0,
+                                                        const int32_t* pod_flags, int R, int n, uint64_t* words) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool brk = true;
+  if (i < n && i > 0 && entry_sim[i] == entry_sim[i - 1]) {
+    const int p = podmap[i], q = podmap[i - 1];
+    bool same = pod_s0[3 * (int64_t)p] == pod_s0[3 * (int64_t)q] && pod_s0[3 * (int64_t)p + 1] == pod_s0[3 * (int64_t)q + 1] &&
+                ((pod_flags[p] ^ pod_flags[q]) & PF_PROVISIONABLE) == 0;
+    for (int r = 0; r < R; r++) same = same && pod_req[(int64_t)p * R + r] == pod_req[(int64_t)q * R + r];
+    brk = !same;
+  }
+  const uint64_t b = __ballot(brk ? 1 : 0);
+  if ((threadIdx.x & 63) == 0 && i < n) words[i >> 6] = b;
+}
+
+// Per entry: the entries from it to the next run start (or the end), i.e. the identical pods left in its run.
+__global__ __launch_bounds__(256) void k_sim_run_len(const uint64_t* words, int n, int32_t* run_len) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int nw = (n + 63) >> 6;
+  int w = (i + 1) >> 6;
+  uint64_t m = w < nw ? words[w] & (~0ull << ((i + 1) & 63)) : 0ull;
+  while (m == 0 && ++w < nw) m = words[w];
+  const int next = m ? (w << 6) + __builtin_ctzll(m) : n;
+  run_len[i] = (next < n ? next : n) - i;
+}
+
+hipError_t sim_run_lengths(const int32_t* podmap, const int32_t* entry_sim, const int64_t* pod_req, const uint64_t* pod_s0,
+                           const int32_t* pod_flags, int R, int n, uint64_t* words, int32_t* run_len, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const int blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(k_sim_run_breaks, dim3(blocks), dim3(256), 0, st, podmap, entry_sim, pod_req, pod_s0, pod_flags, R,
+                     n, words);
+  hipLaunchKernelGGL(k_sim_run_len, dim3(blocks), dim3(256), 0, st, words, n, run_len);
+  return hipGetLastError();
+}
+
 }  // namespace ks

@@ -132,6 +132,21 @@ __device__ __forceinline__ int run_cap(int64_t free, int64_t req, float rq, int 
   return qi < m ? qi : m;
 }
 
+// Contiguous HBM -> LDS copy by the wave with U loads in flight per lane before their stores (a prologue's
+// table staging is otherwise a chain of dependent round trips, one per 64 elements).
+template <int U, class T>
+__device__ __forceinline__ void lds_copy(T KS_L* dst, const T KS_G* src, int n) {
+  int i = lane();
+  for (; i + (U - 1) * kWave < n; i += U * kWave) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = src[i + u * kWave];
+#pragma unroll
+    for (int u = 0; u < U; u++) dst[i + u * kWave] = v[u];
+  }
+  for (; i < n; i += kWave) dst[i] = src[i];
+}
+
 #ifdef KS_PHASE_STATS
 #define PH_BEGIN(v) uint64_t v = __builtin_amdgcn_s_memtime()
 #define PH_END(v, slot) cyc[slot] += __builtin_amdgcn_s_memtime() - v
@@ -192,6 +207,7 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 template <int RT>
 struct Window {
   int p, g, uid, s, flags, toltpl, pf, st;
+  int rl;  // SIM, nothing pushed back yet: identical pods from this queue position to the end of their run
   uint64_t ll, tol0, tol1, hpc, hpu, hpo, vm;
   int64_t req[RT > 0 ? RT : kMaxR];
 };
@@ -207,51 +223,64 @@ struct Window {
 // ks_reqset.h with each key's words spread over the lanes (headers are wave-uniform; one wave,
 // so every lane's reads of a key precede lane 0's header stores).  Returns whether a key of
 // `mask` changed (what rs_equal_keys against the old record would report).
-// A free function kept out of line (no Solver `this` escapes): inlined into claim_full, the compiled Solve diverged from the oracle on the
-// reference scenarios (device requests vs the replayed Merge) although the flag it returned and the
-// record it built matched rs_add + rs_equal_keys lane for lane; the call costs a few instructions.
-__device__ __attribute__((noinline)) bool rs_add_wave(const DevLayout L, LU32 out, LU32 in, uint64_t mask) {
+// Every branch is wave-uniform (the key loop, the per-key case, the 64-word blocks); the per-lane work is
+// branch-free -- a lane past the key's last word computes on a clamped index and stores nothing, `diff` is
+// accumulated by select -- and every header and bound store is a wave-wide store of a uniform value (DESIGN §3:
+// the AMDGPU backend of this toolchain miscompiled divergent per-lane updates in loops; round 2's out-of-line
+// form of this function worked around that without removing the pattern).
+__device__ __forceinline__ bool rs_add_wave(const DevLayout& L, LU32 out, LU32 in, uint64_t mask) {
   const uint64_t pi = rs_present(in), po = rs_present(out);
   uint64_t cm = rs_compl(out), hg = rs_hasgt(out), hl = rs_haslt(out);
   const uint64_t icm = rs_compl(in), ihg = rs_hasgt(in), ihl = rs_haslt(in);
-  bool diff = false;
+  uint32_t diff = 0;
   for (uint64_t m = pi; m; m &= m - 1) {
     const int k = ctz64(m);
     const uint64_t one = 1ull << k;
     const KeyMeta km = L.keys[k];
     const bool watched = (mask & one) != 0;
+    const int base = L.HDR + km.off;
     if (po & one) {
       const KeyIx x = key_ix_header(L, out, in, k);
-      for (int i = lane(); i < km.nw; i += kWave) {
-        const uint32_t old = out[L.HDR + km.off + i];
-        const uint32_t nw = key_ix_word(L, out, in, k, i, x);
-        out[L.HDR + km.off + i] = nw;
-        diff |= watched && nw != old;
+      for (int i0 = 0; i0 < km.nw; i0 += kWave) {
+        const int i = i0 + lane();
+        const bool live = i < km.nw;
+        const int ic = live ? i : i0;
+        const uint32_t old = out[base + ic];
+        const uint32_t nw = key_ix_word(L, out, in, k, ic, x);
+        if (live) out[base + i] = nw;
+        diff |= (live && watched && nw != old) ? 1u : 0u;
       }
       const bool keep = !x.dne && x.compl_;
       const uint64_t ncm = keep ? (cm | one) : (cm & ~one);
       const uint64_t nhg = (keep && x.hg) ? (hg | one) : (hg & ~one);
       const uint64_t nhl = (keep && x.hl) ? (hl | one) : (hl & ~one);
-      diff |= watched && (((ncm ^ cm) | (nhg ^ hg) | (nhl ^ hl)) & one) != 0;
+      diff |= (watched && (((ncm ^ cm) | (nhg ^ hg) | (nhl ^ hl)) & one) != 0) ? 1u : 0u;
       cm = ncm;
       hg = nhg;
       hl = nhl;
       if (km.bslot >= 0) {
         const int64_t ngt = keep && x.hg ? x.gt : 0, nlt = keep && x.hl ? x.lt : 0;
-        diff |= watched && (ngt != rs_gt(out, km.bslot) || nlt != rs_lt(out, km.bslot));
+        diff |= (watched && (ngt != rs_gt(out, km.bslot) || nlt != rs_lt(out, km.bslot))) ? 1u : 0u;
         wsync();
         rs_set_gt(out, km.bslot, ngt);  // wave-wide store of uniform values (see commit_claim)
         rs_set_lt(out, km.bslot, nlt);
       }
     } else {  // rs_copy_key
-      for (int i = lane(); i < km.nw; i += kWave) out[L.HDR + km.off + i] = in[L.HDR + km.off + i];
-      diff |= watched;  // the key appears
+      for (int i0 = 0; i0 < km.nw; i0 += kWave) {
+        const int i = i0 + lane();
+        const bool live = i < km.nw;
+        const uint32_t v = in[base + (live ? i : i0)];
+        if (live) out[base + i] = v;
+      }
+      diff |= watched ? 1u : 0u;  // the key appears
       cm = (cm & ~one) | (icm & one);
       hg = (hg & ~one) | (ihg & one);
       hl = (hl & ~one) | (ihl & one);
-      if (km.bslot >= 0 && lane() == 0) {
-        rs_set_gt(out, km.bslot, rs_gt(in, km.bslot));
-        rs_set_lt(out, km.bslot, rs_lt(in, km.bslot));
+      if (km.bslot >= 0) {
+        const int64_t g = rs_gt(in, km.bslot), l = rs_lt(in, km.bslot);
+        wsync();
+        rs_set_gt(out, km.bslot, g);  // wave-wide store of uniform values
+        rs_set_lt(out, km.bslot, l);
       }
     }
   }
@@ -261,7 +290,7 @@ __device__ __attribute__((noinline)) bool rs_add_wave(const DevLayout L, LU32 ou
   wr64(out, 4, hg);
   wr64(out, 6, hl);
   wsync();
-  return wballot(diff) != 0;
+  return wballot(diff != 0) != 0;
 }
 
 // Requirements.Intersects(IT, X) (requirements.go:241-258) on the keys `keys` of X, for word wc of template
@@ -508,7 +537,6 @@ struct Solver {
   LI32 s_tcs;           // [pl.tcl] the count table's LDS-resident prefix: the small-key groups (a Solve: the
                         // whole table when it fits, make_plan)
   LU32 s_tcd;           // SIM: dirty bits over count words [tgSmall, tgCntWords): set once W.tg_cnt holds the word
-  LI32 s_bnode;         // LEAN SIM: [64] run placement: the node taking the run's pod at each offset (first of a node's pods)
   // Topology-group sets are GMW-word bitsets (ks_problem.h).  Word 0 lives in a register (it is the whole set
   // whenever a problem has <= 64 groups); words 1.. live in LDS, s_gw[set * GMW + w] (sets GS_*).
   LU64 s_gw;            // [GS_N][GMW] when GMW > 1
@@ -571,7 +599,12 @@ struct Solver {
   // buffered, then one coalesced store.  Per-pod global stores would make the next global load wait
   // for their write acknowledgements (vmcnt counts stores on gfx9).
   int lg_p = 0, lg_t = 0;
+  // (A simulation's placements are never read back -- the host reads its record -- so SIM only counts them.)
   __device__ __forceinline__ void log_commit(int p, int tgt, int& nlog) {
+    if constexpr (SIM) {
+      nlog++;
+      return;
+    }
     if (lane() == (nlog & (kWave - 1))) {
       lg_p = p;
       lg_t = tgt;
@@ -584,6 +617,10 @@ struct Solver {
   }
   // Commit-log entries for `n` (<= 64) placements at once: lane t holds entry nlog + t (pod, target).
   __device__ __forceinline__ void log_batch(int n, int pod_t, int tgt_t, int& nlog) {
+    if constexpr (SIM) {
+      nlog += n;
+      return;
+    }
     const int b0 = nlog & (kWave - 1);
     const int src = (lane() - b0) & (kWave - 1);  // the entry this lane buffers: nlog + src
     const int pv = __shfl(pod_t, src), tv = __shfl(tgt_t, src);
@@ -603,6 +640,7 @@ struct Solver {
     nlog += n;
   }
   __device__ __forceinline__ void log_flush(int nlog) {
+    if constexpr (SIM) return;
     const int k = nlog & (kWave - 1);
     if (lane() < k) {
       W.log_pod[nlog - k + lane()] = lg_p;
@@ -1513,7 +1551,7 @@ struct Solver {
     }
     v.cnt[c] = ncnt;
     s_okey[pos] = okNew;
-    if (hpA() && lane() == 0) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add
+    if (hpA()) W.c_hp[c] |= cur_hpu;  // hostPortUsage.Add (wave-wide store of a uniform value)
     if (keys(sflags) || (TOPO && t_any)) copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
     if (!rem_same) copy_words(v.rem + (int64_t)c * d.TW, s_rem, d.TW);
     log_commit(p, c, nlog);
@@ -1701,6 +1739,8 @@ struct Solver {
             } else {
               if (nclaims >= pl.KO) return -1;
               const int c = nclaims++;
+              if (SIM && TOPO)  // the next fresh claim's placeholder counts (a simulation zeroes one column per claim)
+                for (int g = lane(); g < d.G; g += kWave) W.tg_ccnt[(int64_t)g * W.ccs + nclaims] = 0;
               const bool inl = c < pl.KL;
               copy_words(W.c_rs + (int64_t)c * d.RSW, s_rs, d.RSW);
               if (inl) copy_words(lc.rem + (int64_t)c * d.TW, s_rem, d.TW);
@@ -1731,11 +1771,9 @@ struct Solver {
               } else {
                 gc.cnt[c] = cnt;
               }
-              if (lane() == 0) {
-                W.c_tpl[c] = t;
-                W.c_hp[c] = cur_hpu;
-                W.c_host[c] = hostid;
-              }
+              W.c_tpl[c] = t;  // wave-wide stores of uniform values (see commit_claim)
+              W.c_hp[c] = cur_hpu;
+              W.c_host[c] = hostid;
               s_order[c] = c;
               s_okey[c] = 1;
               s_ptpl[c] = t;
@@ -1760,7 +1798,7 @@ struct Solver {
                     const int64_t o = __shfl_xor(m, off);
                     m = o > m ? o : m;
                   }
-                  if (lane() == 0) s_pool[(int64_t)pool * R() + r] -= m;
+                  s_pool[(int64_t)pool * R() + r] -= m;  // wave-wide (m is reduced over the wave)
                 }
                 wsync();
               }
@@ -1769,10 +1807,8 @@ struct Solver {
           }
         }
       }
-      if (lane() == 0) {
-        W.fail_code[(int64_t)p * d.NTPL + t] = code;
-        W.fail_host[(int64_t)p * d.NTPL + t] = hostid;
-      }
+      W.fail_code[(int64_t)p * d.NTPL + t] = code;  // wave-wide stores of uniform values
+      W.fail_host[(int64_t)p * d.NTPL + t] = hostid;
     }
     return 0;
   }
@@ -2163,12 +2199,15 @@ struct Solver {
   }
   // simulateScheduling's post-check (helpers.go:115-124) + computeConsolidation (consolidation.go:
   // 113-194) + filterOutSameType (multinodeconsolidation.go:155-188), into the record W.rec
-  __device__ __forceinline__ void sim_record(int P, int nclaims, int hostCtr, bool allSched, int err) {
-    hbm_release();  // pod statuses written by lane 0
-    bool bad = false;
-    for (int i = lane(); i < P; i += kWave)
-      bad |= ld_sc1(W.pod_status + i) == ST_FAILED && !(D.pod_flags[W.pod_map[i]] & PF_PROVISIONABLE);
-    allSched = allSched && wballot(bad) == 0;
+  // anyPushed: some pod failed an attempt (its status array exists, sim_queue_init); otherwise every pod was placed.
+  __device__ __forceinline__ void sim_record(int P, int nclaims, int hostCtr, bool allSched, int err, bool anyPushed) {
+    if (anyPushed) {
+      hbm_release();  // pod statuses written by lane 0
+      bool bad = false;
+      for (int i = lane(); i < P; i += kWave)
+        bad |= ld_sc1(W.pod_status + i) == ST_FAILED && !(D.pod_flags[W.pod_map[i]] & PF_PROVISIONABLE);
+      allSched = allSched && wballot(bad) == 0;
+    }
     int32_t KS_G* rec = W.rec;
     const int TW = d.TW;
     int32_t KS_G* o_opt = rec + RF_HDR;
@@ -2185,7 +2224,7 @@ struct Solver {
       const uint32_t KS_G* crs = W.c_rs + (int64_t)c * d.RSW;
       wsync();
       for (int i = lane(); i < TW; i += kWave) o_opt[i] = inl ? lc.rem[(int64_t)c * TW + i] : gc.rem[(int64_t)c * TW + i];
-      if (lane() == 0) rec[RF_CLAIM] = c;
+      rec[RF_CLAIM] = c;  // wave-wide store of a uniform value
       {
         int cc = 0;
         for (int i = lane(); i < TW; i += kWave) cc += __popc(inl ? lc.rem[(int64_t)c * TW + i] : gc.rem[(int64_t)c * TW + i]);
@@ -2229,7 +2268,7 @@ struct Solver {
     } else if (allSched && nclaims == 0 && err == KE_OK) {
       action = CA_DELETE;
     }
-    if (lane() == 0) {
+    {  // wave-wide stores of uniform values
       rec[RF_FLAGS] = flags;
       rec[RF_NCLAIMS] = nclaims;
       rec[RF_HOSTINCR] = hostCtr;
@@ -2243,6 +2282,21 @@ struct Solver {
       rec[RF_ALGB_LO] = (int32_t)(uint32_t)(uint64_t)algbytes;
       rec[RF_ALGB_HI] = (int32_t)(uint32_t)((uint64_t)algbytes >> 32);
     }
+  }
+
+  // A simulation's queue state (what k_init does for a Solve), written at its first push-back: until then the
+  // queue is the NewQueue order itself and every pod is pending in its first relaxation state, which the window
+  // reads directly (refill's `ident`) -- most simulations never push a pod back and skip this.
+  __device__ __forceinline__ void sim_queue_init(int P) {
+    for (int i = lane(); i < P; i += kWave) {
+      W.queue[i] = i;
+      W.pod_state[i] = D.pod_state0[W.pod_map[i]];
+      W.pod_status[i] = ST_PENDING;
+      W.pod_fstate[i] = -1;
+      W.last_len[i] = 0;
+    }
+    hbm_release();
+    wsync();
   }
 
   // --- 64-pod queue window: one gather per 64 pops, one entry per lane ------------------------
@@ -2279,6 +2333,7 @@ struct Solver {
         w.tol1 = D.st_tol[2 * w.s + 1];
       }
       w.pf = SIM ? D.pod_flags[w.g] : 0;
+      w.rl = SIM && LEAN && ident ? W.run_len[pos] : 1;
       w.hpc = D.pod_hpc[w.g];
       w.hpu = D.pod_hpu[w.g];
       w.hpo = D.pod_hpo[w.g];
@@ -2347,15 +2402,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   S.s_tcs = (LI32)take(d.G ? 4 * (size_t)pl.tcl : 0);
   const int NWC = SIM && d.G ? (d.tgCntWords - d.tgSmall + 31) >> 5 : 0;
   S.s_tcd = (LU32)take(4 * (size_t)NWC);
-  S.s_bnode = (LI32)take(SIM && LEAN ? 4 * (size_t)kWave : 0);
   S.s_gw = (LU64)take(TOPO && d.G && d.GMW > 1 ? 8 * (size_t)GS_N * d.GMW : 0);
   if constexpr (TOPO) {  // groups in t.topologies at the start: all but the late ones (topology.go:102-119)
     S.t_active = ~D.tg_late[0];
     for (int w = 1 + lane(); w < d.GMW; w += kWave) S.s_gw[GS_ACT * d.GMW + w] = ~D.tg_late[w];
   }
-  for (int i = lane(); i < (d.G ? pl.tcl : 0); i += kWave) S.s_tcs[i] = D.tg_cnt0[i];
+  if (d.G) lds_copy<8>(S.s_tcs, D.tg_cnt0, pl.tcl);
   for (int i = lane(); i < NWC; i += kWave) S.s_tcd[i] = 0;
-  for (int i = lane(); i < d.G * TGM_WORDS; i += kWave) S.s_tgm[i] = D.tg_meta[i];
+  lds_copy<4>(S.s_tgm, D.tg_meta, d.G * TGM_WORDS);
   S.gc.tpl = W.c_tpl;
   S.gc.req = W.c_req;
   S.gc.max = W.c_max;
@@ -2371,58 +2425,62 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     for (int i = lane(); i < NWN; i += kWave) S.s_tchr[i] = 0;
   if constexpr (SIM) {
     // the simulation's fresh Scheduler state (what k_init does for plain Solves): NewQueue order is
-    // the local order (pod_map is sorted), nothing placed, no staleness marks
+    // the local order (pod_map is sorted), nothing placed, no staleness marks.  The per-pod queue arrays
+    // are written at the first push-back (sim_queue_init): until then nothing reads them.
     for (int i = lane(); i < NWN; i += kWave) {
       S.s_rmv[i] = 0;
       S.s_tch[i] = 0;
       S.s_tchr[i] = 0;
       S.s_tvol[i] = 0;
     }
-    for (int i = lane(); i < P; i += kWave) {
-      W.queue[i] = i;
-      W.pod_state[i] = D.pod_state0[W.pod_map[i]];
-      W.pod_status[i] = ST_PENDING;
-      W.pod_fstate[i] = -1;
-      W.last_len[i] = 0;
-    }
     if constexpr (TOPO) {
       // NewTopology for this simulation: the shared counts minus the candidates' pods, which the
       // simulation schedules and NewTopology therefore excludes (topology.go:72-75,262-265); a
       // domain left with no pod and no other registration drops out of TopologyGroup.domains.
       // (copy-on-write: only the words these entries touch get a private copy)
-      for (int i = lane(); i < d.G * W.ccs; i += kWave) W.tg_ccnt[i] = 0;
+      // placeholder counts: column 0 (the first fresh claim's); try_templates zeroes the next one per new claim
+      for (int g = lane(); g < d.G; g += kWave) W.tg_ccnt[(int64_t)g * W.ccs] = 0;
       for (int i = lane(); i < d.G; i += kWave) W.tg_cpos[i] = 0;
       wsync();
-      for (int i = lane(); i < W.ntdel; i += kWave) {  // offsets are distinct within one simulation
-        const int off = W.tdel[2 * i], x = W.tdel[2 * i + 1];
-        const int c = D.tg_cnt0[off] - (x >> 1);
-        const int n = (c == 0 && (x & 1)) ? -1 : c;
-        if (off < d.tgSmall) {
-          S.s_tcs[off] = n;
-        } else {
-          W.tg_cnt[off] = n;
-          const int b = off - d.tgSmall;
-          __hip_atomic_fetch_or(S.s_tcd + (b >> 5), 1u << (b & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      // offsets are distinct within one simulation; 4 entries per lane in flight (a long prefix has thousands)
+      for (int i0 = lane(); i0 < W.ntdel; i0 += 4 * kWave) {
+        int off[4], x[4], c0[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = i0 + u * kWave < W.ntdel ? i0 + u * kWave : i0;
+          off[u] = W.tdel[2 * i];
+          x[u] = W.tdel[2 * i + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) c0[u] = D.tg_cnt0[off[u]];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {  // (guarded stores, no per-lane break: DESIGN §3)
+          const bool live = i0 + u * kWave < W.ntdel;
+          const int c = c0[u] - (x[u] >> 1);
+          const int n = (c == 0 && (x[u] & 1)) ? -1 : c;
+          const bool small = off[u] < d.tgSmall;
+          if (live && small) S.s_tcs[off[u]] = n;
+          if (live && !small) {
+            W.tg_cnt[off[u]] = n;
+            const int b = off[u] - d.tgSmall;
+            __hip_atomic_fetch_or(S.s_tcd + (b >> 5), 1u << (b & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+          }
         }
       }
       hbm_release();
     }
     wsync();
-    if (lane() == 0)
-      for (int i = 0; i < W.nrm; i++) {
-        const int n = W.rm[i];
-        S.s_rmv[n >> 5] |= 1u << (n & 31);
-      }
+    for (int i = lane(); i < W.nrm; i += kWave) {  // the removed candidates (a multi-node prefix: up to 101)
+      const int n = W.rm[i];
+      __hip_atomic_fetch_or(S.s_rmv + (n >> 5), 1u << (n & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
     hbm_release();
   }
-  if (TL)
-    for (int i = lane(); i < d.totalTplIts * R; i += kWave)
-      S.s_talloc[i] = D.it_alloc[(int64_t)D.tpl_its[i / R] * R + i % R];
-  if (TL && pl.tsort)
-    for (int i = lane(); i < d.totalTplIts * R; i += kWave) {
-      S.s_tsa[i] = D.tsort_alloc[i];
-      S.s_tsp[i] = D.tsort_pos[i];
-    }
+  if (TL) lds_copy<8>(S.s_talloc, D.tpl_alloc, d.totalTplIts * R);
+  if (TL && pl.tsort) {
+    lds_copy<8>(S.s_tsa, D.tsort_alloc, d.totalTplIts * R);
+    lds_copy<8>(S.s_tsp, D.tsort_pos, d.totalTplIts * R);
+  }
   S.L.nkeys = d.NK;
   S.L.W = d.W;
   S.L.NB = d.NB;
@@ -2525,95 +2583,94 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       // next pops each fit a node of the register window, the step is Queue.Pop + the window's
       // first-fit ballots + the commit to the owner lane's registers, with nothing else live.  A pod
       // that fits no window node (or a stale queue) leaves it un-popped for the general step below.
+      // (A simulation's placements are not read back -- its record is -- so nothing is logged here.)
       if (d.N > 0) {
         while (wi < wn) {
           const uint64_t fll = (uint64_t)rdl64((int64_t)w.ll, wi);
           if ((uint32_t)(fll >> 32) == epoch && (uint32_t)fll == (uint32_t)qlen) break;
           const uint64_t ft0 = (uint64_t)rdl64((int64_t)w.tol0, wi), ft1 = (uint64_t)rdl64((int64_t)w.tol1, wi);
+          const int fpf = rdl(w.pf, wi);
           int64_t fp[RM];
 #pragma unroll
           for (int r = 0; r < RM; r++) fp[r] = rdl64(w.req[r], wi);
-          // A run of identical pods (same requests and tolerations, none stale when it is popped): pod after
-          // pod, first-fit fills the window's nodes in order, each taking as many as fit (min over resources
-          // of floor(free / request)), so the whole run is placed in one step -- per node its capacity for
-          // the run, an exclusive scan over the node order, and each pod's node from a max-scan.
-          {
+          // A run of identical pods (same requests, tolerations and provisionable flag, none stale when it is
+          // popped): pod after pod, first-fit fills the window's nodes in order, each taking as many as fit (min
+          // over resources of floor(free / request)), so the whole run is placed in one step -- per node its
+          // capacity for the run, an exclusive scan over the node order, each node's share.  While no pod was
+          // pushed back (ident) the queue is the NewQueue order and the run is k_sim_run_len's count at this
+          // position, which may reach past the window; otherwise the identical, non-stale pods that follow in
+          // the window.
+          int m;
+          if (ident) {
+            m = rdl(w.rl, wi);
+            m = m < qlen ? m : qlen;
+          } else {
             bool inrun = false;
             if (lane() >= wi && lane() < wn) {
-              bool same = w.tol0 == ft0 && w.tol1 == ft1;
+              bool same = w.tol0 == ft0 && w.tol1 == ft1 && ((w.pf ^ fpf) & PF_PROVISIONABLE) == 0;
 #pragma unroll
               for (int r = 0; r < RM; r++) same &= w.req[r] == fp[r];
               const uint32_t qx = (uint32_t)(qlen - (lane() - wi));
               inrun = same && !((uint32_t)(w.ll >> 32) == epoch && (uint32_t)w.ll == qx);
             }
             const uint64_t nr = wballot(!inrun) & (~0ull << wi);
-            const int m = (nr ? ctz64(nr) : kWave) - wi;
-            if (m >= KS_RUN_MIN) {
-              PH_BEGIN(tb);
-              float rq[RM];
+            m = (nr ? ctz64(nr) : kWave) - wi;
+          }
+          m = uni(m);
+          if (m >= KS_RUN_MIN) {
+            PH_BEGIN(tb);
+            float rq[RM];
 #pragma unroll
-              for (int r = 0; r < RM; r++) rq[r] = fp[r] > 0 ? 1.0f / (float)fp[r] : 0.f;
-              int tk[NWA], pre[NWA];
-              int base = 0;
+            for (int r = 0; r < RM; r++) rq[r] = fp[r] > 0 ? 1.0f / (float)fp[r] : 0.f;
+            int tk[NWA];
+            int base = 0;
 #pragma unroll
-              for (int k = 0; k < NW; k++) {
-                tk[k] = 0;
-                pre[k] = 0;
-                if (base < m) {
-                  const bool tol = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
-                  int cap = tol ? m : 0;
+            for (int k = 0; k < NW; k++) {
+              tk[k] = 0;
+              if (base < m) {
+                const bool tol = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
+                int cap = tol ? m : 0;
 #pragma unroll
-                  for (int r = 0; r < RM; r++) {
-                    const int c = run_cap(wav[k][r], fp[r], rq[r], m);
-                    cap = c < cap ? c : cap;
-                  }
-                  const int incl = wscan_add(cap);
-                  const int p0 = base + incl - cap, room = m - p0;
-                  tk[k] = room <= 0 ? 0 : (cap < room ? cap : room);
-                  pre[k] = p0;
-                  base += rdl(incl, kWave - 1);
+                for (int r = 0; r < RM; r++) {
+                  const int c = run_cap(wav[k][r], fp[r], rq[r], m);
+                  cap = c < cap ? c : cap;
                 }
+                const int incl = wscan_add(cap);
+                const int p0 = base + incl - cap, room = m - p0;
+                tk[k] = room <= 0 ? 0 : (cap < room ? cap : room);
+                base += rdl(incl, kWave - 1);
               }
-              const int placed = base < m ? base : m;
-              if (placed == 0) break;  // pod wi fits no window node: the general step
-              S.s_bnode[lane()] = -1;
-              wsync();
-#pragma unroll
-              for (int k = 0; k < NW; k++)
-                if (tk[k] > 0) {
-                  S.s_bnode[pre[k]] = k * kWave + lane();
-#pragma unroll
-                  for (int r = 0; r < RM; r++) wav[k][r] -= (int64_t)tk[k] * fp[r];
-                }
-              wsync();
-              const int nt = wscan_max(lane() < placed ? S.s_bnode[lane()] : -1);  // node of the run's pod `lane`
-              const int src = wi + lane() < kWave ? wi + lane() : kWave - 1;
-              const int fpod_t = __shfl(w.p, src);
-              if (winUnusable) {  // AllNonPendingPodsScheduled: a non-provisionable pod on an unusable node
-                int nf = 0;
-#pragma unroll
-                for (int k = 0; k < NW; k++) {
-                  const int v = __shfl(wnf[k], nt & (kWave - 1));
-                  if ((nt >> 6) == k) nf = v;
-                }
-                const int pf_t = __shfl(w.pf, src);
-                if (wballot(lane() < placed && (nf & NF_UNUSABLE) && !(pf_t & PF_PROVISIONABLE))) allSched = false;
-              }
-              const int st_t = __shfl(w.st, src);
-              if (lane() < placed && st_t == ST_FAILED) W.pod_status[fpod_t] = ST_SCHEDULED;
-              S.log_batch(placed, fpod_t, -(nt + 1), nlog);
-              S.algbytes += (int64_t)rdl(wscan_add(lane() < placed ? nt + 1 : 0), kWave - 1) * (16 * R + 16);
-              qhead += placed;
-              if (qhead >= P) qhead -= P;
-              qlen -= placed;
-              pops += placed;
-              wi += placed;
-              runs++;
-              runPods += placed;
-              SPHS_END(S, tb, 1);  // (stats build): runs placed in one step
-              if (placed < m) break;  // the next pod of the run fits no window node
-              continue;
             }
+            const int placed = base < m ? base : m;
+            if (placed == 0) break;  // pod wi fits no window node: the general step
+            // commit: each node's share (branch-free per lane: tk = 0 leaves a node unchanged)
+            bool unusable = false;
+            int64_t ab = 0;
+#pragma unroll
+            for (int k = 0; k < NW; k++) {
+#pragma unroll
+              for (int r = 0; r < RM; r++) wav[k][r] -= (int64_t)tk[k] * fp[r];
+              unusable = unusable || (tk[k] > 0 && (wnf[k] & NF_UNUSABLE));
+              ab += (int64_t)tk[k] * (k * kWave + lane() + 1);
+            }
+            // AllNonPendingPodsScheduled: a non-provisionable pod on an unusable node (helpers.go:118-124)
+            if (winUnusable && !(fpf & PF_PROVISIONABLE) && wballot(unusable)) allSched = false;
+            // a run's pods within the window that had failed before (only after a push-back) are scheduled now
+            if (lane() >= wi && lane() < wi + placed && lane() < wn && w.st == ST_FAILED) W.pod_status[w.p] = ST_SCHEDULED;
+            for (int off = 32; off >= 1; off >>= 1) ab += __shfl_xor(ab, off);
+            S.algbytes += uni64(ab) * (16 * R + 16);
+            nlog += placed;
+            qhead += placed;
+            if (qhead >= P) qhead -= P;
+            qlen -= placed;
+            pops += placed;
+            wi += placed;
+            if (wi > wn) wi = wn;  // the run reached past the window: refill at the loop head
+            runs++;
+            runPods += placed;
+            SPHS_END(S, tb, 1);  // (stats build): runs placed in one step
+            if (placed < m) break;  // the next pod of the run fits no window node
+            continue;
           }
           int kj = -1;
           uint64_t mj = 0;
@@ -2641,9 +2698,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                 for (int r = 0; r < RM; r++) wav[k][r] -= fp[r];
             }
-          if ((rdl(nfv, owner) & NF_UNUSABLE) && !(rdl(w.pf, wi) & PF_PROVISIONABLE)) allSched = false;
-          if (rdl(w.st, wi) == ST_FAILED && lane() == 0) W.pod_status[fpod] = ST_SCHEDULED;
-          S.log_commit(fpod, -(j + 1), nlog);
+          if ((rdl(nfv, owner) & NF_UNUSABLE) && !(fpf & PF_PROVISIONABLE)) allSched = false;
+          if (rdl(w.st, wi) == ST_FAILED) W.pod_status[fpod] = ST_SCHEDULED;  // (wave-wide, uniform)
+          nlog++;
           S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
           qhead = qhead + 1 == P ? 0 : qhead + 1;
           qlen--;
@@ -2934,32 +2991,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       if (r < 0) { err = KE_CLAIM_CAP; break; }
       if (r == 1) placed = true;
       if (r == 2) {  // no templates: add() returns a nil error
-        if (lane() == 0) W.pod_status[p] = ST_SCHEDULED;
+        W.pod_status[p] = ST_SCHEDULED;  // wave-wide store of a uniform value
         placed = true;
       }
     }
     if (U(placed)) {
       // SIM: the epilogue reads the final status; only a pod that failed before needs a store
-      if (SIM && rdl(w.st, wi - 1) == ST_FAILED && lane() == 0) W.pod_status[p] = ST_SCHEDULED;
+      if (SIM && rdl(w.st, wi - 1) == ST_FAILED) W.pod_status[p] = ST_SCHEDULED;  // (wave-wide, uniform)
       continue;
     }
     // failure: Preferences.Relax (preferences.go:38) + Queue.Push (queue.go:64-71)
+    if (SIM && ident) S.sim_queue_init(P);  // the simulation's first push-back: its queue state, lazily
     const int s0 = D.pod_state0[g], ns = D.pod_nstate[g];
     const bool relaxed = U(s - s0 + 1 < ns);
-    if (lane() == 0) {
-      W.pod_status[p] = ST_FAILED;
-      W.pod_fstate[p] = s;
-      if (relaxed) W.pod_state[p] = s + 1;
-    }
+    W.pod_status[p] = ST_FAILED;  // wave-wide stores of uniform values
+    W.pod_fstate[p] = s;
+    if (relaxed) W.pod_state[p] = s + 1;
     if (relaxed) epoch++;
     if (TOPO && relaxed) S.topo_activate_state(s + 1, nclaims, hostCtr);  // Topology.Update (scheduler.go:160-170)
     int tail = qhead + qlen;
     if (tail >= P) tail -= P;
-    if (lane() == 0) W.queue[tail] = p;
+    W.queue[tail] = p;  // wave-wide store of a uniform value
     qlen++;
     pushed = true;
     ident = false;
-    if (!relaxed && lane() == 0) W.last_len[uid] = ((uint64_t)epoch << 32) | (uint32_t)qlen;
+    if (!relaxed) W.last_len[uid] = ((uint64_t)epoch << 32) | (uint32_t)qlen;  // (wave-wide, uniform)
   }
   S.log_flush(nlog);
   // write back LDS-resident claim state for the host
@@ -2989,7 +3045,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     for (int i = 0; i < 4; i++) W.counters[CT_CYC_SUB + i] = (int64_t)S.scyc[i];
 #endif
   }
-  if constexpr (SIM) S.sim_record(P, nclaims, hostCtr, allSched, err);
+  if constexpr (SIM) S.sim_record(P, nclaims, hostCtr, allSched, err, !ident);
 }
 
 // Every translation unit instantiates one k_solve family (KS_TU 0: Solve, 1: Solve + topology,
