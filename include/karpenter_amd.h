@@ -161,7 +161,8 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
  * Requirement records (NewNodeClaims[0].Requirements) stay on the GPU that ran a simulation:
  * ks_cons_needed_sims lists (returns the count; writes up to cap) the simulations the output needs,
  * their owners (rank = sim % world) read them with ks_cons_claim_requirements (requirement_words
- * uint32 each), and rs_table passes them to ks_cons_decide in that order. */
+ * uint32 each), and rs_table passes them to ks_cons_decide in that order.  rs_table may be NULL when world is 1
+ * and this handle's last ks_cons_run covered every simulation: the records are then read from that run. */
 #define KS_CONS_ALL_SIMS 1   /* flags: report every simulation */
 #define KS_CONS_CANDIDATES 2 /* flags: include the ordered candidate list */
 int ks_cons_requirement_words(const ks_cons* c);

@@ -1354,6 +1354,26 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
   if (!c || !records || !json_out || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
   const int32_t* recs = (const int32_t*)records;
   const bool all_sims = (flags & KS_CONS_ALL_SIMS) != 0;
+  if (!rs_table && world == 1 && c->L.lworld == 1) {
+    // One rank ran every simulation: the requirement records the output needs are read from this handle's
+    // launch as the replay reaches them (one pass over the records, no needed_sims dry run).
+    const int RSW = c->pb->host.dims.RSW;
+    std::map<int, std::vector<uint32_t>> cache;
+    auto fetch = [&](int sim) -> const uint32_t* {
+      std::vector<uint32_t>& v = cache[sim];
+      if (v.empty()) {
+        const int32_t claim = recs[(size_t)sim * c->recWords + RF_CLAIM];
+        if (sim < 0 || sim >= (int)c->L.lhost.size() || claim < 0)
+          throw KsError(KS_ERR_INTERNAL, "simulation " + std::to_string(sim) + " has no NodeClaim record");
+        v.resize((size_t)RSW);
+        HIPCHK(hipMemcpy(v.data(), c->L.lhost[(size_t)sim].c_rs + (size_t)claim * RSW, 4 * (size_t)RSW,
+                         hipMemcpyDeviceToHost));
+      }
+      return v.data();
+    };
+    *json_out = strdup(decide_json(*c, recs, world, all_sims, fetch, (flags & KS_CONS_CANDIDATES) != 0, clock).c_str());
+    return KS_OK;
+  }
   std::vector<int> need = needed_sims(*c, recs, world, all_sims);
   if (!need.empty() && !rs_table) throw KsError(KS_ERR_ARG, "requirement records of the needed simulations missing");
   std::map<int, const uint32_t*> table;

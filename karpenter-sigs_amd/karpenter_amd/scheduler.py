@@ -461,20 +461,24 @@ class Consolidator:
         candidates=False leaves out the ordered candidate list (the commands are unchanged);
         clock=(multi_timeout_s, single_timeout_s, sim_seconds): the methods' timeouts on a virtual clock."""
         l = _cons_lib()
-        need = self.needed_sims(records, world, all_sims)
-        fetch = fetch or self.claim_requirements
-        table = b"".join(fetch(s) for s in need)
-        tbuf = ctypes.create_string_buffer(table, max(len(table), 4))
+        if fetch is None and world == 1:
+            tbuf = None  # this handle ran every simulation: the library reads the requirement records it needs
+        else:
+            need = self.needed_sims(records, world, all_sims)
+            fetch = fetch or self.claim_requirements
+            table = b"".join(fetch(s) for s in need)
+            tbuf = ctypes.create_string_buffer(table, max(len(table), 4))
         buf = _records_buffer(records)
         js = ctypes.c_void_p()
         flags = (1 if all_sims else 0) | (2 if candidates else 0)
         if clock is None:
             _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, flags,
-                                    ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(js)))
+                                    None if tbuf is None else ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(js)))
         else:
             clk = _Clock(*clock)
             _check(l.ks_cons_decide_clock(self._h, ctypes.cast(buf, ctypes.c_void_p), world, flags,
-                                          ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(clk), ctypes.byref(js)))
+                                          None if tbuf is None else ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(clk),
+                                          ctypes.byref(js)))
         return json.loads(_take_str(js))
 
     def validate(self, command, device=-1):
