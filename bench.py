@@ -246,6 +246,30 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
                   "ms": round(sorted(vms)[1], 3)}
     name = "C5" if not topology else "C5 + topology (%d apps: spread, pod affinity, anti-affinity)" % topology
     pass_ms = elapsed * 1000.0 / args.cons_steps
+    # Incremental update between passes (ks_cons_update): 10 pods deleted on one node and one node removed,
+    # then the next pass (new plan: pod lists, queue sort, run lengths; simulations; decide), 5 times.
+    update = None
+    if world == 1 and not topology:
+        nodes = json.loads(snap)["stateNodes"]
+        ums, pms = [], []
+        for i in range(5):
+            a, b = nodes[200 + 2 * i], nodes[201 + 2 * i]
+            delta = {"deletePods": [p["metadata"]["uid"] for p in a.get("pods", [])[:10]], "removeNodes": [b["name"]]}
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            c.update(delta)
+            t1 = time.perf_counter()
+            one_pass()
+            t2 = time.perf_counter()
+            ums.append((t1 - t0) * 1000.0)
+            pms.append((t2 - t1) * 1000.0)
+        tot = sorted(u + p for u, p in zip(ums, pms))
+        update = {"events": "10 pod deletions + 1 node removal per update", "updates": len(ums),
+                  "update_ms": round(sorted(ums)[len(ums) // 2], 3),
+                  "pass_after_update_ms": round(sorted(pms)[len(pms) // 2], 3),
+                  "update_plus_pass_ms": round(tot[len(tot) // 2], 3),
+                  "update_plus_pass_ms_max": round(tot[-1], 3),
+                  "vs_create_plus_first_pass_ms": round(create_ms + first_ms, 3)}
     return {
         "metric": "consolidation cands/sec (%s: %d nodes x 20 pods, 400 instance types)" % (name, args.cons_nodes),
         "value": round(c.num_sims * args.cons_steps / elapsed, 1),
@@ -274,6 +298,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
         "cpu_baseline": cpu,
         "cpu_baseline_1thread": cpu1,
         "validation": validation,
+        **({"incremental_update": update} if update else {}),
         **({"shards_on_one_gpu": shards} if shards else {}),
     }
 

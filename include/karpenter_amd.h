@@ -143,6 +143,21 @@ int ks_cons_save(const ks_cons* c, void** buf, size_t* len);
 int ks_cons_create_binary(const void* buf, size_t len, ks_cons** out);
 /* Host-only (no device): JSON {candidates:[{name, disruptionCost, pods}], sims, multiPrefixes, recordBytes}. */
 int ks_cons_inspect(const char* snapshot_json, size_t len, char** out_json);
+/* Cluster-state events between two passes against the resident handle (replaces re-reading the cluster
+ * and rebuilding the scheduler per pass: state/cluster.go:220-512 UpdatePod/DeletePod/DeleteNode,
+ * provisioner.go:204-296).  update_json: {"deletePods":[uid], "bindPods":[{"uid","node"}],
+ * "removeNodes":[name]}, applied in that order: a deleted pod frees its node's requests; a bound pod
+ * (pending until now) is Running on an active node and takes its requests; a removed node takes its pods
+ * with it and returns its capacity to its NodePool's limits.  Candidates, their costs and order, and
+ * the simulations are re-derived; the next ks_cons_run sees the new state.  All or nothing:
+ * KS_ERR_ARG for unknown / already-deleted / not-pending pods or unknown nodes, KS_ERR_UNSUPPORTED
+ * for clusters with topology groups or volume limits and pods with host ports (rebuild with
+ * ks_cons_create there). */
+int ks_cons_update(ks_cons* c, const char* update_json, size_t len);
+/* Host-only: the snapshot with update_json applied ("{}" for none, an array for a sequence), as ks_cons_inspect plus
+ * "nodeRows" {name: {available (device units), pods}} for every active node and "poolRemaining". */
+int ks_cons_inspect_update(const char* snapshot_json, size_t len, const char* update_json, size_t ulen,
+                           char** out_json);
 void ks_cons_free(ks_cons* c);
 int ks_cons_num_candidates(const ks_cons* c);
 int ks_cons_num_sims(const ks_cons* c);

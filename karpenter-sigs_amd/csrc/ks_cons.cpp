@@ -26,6 +26,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/karpenter_amd.h"
@@ -201,6 +202,24 @@ struct ks_cons {
   int64_t hostnameSeed = 0;
   int recWords = 0;
 
+  // What the candidates are re-derived from after ks_cons_update (pod and node deltas between passes):
+  // every node that passed NewCandidate's node tests, in the snapshot's "candidates" order, blocked or not;
+  // the pods of every active node (GetNodePods order); and per pod its cost and filterCandidates verdict.
+  struct CandIn {
+    Cand k;                // pods and cost filled in by order_candidates
+    double remaining = 1;  // lifetimeRemaining (types.go:136-145)
+    bool passOk = true;    // ShouldDisrupt for the pass (consolidateAfter is not Never)
+  };
+  enum : int32_t { PN_PENDING = -1, PN_DELETING = -2, PN_GONE = -3 };
+  std::vector<CandIn> candIn;
+  std::vector<std::vector<int>> nodePods;  // [host node] GetNodePods
+  std::vector<int32_t> podNode;            // [pod] host node index or PN_*
+  std::vector<uint8_t> podBlock;           // [pod] bit 0: blocks its node; bit 1: would block once bound and Running
+  std::vector<double> podCost;             // [pod] GetPodEvictionCost
+  std::vector<uint8_t> nodeGone;           // [host node] removed by an update
+  std::unordered_map<std::string, int> uidIndex, nodeIndex;  // built at the first update
+  int64_t updates = 0;
+
   // A launch of one rank's simulations, cached per (rank, world).  Validation runs its one
   // re-simulation in a launch of its own, so the pass's launch (records, requirement records,
   // counters) survives it.
@@ -224,12 +243,23 @@ struct ks_cons {
     bool lsorted = false;  // lpodmap holds every simulation's NewQueue order (a plan's pods never change)
     Plan lplan{};
     std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
+    // allocation capacities: a new plan (another rank / world, an update) reuses the buffers that fit
+    size_t capBuf = 0, capWorks = 0, capRec = 0, capHrec = 0, capEnt = 0, capRunw = 0, capTemp = 0;
     void release() {
       for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
                       (void*)lrunlen, (void*)lrunw, (void*)lkeys, (void*)lvals, ltemp})
         if (p) (void)hipFree(p);
       if (hrec) (void)hipHostFree(hrec);
       *this = Launch{};  // stale lookups (claim requirements, counters) now fail cleanly
+    }
+    // drop the plan, keep the allocations
+    void invalidate() {
+      lrank = lworld = -1;
+      lsims.clear();
+      lhost.clear();
+      lnent = lrbits = lsbits = 0;
+      lsorted = false;
+      lplan = Plan{};
     }
   };
   Launch L;
@@ -241,6 +271,7 @@ struct ks_cons {
   int per_rank(int world) const { return ((int)sims.size() + world - 1) / world; }
 
   void free_launch() { L.release(); }
+  void invalidate_launch() { L.invalidate(); }
   ~ks_cons() {
     int prev = -1;
     // (a handle whose load failed before device init has device -1: nothing to select, and hipSetDevice(-1)
@@ -255,6 +286,67 @@ struct ks_cons {
 };
 
 namespace {
+
+// The pass's candidates and simulations from candIn and the current pods: disruptionCost (helpers.go:170-176,
+// summed in GetNodePods order) x lifetimeRemaining, filterCandidates, sort.Slice by cost, then the multi-node
+// prefixes and the singles.  Run by build_cons and after every ks_cons_update.
+void order_candidates(ks_cons& c) {
+  c.cands.clear();
+  c.sims.clear();
+  c.multiHi = 0;
+  std::vector<ks_cons::Cand> cands, valOnly;
+  for (const ks_cons::CandIn& ci : c.candIn) {
+    if (c.nodeGone[(size_t)ci.k.node]) continue;
+    const std::vector<int>& pods = c.nodePods[(size_t)ci.k.node];
+    double cost = 0;
+    bool blocked = false;
+    for (int p : pods) {
+      cost += c.podCost[(size_t)p];
+      blocked = blocked || (c.podBlock[(size_t)p] & 1);
+    }
+    if (blocked) continue;
+    ks_cons::Cand k = ci.k;
+    k.pods = pods;
+    k.cost = cost * ci.remaining;
+    (ci.passOk ? cands : valOnly).push_back(std::move(k));
+  }
+  // sort.Slice(candidates, disruptionCost <): pdqsort only observes less(), so the costs' dense ranks
+  // reproduce its swap sequence exactly.
+  {
+    const int n = (int)cands.size();
+    std::vector<double> vals;
+    for (auto& k : cands) vals.push_back(k.cost);
+    std::sort(vals.begin(), vals.end());
+    std::vector<int32_t> key(n), idx(n);
+    for (int i = 0; i < n; i++) {
+      key[i] = (int32_t)(std::lower_bound(vals.begin(), vals.end(), cands[i].cost) - vals.begin());
+      idx[i] = i;
+    }
+    GoSortExact g{GoSort{key.data(), idx.data()}};
+    g.run(n);
+    for (int i = 0; i < n; i++) c.cands.push_back(std::move(cands[(size_t)idx[i]]));
+  }
+  c.nPass = (int)c.cands.size();
+  for (auto& k : valOnly) c.cands.push_back(std::move(k));
+  // the simulations: multi-node prefixes (firstNConsolidationOption's search space) and single nodes
+  const int n = c.nPass;
+  if (n >= 2) {
+    int hi = std::min(n, 100);
+    if (n <= hi) hi = n - 1;
+    c.multiHi = hi;
+  }
+  for (int mid = c.multiHi; mid >= 1; mid--) {
+    ks_cons::Sim s;
+    s.multi = true;
+    for (int i = 0; i <= mid; i++) s.cands.push_back(i);
+    c.sims.push_back(s);
+  }
+  for (int i = 0; i < n; i++) {
+    ks_cons::Sim s;
+    s.cands.push_back(i);
+    c.sims.push_back(s);
+  }
+}
 
 // Parse the cluster snapshot into the resident problem + candidates + sims.
 void build_cons(ks_cons& c, const Value& rootIn) {
@@ -377,8 +469,40 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   const int64_t nowNs = parse_rfc3339(jstr(&root, "now")) * 1000000000;
   const std::vector<Pdb> pdbs = parse_pdbs(root);
 
+  // per pod: where it is, its eviction cost and whether it blocks its node (filterCandidates, helpers.go:47-71:
+  // a PDB allowing no eviction or a do-not-disrupt pod); bit 1 is the verdict for a pending pod once bound
+  // and Running (ks_cons_update), when a Ready=False condition no longer applies
+  const int P = (int)podH.size();
+  c.podNode.assign((size_t)P, ks_cons::PN_GONE);
+  c.podBlock.assign((size_t)P, 0);
+  c.podCost.assign((size_t)P, 0.0);
+  c.nodePods.assign(h.nodes.size(), {});
+  c.nodeGone.assign(h.nodes.size(), 0);
+  for (int p : c.pending) c.podNode[(size_t)p] = ks_cons::PN_PENDING;
+  for (int p : c.deleting) c.podNode[(size_t)p] = ks_cons::PN_DELETING;
+  for (const auto& kv : nodeByName) {
+    if (deletingNode[(size_t)kv.second]) continue;
+    auto hn = hostNode.find(kv.first);
+    if (hn == hostNode.end()) continue;
+    c.nodePods[(size_t)hn->second] = nodePods[(size_t)kv.second];
+    for (int p : nodePods[(size_t)kv.second]) c.podNode[(size_t)p] = hn->second;
+  }
+  parallel_for(P, 1024, [&](int p) {
+    const PodH& ph = podH[(size_t)p];
+    c.podCost[(size_t)p] = eviction_cost(ph);
+    const bool dnd = do_not_disrupt(ph);
+    uint8_t b = (!can_evict(pdbs, ph) || dnd) ? 1 : 0;
+    if (ph.notReady) {
+      PodH ready = ph;
+      ready.notReady = false;
+      b |= (!can_evict(pdbs, ready) || dnd) ? 2 : 0;
+    } else {
+      b |= b << 1;
+    }
+    c.podBlock[(size_t)p] = b;
+  });
+
   // NewCandidate for the listed nodes; nodes that would fail it are not candidates
-  std::vector<ks_cons::Cand> cands, valOnly;
   if (const Value* cs = root.get("candidates"))
     for (auto& v : cs->arr()) {
       const std::string name = v.str();
@@ -403,67 +527,25 @@ void build_cons(ks_cons& c, const Value& rootIn) {
       // test) admits the rest for mapCandidates after the wait
       if (ann && ann->is_obj() && jstr(ann, "karpenter.sh/do-not-consolidate") == "true") continue;
       if (policyOff.count(lp->second)) continue;
-      const bool passOk = !afterNever.count(lp->second);
-      ks_cons::Cand k;
+      ks_cons::CandIn ci;
+      ci.passOk = !afterNever.count(lp->second);
+      ks_cons::Cand& k = ci.k;
       k.node = hn->second;
       k.name = name;
       k.pool = lp->second;
       k.ct = lct->second;
       k.zone = lz->second;
       k.it = pt->second.at(lit->second);
-      k.pods = nodePods[(size_t)it->second];
-      double cost = 0;
-      for (int p : k.pods) cost += eviction_cost(podH[(size_t)p]);  // disruptionCost helpers.go:170-176
-      double remaining = 1.0;                                           // lifetimeRemaining types.go:136-145
-      auto ex = expire.find(k.pool);
+      auto ex = expire.find(k.pool);  // lifetimeRemaining types.go:136-145
       if (ex != expire.end()) {
         const int64_t created = parse_rfc3339(jstr(&nv, "creationTimestamp")) * 1000000000;
         const double age = dur_seconds(nowNs - created), total = dur_seconds(ex->second);
-        remaining = clampf(0.0, (total - age) / total, 1.0);
+        ci.remaining = clampf(0.0, (total - age) / total, 1.0);
       }
-      k.cost = cost * remaining;
-      // filterCandidates (helpers.go:47-71): a PDB allowing no eviction or a do-not-disrupt pod blocks it
-      bool blocked = false;
-      for (int p : k.pods) blocked = blocked || !can_evict(pdbs, podH[(size_t)p]) || do_not_disrupt(podH[(size_t)p]);
-      if (!blocked) (passOk ? cands : valOnly).push_back(std::move(k));
+      c.candIn.push_back(std::move(ci));
     }
   pt.mark("candidates");
-  // sort.Slice(candidates, disruptionCost <): pdqsort only observes less(), so the costs' dense ranks
-  // reproduce its swap sequence exactly.
-  {
-    const int n = (int)cands.size();
-    std::vector<double> vals;
-    for (auto& k : cands) vals.push_back(k.cost);
-    std::sort(vals.begin(), vals.end());
-    std::vector<int32_t> key(n), idx(n);
-    for (int i = 0; i < n; i++) {
-      key[i] = (int32_t)(std::lower_bound(vals.begin(), vals.end(), cands[i].cost) - vals.begin());
-      idx[i] = i;
-    }
-    GoSortExact g{GoSort{key.data(), idx.data()}};
-    g.run(n);
-    for (int i = 0; i < n; i++) c.cands.push_back(cands[(size_t)idx[i]]);
-  }
-  c.nPass = (int)c.cands.size();
-  for (auto& k : valOnly) c.cands.push_back(std::move(k));
-  // the simulations: multi-node prefixes (firstNConsolidationOption's search space) and single nodes
-  const int n = c.nPass;
-  if (n >= 2) {
-    int hi = std::min(n, 100);
-    if (n <= hi) hi = n - 1;
-    c.multiHi = hi;
-  }
-  for (int mid = c.multiHi; mid >= 1; mid--) {
-    ks_cons::Sim s;
-    s.multi = true;
-    for (int i = 0; i <= mid; i++) s.cands.push_back(i);
-    c.sims.push_back(s);
-  }
-  for (int i = 0; i < n; i++) {
-    ks_cons::Sim s;
-    s.cands.push_back(i);
-    c.sims.push_back(s);
-  }
+  order_candidates(c);
   c.recWords = rec_words(h.dims.TW);
   pt.mark("sort + sims");
 }
@@ -537,7 +619,8 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
 // Build and upload the launch of this rank's simulations (cached per (rank, world)).
 void prepare_launch(ks_cons& c, int rank, int world) {
   if (c.L.lrank == rank && c.L.lworld == world) return;
-  c.free_launch();
+  PhaseTimer pt("prepare_launch");
+  c.invalidate_launch();
   ks_problem& pb = *c.pb;
   Host& h = pb.host;
   const KsDims& d = h.dims;
@@ -622,21 +705,43 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   }
   c.L.lnent = (int)entries.size();
   const size_t inBase = a.total;
-  HIPCHK(hipMalloc(&c.L.lbuf, std::max<size_t>(inBase + ai.total, 256)));
+  pt.mark("pod lists + layout");
+  // device buffers grow to the largest plan seen and are reused (a plan per update must not pay hipMalloc)
+  auto grow = [](auto*& p, size_t& cap, size_t bytes) {
+    if (bytes <= cap && p) return;
+    if (p) HIPCHK(hipFree((void*)p));
+    p = nullptr;
+    HIPCHK(hipMalloc((void**)&p, bytes));
+    cap = bytes;
+  };
+  const size_t ne = (size_t)std::max(c.L.lnent, 1), nsz = (size_t)std::max(ns, 1);
+  grow(c.L.lbuf, c.L.capBuf, std::max<size_t>(inBase + ai.total, 256));
   char* base = (char*)c.L.lbuf;
   char* ibase = base + inBase;
-  HIPCHK(hipMalloc(&c.L.lworks, sizeof(KsWork) * std::max(ns, 1)));
-  HIPCHK(hipMalloc(&c.L.lrec, 4 * (size_t)c.recWords * std::max(ns, 1)));
-  HIPCHK(hipHostMalloc((void**)&c.L.hrec, 4 * (size_t)c.recWords * std::max(ns, 1), hipHostMallocDefault));
-  HIPCHK(hipMalloc(&c.L.lentries, 4 * (size_t)std::max(c.L.lnent, 1)));
-  HIPCHK(hipMalloc(&c.L.lentrySim, 4 * (size_t)std::max(c.L.lnent, 1)));
-  HIPCHK(hipMalloc(&c.L.lpodmap, 4 * (size_t)std::max(c.L.lnent, 1)));
-  HIPCHK(hipMalloc(&c.L.lrunlen, 4 * (size_t)std::max(c.L.lnent, 1)));
-  HIPCHK(hipMalloc(&c.L.lrunw, 8 * (size_t)std::max((c.L.lnent + 63) / 64, 1)));
-  HIPCHK(hipMalloc(&c.L.lkeys, 16 * (size_t)std::max(c.L.lnent, 1)));
-  HIPCHK(hipMalloc(&c.L.lvals, 8 * (size_t)std::max(c.L.lnent, 1)));
+  grow(c.L.lworks, c.L.capWorks, sizeof(KsWork) * nsz);
+  grow(c.L.lrec, c.L.capRec, 4 * (size_t)c.recWords * nsz);
+  if (!c.L.hrec || 4 * (size_t)c.recWords * nsz > c.L.capHrec) {
+    if (c.L.hrec) HIPCHK(hipHostFree(c.L.hrec));
+    c.L.hrec = nullptr;
+    HIPCHK(hipHostMalloc((void**)&c.L.hrec, 4 * (size_t)c.recWords * nsz, hipHostMallocDefault));
+    c.L.capHrec = 4 * (size_t)c.recWords * nsz;
+  }
+  if (ne > c.L.capEnt || !c.L.lentries) {
+    size_t cap = 0;  // the per-entry buffers share one capacity
+    for (int32_t** q : {&c.L.lentries, &c.L.lentrySim, &c.L.lpodmap, &c.L.lrunlen}) {
+      cap = 0;
+      grow(*q, cap, 4 * ne);
+    }
+    cap = 0;
+    grow(c.L.lkeys, cap, 16 * ne);
+    cap = 0;
+    grow(c.L.lvals, cap, 8 * ne);
+    c.L.capEnt = ne;
+  }
+  grow(c.L.lrunw, c.L.capRunw, 8 * (size_t)std::max((c.L.lnent + 63) / 64, 1));
   c.L.ltempBytes = std::max<size_t>(queue_sort_temp_bytes(std::max(c.L.lnent, 1)), 256);
-  HIPCHK(hipMalloc(&c.L.ltemp, c.L.ltempBytes));
+  grow(c.L.ltemp, c.L.capTemp, c.L.ltempBytes);
+  pt.mark("device buffers");
   if (c.L.lnent) {
     HIPCHK(hipMemcpy(c.L.lentries, entries.data(), 4 * entries.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c.L.lentrySim, entrySim.data(), 4 * entrySim.size(), hipMemcpyHostToDevice));
@@ -647,7 +752,15 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   while ((1ll << c.L.lsbits) < std::max(ns, 2)) c.L.lsbits++;
 
   // per-simulation inputs: removed nodes, limits, prices
+  pt.mark("entries upload");
   std::vector<char> stage(ai.total, 0);
+  std::vector<int> itName((size_t)std::max(d.T, 1), 0);  // instance type -> dense id of its name
+  {
+    std::map<std::string, int> ids;
+    for (int t = 0; t < d.T; t++) itName[(size_t)t] = ids.emplace(h.its[(size_t)t].name, (int)ids.size()).first->second;
+  }
+  std::vector<char> nameSeen(itName.size(), 0), nameHas(itName.size(), 0);
+  std::vector<double> nameBest(itName.size(), 0.0);
   std::vector<KsWork> works(ns);
   for (int k = 0; k < ns; k++) {
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
@@ -683,26 +796,32 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     if (allSpot) cflags |= CF_ALL_SPOT;
     if (sm.multi) {
       cflags |= CF_MULTI;
-      // filterOutSameType: the cheapest candidate offering per candidate instance type (by name)
-      std::set<std::string> existing;
-      std::map<std::string, double> prices;
+      // filterOutSameType: the cheapest candidate offering per candidate instance type (by name); names as
+      // dense ids (itName), the per-name state reset through the touched list
+      std::vector<int> touched;
       for (int ci : sm.cands) {
         const ks_cons::Cand& k = c.cands[(size_t)ci];
-        const Host::IT& it = h.its[(size_t)k.it];
-        existing.insert(it.name);
-        double pr;
-        if (!offering_price(it, k.ct, k.zone, pr)) continue;
-        auto f = prices.find(it.name);
-        const double cur = f == prices.end() ? std::numeric_limits<double>::max() : f->second;
-        if (pr < cur) prices[it.name] = pr;
-      }
-      std::vector<double> st(std::max(d.T, 1), std::numeric_limits<double>::quiet_NaN());
-      for (int t = 0; t < d.T; t++)
-        if (existing.count(h.its[(size_t)t].name)) {
-          auto f = prices.find(h.its[(size_t)t].name);
-          st[(size_t)t] = f == prices.end() ? 0.0 : f->second;  // a missing map entry reads as 0
+        const int id = itName[(size_t)k.it];
+        if (!nameSeen[(size_t)id]) {
+          nameSeen[(size_t)id] = 1;
+          touched.push_back(id);
         }
-      memcpy(stage.data() + o.st_price, st.data(), 8 * st.size());
+        double pr;
+        if (!offering_price(h.its[(size_t)k.it], k.ct, k.zone, pr)) continue;
+        const double cur = nameHas[(size_t)id] ? nameBest[(size_t)id] : std::numeric_limits<double>::max();
+        if (pr < cur) {
+          nameBest[(size_t)id] = pr;
+          nameHas[(size_t)id] = 1;
+        }
+      }
+      double* st = (double*)(stage.data() + o.st_price);
+      for (int t = 0; t < std::max(d.T, 1); t++) {
+        const int id = t < d.T ? itName[(size_t)t] : -1;
+        // a missing map entry reads as 0; types that are no candidate's are NaN (not filtered)
+        st[t] = id >= 0 && nameSeen[(size_t)id] ? (nameHas[(size_t)id] ? nameBest[(size_t)id] : 0.0)
+                                               : std::numeric_limits<double>::quiet_NaN();
+      }
+      for (int id : touched) nameSeen[(size_t)id] = nameHas[(size_t)id] = 0;
       w.st_price = (const double*)(ibase + o.st_price);
     }
     w.c_tpl = (int32_t*)(base + o.c_tpl);
@@ -759,6 +878,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   }
   // The workspaces (~120 KB per simulation on C5, mostly the node-indexed copy-on-write request slots)
   // are zeroed on the device; only the inputs cross PCIe.
+  pt.mark("per-simulation inputs");
   HIPCHK(hipMemset(c.L.lbuf, 0, inBase));
   if (ai.total) HIPCHK(hipMemcpy(ibase, stage.data(), ai.total, hipMemcpyHostToDevice));
   if (ns) HIPCHK(hipMemcpy(c.L.lworks, works.data(), sizeof(KsWork) * ns, hipMemcpyHostToDevice));
@@ -773,6 +893,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   if (c.L.lplan.lds > 160 * 1024 || c.L.lplan.KO < 1) throw KsError(KS_ERR_CAPACITY, "simulation state does not fit in LDS");
   c.L.lrank = rank;
   c.L.lworld = world;
+  pt.mark("zero + upload + LDS plan");
 }
 
 std::string names_json(const Host& h, const std::vector<int>& its) {
@@ -1105,6 +1226,223 @@ std::string validate_json(ks_cons& c, const Value& cmd) {
   return out(true, "", sim);
 }
 
+// ks_cons_update: the cluster-state events between two passes (state/cluster.go:220-512 UpdatePod /
+// DeletePod / DeleteNode) applied to the resident handle, so the next pass needs no re-parse, no
+// re-encode and no re-upload of the problem.  Applied in order: deletePods, bindPods (a pending pod now
+// bound to an active node, Running and scheduled), removeNodes (with the pods still on them).  The node
+// rows move with StateNode.Available() (allocatable minus pod requests, lhs keys only, resources.go
+// Subtract), a removed node's capacity returns to its pool's limits (provisioner.go:204-296 re-reads them
+// per pass) and the node can take no pod in any simulation.  The candidates and simulations are re-derived
+// (order_candidates).  Refused (KS_ERR_UNSUPPORTED, nothing applied): clusters with topology groups or
+// volume limits (their counts are encoded per pod and node) and pods with host ports.
+void apply_update(ks_cons& c, const Value& delta, bool device) {
+  ks_problem& pb = *c.pb;
+  Host& h = pb.host;
+  const KsDims& d = h.dims;
+  const int R = d.R;
+  if (!delta.is_obj()) throw KsError(KS_ERR_PARSE, "update is not an object");
+  for (const auto& kv : delta.obj())
+    if (kv.first != "deletePods" && kv.first != "bindPods" && kv.first != "removeNodes")
+      throw KsError(KS_ERR_PARSE, "update: unknown field " + kv.first);
+  if (d.G) throw KsError(KS_ERR_UNSUPPORTED, "update: the cluster has topology groups");
+  if (d.volAny) throw KsError(KS_ERR_UNSUPPORTED, "update: the cluster has volume limits");
+  if (c.uidIndex.empty())
+    for (size_t i = 0; i < h.pods.size(); i++) c.uidIndex.emplace(h.pods[i].uid, (int)i);
+  if (c.nodeIndex.empty())
+    for (size_t i = 0; i < h.nodes.size(); i++) c.nodeIndex.emplace(h.nodes[i].name, (int)i);
+  auto podOf = [&](const Value& v) {
+    if (!v.is_str()) throw KsError(KS_ERR_PARSE, "update: pod uid is not a string");
+    auto it = c.uidIndex.find(v.str());
+    if (it == c.uidIndex.end()) throw KsError(KS_ERR_ARG, "update: unknown pod " + v.str());
+    return it->second;
+  };
+  auto nodeOf = [&](const Value* v) {
+    if (!v || !v->is_str()) throw KsError(KS_ERR_PARSE, "update: node name is not a string");
+    auto it = c.nodeIndex.find(v->str());
+    if (it == c.nodeIndex.end() || c.nodeGone[(size_t)it->second])
+      throw KsError(KS_ERR_ARG, "update: no active node " + v->str());
+    return it->second;
+  };
+  static const Value kNone;
+  const Value* dv = delta.get("deletePods");
+  const Value* bv = delta.get("bindPods");
+  const Value* rv = delta.get("removeNodes");
+  // validate the whole update against the state it will meet, then apply it
+  std::vector<int> del, bind, bindNode, rm;
+  std::set<int> seenPod, seenNode;
+  for (const Value& v : (dv ? *dv : kNone).arr()) {
+    const int p = podOf(v);
+    if (c.podNode[(size_t)p] == ks_cons::PN_GONE || !seenPod.insert(p).second)
+      throw KsError(KS_ERR_ARG, "update: pod " + v.str() + " is already deleted");
+    if (h.pods[(size_t)p].hostPorts) throw KsError(KS_ERR_UNSUPPORTED, "update: pod " + v.str() + " has host ports");
+    del.push_back(p);
+  }
+  for (const Value& v : (bv ? *bv : kNone).arr()) {
+    if (!v.is_obj() || !v.get("uid")) throw KsError(KS_ERR_PARSE, "update: bindPods entries are {uid, node}");
+    const int p = podOf(*v.get("uid")), n = nodeOf(v.get("node"));
+    if (c.podNode[(size_t)p] != ks_cons::PN_PENDING || !seenPod.insert(p).second)
+      throw KsError(KS_ERR_ARG, "update: pod " + v.get("uid")->str() + " is not pending");
+    if (h.pods[(size_t)p].hostPorts) throw KsError(KS_ERR_UNSUPPORTED, "update: pod has host ports");
+    bind.push_back(p);
+    bindNode.push_back(n);
+  }
+  for (const Value& v : (rv ? *rv : kNone).arr()) {
+    const int n = nodeOf(&v);
+    if (!seenNode.insert(n).second) throw KsError(KS_ERR_ARG, "update: node " + v.str() + " removed twice");
+    rm.push_back(n);
+  }
+
+  std::set<int> rows;  // node rows to re-derive
+  auto move = [&](int n, const PodH& p, int sign) {  // StateNode.Available() after a pod leaves / lands
+    Host::Node& hn = h.nodes[(size_t)n];
+    for (const auto& kv : p.requests) {
+      auto a = hn.available.find(kv.first);
+      if (a == hn.available.end()) continue;
+      a->second.n += sign * kv.second.n;
+    }
+    rows.insert(n);
+  };
+  auto erase = [](std::vector<int>& v, int x) {
+    auto it = std::find(v.begin(), v.end(), x);
+    if (it != v.end()) v.erase(it);
+  };
+  for (int p : del) {
+    const int32_t where = c.podNode[(size_t)p];
+    if (where >= 0) {
+      erase(c.nodePods[(size_t)where], p);
+      move(where, h.pods[(size_t)p], +1);
+    } else if (where == ks_cons::PN_PENDING) {
+      erase(c.pending, p);
+    } else if (where == ks_cons::PN_DELETING) {
+      erase(c.deleting, p);
+    }
+    c.podNode[(size_t)p] = ks_cons::PN_GONE;
+  }
+  for (size_t i = 0; i < bind.size(); i++) {
+    const int p = bind[i], n = bindNode[i];
+    PodH& ph = h.pods[(size_t)p];
+    erase(c.pending, p);
+    ph.nodeName = h.nodes[(size_t)n].name;
+    ph.phase = "Running";
+    ph.provisionable = false;  // IsProvisionable: a bound pod (pkg/utils/pod/scheduling.go:28-34)
+    ph.notReady = false;
+    c.podBlock[(size_t)p] = (uint8_t)(((c.podBlock[(size_t)p] >> 1) & 1) * 3);
+    h.tab.pod_flags[(size_t)p] &= ~PF_PROVISIONABLE;
+    c.podNode[(size_t)p] = n;
+    if (!(ph.ownedByNode || ph.ownedByDaemonSet || ph.terminal || ph.deleting))  // node.go:32-53
+      c.nodePods[(size_t)n].push_back(p);
+    move(n, ph, -1);
+  }
+  bool pools = false;
+  for (int n : rm) {
+    Host::Node& hn = h.nodes[(size_t)n];
+    for (int p : c.nodePods[(size_t)n]) c.podNode[(size_t)p] = ks_cons::PN_GONE;
+    for (size_t p = 0; p < c.podNode.size(); p++)  // bound pods GetNodePods leaves out
+      if (c.podNode[p] == n) c.podNode[p] = ks_cons::PN_GONE;
+    c.nodePods[(size_t)n].clear();
+    c.nodeGone[(size_t)n] = 1;
+    rows.erase(n);
+    // the NodePool's remaining limits: its nodes' capacity is no longer subtracted (ks_host.cpp limits)
+    auto l = hn.labels.find(kPoolKey);
+    for (size_t q = 0; l != hn.labels.end() && q < h.pools.size(); q++) {
+      if (h.pools[q].name != l->second) continue;
+      for (auto& kv : h.pools[q].remaining) {
+        auto cap = hn.capacity.find(kv.first);
+        if (cap == hn.capacity.end()) continue;
+        kv.second.n += cap->second.n;
+        auto id = h.resId.find(kv.first);
+        if (id != h.resId.end()) h.tab.pool_rem0[q * (size_t)R + (size_t)id->second] = h.toDev(id->second, kv.second);
+      }
+      pools = true;
+    }
+    int64_t* row = &h.tab.n_avail[(size_t)n * R];
+    row[0] = -1;  // Fits fails on any negative total: no pod lands on a removed node
+  }
+  for (int n : rows) {
+    int64_t* row = &h.tab.n_avail[(size_t)n * R];
+    for (int r = 0; r < R; r++) row[r] = 0;
+    for (const auto& kv : h.nodes[(size_t)n].available) {
+      auto id = h.resId.find(kv.first);
+      if (id != h.resId.end()) row[id->second] = h.toDev(id->second, kv.second);
+    }
+  }
+  order_candidates(c);
+  c.updates++;
+  if (!device) return;
+  // the changed device tables (a few hundred KB at most; the problem itself stays resident)
+  c.free_launch();
+  KsDev& D = pb.dev;
+  if (!rows.empty() || !rm.empty())
+    HIPCHK(hipMemcpyAsync((void*)D.n_avail, h.tab.n_avail.data(), 8 * h.tab.n_avail.size(), hipMemcpyHostToDevice,
+                          pb.stream));
+  if (!bind.empty())
+    HIPCHK(hipMemcpyAsync((void*)D.pod_flags, h.tab.pod_flags.data(), 4 * h.tab.pod_flags.size(),
+                          hipMemcpyHostToDevice, pb.stream));
+  if (pools)
+    HIPCHK(hipMemcpyAsync((void*)D.pool_rem0, h.tab.pool_rem0.data(), 8 * h.tab.pool_rem0.size(),
+                          hipMemcpyHostToDevice, pb.stream));
+  HIPCHK(hipStreamSynchronize(pb.stream));
+}
+
+// Host-only description of a handle: the pass's candidates, the pending pods, the simulation plan and the
+// active nodes' encoded rows (ks_cons_inspect, ks_cons_inspect_update).
+std::string inspect_json(const ks_cons& c, bool nodes) {
+  std::string o = "{\"candidates\":[";
+  for (size_t i = 0; i < (size_t)c.nPass; i++) {
+    if (i) o += ",";
+    o += "{\"name\":";
+    ksjson::quote(o, c.cands[i].name);
+    char buf[96];
+    snprintf(buf, sizeof buf, ",\"disruptionCost\":%.17g,\"pods\":%zu}", c.cands[i].cost, c.cands[i].pods.size());
+    o += buf;
+  }
+  // the pending pods every simulation schedules, as encoded (name + device request vector)
+  const Host& h = c.pb->host;
+  o += "],\"pendingPods\":[";
+  for (size_t i = 0; i < c.pending.size(); i++) {
+    const int p = c.pending[i];
+    o += i ? ",{\"name\":" : "{\"name\":";
+    ksjson::quote(o, h.pods[(size_t)p].name);
+    o += ",\"requests\":[";
+    for (int r = 0; r < h.dims.R; r++)
+      o += (r ? "," : "") + std::to_string(h.tab.pod_req[(size_t)p * h.dims.R + r]);
+    o += "]}";
+  }
+  o += "],\"resources\":[";
+  for (int r = 0; r < h.dims.R; r++) {
+    if (r) o += ",";
+    ksjson::quote(o, h.resNames[(size_t)r]);
+  }
+  o += "]";
+  if (nodes) {
+    // per active node: available and the pods GetNodePods yields (by name, in order); per pool: limits left
+    o += ",\"nodeRows\":{";
+    bool first = true;
+    for (size_t n = 0; n < h.nodes.size(); n++) {
+      if (c.nodeGone[n]) continue;
+      o += first ? "" : ",";
+      first = false;
+      ksjson::quote(o, h.nodes[n].name);
+      o += ":{\"available\":[";
+      for (int r = 0; r < h.dims.R; r++) o += (r ? "," : "") + std::to_string(h.tab.n_avail[n * (size_t)h.dims.R + r]);
+      o += "],\"pods\":[";
+      for (size_t i = 0; i < c.nodePods[n].size(); i++) {
+        o += i ? "," : "";
+        ksjson::quote(o, h.pods[(size_t)c.nodePods[n][i]].name);
+      }
+      o += "]}";
+    }
+    o += "},\"poolRemaining\":[";
+    for (size_t i = 0; i < h.tab.pool_rem0.size(); i++) o += (i ? "," : "") + std::to_string(h.tab.pool_rem0[i]);
+    o += "]";
+  }
+  o += ",\"sims\":" + std::to_string(c.sims.size()) + ",\"multiPrefixes\":" + std::to_string(c.multiHi) +
+       ",\"recordBytes\":" + std::to_string(4 * c.recWords) + ",\"pods\":" + std::to_string(h.dims.P) +
+       ",\"nodes\":" + std::to_string(h.dims.N) + ",\"groups\":" + std::to_string(h.dims.G) +
+       ",\"groupsOwned\":" + std::to_string(h.dims.G1) + "}";
+  return o;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1157,11 +1495,13 @@ extern "C++" {
 namespace ks {
 template <class A> void io(A& a, ks_cons::Cand& x) { io_all(a, x.node, x.name, x.pool, x.ct, x.zone, x.it, x.cost, x.pods); }
 template <class A> void io(A& a, ks_cons::Sim& x) { io_all(a, x.cands, x.multi); }
+template <class A> void io(A& a, ks_cons::CandIn& x) { io_all(a, x.k, x.remaining, x.passOk); }
 }  // namespace ks
 namespace {
-constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '1'};
+constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '2'};
 template <class A> void cons_io(A& a, ks_cons& c) {
-  io_all(a, c.cands, c.nPass, c.sims, c.multiHi, c.pending, c.deleting, c.nominated, c.hostnameSeed, c.recWords);
+  io_all(a, c.cands, c.nPass, c.sims, c.multiHi, c.pending, c.deleting, c.nominated, c.hostnameSeed, c.recWords,
+         c.candIn, c.nodePods, c.podNode, c.podBlock, c.podCost, c.nodeGone, c.updates);
 }
 // The loaded plan's indices must lie inside the loaded model (host_check covers the model itself).
 void cons_check(const ks_cons& c) {
@@ -1182,6 +1522,16 @@ void cons_check(const ks_cons& c) {
   for (const std::vector<int>* v : {&c.pending, &c.deleting})
     for (int p : *v)
       if (p < 0 || p >= P) bad("pending / deleting pod");
+  if ((int)c.nodePods.size() != N || (int)c.nodeGone.size() != N || (int)c.podNode.size() != P ||
+      (int)c.podBlock.size() != P || (int)c.podCost.size() != P)
+    bad("update state sizes");
+  for (auto& ci : c.candIn)
+    if (ci.k.node < 0 || ci.k.node >= N || ci.k.it < 0 || ci.k.it >= h.dims.T) bad("candidate input node");
+  for (auto& v : c.nodePods)
+    for (int p : v)
+      if (p < 0 || p >= P) bad("node pod");
+  for (int32_t w : c.podNode)
+    if (w < ks_cons::PN_GONE || w >= N) bad("pod placement");
 }
 }  // namespace
 }  // extern "C++"
@@ -1234,37 +1584,37 @@ int ks_cons_inspect(const char* json, size_t len, char** out) {
   pt.mark("build_cons");
   root = ksjson::Value();
   pt.mark("json free");
-  std::string o = "{\"candidates\":[";
-  for (size_t i = 0; i < (size_t)c.nPass; i++) {
-    if (i) o += ",";
-    o += "{\"name\":";
-    ksjson::quote(o, c.cands[i].name);
-    char buf[96];
-    snprintf(buf, sizeof buf, ",\"disruptionCost\":%.17g,\"pods\":%zu}", c.cands[i].cost, c.cands[i].pods.size());
-    o += buf;
+  *out = strdup(inspect_json(c, false).c_str());
+  return KS_OK;
+  API_CATCH
+}
+
+// Host-only: a snapshot with an update applied (ks_cons_update's host half), described with the active
+// nodes' rows, to compare against the snapshot the update leads to.
+int ks_cons_inspect_update(const char* json, size_t len, const char* update_json, size_t ulen, char** out) {
+  API_TRY
+  if (!json || !update_json || !out) throw KsError(KS_ERR_ARG, "null argument");
+  ksjson::Value root = ksjson::Parser(json, len ? len : strlen(json)).parse();
+  ks_cons c;
+  build_cons(c, root);
+  root = ksjson::Value();
+  const ksjson::Value delta = ksjson::Parser(update_json, ulen ? ulen : strlen(update_json)).parse();
+  if (delta.kind == ksjson::Value::Arr) {  // a sequence of updates
+    for (const ksjson::Value& u : delta.arr()) apply_update(c, u, false);
+  } else if (!(delta.is_obj() && delta.obj().empty())) {
+    apply_update(c, delta, false);
   }
-  // the pending pods every simulation schedules, as encoded (name + device request vector)
-  const Host& h = c.pb->host;
-  o += "],\"pendingPods\":[";
-  for (size_t i = 0; i < c.pending.size(); i++) {
-    const int p = c.pending[i];
-    o += i ? ",{\"name\":" : "{\"name\":";
-    ksjson::quote(o, h.pods[(size_t)p].name);
-    o += ",\"requests\":[";
-    for (int r = 0; r < h.dims.R; r++)
-      o += (r ? "," : "") + std::to_string(h.tab.pod_req[(size_t)p * h.dims.R + r]);
-    o += "]}";
-  }
-  o += "],\"resources\":[";
-  for (int r = 0; r < h.dims.R; r++) {
-    if (r) o += ",";
-    ksjson::quote(o, h.resNames[(size_t)r]);
-  }
-  o += "],\"sims\":" + std::to_string(c.sims.size()) + ",\"multiPrefixes\":" + std::to_string(c.multiHi) +
-       ",\"recordBytes\":" + std::to_string(4 * c.recWords) + ",\"pods\":" + std::to_string(c.pb->host.dims.P) +
-       ",\"nodes\":" + std::to_string(c.pb->host.dims.N) + ",\"groups\":" + std::to_string(c.pb->host.dims.G) +
-       ",\"groupsOwned\":" + std::to_string(c.pb->host.dims.G1) + "}";
-  *out = strdup(o.c_str());
+  *out = strdup(inspect_json(c, true).c_str());
+  return KS_OK;
+  API_CATCH
+}
+
+int ks_cons_update(ks_cons* c, const char* update_json, size_t len) {
+  API_TRY
+  if (!c || !update_json) throw KsError(KS_ERR_ARG, "null argument");
+  DeviceGuard guard(c->pb->device, nullptr);
+  const ksjson::Value delta = ksjson::Parser(update_json, len ? len : strlen(update_json)).parse();
+  apply_update(*c, delta, true);
   return KS_OK;
   API_CATCH
 }

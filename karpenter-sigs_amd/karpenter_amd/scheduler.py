@@ -346,6 +346,9 @@ def _cons_lib():
         l.ks_cons_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
         l.ks_cons_free.argtypes = [vp]
         l.ks_cons_inspect.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
+        l.ks_cons_inspect_update.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                             ctypes.POINTER(vp)]
+        l.ks_cons_update.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
         for f in ("ks_cons_num_candidates", "ks_cons_num_sims", "ks_cons_record_bytes"):
             getattr(l, f).argtypes = [vp]
         l.ks_cons_records_per_rank.argtypes = [vp, ctypes.c_int]
@@ -370,6 +373,16 @@ def inspect_consolidation(snapshot):
     b = _encode(snapshot)
     out = ctypes.c_void_p()
     _check(_cons_lib().ks_cons_inspect(b, len(b), ctypes.byref(out)))
+    return json.loads(_take_str(out))
+
+
+def inspect_consolidation_update(snapshot, update=None):
+    """Host-only: the snapshot with a ks_cons_update delta applied (None: as it is), with every active
+    node's encoded available row and pods and the pools' remaining limits ("nodeRows", "poolRemaining")."""
+    b = _encode(snapshot)
+    u = _encode(update if update is not None else {})
+    out = ctypes.c_void_p()
+    _check(_cons_lib().ks_cons_inspect_update(b, len(b), u, len(u), ctypes.byref(out)))
     return json.loads(_take_str(out))
 
 
@@ -410,6 +423,17 @@ class Consolidator:
 
     def records_per_rank(self, world=1):
         return _cons_lib().ks_cons_records_per_rank(self._h, world)
+
+    def update(self, delta):
+        """Cluster-state events since the snapshot or the last update (ks_cons_update):
+        {"deletePods": [uid], "bindPods": [{"uid", "node"}], "removeNodes": [name]}.  The next run()
+        simulates the updated cluster; the candidate and simulation counts are refreshed."""
+        l = _cons_lib()
+        b = _encode(delta)
+        _check(l.ks_cons_update(self._h, b, len(b)))
+        self.num_candidates = l.ks_cons_num_candidates(self._h)
+        self.num_sims = l.ks_cons_num_sims(self._h)
+        self._recbuf = None
 
     def run(self, rank=0, world=1, device=-1, out_ptr=None):
         """Run this rank's simulations.  out_ptr: device pointer for records_per_rank*record_bytes

@@ -1,0 +1,156 @@
+"""Incremental consolidation updates (ks_cons_update).
+
+Between two disruption passes the cluster changes: pods are deleted, pending pods get bound, nodes go away
+(state/cluster.go:220-512).  The reference re-reads the cluster and rebuilds its scheduler for every
+simulation (provisioner.go:204-296); the resident handle applies the events instead.  The check is always
+against a from-scratch build of the snapshot the events lead to (tests/cons_delta.apply_delta edits the
+JSON independently of the C++ update):
+  CPU: the host half (candidates, costs and order, pending pods, every active node's encoded available row
+       and pods, pool limits, simulation plan) equals the from-scratch encode after a sequence of deltas;
+       invalid deltas are refused whole; the binary snapshot of an updated handle round-trips.
+  GPU: after every delta of a sequence, a pass on the updated handle equals the oracle's consolidation of
+       the edited snapshot (every simulation's outcome and both commands), also through save/from_binary.
+"""
+import json
+
+import pytest
+
+from cons_delta import apply_delta, delta_sequence
+from karpenter_amd import Consolidator, KsError, inspect_consolidation_update, synth
+from oracle import bridge
+
+SEEDS = [1, 2, 3, 4]
+
+
+def _snap(seed, n_nodes=40, pods_per_node=5, n_pending=8, pdbs=True):
+    return synth.cluster_snapshot(n_nodes=n_nodes, pods_per_node=pods_per_node, n_its=40, seed=seed,
+                                  n_pending=n_pending, pdbs=pdbs, limits={"cpu": "2000"} if seed % 2 else None)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_update_sequence_host_state(seed):
+    snap = _snap(seed)
+    deltas, final = delta_sequence(seed, snap, steps=4)
+    got = inspect_consolidation_update(json.dumps(snap), deltas)
+    want = inspect_consolidation_update(json.dumps(final))
+    for k in ("candidates", "pendingPods", "nodeRows", "poolRemaining", "sims", "multiPrefixes", "resources"):
+        assert got[k] == want[k], k
+    # the deltas did move the state
+    before = inspect_consolidation_update(json.dumps(snap))
+    assert before["nodeRows"] != got["nodeRows"] and before["pendingPods"] != got["pendingPods"]
+
+
+def test_update_each_kind_alone():
+    snap = _snap(7)
+    node = snap["stateNodes"][3]
+    pend = snap["pendingPods"][0]["metadata"]["uid"]
+    for d in ({"deletePods": [node["pods"][0]["metadata"]["uid"]]},
+              {"deletePods": [pend]},
+              {"bindPods": [{"uid": pend, "node": node["name"]}]},
+              {"removeNodes": [node["name"]]},
+              {"removeNodes": [snap["stateNodes"][0]["name"], snap["stateNodes"][-1]["name"]]}):
+        got = inspect_consolidation_update(json.dumps(snap), d)
+        want = inspect_consolidation_update(json.dumps(apply_delta(snap, d)))
+        for k in ("candidates", "pendingPods", "nodeRows", "poolRemaining", "sims"):
+            assert got[k] == want[k], (d, k)
+
+
+def test_bind_unblocks_and_blocks():
+    # a do-not-disrupt pending pod bound to a candidate takes that candidate out of the pass
+    snap = _snap(8, pdbs=False)
+    p = snap["pendingPods"][0]
+    p["metadata"]["annotations"] = {"karpenter.sh/do-not-disrupt": "true"}
+    target = snap["stateNodes"][5]["name"]
+    d = {"bindPods": [{"uid": p["metadata"]["uid"], "node": target}]}
+    got = inspect_consolidation_update(json.dumps(snap), d)
+    assert target not in [c["name"] for c in got["candidates"]]
+    assert got["candidates"] == inspect_consolidation_update(json.dumps(apply_delta(snap, d)))["candidates"]
+    # deleting it again brings the candidate back
+    d2 = {"deletePods": [p["metadata"]["uid"]]}
+    got2 = inspect_consolidation_update(json.dumps(snap), [d, d2])
+    assert target in [c["name"] for c in got2["candidates"]]
+
+
+@pytest.mark.parametrize("bad,code", [
+    ({"deletePods": ["no-such-pod"]}, "KS_ERR_ARG"),
+    ({"bindPods": [{"uid": "pod-uid-000000", "node": "node-00001"}]}, "KS_ERR_ARG"),  # bound, not pending
+    ({"removeNodes": ["node-99999"]}, "KS_ERR_ARG"),
+    ({"removeNodes": ["node-00001", "node-00001"]}, "KS_ERR_ARG"),
+    ({"deletePods": ["pod-uid-000000", "pod-uid-000000"]}, "KS_ERR_ARG"),
+    ({"evictPods": []}, "KS_ERR_PARSE"),
+])
+def test_invalid_updates_are_refused(bad, code):
+    snap = _snap(9)
+    with pytest.raises(KsError) as e:
+        inspect_consolidation_update(json.dumps(snap), bad)
+    assert code in str(e.value)
+    # a sequence stops at the refused delta
+    with pytest.raises(KsError):
+        inspect_consolidation_update(json.dumps(snap), [{"deletePods": ["pod-uid-000001"]}, bad])
+
+
+def test_topology_cluster_refused():
+    snap = synth.cluster_snapshot(n_nodes=10, pods_per_node=4, n_its=40, seed=3, n_pending=2, topology=3)
+    with pytest.raises(KsError):
+        inspect_consolidation_update(json.dumps(snap), {"deletePods": [snap["stateNodes"][0]["pods"][0]["metadata"]["uid"]]})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_update_sequence_gpu_parity(seed):
+    snap = _snap(seed)
+    deltas, _ = delta_sequence(seed, snap, steps=4)
+    c = Consolidator(json.dumps(snap))
+    # all or nothing: a refused delta (its first events valid) leaves the handle as it was
+    with pytest.raises(KsError):
+        c.update({"deletePods": [deltas[0]["deletePods"][0]], "removeNodes": ["node-99999"]})
+    want, _ = bridge.consolidate(json.dumps(snap), all_sims=True)
+    got = c.consolidate(all_sims=True)
+    got.pop("kernel_ms")
+    assert got == want
+    cur = snap
+    for i, d in enumerate(deltas):
+        c.update(d)
+        cur = apply_delta(cur, d)
+        want, _ = bridge.consolidate(json.dumps(cur), all_sims=True)
+        got = c.consolidate(all_sims=True)
+        got.pop("kernel_ms")
+        assert got == want, (seed, i)
+    # the updated handle's binary snapshot is the updated cluster
+    c2 = Consolidator.from_binary(c.save())
+    got = c2.consolidate(all_sims=True)
+    got.pop("kernel_ms")
+    assert got == want
+    # and updates continue from a loaded handle
+    d, _ = delta_sequence(seed + 100, cur, steps=1)
+    c2.update(d[0])
+    want, _ = bridge.consolidate(json.dumps(apply_delta(cur, d[0])), all_sims=True)
+    got = c2.consolidate(all_sims=True)
+    got.pop("kernel_ms")
+    assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11, 12])
+def test_update_then_validate_gpu(seed):
+    """Validation after the wait (validation.go:68-180) against an updated handle == the oracle's
+    validation against the edited snapshot, for the pass's commands and single-node replacements."""
+    snap = _snap(seed)
+    c = Consolidator(json.dumps(snap))
+    doc = c.consolidate(all_sims=True)
+    cmds = [doc["multi"]["command"], doc["single"]["command"]]
+    for sim in doc["single"]["sims"][:6]:
+        cmd = {"action": "replace", "candidates": sim["candidates"]}
+        if sim.get("claim0"):
+            cmd["replacement"] = {"instanceTypeOptions": sim["claim0"]["instanceTypeOptions"][:5]}
+        cmds.append(cmd)
+    deltas, cur = delta_sequence(seed, snap, steps=2, n_rm=2)
+    for d in deltas:
+        c.update(d)
+    reasons = set()
+    for cmd in cmds:
+        want = bridge.validate(cur, cmd)
+        got = c.validate(cmd)
+        assert got == want, cmd
+        reasons.add(got["reason"])
+    assert len(reasons) >= 2
