@@ -124,7 +124,7 @@ struct ks_results {
     int tpl;
     int64_t host;
     std::vector<int32_t> pods, its;
-    std::string json;
+    std::vector<uint32_t> rec;  // the NodeClaim's requirement record (RSW words)
     // structured accessors (ks_results_nodeclaim_requests / _requirements); the pointer arrays point
     // into the string vectors, rebuilt by bind() after every move
     std::vector<std::string> reqNames, reqQty;
@@ -135,14 +135,20 @@ struct ks_results {
       int hasGt = 0, hasLt = 0;
       int64_t gt = 0, lt = 0;
     };
-    std::vector<Req> reqs;
-    std::vector<std::vector<const char*>> reqValP;
-    std::vector<ks_requirement> reqC;
+    // Rendered on first use (finish_claim): the requirement list, the JSON text (requirementsString, the
+    // launch list) -- a caller reading only pods and options pays for none of it
+    mutable bool finished = false;
+    mutable std::string json;
+    mutable std::vector<Req> reqs;
+    mutable std::vector<std::vector<const char*>> reqValP;
+    mutable std::vector<ks_requirement> reqC;
     void bind() {
       reqNameP.clear();
       reqQtyP.clear();
       for (auto& x : reqNames) reqNameP.push_back(x.c_str());
       for (auto& x : reqQty) reqQtyP.push_back(x.c_str());
+    }
+    void bind_reqs() const {
       reqValP.assign(reqs.size(), {});
       reqC.clear();
       for (size_t i = 0; i < reqs.size(); i++) {
@@ -152,6 +158,10 @@ struct ks_results {
       }
     }
   };
+  ks_problem* pb = nullptr;  // a reference on the problem the lazy rendering reads (ks_problem_free defers)
+  ~ks_results() {
+    if (pb && --pb->refs == 0) delete pb;
+  }
   struct ENode {
     int index;
     std::string name;
@@ -494,6 +504,94 @@ static void replay_check(const Host& h, int nc, int nl, const std::vector<int32_
   }
 }
 
+// The rendered half of a NodeClaim result (first use): Requirements after FinalizeScheduling, the JSON text.
+static void finish_claim(const Host& h, const ks_results::Claim& cl) {
+  if (cl.finished) return;
+  const KsDims& d = h.dims;
+  const Host::Tpl& tp = h.tpls[(size_t)cl.tpl];
+  const uint32_t* rec = cl.rec.data();
+  std::string j = "{\"nodePoolName\":";
+  ksjson::quote(j, tp.pool);
+  j += ",\"hostname\":";
+  ksjson::quote(j, h.placeholder(cl.host));
+  j += ",\"pods\":[";
+  for (size_t i = 0; i < cl.pods.size(); i++) j += (i ? "," : "") + std::to_string(cl.pods[i]);
+  j += "],\"instanceTypeOptions\":[";
+  for (size_t i = 0; i < cl.its.size(); i++) {
+    if (i) j += ",";
+    ksjson::quote(j, h.its[cl.its[i]].name);
+  }
+  j += "],\"requests\":{";
+  bool first = true;
+  for (size_t i = 0; i < cl.reqNames.size(); i++) {
+    if (!first) j += ",";
+    first = false;
+    ksjson::quote(j, cl.reqNames[i]);
+    j += ":";
+    ksjson::quote(j, cl.reqQty[i]);
+  }
+  j += "},\"requirements\":[";
+  first = true;
+  uint64_t pr = rs_present(rec);
+  for (int kk = 0; kk < d.NK; kk++) {  // FinalizeScheduling drops the hostname requirement
+    if (!bit(pr, kk) || kk == h.hostKey) continue;
+    if (!first) j += ",";
+    first = false;
+    ksjson::quote(j, h.reqString(rec, kk, true, cl.host));
+    static const char* opn[] = {"In", "NotIn", "Exists", "DoesNotExist"};
+    ks_results::Claim::Req q;
+    q.key = h.keyNames[(size_t)kk];
+    const int op = rs_op(h.L, rec, kk);
+    q.op = opn[op];
+    if (op == OP_IN || op == OP_NOTIN) {
+      const KeyMeta& km = h.keys[(size_t)kk];
+      for (int b = 0; b < km.nv; b++)
+        if ((rec[h.L.HDR + km.off + (b >> 5)] >> (b & 31)) & 1u) q.values.push_back(h.values[(size_t)kk][(size_t)b]);
+      std::sort(q.values.begin(), q.values.end());
+    }
+    const KeyMeta& km = h.keys[(size_t)kk];
+    if (km.bslot >= 0) {
+      q.hasGt = bit(rs_hasgt(rec), kk) ? 1 : 0;
+      q.hasLt = bit(rs_haslt(rec), kk) ? 1 : 0;
+      if (q.hasGt) q.gt = rs_gt(rec, km.bslot);
+      if (q.hasLt) q.lt = rs_lt(rec, km.bslot);
+    }
+    cl.reqs.push_back(std::move(q));
+  }
+  j += "],\"requirementsString\":";
+  ksjson::quote(j, h.reqsString(rec, cl.host));
+  // NodeClaimTemplate.ToNodeClaim's launch list (nodeclaimtemplate.go:55-60): the options ordered by
+  // (cheapest available offering the claim's zone / capacity-type requirements allow, name)
+  // (OrderByPrice, types.go:62-79; Offerings.Requirements / Cheapest :147-166), first 100.
+  auto allows = [&](int key, const std::string& v) {  // Requirements.Get(key).Has(v); missing key = Exists
+    if (key < 0 || !bit(rs_present(rec), key)) return true;
+    auto id = h.valueId[(size_t)key].find(v);
+    if (id != h.valueId[(size_t)key].end()) return rs_member(h.L, rec, key, id->second);
+    return bit(rs_compl(rec), key);  // a value outside the universe: only a complement set holds it
+  };
+  std::vector<std::pair<double, std::string>> launch;
+  for (int it : cl.its) {
+    double price = std::numeric_limits<double>::max();
+    bool any = false;
+    for (auto& of : h.its[(size_t)it].all) {
+      if (!of.available || !allows(h.zoneKey, of.zone) || !allows(h.ctKey, of.ct)) continue;
+      if (!any || of.price < price) price = of.price;
+      any = true;
+    }
+    launch.push_back({price, h.its[(size_t)it].name});
+  }
+  std::sort(launch.begin(), launch.end());
+  j += ",\"launchInstanceTypes\":[";
+  for (size_t i = 0; i < launch.size() && i < 100; i++) {
+    if (i) j += ",";
+    ksjson::quote(j, launch[i].second);
+  }
+  j += "]}";
+  cl.json = j;
+  cl.bind_reqs();
+  cl.finished = true;
+}
+
 // Rebuild Results from the replica-0 workspace.
 static ks_results* collect(ks_problem* pb, const KsWork& W) {
   Host& h = pb->host;
@@ -552,6 +650,8 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
 
   replay_check(h, nc, nl, order, ctpl, creq, crem, logp, logt);
   auto* res = new ks_results();
+  res->pb = pb;
+  pb->refs++;
   res->counters = ctr;
   res->algbytes = (double)ctr[CT_ALGBYTES];
   std::vector<std::vector<int32_t>> claimPods(nc), nodePods(d.N);
@@ -599,87 +699,11 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
       q.f = (QFmt)fmt[r];
       req.emplace_hint(req.end(), h.resNames[(size_t)r], q);  // resource ids are in name order
     }
-    const uint32_t* rec = &crs[(size_t)c * d.RSW];
-    std::string j = "{\"nodePoolName\":";
-    ksjson::quote(j, tp.pool);
-    j += ",\"hostname\":";
-    ksjson::quote(j, h.placeholder(cl.host));
-    j += ",\"pods\":[";
-    for (size_t i = 0; i < cl.pods.size(); i++) j += (i ? "," : "") + std::to_string(cl.pods[i]);
-    j += "],\"instanceTypeOptions\":[";
-    for (size_t i = 0; i < cl.its.size(); i++) {
-      if (i) j += ",";
-      ksjson::quote(j, h.its[cl.its[i]].name);
-    }
-    j += "],\"requests\":{";
-    bool first = true;
     for (auto& kv : req) {
-      if (!first) j += ",";
-      first = false;
-      ksjson::quote(j, kv.first);
-      j += ":";
-      ksjson::quote(j, qty_str(kv.second));
       cl.reqNames.push_back(kv.first);
       cl.reqQty.push_back(qty_str(kv.second));
     }
-    j += "},\"requirements\":[";
-    first = true;
-    uint64_t pr = rs_present(rec);
-    for (int kk = 0; kk < d.NK; kk++) {  // FinalizeScheduling drops the hostname requirement
-      if (!bit(pr, kk) || kk == h.hostKey) continue;
-      if (!first) j += ",";
-      first = false;
-      ksjson::quote(j, h.reqString(rec, kk, true, cl.host));
-      static const char* opn[] = {"In", "NotIn", "Exists", "DoesNotExist"};
-      ks_results::Claim::Req q;
-      q.key = h.keyNames[(size_t)kk];
-      const int op = rs_op(h.L, rec, kk);
-      q.op = opn[op];
-      if (op == OP_IN || op == OP_NOTIN) {
-        const KeyMeta& km = h.keys[(size_t)kk];
-        for (int b = 0; b < km.nv; b++)
-          if ((rec[h.L.HDR + km.off + (b >> 5)] >> (b & 31)) & 1u) q.values.push_back(h.values[(size_t)kk][(size_t)b]);
-        std::sort(q.values.begin(), q.values.end());
-      }
-      const KeyMeta& km = h.keys[(size_t)kk];
-      if (km.bslot >= 0) {
-        q.hasGt = bit(rs_hasgt(rec), kk) ? 1 : 0;
-        q.hasLt = bit(rs_haslt(rec), kk) ? 1 : 0;
-        if (q.hasGt) q.gt = rs_gt(rec, km.bslot);
-        if (q.hasLt) q.lt = rs_lt(rec, km.bslot);
-      }
-      cl.reqs.push_back(std::move(q));
-    }
-    j += "],\"requirementsString\":";
-    ksjson::quote(j, h.reqsString(rec, cl.host));
-    // NodeClaimTemplate.ToNodeClaim's launch list (nodeclaimtemplate.go:55-60): the options ordered by
-    // (cheapest available offering the claim's zone / capacity-type requirements allow, name)
-    // (OrderByPrice, types.go:62-79; Offerings.Requirements / Cheapest :147-166), first 100.
-    auto allows = [&](int key, const std::string& v) {  // Requirements.Get(key).Has(v); missing key = Exists
-      if (key < 0 || !bit(rs_present(rec), key)) return true;
-      auto id = h.valueId[(size_t)key].find(v);
-      if (id != h.valueId[(size_t)key].end()) return rs_member(h.L, rec, key, id->second);
-      return bit(rs_compl(rec), key);  // a value outside the universe: only a complement set holds it
-    };
-    std::vector<std::pair<double, std::string>> launch;
-    for (int it : cl.its) {
-      double price = std::numeric_limits<double>::max();
-      bool any = false;
-      for (auto& of : h.its[(size_t)it].all) {
-        if (!of.available || !allows(h.zoneKey, of.zone) || !allows(h.ctKey, of.ct)) continue;
-        if (!any || of.price < price) price = of.price;
-        any = true;
-      }
-      launch.push_back({price, h.its[(size_t)it].name});
-    }
-    std::sort(launch.begin(), launch.end());
-    j += ",\"launchInstanceTypes\":[";
-    for (size_t i = 0; i < launch.size() && i < 100; i++) {
-      if (i) j += ",";
-      ksjson::quote(j, launch[i].second);
-    }
-    j += "]}";
-    cl.json = j;
+    cl.rec.assign(crs.begin() + (size_t)c * d.RSW, crs.begin() + (size_t)(c + 1) * d.RSW);
     res->claims.push_back(std::move(cl));
   }
   for (auto& c : res->claims) c.bind();  // after the last move of the claims vector
@@ -1011,7 +1035,10 @@ int ks_problem_inspect(const char* json, size_t len, char** out) {
   API_CATCH
 }
 
-void ks_problem_free(ks_problem* p) { delete p; }
+// A problem lives until its last Results is freed too (Results render lazily from it).
+void ks_problem_free(ks_problem* p) {
+  if (p && --p->refs == 0) delete p;
+}
 void ks_results_free(ks_results* r) { delete r; }
 
 int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
@@ -1117,7 +1144,10 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
 int ks_results_json(const ks_results* r, char** json_out) {
   API_TRY
   std::string o = "{\"newNodeClaims\":[";
-  for (size_t i = 0; i < r->claims.size(); i++) o += (i ? "," : "") + r->claims[i].json;
+  for (size_t i = 0; i < r->claims.size(); i++) {
+    finish_claim(r->pb->host, r->claims[i]);
+    o += (i ? "," : "") + r->claims[i].json;
+  }
   o += "],\"existingNodes\":[";
   // existing nodes are reported by name in calculateExistingNodeClaims order
   for (size_t i = 0; i < r->nodes.size(); i++) {
@@ -1170,6 +1200,7 @@ int ks_results_nodeclaim_requests(const ks_results* r, int i, int* n, const char
 int ks_results_nodeclaim_requirements(const ks_results* r, int i, int* n, const ks_requirement** reqs) {
   if (!r || i < 0 || i >= (int)r->claims.size()) return KS_ERR_ARG;
   const auto& c = r->claims[(size_t)i];
+  finish_claim(r->pb->host, c);
   if (n) *n = (int)c.reqC.size();
   if (reqs) *reqs = c.reqC.data();
   return KS_OK;

@@ -219,6 +219,10 @@ struct ks_cons {
   std::vector<uint8_t> nodeGone;           // [host node] removed by an update
   std::unordered_map<std::string, int> uidIndex, nodeIndex;  // built at the first update
   int64_t updates = 0;
+  // per host node, for the per-simulation limits (prepare_launch): the NodePools it counts against and its
+  // capacity in device units (static for the handle; built on first use)
+  std::vector<std::vector<int>> nodePoolIdx;
+  std::vector<int64_t> nodeCapDev;
 
   // A launch of one rank's simulations, cached per (rank, world).  Validation runs its one
   // re-simulation in a launch of its own, so the pass's launch (records, requirement records,
@@ -240,6 +244,7 @@ struct ks_cons {
     void* ltemp = nullptr;
     size_t ltempBytes = 0;
     int lnent = 0, lrbits = 0, lsbits = 0;
+    int lnmw = 0;  // the plan's first lnmw simulations (the long multi-node prefixes) run on 4-wave workgroups
     bool lsorted = false;  // lpodmap holds every simulation's NewQueue order (a plan's pods never change)
     Plan lplan{};
     std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
@@ -257,13 +262,15 @@ struct ks_cons {
       lrank = lworld = -1;
       lsims.clear();
       lhost.clear();
-      lnent = lrbits = lsbits = 0;
+      lnent = lrbits = lsbits = lnmw = 0;
       lsorted = false;
       lplan = Plan{};
     }
   };
   Launch L;
   hipEvent_t ev[2] = {nullptr, nullptr};  // run_sims' timing events
+  hipStream_t st2 = nullptr;               // the multi-wave launch's stream (launch_sims_split)
+  hipEvent_t evFork = nullptr, evJoin = nullptr;
   int32_t* rank = nullptr;  // global NewQueue rank of every pod
 
   int sim_of_multi(int mid) const { return multiHi - mid; }  // mid in [1, multiHi]
@@ -281,6 +288,9 @@ struct ks_cons {
     if (rank) (void)hipFree(rank);
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {evFork, evJoin})
+      if (e) (void)hipEventDestroy(e);
+    if (st2) (void)hipStreamDestroy(st2);
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
@@ -761,6 +771,24 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   }
   std::vector<char> nameSeen(itName.size(), 0), nameHas(itName.size(), 0);
   std::vector<double> nameBest(itName.size(), 0.0);
+  // per candidate: its offering's price (Offerings.Get(ct, zone), first match) and capacity type
+  std::vector<double> candPrice(c.cands.size(), 0.0);
+  std::vector<char> candPriceOk(c.cands.size(), 0), candSpot(c.cands.size(), 0);
+  for (size_t i = 0; i < c.cands.size(); i++) {
+    const ks_cons::Cand& k = c.cands[i];
+    candPriceOk[i] = offering_price(h.its[(size_t)k.it], k.ct, k.zone, candPrice[i]) ? 1 : 0;
+    candSpot[i] = k.ct == "spot" ? 1 : 0;
+  }
+  if (c.nodePoolIdx.size() != h.nodes.size()) {
+    c.nodePoolIdx.assign(h.nodes.size(), {});
+    c.nodeCapDev.assign(h.nodes.size() * (size_t)R, 0);
+    for (size_t n = 0; n < h.nodes.size(); n++) {
+      auto l = h.nodes[n].labels.find(kPoolKey);
+      for (int p = 0; l != h.nodes[n].labels.end() && p < d.NPOOL; p++)
+        if (l->second == h.pools[(size_t)p].name) c.nodePoolIdx[n].push_back(p);
+      for (int r = 0; r < R; r++) c.nodeCapDev[n * (size_t)R + r] = nodeCap((int)n, r);
+    }
+  }
   std::vector<KsWork> works(ns);
   for (int k = 0; k < ns; k++) {
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
@@ -769,30 +797,25 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     for (int ci : sm.cands) rm.push_back(c.cands[(size_t)ci].node);
     std::sort(rm.begin(), rm.end());
     memcpy(stage.data() + o.rm, rm.data(), 4 * rm.size());
-    std::vector<int64_t> pool0(h.tab.pool_rem0.begin(), h.tab.pool_rem0.begin() + (size_t)NP * R);
-    for (int p = 0; p < d.NPOOL; p++)
-      for (int node : rm) {
-        auto l = h.nodes[(size_t)node].labels.find(kPoolKey);
-        if (l == h.nodes[(size_t)node].labels.end() || l->second != h.pools[(size_t)p].name) continue;
+    int64_t* pool0 = (int64_t*)(stage.data() + o.pool0);
+    std::copy(h.tab.pool_rem0.begin(), h.tab.pool_rem0.begin() + (size_t)NP * R, pool0);
+    for (int node : rm)
+      for (int p : c.nodePoolIdx[(size_t)node])
         for (int r = 0; r < R; r++)
-          if ((h.tab.pool_mask[(size_t)p] >> r) & 1u) pool0[(size_t)p * R + r] += nodeCap(node, r);
-      }
-    memcpy(stage.data() + o.pool0, pool0.data(), 8 * pool0.size());
+          if ((h.tab.pool_mask[(size_t)p] >> r) & 1u) pool0[(size_t)p * R + r] += c.nodeCapDev[(size_t)node * R + r];
     KsWork w{};
     // getCandidatePrices (consolidation.go:197-207): float64 sum in candidate order
     double price = 0;
     int cflags = 0;
     bool allSpot = true;
     for (int ci : sm.cands) {
-      const ks_cons::Cand& k = c.cands[(size_t)ci];
-      double pr;
-      if (!offering_price(h.its[(size_t)k.it], k.ct, k.zone, pr)) {
+      if (!candPriceOk[(size_t)ci]) {
         cflags |= CF_PRICE_ERR;
         break;
       }
-      price += pr;
+      price += candPrice[(size_t)ci];
     }
-    for (int ci : sm.cands) allSpot = allSpot && c.cands[(size_t)ci].ct == "spot";
+    for (int ci : sm.cands) allSpot = allSpot && candSpot[(size_t)ci];
     if (allSpot) cflags |= CF_ALL_SPOT;
     if (sm.multi) {
       cflags |= CF_MULTI;
@@ -806,8 +829,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
           nameSeen[(size_t)id] = 1;
           touched.push_back(id);
         }
-        double pr;
-        if (!offering_price(h.its[(size_t)k.it], k.ct, k.zone, pr)) continue;
+        if (!candPriceOk[(size_t)ci]) continue;
+        const double pr = candPrice[(size_t)ci];
         const double cur = nameHas[(size_t)id] ? nameBest[(size_t)id] : std::numeric_limits<double>::max();
         if (pr < cur) {
           nameBest[(size_t)id] = pr;
@@ -891,6 +914,14 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   c.L.lplan = make_plan(dd, d.G ? 64 * 1024 : 40 * 1024, true);
   if (c.L.lplan.lds > 80 * 1024 || c.L.lplan.KO < 1) c.L.lplan = make_plan(dd, 160 * 1024 - 256, true);
   if (c.L.lplan.lds > 160 * 1024 || c.L.lplan.KO < 1) throw KsError(KS_ERR_CAPACITY, "simulation state does not fit in LDS");
+  // simulations of at least 256 pods (the multi-node prefixes lead the plan) get 4-wave workgroups
+  // (KS_SIM_MW=0 turns this off, for comparison; KS_SIM_MW_MIN sets the pod threshold, for tests)
+  const char* mwEnv = std::getenv("KS_SIM_MW");
+  const char* mwMinEnv = std::getenv("KS_SIM_MW_MIN");
+  const int mwMin = mwMinEnv ? std::max(1, std::atoi(mwMinEnv)) : 256;
+  c.L.lnmw = 0;
+  if (!(mwEnv && mwEnv[0] == '0') && sims_mw_supported(pb.dev, c.L.lplan))
+    while (c.L.lnmw < ns && simP[(size_t)c.L.lnmw] >= mwMin) c.L.lnmw++;
   c.L.lrank = rank;
   c.L.lworld = world;
   pt.mark("zero + upload + LDS plan");
@@ -1132,7 +1163,16 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
                            c.L.lnent, c.L.lrunw, c.L.lrunlen, pb.stream));
     c.L.lsorted = true;
   }
-  HIPCHK(launch_sims(pb.dev, c.L.lworks, ns, c.L.lplan, pb.stream));
+  if (c.L.lnmw > 0 && !c.st2) {
+    // the long simulations' stream at the highest priority: their workgroups must be dispatched before the
+    // 5000 short ones fill the chip, or the pass becomes short ones + long chain instead of their max
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(hipStreamCreateWithPriority(&c.st2, hipStreamNonBlocking, greatest));
+    HIPCHK(hipEventCreateWithFlags(&c.evFork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c.evJoin, hipEventDisableTiming));
+  }
+  HIPCHK(launch_sims_split(pb.dev, c.L.lworks, ns, c.L.lnmw, c.L.lplan, pb.stream, c.st2, c.evFork, c.evJoin));
   HIPCHK(hipEventRecord(c.ev[1], pb.stream));
   // the records follow on the same stream; one synchronisation covers both
   const size_t bytes = 4 * (size_t)c.recWords * ns, all = 4 * (size_t)c.recWords * c.per_rank(world);
@@ -1236,6 +1276,7 @@ std::string validate_json(ks_cons& c, const Value& cmd) {
 // (order_candidates).  Refused (KS_ERR_UNSUPPORTED, nothing applied): clusters with topology groups or
 // volume limits (their counts are encoded per pod and node) and pods with host ports.
 void apply_update(ks_cons& c, const Value& delta, bool device) {
+  PhaseTimer pt("ks_cons_update");
   ks_problem& pb = *c.pb;
   Host& h = pb.host;
   const KsDims& d = h.dims;
@@ -1292,6 +1333,7 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     rm.push_back(n);
   }
 
+  pt.mark("validate");
   std::set<int> rows;  // node rows to re-derive
   auto move = [&](int n, const PodH& p, int sign) {  // StateNode.Available() after a pod leaves / lands
     Host::Node& hn = h.nodes[(size_t)n];
@@ -1366,11 +1408,14 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
       if (id != h.resId.end()) row[id->second] = h.toDev(id->second, kv.second);
     }
   }
+  pt.mark("apply");
   order_candidates(c);
+  pt.mark("order candidates + plan");
   c.updates++;
   if (!device) return;
-  // the changed device tables (a few hundred KB at most; the problem itself stays resident)
-  c.free_launch();
+  // the changed device tables (a few hundred KB at most; the problem itself stays resident); the next pass
+  // builds its plan into the previous plan's buffers
+  c.invalidate_launch();
   KsDev& D = pb.dev;
   if (!rows.empty() || !rm.empty())
     HIPCHK(hipMemcpyAsync((void*)D.n_avail, h.tab.n_avail.data(), 8 * h.tab.n_avail.size(), hipMemcpyHostToDevice,
@@ -1382,6 +1427,7 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     HIPCHK(hipMemcpyAsync((void*)D.pool_rem0, h.tab.pool_rem0.data(), 8 * h.tab.pool_rem0.size(),
                           hipMemcpyHostToDevice, pb.stream));
   HIPCHK(hipStreamSynchronize(pb.stream));
+  pt.mark("upload rows");
 }
 
 // Host-only description of a handle: the pass's candidates, the pending pods, the simulation plan and the

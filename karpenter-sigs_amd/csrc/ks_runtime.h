@@ -1,6 +1,7 @@
 // ks_runtime.h — internals shared by the C-ABI translation units (ks_capi.cpp: Solve,
 // ks_cons.cpp: consolidation): the resident problem, device arena helper and kernel launchers.
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime_api.h>
 
 #include <string>
@@ -14,6 +15,11 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
                         hipEvent_t mid, const int32_t* fixed_order = nullptr, hipEvent_t* feas = nullptr);
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st);
+// The first nmw simulations (the long multi-node prefixes) on 4-wave workgroups when the problem allows it
+// (sims_mw_supported: resource-only pods, no topology), concurrently with the rest.
+bool sims_mw_supported(const KsDev& D, const Plan& pl);
+hipError_t launch_sims_split(const KsDev& D, const KsWork* works_dev, int nsims, int nmw, const Plan& pl, hipStream_t st,
+                             hipStream_t st2, hipEvent_t fork, hipEvent_t join);
 Plan make_plan(const KsDims& d, size_t budget, bool sim = false, bool wideKO = false);
 size_t queue_sort_temp_bytes(int n);
 hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
@@ -46,6 +52,7 @@ void set_last_error(const std::string& m);
 
 // The encoded problem resident in HBM (ks_problem_create = NewScheduler).
 struct ks_problem {
+  std::atomic<int> refs{1};  // the handle + every ks_results that renders from it
   ks::Host host;
   ks::KsDev dev{};
   void* dbuf = nullptr;

@@ -118,18 +118,51 @@ __device__ __forceinline__ int wscan_max(int v) {  // values >= -1
   const int r2 = mx(r1, __builtin_amdgcn_readlane(v, 47)), l = lane();
   return mx(v, l >= 48 ? r2 : l >= 32 ? r1 : l >= 16 ? r0 : -1);
 }
-// How many more pods requesting `req` of a resource fit a node with `free` of it, capped at m (<= 64):
-// floor(free / req) from a float estimate (error < 1e-4 below m + 2) corrected exactly by one int64
-// multiply.  free < 0 (INT64_MIN marks a node that never fits) takes none.
+// Wave-wide reductions to a uniform value: DPP row_shr steps leave each 16-lane row's total in its lane 15,
+// four readlanes combine the rows (no LDS round trip, unlike a __shfl_xor butterfly: ds_bpermute per step).
+// Every lane must be active; `fill` is the operation's identity.
+template <int CTRL>
+__device__ __forceinline__ int dpp32(int old, int v) { return __builtin_amdgcn_update_dpp(old, v, CTRL, 0xf, 0xf, false); }
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp64(int64_t old, int64_t v) {
+  const int lo = dpp32<CTRL>((int)old, (int)v), hi = dpp32<CTRL>((int)(old >> 32), (int)(v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int CTRL> __device__ __forceinline__ int dppT(int old, int v) { return dpp32<CTRL>(old, v); }
+template <int CTRL> __device__ __forceinline__ uint32_t dppT(uint32_t old, uint32_t v) { return (uint32_t)dpp32<CTRL>((int)old, (int)v); }
+template <int CTRL> __device__ __forceinline__ int64_t dppT(int64_t old, int64_t v) { return dpp64<CTRL>(old, v); }
+template <int CTRL> __device__ __forceinline__ uint64_t dppT(uint64_t old, uint64_t v) { return (uint64_t)dpp64<CTRL>((int64_t)old, (int64_t)v); }
+__device__ __forceinline__ int rdlT(int x, int l) { return rdl(x, l); }
+__device__ __forceinline__ uint32_t rdlT(uint32_t x, int l) { return (uint32_t)rdl((int)x, l); }
+__device__ __forceinline__ int64_t rdlT(int64_t x, int l) { return rdl64(x, l); }
+__device__ __forceinline__ uint64_t rdlT(uint64_t x, int l) { return (uint64_t)rdl64((int64_t)x, l); }
+template <class T, class F>
+__device__ __forceinline__ T wred(T v, T fill, F op) {
+  v = op(v, dppT<0x111>(fill, v));  // row_shr:1
+  v = op(v, dppT<0x112>(fill, v));  // row_shr:2
+  v = op(v, dppT<0x114>(fill, v));  // row_shr:4
+  v = op(v, dppT<0x118>(fill, v));  // row_shr:8
+  return op(op(rdlT(v, 15), rdlT(v, 31)), op(rdlT(v, 47), rdlT(v, 63)));
+}
+template <class T> __device__ __forceinline__ T wred_min(T v, T fill) { return wred(v, fill, [](T a, T b) { return b < a ? b : a; }); }
+template <class T> __device__ __forceinline__ T wred_max(T v, T fill) { return wred(v, fill, [](T a, T b) { return b > a ? b : a; }); }
+template <class T> __device__ __forceinline__ T wred_add(T v) { return wred(v, (T)0, [](T a, T b) { return a + b; }); }
+// How many more pods requesting `req` of a resource fit a node with `free` of it, capped at m:
+// floor(free / req) from a float estimate (rq ~ 1 / req from v_rcp_f32; relative error ~1e-7, so the
+// estimate is within one of the quotient below m + 2 for any m < 10^6) corrected exactly by int64 multiplies.
+// free < 0 (INT64_MIN marks a node that never fits) takes none.  req is wave-uniform (its branches are
+// scalar); the per-lane part is branch-free: the estimate is clamped before the conversion and
+// the correction and the bounds are selects.  req == 1 (the pods resource) needs no division.
+__device__ __forceinline__ float run_rcp(int64_t req) { return req > 0 ? __builtin_amdgcn_rcpf((float)req) : 0.f; }
 __device__ __forceinline__ int run_cap(int64_t free, int64_t req, float rq, int m) {
   if (req == 0) return free >= 0 ? m : 0;
-  if (free < req) return 0;
-  const float q = (float)free * rq;
-  if (q >= (float)(m + 2)) return m;
-  int qi = (int)q;
-  if ((int64_t)qi * req > free) qi--;
-  else if ((int64_t)(qi + 1) * req <= free) qi++;
-  return qi < m ? qi : m;
+  if (req == 1) return free <= 0 ? 0 : (free < (int64_t)m ? (int)free : m);
+  const float q = fminf((float)free * rq, (float)(m + 2));
+  int qi = q > 0.f ? (int)q : 0;
+  qi -= (int64_t)qi * req > free ? 1 : 0;
+  qi += (int64_t)(qi + 1) * req <= free ? 1 : 0;
+  qi = qi < m ? qi : m;
+  return free >= req ? qi : 0;
 }
 
 // Contiguous HBM -> LDS copy by the wave with U loads in flight per lane before their stores (a prologue's
@@ -209,6 +242,7 @@ struct Window {
   int p, g, uid, s, flags, toltpl, pf, st;
   int rl;  // SIM, nothing pushed back yet: identical pods from this queue position to the end of their run
   uint64_t ll, tol0, tol1, hpc, hpu, hpo, vm;
+  uint64_t tsel, tinv, town, trss;  // TOPO: word 0 of the pod's selecting / inverse / owned group sets, st_rss keys
   int64_t req[RT > 0 ? RT : kMaxR];
 };
 
@@ -546,6 +580,7 @@ struct Solver {
   bool t_any = false;   // t_mask is not empty (any word)
   bool t_rec = false;   // t_sel | t_inv is not empty (any word): Topology.Record has groups to visit
   int t_s = 0;          // the popped pod's relaxation state
+  uint64_t t_rss = 0;   // keys the state's strict pod requirements name (rs_present of its st_rss row)
   const uint32_t KS_G* fnp = nullptr;  // k_feasibility_nodes's row of the popped pod's state (null: none)
   bool t_nonode = false;  // some matching group admits no domain at all: no existing node can pass
   uint64_t t_active = ~0ull;  // groups in t.topologies so far (late groups join at their relaxation), word 0
@@ -732,8 +767,7 @@ struct Solver {
   __device__ __forceinline__ int popc_words(LU32 w, int n) const {
     int c = 0;
     for (int i = lane(); i < n; i += kWave) c += __popc(w[i]);
-    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
-    return uni(c);
+    return wred_add(c);
   }
 
 
@@ -913,8 +947,13 @@ struct Solver {
     }
   }
   __device__ __forceinline__ int tccnt(int g, int claim) const { return ld_sc1(W.tg_ccnt + (int64_t)g * W.ccs + claim); }  // claim <= Kcap (a fresh claim at the cap)
-  __device__ __forceinline__ bool tpod_has(int g, int v) const {  // podDomains.Has (strict pod requirements)
-    return rs_member(L, D.st_rss + (int64_t)t_s * d.RSW, tg(g, TGM_KEY), v);
+  // podDomains.Has (strict pod requirements).  A key the pod's strict requirements do not name admits every value
+  // (Get() of a missing key is Exists), which is the common case: the row's presence mask (t_rss, read with the
+  // pop's other group words) answers it without a load.
+  __device__ __forceinline__ bool tpod_has(int g, int v) const {
+    const int k = tg(g, TGM_KEY);
+    if (!((t_rss >> k) & 1ull)) return true;
+    return rs_member(L, D.st_rss + (int64_t)t_s * d.RSW, k, v);
   }
   // Per pop: the matching groups (getMatchingTopologies, topology.go:366-379: owned groups, then
   // inverse groups whose selector selects the pod), domainMinCount per spread group (:192-213) and,
@@ -932,15 +971,18 @@ struct Solver {
   __device__ __forceinline__ bool sel_has(int g) const {  // the popped pod is selected by group g
     return ((gword(GS_SEL, g >> 6, t_sel) >> (g & 63)) & 1ull) != 0;
   }
-  __device__ __forceinline__ void topo_pop(int s, int gpod) {
+  // sel0 / inv0 / own0 / rss0: word 0 of the pod's group sets and its strict keys, gathered with the queue
+  // window (refill), so a pop's group evaluation starts without a memory round trip
+  __device__ __forceinline__ void topo_pop(int s, int gpod, uint64_t sel0, uint64_t inv0, uint64_t own0, uint64_t rss0) {
     t_s = s;
     const int GMW = d.GMW;
     const uint64_t KS_G* sel = D.pod_gsel + (int64_t)gpod * GMW;
     const uint64_t KS_G* inv = D.pod_ginv + (int64_t)gpod * GMW;
     const uint64_t KS_G* own = D.st_gown + (int64_t)s * GMW;
-    t_sel = sel[0];
-    t_inv = inv[0];
-    t_mask = own[0] | (t_sel & bits_below(d.G, 0) & ~bits_below(d.G1, 0));
+    t_sel = sel0;
+    t_inv = inv0;
+    t_rss = rss0;
+    t_mask = own0 | (t_sel & bits_below(d.G, 0) & ~bits_below(d.G1, 0));
     if (SIM) t_mask &= ~W.tdead[0];
     bool anyM = t_mask != 0, anyR = (t_sel | t_inv) != 0;
     if (GMW > 1) {  // words 1.. (more than 64 groups), one lane each, into LDS
@@ -1004,12 +1046,9 @@ struct Solver {
               mn = c < mn ? c : mn;
             }
           }
-          for (int off = 32; off >= 1; off >>= 1) {
-            const int o = __shfl_xor(mn, off), l = __shfl_xor(lo, off);
-            mn = o < mn ? o : mn;
-            lo = l < lo ? l : lo;
-            num += __shfl_xor(num, off);
-          }
+          mn = wred_min(mn, 0x7fffffff);
+          lo = wred_min(lo, 0x7fffffff);
+          num = wred_add(num);
           if (tg(g, TGM_MIND) >= 0 && num < tg(g, TGM_MIND)) mn = 0;
           const int self = sel_has(g) ? 1 : 0;
           if (lo == 0x7fffffff || (int64_t)lo + self - mn > tg(g, TGM_SKEW)) t_nonode = true;
@@ -1143,10 +1182,7 @@ struct Solver {
             best = key < best ? key : best;
           }
         });
-        for (int off = 32; off >= 1; off >>= 1) {
-          const uint64_t o = __shfl_xor(best, off);
-          best = o < best ? o : best;
-        }
+        best = wred_min(best, (uint64_t)~0ull);
         if (best == ~0ull) return FC_TOPO | ((uint32_t)g << 16);
         const int bv = (int)(uint32_t)best;
         if (lane() == 0) s_trs1[L.HDR + km.off + (bv >> 5)] = 1u << (bv & 31);
@@ -1170,11 +1206,8 @@ struct Solver {
             if (rs_member(L, s_trs0, k, v)) z1 = (uint32_t)v < z1 ? (uint32_t)v : z1;
             if (v >= nv) z2 = z2 == ~0u ? (uint32_t)v : z2;  // registered, so the options are not empty
           }
-          for (int off = 32; off >= 1; off >>= 1) {
-            const uint32_t a = __shfl_xor(z1, off), b = __shfl_xor(z2, off);
-            z1 = a < z1 ? a : z1;
-            z2 = b < z2 ? b : z2;
-          }
+          z1 = wred_min(z1, ~0u);
+          z2 = wred_min(z2, ~0u);
           if (z1 == ~0u && z2 == ~0u) return FC_TOPO | ((uint32_t)g << 16);
           if (lane() == 0) {
             if (z1 != ~0u) s_trs1[L.HDR + km.off + (z1 >> 5)] |= 1u << (z1 & 31);
@@ -1261,7 +1294,7 @@ struct Solver {
         if (ownedGroup && tg(g, TGM_TYPE) != TG_ANTI) {  // spread / affinity: only a collapsed domain
           int tot = 0;
           for (int wd = lane(); wd < km.nw; wd += kWave) tot += __popc(F[L.HDR + km.off + wd]);
-          for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off);
+          tot = wred_add(tot);
           if (bit(compl_, k) || tot != 1) continue;
         }
         bool any = false;
@@ -1513,10 +1546,7 @@ struct Solver {
             const int64_t a = alloc_pos(tb + q, r);
             m = a > m ? a : m;
           }
-        for (int off = 32; off >= 1; off >>= 1) {
-          const int64_t o = __shfl_xor(m, off);
-          m = o > m ? o : m;
-        }
+        m = wred_max(m, (int64_t)INT64_MIN);
       }
       m = rdl64(m, 0);  // lane 0's value, stored by every lane (claim state is written wave-wide, see commit_claim)
       v.max[(int64_t)c * R() + r] = m;
@@ -1584,7 +1614,7 @@ struct Solver {
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= d.R) break;
-      rq[r] = pod[r] > 0 ? 1.0f / (float)pod[r] : 0.f;
+      rq[r] = run_rcp(pod[r]);
       rc[r] = v.req[(int64_t)c * R() + r];
     }
     int best = 0;
@@ -1601,11 +1631,7 @@ struct Solver {
         best = cap > best ? cap : best;
       }
     }
-    for (int off = 32; off >= 1; off >>= 1) {
-      const int o = __shfl_xor(best, off);
-      best = o > best ? o : best;
-    }
-    return uni(best);
+    return wred_max(best, (int)0x80000000);
   }
   // Commit of k identical pods (podk = k x pod, claim_full already applied to it) to claim c at sorted
   // position pos: commit_claim's stores with the count advanced by k.  Returns whether s.newNodeClaims
@@ -1794,10 +1820,7 @@ struct Solver {
                       const int64_t v = D.it_cap[(int64_t)D.tpl_its[tb + pos] * R() + r];
                       m = v > m ? v : m;
                     }
-                  for (int off = 32; off >= 1; off >>= 1) {
-                    const int64_t o = __shfl_xor(m, off);
-                    m = o > m ? o : m;
-                  }
+                  m = wred_max(m, (int64_t)INT64_MIN);
                   s_pool[(int64_t)pool * R() + r] -= m;  // wave-wide (m is reduced over the wave)
                 }
                 wsync();
@@ -1809,6 +1832,34 @@ struct Solver {
       }
       W.fail_code[(int64_t)p * d.NTPL + t] = code;  // wave-wide stores of uniform values
       W.fail_host[(int64_t)p * d.NTPL + t] = hostid;
+    }
+    return 0;
+  }
+
+  // try_templates' NewNodeClaim calls for a pod every template fails on topology (simNoClaim): a template whose
+  // instance types all exceed its NodePool's remaining limits fails before NewNodeClaim (scheduler.go:262-268);
+  // every other one increments the hostname counter (nodeclaim.go:44-48).  Returns 0 (the pod is not placed).
+  __device__ __forceinline__ int sim_template_calls(int& hostCtr) const {
+    for (int t = 0; t < d.NTPL; t++) {
+      const int pool = D.tpl_pool[t];
+      bool call = pool < 0;
+      if (!call) {
+        const int tb = s_tbeg[t], nIT = s_tbeg[t + 1] - tb;
+        const uint32_t mask = D.pool_mask[pool];
+        uint64_t anyCand = 0;
+        for (int base = 0; base < nIT && !anyCand; base += kWave) {
+          const int pos = base + lane();
+          bool ok = pos < nIT;
+          if (ok) {
+            const int64_t KS_G* cap = D.it_cap + (int64_t)D.tpl_its[tb + pos] * R();
+            for (int r = 0; r < R(); r++)
+              ok = ok && !(((mask >> r) & 1u) && cap[r] > s_pool[(int64_t)pool * R() + r]);
+          }
+          anyCand = wballot(ok);
+        }
+        call = anyCand != 0;
+      }
+      if (call) hostCtr = uni(hostCtr + 1);
     }
     return 0;
   }
@@ -2228,8 +2279,7 @@ struct Solver {
       {
         int cc = 0;
         for (int i = lane(); i < TW; i += kWave) cc += __popc(inl ? lc.rem[(int64_t)c * TW + i] : gc.rem[(int64_t)c * TW + i]);
-        for (int off = 32; off >= 1; off >>= 1) cc += __shfl_xor(cc, off);
-        nopt = uni(cc);
+        nopt = wred_add(cc);
       }
       const bool spot = rs_member(L, crs, d.ctKey, d.spotBit), od = rs_member(L, crs, d.ctKey, d.odBit);
       flags |= (spot ? RB_HAS_SPOT : 0) | (od ? RB_HAS_OD : 0);
@@ -2338,6 +2388,12 @@ struct Solver {
       w.hpu = D.pod_hpu[w.g];
       w.hpo = D.pod_hpo[w.g];
       w.vm = D.pod_vm[w.g];
+      if (TOPO) {
+        w.tsel = D.pod_gsel[(int64_t)w.g * d.GMW];
+        w.tinv = D.pod_ginv[(int64_t)w.g * d.GMW];
+        w.town = D.st_gown[(int64_t)w.s * d.GMW];
+        w.trss = rs_present(D.st_rss + (int64_t)w.s * d.RSW);
+      }
 #pragma unroll
       for (int r = 0; r < RM; r++) {
         if (RT == 0 && r >= d.R) break;
@@ -2347,8 +2403,165 @@ struct Solver {
   }
 };
 
-template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_solve(KsDev D, const KsWork* works, Plan pl) {
+// --- Multi-wave simulations (MW) ------------------------------------------------------------------
+// A long simulation (a multi-node prefix re-schedules thousands of pods as one dependent chain) runs on a
+// 4-wave workgroup: wave 0 runs the simulation as the single-wave kernel does, and the register window's
+// 64-node blocks are spread over the waves (wave k holds nodes [64k, 64k + 64)).  The window steps of the
+// resource-only fast path are split by block: a run of identical pods computes each block's per-node
+// capacity and scan on its own wave, the blocks' totals meet in an LDS mailbox, and each wave commits its
+// block's shares; a single pod's first fit is one ballot per block.  Two workgroup barriers per step
+// (parameters posted / block results posted).  Everything else -- queue, node scan past the window,
+// NodeClaims, templates, relaxation, the decision -- stays on wave 0.  The helpers keep their
+// AllNonPendingPodsScheduled and algorithmic-byte contributions and hand them over at MW_EXIT.
+enum MwCmd : int { MW_RUN = 1, MW_FIT = 2, MW_EXIT = 3 };
+enum MwSlot : int {  // uint32 words of the mailbox (LDS, after the plan's dynamic LDS)
+  MB_CMD = 0, MB_SEQ = 1, MB_M = 2, MB_FPF = 3, MB_FT0 = 4, MB_FT1 = 6, MB_FP = 8,  // FP: 2 words per resource
+  MB_TOT = 40, MB_MASK = 48, MB_UMASK = 56, MB_ALL = 64, MB_AB = 72, MB_WORDS = 80
+};
+constexpr int kMwWaves = 4;
+constexpr size_t kMwBytes = 4 * MB_WORDS;
+__device__ __forceinline__ void mb_st64(LU32 mb, int i, uint64_t v) {
+  mb[i] = (uint32_t)v;
+  mb[i + 1] = (uint32_t)(v >> 32);
+}
+__device__ __forceinline__ uint64_t mb_ld64(LU32 mb, int i) { return (uint64_t)mb[i] | ((uint64_t)mb[i + 1] << 32); }
+__device__ __forceinline__ void mw_barrier() { __syncthreads(); }
+
+// One 64-node block of the register window, free capacity form (FREEW): as k_solve's window init.
+template <int RM>
+struct MwBlock {
+  uint64_t tx, ty;
+  int64_t av[RM];
+  int nf;
+};
+template <int RM>
+__device__ __forceinline__ void mw_block_init(MwBlock<RM>& b, const KsDev& D, LU32 s_rmv, int kb) {
+  const KsDims& d = D.d;
+  const int n = kb * kWave + lane(), c = n < d.N ? n : d.N - 1;
+  b.tx = D.n_taint[2 * c];
+  b.ty = D.n_taint[2 * c + 1];
+  bool never = n >= d.N || ((s_rmv[c >> 5] >> (c & 31)) & 1u) != 0;
+#pragma unroll
+  for (int r = 0; r < RM; r++) {
+    const int64_t a = D.n_avail[(int64_t)c * RM + r], q = D.n_req0[(int64_t)c * RM + r];
+    never |= a < 0;
+    b.av[r] = a - q;
+  }
+#pragma unroll
+  for (int r = 0; r < RM; r++) b.av[r] = never ? INT64_MIN : b.av[r];
+  b.nf = D.n_flags[c];
+}
+// A run of m identical pods: this lane's node capacity for it (as the single-wave run step).
+template <int RM>
+__device__ __forceinline__ int mw_run_cap(const MwBlock<RM>& b, int m, const int64_t* fp, const float* rq, uint64_t ft0,
+                                          uint64_t ft1) {
+  const bool tol = (((b.tx & ~ft0) | (b.ty & ~ft1)) == 0);
+  int cap = tol ? m : 0;
+#pragma unroll
+  for (int r = 0; r < RM; r++) {
+    const int c = run_cap(b.av[r], fp[r], rq[r], m);
+    cap = c < cap ? c : cap;
+  }
+  return cap;
+}
+// The lane's share of the run given the pods the blocks before this one take (base); branch-free.
+template <int RM>
+__device__ __forceinline__ int mw_run_commit(MwBlock<RM>& b, int base, int cap, int incl, int m, const int64_t* fp) {
+  const int p0 = base + incl - cap, room = m - p0;
+  const int tk = room <= 0 ? 0 : (cap < room ? cap : room);
+#pragma unroll
+  for (int r = 0; r < RM; r++) b.av[r] -= (int64_t)tk * fp[r];
+  return tk;
+}
+template <int RM>
+__device__ __forceinline__ bool mw_fits(const MwBlock<RM>& b, const int64_t* fp, uint64_t ft0, uint64_t ft1) {
+  bool ok = (((b.tx & ~ft0) | (b.ty & ~ft1)) == 0);
+#pragma unroll
+  for (int r = 0; r < RM; r++) ok &= fp[r] <= b.av[r];
+  return ok;
+}
+// The first block (in node order) whose ballot holds a fit: (block, its ballot), uniform; -1 if none.
+__device__ __forceinline__ int mw_first_fit(LU32 mb, uint64_t& mj) {
+  int kj = -1;
+  mj = 0;
+#pragma unroll
+  for (int q = 0; q < kMwWaves; q++) {
+    const uint64_t mq = mb_ld64(mb, MB_MASK + 2 * q);
+    const bool take = kj < 0 && mq != 0;
+    kj = take ? q : kj;
+    mj = take ? mq : mj;
+  }
+  mj = (uint64_t)uni64((int64_t)mj);
+  return uni(kj);
+}
+
+// Waves 1..3 of an MW simulation: their window block, the mailbox loop, then their contributions.
+template <int RM>
+__device__ void mw_helper(const KsDev& D, const KsWork& W, LU32 s_rmv, LU32 mb, int k) {
+  const int R = D.d.R;
+  mw_barrier();  // B0a: wave 0's prologue (the removed-node mask) is in LDS
+  MwBlock<RM> b;
+  mw_block_init<RM>(b, D, s_rmv, k);
+  mb_st64(mb, MB_UMASK + 2 * k, wballot(b.nf & NF_UNUSABLE));  // wave-wide store of a uniform value
+  mw_barrier();  // B0b
+  bool winUnusable = false;
+#pragma unroll
+  for (int q = 0; q < kMwWaves; q++) winUnusable |= mb_ld64(mb, MB_UMASK + 2 * q) != 0;
+  winUnusable = ub(winUnusable);
+  bool all = true;
+  int64_t ab = 0;
+  int seen = 0;
+  // every wave-0 step posts a new sequence number; a bound on the steps and a stale number (wave 0 gone
+  // without MW_EXIT, which the kernel never does) both end the loop, so no helper can outlive wave 0
+  const int maxOps = 4 * W.P + 64;
+  for (int it = 0; it < maxOps; it++) {
+    mw_barrier();  // B1: a step's parameters are posted
+    const int seq = uni((int)mb[MB_SEQ]), cmd = uni((int)mb[MB_CMD]);
+    if (seq == seen) return;
+    seen = seq;
+    if (cmd == MW_EXIT) {
+      mb[MB_ALL + k] = all ? 1u : 0u;  // wave-wide stores of uniform values
+      mb_st64(mb, MB_AB + 2 * k, (uint64_t)ab);
+      mw_barrier();  // B2
+      return;
+    }
+    const int m = uni((int)mb[MB_M]), fpf = uni((int)mb[MB_FPF]);
+    const uint64_t ft0 = (uint64_t)uni64((int64_t)mb_ld64(mb, MB_FT0)), ft1 = (uint64_t)uni64((int64_t)mb_ld64(mb, MB_FT1));
+    int64_t fp[RM];
+#pragma unroll
+    for (int r = 0; r < RM; r++) fp[r] = uni64((int64_t)mb_ld64(mb, MB_FP + 2 * r));
+    if (cmd == MW_RUN) {
+      float rq[RM];
+#pragma unroll
+      for (int r = 0; r < RM; r++) rq[r] = run_rcp(fp[r]);
+      const int cap = mw_run_cap<RM>(b, m, fp, rq, ft0, ft1);
+      const int incl = wscan_add(cap);
+      mb[MB_TOT + k] = (uint32_t)rdl(incl, kWave - 1);  // wave-wide store of a uniform value
+      mw_barrier();  // B2: every block's total is posted
+      int base = 0;
+#pragma unroll
+      for (int q = 0; q < kMwWaves; q++) base += q < k ? (int)mb[MB_TOT + q] : 0;
+      base = uni(base);
+      const int tk = mw_run_commit<RM>(b, base, cap, incl, m, fp);
+      const bool unusable = tk > 0 && (b.nf & NF_UNUSABLE);
+      if (winUnusable && !(fpf & PF_PROVISIONABLE) && wballot(unusable)) all = false;
+      ab += (int64_t)rdl(wscan_add(tk * (k * kWave + lane() + 1)), kWave - 1) * (16 * R + 16);
+    } else {  // MW_FIT: a single pod's first fit over the window
+      mb_st64(mb, MB_MASK + 2 * k, wballot(mw_fits<RM>(b, fp, ft0, ft1)));
+      mw_barrier();  // B2: every block's ballot is posted
+      uint64_t mj;
+      const int kj = mw_first_fit(mb, mj);
+      if (kj == k) {
+        const bool own = lane() == ctz64(mj);
+#pragma unroll
+        for (int r = 0; r < RM; r++) b.av[r] -= own ? fp[r] : 0;
+      }
+    }
+  }
+}
+
+template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN, bool MW = false>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, MW ? 256 : 64))) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_solve(KsDev D, const KsWork* works, Plan pl) {
   constexpr int RM = Solver<RT, TL, SIM, TOPO, LEAN>::RM;
   // The loop's branch conditions are forced scalar (ub / uni): its control flow is wave-uniform by
   // construction, and left to prove that itself the compiler falls back to exec-masked code for the whole
@@ -2403,6 +2616,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int NWC = SIM && d.G ? (d.tgCntWords - d.tgSmall + 31) >> 5 : 0;
   S.s_tcd = (LU32)take(4 * (size_t)NWC);
   S.s_gw = (LU64)take(TOPO && d.G && d.GMW > 1 ? 8 * (size_t)GS_N * d.GMW : 0);
+  // MW: waves 1..3 hold window blocks 1..3 and serve wave 0's window steps (mw_helper); the mailbox follows
+  // the plan's LDS
+  constexpr bool MWK = MW && SIM && LEAN && !TOPO && RT > 0;
+  const LU32 mb = (LU32)(smem + pl.lds);
+  if constexpr (MWK) {
+    const int wv = (int)(threadIdx.x >> 6);
+    if (wv > 0) {
+      mw_helper<RM>(D, W, S.s_rmv, mb, wv);
+      return;
+    }
+  }
   if constexpr (TOPO) {  // groups in t.topologies at the start: all but the late ones (topology.go:102-119)
     S.t_active = ~D.tg_late[0];
     for (int w = 1 + lane(); w < d.GMW; w += kWave) S.s_gw[GS_ACT * d.GMW + w] = ~D.tg_late[w];
@@ -2505,10 +2729,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   uint64_t wtx[NWA], wty[NWA], whp[NWA];
   int64_t wav[NWA][RM], wrq[NWQ][RM];  // FREEW: wav = free capacity, wrq unused
   int wnf[NWA];
+  if constexpr (MWK) mw_barrier();  // B0a: the prologue's LDS (removed-node mask) is ready for the helpers
   if constexpr (NW > 0) {
     if (d.N > 0) {
 #pragma unroll
-      for (int k = 0; k < NW; k++) {
+      for (int k = 0; k < (MWK ? 1 : NW); k++) {
         const int n = k * kWave + lane(), c = n < d.N ? n : d.N - 1;
         wtx[k] = D.n_taint[2 * c];
         wty[k] = D.n_taint[2 * c + 1];
@@ -2534,10 +2759,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
   }
   bool winUnusable = false;  // some register-window node is NF_UNUSABLE (a run's placements check it)
-  if constexpr (NW > 0)
+  if constexpr (MWK) {  // each wave's block ballot through the mailbox
+    mb_st64(mb, MB_UMASK, d.N > 0 ? wballot(wnf[0] & NF_UNUSABLE) : 0ull);  // wave-wide store of a uniform value
+    mw_barrier();  // B0b
+#pragma unroll
+    for (int q = 0; q < kMwWaves; q++) winUnusable |= mb_ld64(mb, MB_UMASK + 2 * q) != 0;
+    winUnusable = ub(winUnusable);
+  } else if constexpr (NW > 0) {
     if (d.N > 0)
 #pragma unroll
       for (int k = 0; k < NW; k++) winUnusable |= wballot(wnf[k] & NF_UNUSABLE) != 0;
+  }
+  int mwseq = 0;
+  // MW: post a window step to the helpers (wave-wide stores of uniform values), then B1
+  auto mw_post = [&](int cmd, int m, const int64_t* fpp, uint64_t ft0, uint64_t ft1, int fpf) {
+    mb[MB_M] = (uint32_t)m;
+    mb[MB_FPF] = (uint32_t)fpf;
+    mb_st64(mb, MB_FT0, ft0);
+    mb_st64(mb, MB_FT1, ft1);
+#pragma unroll
+    for (int r = 0; r < RM; r++) mb_st64(mb, MB_FP + 2 * r, (uint64_t)fpp[r]);
+    mb[MB_SEQ] = (uint32_t)++mwseq;
+    mb[MB_CMD] = (uint32_t)cmd;
+    mw_barrier();  // B1
+  };
+  // MW: block 0's first-fit ballot, then every block's (B2); returns the first block holding a fit
+  auto mw_fit = [&](const int64_t* fpp, uint64_t ft0, uint64_t ft1, uint64_t& mj) {
+    mw_post(MW_FIT, 0, fpp, ft0, ft1, 0);
+    bool ok = (((wtx[0] & ~ft0) | (wty[0] & ~ft1)) == 0);
+#pragma unroll
+    for (int r = 0; r < RM; r++) ok &= fpp[r] <= wav[0][r];
+    mb_st64(mb, MB_MASK, wballot(ok));
+    mw_barrier();  // B2
+    return mw_first_fit(mb, mj);
+  };
   int nclaims = 0, nlog = 0, hostCtr = SIM ? 0 : d.hostnameSeed;
   bool allSched = true;  // SIM: AllNonPendingPodsScheduled so far (pods placed on unusable nodes)
   int nrs = 0;           // SIM: compact node-requirement slots in use
@@ -2621,44 +2876,77 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             PH_BEGIN(tb);
             float rq[RM];
 #pragma unroll
-            for (int r = 0; r < RM; r++) rq[r] = fp[r] > 0 ? 1.0f / (float)fp[r] : 0.f;
-            int tk[NWA];
-            int base = 0;
-#pragma unroll
-            for (int k = 0; k < NW; k++) {
-              tk[k] = 0;
-              if (base < m) {
-                const bool tol = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
-                int cap = tol ? m : 0;
-#pragma unroll
-                for (int r = 0; r < RM; r++) {
-                  const int c = run_cap(wav[k][r], fp[r], rq[r], m);
-                  cap = c < cap ? c : cap;
-                }
-                const int incl = wscan_add(cap);
-                const int p0 = base + incl - cap, room = m - p0;
-                tk[k] = room <= 0 ? 0 : (cap < room ? cap : room);
-                base += rdl(incl, kWave - 1);
-              }
-            }
-            const int placed = base < m ? base : m;
-            if (placed == 0) break;  // pod wi fits no window node: the general step
-            // commit: each node's share (branch-free per lane: tk = 0 leaves a node unchanged)
+            for (int r = 0; r < RM; r++) rq[r] = run_rcp(fp[r]);
+            int placed = 0;
             bool unusable = false;
-            int64_t ab = 0;
+            int ab = 0;  // sum over the run's pods of their node's position + 1 (< 2^31 below 8M pods per run)
+            if constexpr (MWK) {
+              // block 0 here, blocks 1..3 on the helpers; the blocks' totals give each its base
+              mw_post(MW_RUN, m, fp, ft0, ft1, fpf);
+              const bool tol = (((wtx[0] & ~ft0) | (wty[0] & ~ft1)) == 0);
+              int cap = tol ? m : 0;
 #pragma unroll
-            for (int k = 0; k < NW; k++) {
+              for (int r = 0; r < RM; r++) {
+                const int c = run_cap(wav[0][r], fp[r], rq[r], m);
+                cap = c < cap ? c : cap;
+              }
+              const int incl = wscan_add(cap);
+              mb[MB_TOT] = (uint32_t)rdl(incl, kWave - 1);  // wave-wide store of a uniform value
+              mw_barrier();  // B2
+              int tot = 0;
 #pragma unroll
-              for (int r = 0; r < RM; r++) wav[k][r] -= (int64_t)tk[k] * fp[r];
-              unusable = unusable || (tk[k] > 0 && (wnf[k] & NF_UNUSABLE));
-              ab += (int64_t)tk[k] * (k * kWave + lane() + 1);
+              for (int q = 0; q < kMwWaves; q++) tot += (int)mb[MB_TOT + q];
+              tot = uni(tot);
+              placed = tot < m ? tot : m;
+              // (placed == 0: every block's capacity is 0, so every share below is 0)
+              const int p0 = incl - cap, room = m - p0;
+              const int tk0 = room <= 0 ? 0 : (cap < room ? cap : room);
+#pragma unroll
+              for (int r = 0; r < RM; r++) wav[0][r] -= (int64_t)tk0 * fp[r];
+              unusable = tk0 > 0 && (wnf[0] & NF_UNUSABLE);
+              ab = tk0 * (lane() + 1);
+              if (placed == 0) break;  // pod wi fits no window node: the general step
+            } else {
+              int tk[NWA];
+              int base = 0, nb = 0;  // nb: the window blocks the run reaches (the rest take nothing)
+#pragma unroll
+              for (int k = 0; k < NW; k++) {
+                tk[k] = 0;
+                if (base < m) {
+                  nb = k + 1;
+                  const bool tol = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
+                  int cap = tol ? m : 0;
+#pragma unroll
+                  for (int r = 0; r < RM; r++) {
+                    const int c = run_cap(wav[k][r], fp[r], rq[r], m);
+                    cap = c < cap ? c : cap;
+                  }
+                  const int incl = wscan_add(cap);
+                  const int p0 = base + incl - cap, room = m - p0;
+                  tk[k] = room <= 0 ? 0 : (cap < room ? cap : room);
+                  base += rdl(incl, kWave - 1);
+                }
+              }
+              placed = base < m ? base : m;
+              if (placed == 0) break;  // pod wi fits no window node: the general step
+              // commit: each node's share, in the blocks the run reached (branch-free per lane: tk = 0 leaves a
+              // node unchanged)
+#pragma unroll
+              for (int k = 0; k < NW; k++) {
+                if (k < nb) {
+#pragma unroll
+                  for (int r = 0; r < RM; r++) wav[k][r] -= (int64_t)tk[k] * fp[r];
+                  unusable = unusable || (tk[k] > 0 && (wnf[k] & NF_UNUSABLE));
+                  ab += tk[k] * (k * kWave + lane() + 1);
+                }
+              }
             }
             // AllNonPendingPodsScheduled: a non-provisionable pod on an unusable node (helpers.go:118-124)
             if (winUnusable && !(fpf & PF_PROVISIONABLE) && wballot(unusable)) allSched = false;
             // a run's pods within the window that had failed before (only after a push-back) are scheduled now
-            if (lane() >= wi && lane() < wi + placed && lane() < wn && w.st == ST_FAILED) W.pod_status[w.p] = ST_SCHEDULED;
-            for (int off = 32; off >= 1; off >>= 1) ab += __shfl_xor(ab, off);
-            S.algbytes += uni64(ab) * (16 * R + 16);
+            if (!ident && lane() >= wi && lane() < wi + placed && lane() < wn && w.st == ST_FAILED)
+              W.pod_status[w.p] = ST_SCHEDULED;
+            S.algbytes += (int64_t)rdl(wscan_add(ab), kWave - 1) * (16 * R + 16);
             nlog += placed;
             qhead += placed;
             if (qhead >= P) qhead -= P;
@@ -2674,30 +2962,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           }
           int kj = -1;
           uint64_t mj = 0;
+          if constexpr (MWK) {
+            kj = mw_fit(fp, ft0, ft1, mj);
+          } else {
 #pragma unroll
-          for (int k = 0; k < NW; k++) {
-            bool ok = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
+            for (int k = 0; k < NW; k++) {
+              bool ok = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
 #pragma unroll
-            for (int r = 0; r < RM; r++) ok &= fp[r] <= wav[k][r];
-            const uint64_t m = wballot(ok);
-            if (m) {
-              kj = k;
-              mj = m;
-              break;
+              for (int r = 0; r < RM; r++) ok &= fp[r] <= wav[k][r];
+              const uint64_t m = wballot(ok);
+              if (m) {
+                kj = k;
+                mj = m;
+                break;
+              }
             }
           }
           if (kj < 0) break;
           const int fpod = rdl(w.p, wi);
           const int j = kj * kWave + ctz64(mj), owner = j & (kWave - 1);
           int nfv = 0;
+          if constexpr (MWK) {  // block 0 commits here, the helper owning block kj commits there
+            const bool own = kj == 0 && lane() == owner;
 #pragma unroll
-          for (int k = 0; k < NW; k++)
-            if (k == kj) {
-              nfv = wnf[k];
-              if (lane() == owner)
+            for (int r = 0; r < RM; r++) wav[0][r] -= own ? fp[r] : 0;
+            nfv = ((mb_ld64(mb, MB_UMASK + 2 * kj) >> owner) & 1ull) ? NF_UNUSABLE : 0;
+          } else {
 #pragma unroll
-                for (int r = 0; r < RM; r++) wav[k][r] -= fp[r];
-            }
+            for (int k = 0; k < NW; k++)
+              if (k == kj) {
+                nfv = wnf[k];
+                if (lane() == owner)
+#pragma unroll
+                  for (int r = 0; r < RM; r++) wav[k][r] -= fp[r];
+              }
+          }
           if ((rdl(nfv, owner) & NF_UNUSABLE) && !(fpf & PF_PROVISIONABLE)) allSched = false;
           if (rdl(w.st, wi) == ST_FAILED) W.pod_status[fpod] = ST_SCHEDULED;  // (wave-wide, uniform)
           nlog++;
@@ -2739,7 +3038,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       S.fnp = d.fnOn ? D.st_fn + (int64_t)uni(D.st_fnrow[s]) * ((d.N + 31) >> 5) : nullptr;
       wsync();
     }
-    if (TOPO) S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi));
+    if (TOPO)
+      S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi), (uint64_t)rdl64((int64_t)w.tsel, wi),
+                 (uint64_t)rdl64((int64_t)w.tinv, wi), (uint64_t)rdl64((int64_t)w.town, wi),
+                 (uint64_t)rdl64((int64_t)w.trss, wi));
 #pragma unroll
     for (int r = 0; r < RM; r++) {
       if (RT == 0 && r >= R) break;
@@ -2759,8 +3061,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         int kj = -1;
         uint64_t mj = 0;
         asm volatile("; KS_MARK window_begin");
+        if constexpr (MWK) kj = mw_fit(pod, tol0, tol1, mj);  // (LEAN: no host ports, volumes, keys)
 #pragma unroll
-        for (int k = 0; k < NW; k++) {
+        for (int k = 0; k < (MWK ? 0 : NW); k++) {
           const int n = k * kWave + lane();
           bool ok = (((wtx[k] & ~tol0) | (wty[k] & ~tol1)) == 0);
           if constexpr (FREEW) {
@@ -2791,8 +3094,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         if (U(kj >= 0)) {
           const int j = kj * kWave + ctz64(mj), owner = j & (kWave - 1);
           int nfv = 0;
+          if constexpr (MWK) {
+            const bool own = kj == 0 && lane() == owner;
 #pragma unroll
-          for (int k = 0; k < NW; k++)
+            for (int r = 0; r < RM; r++) wav[0][r] -= own ? pod[r] : 0;
+            nfv = ((mb_ld64(mb, MB_UMASK + 2 * kj) >> owner) & 1ull) ? NF_UNUSABLE : 0;
+          }
+#pragma unroll
+          for (int k = 0; k < (MWK ? 0 : NW); k++)
             if (k == kj) {
               nfv = wnf[k];
               if (lane() == owner) {
@@ -2891,6 +3200,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
     PH_END(t1, 1);
+    // A simulation's pod one of whose (non-hostname) groups admits no domain at all (t_nonode) fails every
+    // NodeClaim too: the claims' domain choices are a subset of the domains topo_pop already found empty
+    // (nextDomainTopologySpread / Affinity / AntiAffinity over fewer values), and a failed topo_apply has no
+    // side effect.  Simulations render no messages, so only the NewNodeClaim calls are counted (the
+    // record's RF_HOSTINCR).  The claim re-sort of this add() still runs: s.newNodeClaims' order after the last
+    // add() is what NewNodeClaims[0] of the record reads.
+    const bool simNoClaim = SIM && TOPO && S.t_nonode && d.NTPL > 0;
     // 2) in-flight NodeClaims, sorted by pod count
     if (U(!placed && nclaims > 0)) {
       PH_BEGIN(t2);
@@ -2901,7 +3217,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         srt = true;
       }
       PH_END(t2, 2);
-      for (int base = 0; U(base < nclaims && !placed); base += kWave) {
+      for (int base = 0; U(base < nclaims && !placed && !simNoClaim); base += kWave) {
         PH_BEGIN(t3);
         const int j = base + lane();
         const bool q = j < nclaims && S.claim_quick(j, s, sflags, toltpl, pod);
@@ -2983,7 +3299,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     // 3) new NodeClaim per template
     if (!U(placed)) {
       PH_BEGIN(t6);
-      const int r = UI(S.try_templates(p, s, sflags, toltpl, pod, nclaims, nlog, hostCtr, srt));
+      const int r = U(simNoClaim) ? S.sim_template_calls(hostCtr)
+                                  : UI(S.try_templates(p, s, sflags, toltpl, pod, nclaims, nlog, hostCtr, srt));
       PH_END(t6, 6);
       nclaims = UI(nclaims);
       hostCtr = UI(hostCtr);
@@ -3016,6 +3333,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     pushed = true;
     ident = false;
     if (!relaxed) W.last_len[uid] = ((uint64_t)epoch << 32) | (uint32_t)qlen;  // (wave-wide, uniform)
+  }
+  if constexpr (MWK) {  // the helpers' contributions, then they leave
+    mw_post(MW_EXIT, 0, pod, 0, 0, 0);
+    mw_barrier();  // B2
+    bool hall = true;
+    int64_t hab = 0;
+#pragma unroll
+    for (int q = 1; q < kMwWaves; q++) {
+      hall = hall && mb[MB_ALL + q] != 0;
+      hab += (int64_t)mb_ld64(mb, MB_AB + 2 * q);
+    }
+    allSched = allSched && ub(hall);
+    S.algbytes += uni64(hab);
   }
   S.log_flush(nlog);
   // write back LDS-resident claim state for the host
@@ -3072,6 +3402,7 @@ hipError_t launch_solve_plain(const KsDev& D, const KsWork* w, int n, const Plan
 hipError_t launch_solve_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
 hipError_t launch_sims_plain(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
 hipError_t launch_sims_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
+hipError_t launch_sims_mw(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
 
 #if KS_TU == 1
 hipError_t launch_solve_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
@@ -3080,6 +3411,19 @@ hipError_t launch_solve_topo(const KsDev& D, const KsWork* w, int n, const Plan&
 #elif KS_TU == 2
 hipError_t launch_sims_plain(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
   return launch_family<true, false>(D, w, n, pl, st);
+}
+// The long simulations on 4-wave workgroups (MW): resource-only pods with the window in free-capacity form
+// (the LEAN instantiations); hipErrorNotSupported for other problems (the caller runs them single-wave).
+hipError_t launch_sims_mw(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (D.d.G || !D.d.lean || !pl.talloc || D.d.N <= 0 || pl.lds + kMwBytes > 160 * 1024) return hipErrorNotSupported;
+  const dim3 blk(kMwWaves * kWave);
+  switch (D.d.R) {
+    case 3: hipLaunchKernelGGL((k_solve<3, true, true, false, true, true>), dim3(n), blk, pl.lds + kMwBytes, st, D, w, pl); break;
+    case 4: hipLaunchKernelGGL((k_solve<4, true, true, false, true, true>), dim3(n), blk, pl.lds + kMwBytes, st, D, w, pl); break;
+    default: return hipErrorNotSupported;
+  }
+  return hipGetLastError();
 }
 #elif KS_TU == 3
 hipError_t launch_sims_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
@@ -3198,6 +3542,25 @@ hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const
   if (D.d.fmOn) launch_feasibility(D, st);
   if (D.d.fnOn) launch_feasibility_nodes(D, st);
   return (D.d.G ? launch_sims_topo : launch_sims_plain)(D, works_dev, nsims, pl, st);
+}
+bool sims_mw_supported(const KsDev& D, const Plan& pl) {
+  return !D.d.G && D.d.lean && pl.talloc && D.d.N > 0 && pl.lds + kMwBytes <= 160 * 1024 && (D.d.R == 3 || D.d.R == 4);
+}
+// The first nmw simulations (the long ones) on 4-wave workgroups on st2, the rest single-wave on st,
+// concurrently: st2 waits for st's work so far (fork), st waits for st2 at the end (join).
+hipError_t launch_sims_split(const KsDev& D, const KsWork* works_dev, int nsims, int nmw, const Plan& pl, hipStream_t st,
+                             hipStream_t st2, hipEvent_t fork, hipEvent_t join) {
+  if (nmw <= 0 || !sims_mw_supported(D, pl)) return launch_sims(D, works_dev, nsims, pl, st);
+  if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
+  if (D.d.fmOn) launch_feasibility(D, st);
+  if (D.d.fnOn) launch_feasibility_nodes(D, st);
+  hipError_t e = hipEventRecord(fork, st);
+  if (e == hipSuccess) e = hipStreamWaitEvent(st2, fork, 0);
+  if (e == hipSuccess) e = launch_sims_mw(D, works_dev, nmw, pl, st2);
+  if (e == hipSuccess && nsims > nmw) e = launch_sims_plain(D, works_dev + nmw, nsims - nmw, pl, st);
+  if (e == hipSuccess) e = hipEventRecord(join, st2);
+  if (e == hipSuccess) e = hipStreamWaitEvent(st, join, 0);
+  return e;
 }
 #endif
 
