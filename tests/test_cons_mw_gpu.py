@@ -1,8 +1,8 @@
 """Multi-wave simulations (MW, ks_solve.hip mw_helper): a long simulation's register window spread over a
 4-wave workgroup (intra-simulation parallelism for the multi-node prefixes).
 
-The bench clusters only route simulations of 256+ pods there (the C5 / C5R full-size digests cover those);
-here KS_SIM_MW_MIN=1 sends every simulation of small clusters through the 4-wave kernel, so runs that cross
+The 4-wave kernel is opt-in (KS_SIM_MW=1; measured slower end to end); here KS_SIM_MW_MIN=1
+sends every simulation of small clusters through it, so runs that cross
 window blocks, first fits in each block, pods that fall past the window to the general step, removed and
 unusable nodes (AllNonPendingPodsScheduled) and pending pods are all compared with the oracle, simulation by
 simulation, and with the single-wave kernel (KS_SIM_MW=0)."""
@@ -44,7 +44,7 @@ def test_multi_wave_simulations_parity(seed, nodes, ppn, pending, nr, un):
     snap = synth.cluster_snapshot(nodes, ppn, n_its=60, seed=seed, n_pending=pending, not_ready_frac=nr,
                                   uninitialized_frac=un, spot_frac=0.3, it_range=(4, 40))
     want, _ = bridge.consolidate(json.dumps(snap), all_sims=True)
-    mw = _run(snap, {"KS_SIM_MW_MIN": "1"})
+    mw = _run(snap, {"KS_SIM_MW": "1", "KS_SIM_MW_MIN": "1"})
     assert mw == want
     single = _run(snap, {"KS_SIM_MW": "0"})
     assert single == want
