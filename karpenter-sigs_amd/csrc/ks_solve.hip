@@ -2497,7 +2497,7 @@ __device__ __forceinline__ int mw_first_fit(LU32 mb, uint64_t& mj) {
 
 // Waves 1..3 of an MW simulation: their window block, the mailbox loop, then their contributions.
 template <int RM>
-__device__ void mw_helper(const KsDev& D, const KsWork& W, LU32 s_rmv, LU32 mb, int k) {
+__device__ __forceinline__ void mw_helper(const KsDev& D, const KsWork& W, LU32 s_rmv, LU32 mb, int k) {
   const int R = D.d.R;
   mw_barrier();  // B0a: wave 0's prologue (the removed-node mask) is in LDS
   MwBlock<RM> b;
