@@ -66,6 +66,20 @@ def _ref_bytes(name, snap_json):
     return d.get("algBytesRef")
 
 
+def _oracle_full(name, snap_json, units, unit):
+    """The oracle on the whole workload (not a sample), as timed when tests/golden/full_size_digests.json was
+    made: single-threaded for Solve, the threaded precompute for consolidation, in the build container (not
+    on this host).  None if the workload is not the committed one."""
+    try:
+        d = json.load(open(DIGESTS)).get(name)
+    except OSError:
+        return None
+    if not d or not d.get("oracle_seconds") or hashlib.sha256(snap_json.encode()).hexdigest() != d.get("snapshot"):
+        return None
+    return {"seconds": d["oracle_seconds"], "value": round(units / d["oracle_seconds"], 2), "unit": unit,
+            "where": "build container, when the full-size digests were made (tests/golden/full_size_digests.json)"}
+
+
 def _traffic(tag):
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % tag)
     if os.path.exists(tpath):
@@ -297,6 +311,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
                               extra={"kernel_ms_max_rank": round(kmax, 3)}),
         "cpu_baseline": cpu,
         "cpu_baseline_1thread": cpu1,
+        "oracle_full_size": _oracle_full("C5T" if topology else "C5", snap, c.num_sims, "cands/s"),
         "validation": validation,
         **({"incremental_update": update} if update else {}),
         **({"shards_on_one_gpu": shards} if shards else {}),
@@ -332,7 +347,7 @@ def solve_line(args, local, name, snap, metric, reps, cpu_sample=None, extra=Non
            "new_nodeclaims": len(r.new_nodeclaims), "pods_on_existing_nodes": sum(len(n["pods"]) for n in r.existing_nodes),
            "pod_errors": len(r.pod_errors),
            "roofline": _roofline("k_solve", k_ms, sum(algb) / len(algb), _ref_bytes(name, snap_json), traffic_tag),
-           "cpu_baseline": None}
+           "cpu_baseline": None, "oracle_full_size": _oracle_full(name, snap_json, npods, "pods/s")}
     if fbytes > 0:  # k_feasibility (pod-state x instance-type rows) launched inside each Solve: its own roofline
         f_ms = sum(fms) / len(fms)
         out["feasibility"] = _roofline("k_feasibility", f_ms, fbytes, None, (traffic_tag or name.lower()) + "_feasibility"
@@ -536,6 +551,7 @@ def main():
             # SURVEY §8d timing protocol: median and p90 (nearest rank) of the timed Solves
             "kernel_ms_p50": round(_pct(solve_ms, 50), 3), "kernel_ms_p90": round(_pct(solve_ms, 90), 3)}),
         "cpu_baseline": cpu,
+        "oracle_full_size": _oracle_full("C2", snap_json, args.pods, "pods/s"),
     }
     out.update(lines)
     out["consolidation"] = cons
