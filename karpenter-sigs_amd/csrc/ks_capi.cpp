@@ -135,9 +135,9 @@ struct ks_results {
       int hasGt = 0, hasLt = 0;
       int64_t gt = 0, lt = 0;
     };
-    // Rendered on first use (finish_claim): the requirement list, the JSON text (requirementsString, the
-    // launch list) -- a caller reading only pods and options pays for none of it
-    mutable bool finished = false;
+    // Rendered on first use: the requirement list (finish_reqs) and the JSON text (finish_json:
+    // requirementsString, the launch list) -- a caller reading only pods and options pays for neither
+    mutable bool reqsDone = false, jsonDone = false;
     mutable std::string json;
     mutable std::vector<Req> reqs;
     mutable std::vector<std::vector<const char*>> reqValP;
@@ -504,9 +504,40 @@ static void replay_check(const Host& h, int nc, int nl, const std::vector<int32_
   }
 }
 
-// The rendered half of a NodeClaim result (first use): Requirements after FinalizeScheduling, the JSON text.
-static void finish_claim(const Host& h, const ks_results::Claim& cl) {
-  if (cl.finished) return;
+// The rendered halves of a NodeClaim result, each on first use: the structured Requirements after
+// FinalizeScheduling (ks_results_nodeclaim_requirements), and the JSON text (ks_results_json: requirement
+// strings, requirementsString, the launch list).
+static void finish_reqs(const Host& h, const ks_results::Claim& cl) {
+  if (cl.reqsDone) return;
+  const KsDims& d = h.dims;
+  const uint32_t* rec = cl.rec.data();
+  const uint64_t pr = rs_present(rec);
+  static const char* opn[] = {"In", "NotIn", "Exists", "DoesNotExist"};
+  for (int kk = 0; kk < d.NK; kk++) {  // FinalizeScheduling drops the hostname requirement
+    if (!bit(pr, kk) || kk == h.hostKey) continue;
+    ks_results::Claim::Req q;
+    q.key = h.keyNames[(size_t)kk];
+    const int op = rs_op(h.L, rec, kk);
+    q.op = opn[op];
+    const KeyMeta& km = h.keys[(size_t)kk];
+    if (op == OP_IN || op == OP_NOTIN) {
+      for (int b = 0; b < km.nv; b++)
+        if ((rec[h.L.HDR + km.off + (b >> 5)] >> (b & 31)) & 1u) q.values.push_back(h.values[(size_t)kk][(size_t)b]);
+      std::sort(q.values.begin(), q.values.end());
+    }
+    if (km.bslot >= 0) {
+      q.hasGt = bit(rs_hasgt(rec), kk) ? 1 : 0;
+      q.hasLt = bit(rs_haslt(rec), kk) ? 1 : 0;
+      if (q.hasGt) q.gt = rs_gt(rec, km.bslot);
+      if (q.hasLt) q.lt = rs_lt(rec, km.bslot);
+    }
+    cl.reqs.push_back(std::move(q));
+  }
+  cl.bind_reqs();
+  cl.reqsDone = true;
+}
+static void finish_json(const Host& h, const ks_results::Claim& cl) {
+  if (cl.jsonDone) return;
   const KsDims& d = h.dims;
   const Host::Tpl& tp = h.tpls[(size_t)cl.tpl];
   const uint32_t* rec = cl.rec.data();
@@ -522,41 +553,20 @@ static void finish_claim(const Host& h, const ks_results::Claim& cl) {
     ksjson::quote(j, h.its[cl.its[i]].name);
   }
   j += "],\"requests\":{";
-  bool first = true;
   for (size_t i = 0; i < cl.reqNames.size(); i++) {
-    if (!first) j += ",";
-    first = false;
+    if (i) j += ",";
     ksjson::quote(j, cl.reqNames[i]);
     j += ":";
     ksjson::quote(j, cl.reqQty[i]);
   }
   j += "},\"requirements\":[";
-  first = true;
-  uint64_t pr = rs_present(rec);
+  bool first = true;
+  const uint64_t pr = rs_present(rec);
   for (int kk = 0; kk < d.NK; kk++) {  // FinalizeScheduling drops the hostname requirement
     if (!bit(pr, kk) || kk == h.hostKey) continue;
     if (!first) j += ",";
     first = false;
     ksjson::quote(j, h.reqString(rec, kk, true, cl.host));
-    static const char* opn[] = {"In", "NotIn", "Exists", "DoesNotExist"};
-    ks_results::Claim::Req q;
-    q.key = h.keyNames[(size_t)kk];
-    const int op = rs_op(h.L, rec, kk);
-    q.op = opn[op];
-    if (op == OP_IN || op == OP_NOTIN) {
-      const KeyMeta& km = h.keys[(size_t)kk];
-      for (int b = 0; b < km.nv; b++)
-        if ((rec[h.L.HDR + km.off + (b >> 5)] >> (b & 31)) & 1u) q.values.push_back(h.values[(size_t)kk][(size_t)b]);
-      std::sort(q.values.begin(), q.values.end());
-    }
-    const KeyMeta& km = h.keys[(size_t)kk];
-    if (km.bslot >= 0) {
-      q.hasGt = bit(rs_hasgt(rec), kk) ? 1 : 0;
-      q.hasLt = bit(rs_haslt(rec), kk) ? 1 : 0;
-      if (q.hasGt) q.gt = rs_gt(rec, km.bslot);
-      if (q.hasLt) q.lt = rs_lt(rec, km.bslot);
-    }
-    cl.reqs.push_back(std::move(q));
   }
   j += "],\"requirementsString\":";
   ksjson::quote(j, h.reqsString(rec, cl.host));
@@ -588,12 +598,12 @@ static void finish_claim(const Host& h, const ks_results::Claim& cl) {
   }
   j += "]}";
   cl.json = j;
-  cl.bind_reqs();
-  cl.finished = true;
+  cl.jsonDone = true;
 }
 
 // Rebuild Results from the replica-0 workspace.
 static ks_results* collect(ks_problem* pb, const KsWork& W) {
+  PhaseTimer pt("collect");
   Host& h = pb->host;
   const KsDims& d = h.dims;
   hipStream_t st = pb->stream;
@@ -648,7 +658,9 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     }
   }
 
+  pt.mark("download");
   replay_check(h, nc, nl, order, ctpl, creq, crem, logp, logt);
+  pt.mark("replay check");
   auto* res = new ks_results();
   res->pb = pb;
   pb->refs++;
@@ -707,6 +719,7 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     res->claims.push_back(std::move(cl));
   }
   for (auto& c : res->claims) c.bind();  // after the last move of the claims vector
+  pt.mark("claims");
   for (int n = 0; n < d.N; n++) res->nodes.push_back(ks_results::ENode{h.nodes[n].origIndex, h.nodes[n].name, nodePods[n]});
   // PodErrors (scheduler.go:179-183 keeps non-nil errors only)
   // k_solve records ST_FAILED at each failed attempt and nothing on success: a pod is an error iff
@@ -828,6 +841,7 @@ static ks_results* collect(ks_problem* pb, const KsWork& W) {
     for (size_t i = 0; i < segs.size(); i++) msg += (i ? "; " : "") + segs[i];
     res->errors.push_back({p, msg});
   }
+  pt.mark("nodes + pod errors");
   return res;
 }
 
@@ -1145,7 +1159,7 @@ int ks_results_json(const ks_results* r, char** json_out) {
   API_TRY
   std::string o = "{\"newNodeClaims\":[";
   for (size_t i = 0; i < r->claims.size(); i++) {
-    finish_claim(r->pb->host, r->claims[i]);
+    finish_json(r->pb->host, r->claims[i]);
     o += (i ? "," : "") + r->claims[i].json;
   }
   o += "],\"existingNodes\":[";
@@ -1200,7 +1214,7 @@ int ks_results_nodeclaim_requests(const ks_results* r, int i, int* n, const char
 int ks_results_nodeclaim_requirements(const ks_results* r, int i, int* n, const ks_requirement** reqs) {
   if (!r || i < 0 || i >= (int)r->claims.size()) return KS_ERR_ARG;
   const auto& c = r->claims[(size_t)i];
-  finish_claim(r->pb->host, c);
+  finish_reqs(r->pb->host, c);
   if (n) *n = (int)c.reqC.size();
   if (reqs) *reqs = c.reqC.data();
   return KS_OK;
