@@ -467,6 +467,10 @@ def main():
         sch.solve_structured(device=local)
     barrier_sync()
     structured_ms = (time.perf_counter() - t1) * 1000.0 / args.steps
+    # the C-ABI part of that return path alone: ks_solve with the Results collected (the copy-back, the
+    # replayed checks and the claim/node/error tables the accessors hand out) and ks_results_free -- what a cgo
+    # caller pays before its own (C-speed) accessor walk; the Python walk above adds ctypes per field
+    collected_ms = sch.timed_collect(args.steps, device=local)
     if dist is not None:
         import torch
 
@@ -544,6 +548,8 @@ def main():
         # a Solve with its Results read through the structured accessors, per step, and that rate
         "structured_solve_ms": round(structured_ms, 3),
         "structured_pods_per_s": round(args.pods * world / (structured_ms / 1000.0), 1),
+        "collected_solve_ms": round(collected_ms, 3),
+        "collected_over_kernel_only": round(collected_ms / (elapsed * 1000.0 / args.steps), 3) if elapsed else None,
         "e2e_pods_per_s": round(args.pods / ((create_ms + full_ms) / 1000.0), 1),
         "roofline": _roofline("k_solve", k_ms, bytes_per_launch, ref, "c2", extra={
             "setup_kernels_ms": round(sum(total_ms) / len(total_ms) - k_ms, 3),

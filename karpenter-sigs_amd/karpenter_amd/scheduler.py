@@ -327,6 +327,19 @@ class Scheduler:
         finally:
             l.ks_results_free(r)
 
+    def timed_collect(self, steps, device=-1, simulation_mode=True):
+        """Mean ms of `steps` ks_solve calls with the Results collected (no accessor walk) + ks_results_free:
+        the C-ABI cost of the drop-in return path, without Python's per-field ctypes overhead."""
+        import time
+        l = lib()
+        o = _Opts(device, 1 if simulation_mode else 0, 1, 0, 0)
+        r = ctypes.c_void_p()
+        t = time.perf_counter()
+        for _ in range(steps):
+            _check(l.ks_solve(self._h, ctypes.byref(o), ctypes.byref(r)))
+            l.ks_results_free(r)
+        return (time.perf_counter() - t) * 1000.0 / steps
+
     def close(self):
         if self._h:
             lib().ks_problem_free(self._h)
