@@ -175,8 +175,8 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
         gathered = torch.empty(world * per * rb, dtype=torch.uint8, device=dev)
 
     def one_pass():
-        if world == 1:
-            recs, ms = c.run(0, 1, device=local)
+        if world == 1:  # the records stay in the handle's pinned buffer (decide reads them there)
+            recs, ms = c.run(0, 1, device=local, keep=True)
         else:
             _, ms = c.run(rank, world, device=local, out_ptr=out.data_ptr())
             dist.all_gather_into_tensor(gathered, out)

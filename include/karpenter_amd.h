@@ -169,6 +169,9 @@ int ks_cons_records_per_rank(const ks_cons* c, int world);
  * queue sort + simulation kernel on the stream they ran on. */
 int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void* records, int records_on_device,
                 double* kernel_ms);
+/* records may be NULL at world 1 (records_on_device 0): the records stay in the handle's pinned host buffer
+ * until its next run, and ks_cons_decide / ks_cons_needed_sims / ks_cons_records_alg_bytes take records NULL
+ * to read them there (no copy of the pass's records). */
 /* Replay the reference's sequential choice over the gathered records ([rank][slot] layout):
  * JSON {"candidates":[{name, disruptionCost}], "multi":{"command", "sims"}, "single":{"command", "sims"}}.
  * flags: KS_CONS_ALL_SIMS reports every simulation (otherwise only those the reference would have

@@ -1186,7 +1186,7 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
   HIPCHK(hipStreamSynchronize(pb.stream));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, c.ev[0], c.ev[1]));
-  if (!onDevice) {
+  if (!onDevice && records) {  // (records == NULL: they stay in the handle's pinned buffer, host_records)
     memcpy(records, c.L.hrec, bytes);
     if (all > bytes) memset((char*)records + bytes, 0, all - bytes);
   }
@@ -1673,10 +1673,19 @@ int ks_cons_num_sims(const ks_cons* c) { return c ? (int)c->sims.size() : 0; }
 int ks_cons_record_bytes(const ks_cons* c) { return c ? 4 * c->recWords : 0; }
 int ks_cons_records_per_rank(const ks_cons* c, int world) { return c && world > 0 ? c->per_rank(world) : 0; }
 
+// The gathered records: the caller's, or (NULL) those a world-1 ks_cons_run left in the handle's pinned buffer.
+static const int32_t* host_records(const ks_cons* c, const void* records, int world) {
+  if (records) return (const int32_t*)records;
+  if (world != 1 || c->L.lworld != 1 || !c->L.hrec || c->L.lsims.size() != c->sims.size())
+    throw KsError(KS_ERR_ARG, "records NULL without a world-1 run of every simulation on this handle");
+  return c->L.hrec;
+}
+
 int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void* records, int records_on_device,
                 double* kernel_ms) {
   API_TRY
-  if (!c || !records || world < 1 || rank < 0 || rank >= world) throw KsError(KS_ERR_ARG, "bad argument");
+  if (!c || (!records && (records_on_device || world != 1)) || world < 1 || rank < 0 || rank >= world)
+    throw KsError(KS_ERR_ARG, "bad argument");
   DeviceGuard guard(c->pb->device, opts);
   const double ms = run_sims(*c, rank, world, records, records_on_device != 0);
   if (kernel_ms) *kernel_ms = ms;
@@ -1715,8 +1724,8 @@ int ks_cons_requirement_words(const ks_cons* c) { return c ? c->pb->host.dims.RS
 
 int ks_cons_needed_sims(const ks_cons* c, const void* records, int world, int flags, int32_t* out, int cap) {
   API_TRY
-  if (!c || !records || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
-  std::vector<int> need = needed_sims(*c, (const int32_t*)records, world, (flags & KS_CONS_ALL_SIMS) != 0);
+  if (!c || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
+  std::vector<int> need = needed_sims(*c, host_records(c, records, world), world, (flags & KS_CONS_ALL_SIMS) != 0);
   for (int i = 0; i < (int)need.size() && i < cap; i++) out[i] = need[(size_t)i];
   return (int)need.size();
   API_CATCH
@@ -1748,8 +1757,8 @@ int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, 
 int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
                          const ks_cons_clock* clock, char** json_out) {
   API_TRY
-  if (!c || !records || !json_out || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
-  const int32_t* recs = (const int32_t*)records;
+  if (!c || !json_out || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
+  const int32_t* recs = host_records(c, records, world);
   const bool all_sims = (flags & KS_CONS_ALL_SIMS) != 0;
   if (!rs_table && world == 1 && c->L.lworld == 1) {
     // One rank ran every simulation: the requirement records the output needs are read from this handle's
@@ -1803,8 +1812,8 @@ int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n) {
 }
 
 double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world) {
-  if (!c || !records || world < 1) return 0;
-  const int32_t* r = (const int32_t*)records;
+  if (!c || world < 1 || (!records && !(world == 1 && c->L.lworld == 1 && c->L.hrec))) return 0;
+  const int32_t* r = records ? (const int32_t*)records : c->L.hrec;
   double sum = 0;
   for (size_t i = 0; i < (size_t)c->per_rank(world) * world; i++) {
     const int32_t* x = r + i * c->recWords;

@@ -448,7 +448,7 @@ class Consolidator:
         self.num_sims = l.ks_cons_num_sims(self._h)
         self._recbuf = None
 
-    def run(self, rank=0, world=1, device=-1, out_ptr=None):
+    def run(self, rank=0, world=1, device=-1, out_ptr=None, keep=False):
         """Run this rank's simulations.  out_ptr: device pointer for records_per_rank*record_bytes
         bytes (e.g. a torch tensor's data_ptr()); None returns the records in host memory.
         Returns (records or None, kernel ms).
@@ -459,6 +459,9 @@ class Consolidator:
         l = _cons_lib()
         o = _Opts(device, 1, 1, 0, 0)
         ms = ctypes.c_double()
+        if keep:  # world 1: the records stay in the handle's pinned buffer; pass records=None to decide()
+            _check(l.ks_cons_run(self._h, rank, world, ctypes.byref(o), None, 0, ctypes.byref(ms)))
+            return None, ms.value
         if out_ptr is None:
             # one host buffer per handle, reused by every pass and handed on without copies (a memoryview,
             # valid until the handle's next run; bytes(view) keeps a copy)
@@ -505,7 +508,7 @@ class Consolidator:
             fetch = fetch or self.claim_requirements
             table = b"".join(fetch(s) for s in need)
             tbuf = ctypes.create_string_buffer(table, max(len(table), 4))
-        buf = _records_buffer(records)
+        buf = None if records is None else _records_buffer(records)  # None: the handle's own records (run(keep=True))
         js = ctypes.c_void_p()
         flags = (1 if all_sims else 0) | (2 if candidates else 0)
         if clock is None:
@@ -537,6 +540,8 @@ class Consolidator:
         return list(out)[:n]
 
     def alg_bytes(self, records, world=1):
+        if records is None:
+            return _cons_lib().ks_cons_records_alg_bytes(self._h, None, world)
         buf = _records_buffer(records)
         return _cons_lib().ks_cons_records_alg_bytes(self._h, ctypes.cast(buf, ctypes.c_void_p), world)
 

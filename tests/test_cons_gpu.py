@@ -352,3 +352,17 @@ def test_consolidation_timeouts_parity(clock, which):
     got = Consolidator(snap).consolidate(clock=clock)
     got.pop("kernel_ms")
     assert _first_diff(want, got) is None, _first_diff(want, got)
+
+
+def test_records_kept_in_handle_gpu():
+    """ks_cons_run with records NULL (world 1): decide / alg_bytes read the handle's pinned records; same
+    decision and bytes as with the records copied out."""
+    snap = synth.cluster_snapshot(30, 6, n_its=40, seed=77, n_pending=2)
+    c = Consolidator(json.dumps(snap))
+    recs, _ = c.run(0, 1)
+    want = c.decide(bytes(recs), 1, all_sims=True)
+    wb = c.alg_bytes(bytes(recs))
+    none, _ = c.run(0, 1, keep=True)
+    assert none is None
+    assert c.decide(None, 1, all_sims=True) == want
+    assert c.alg_bytes(None) == wb

@@ -62,3 +62,27 @@ def test_structured_c2_10k():
 
 def test_structured_topology_errors():
     _check(problems.hostname_failure_problem(503))
+
+
+def test_results_outlive_their_problem():
+    """Results render their JSON and requirement lists on first use (finish_json / finish_reqs), from the
+    problem's host model: freeing the problem first defers its release to the last Results (refcount)."""
+    import ctypes
+
+    from karpenter_amd import scheduler as ks
+
+    snap = json.dumps(problems.random_problem(5, n_pods=80))
+    want = Scheduler(snap).solve().canonical()
+    l = ks.lib()
+    sch = Scheduler(snap)
+    o = ks._Opts(-1, 1, 1, 0, 0)
+    r = ctypes.c_void_p()
+    ks._check(l.ks_solve(sch._h, ctypes.byref(o), ctypes.byref(r)))
+    sch.close()  # the problem handle is gone; the Results still hold its host model
+    claims, nodes, errors = ks._read_structured(l, r)
+    out = ctypes.c_void_p()
+    ks._check(l.ks_results_json(r, ctypes.byref(out)))
+    got = json.loads(ks._take_str(out))
+    l.ks_results_free(r)  # releases the problem too
+    assert problems.canonical(got) == want
+    assert len(claims) == len(got["newNodeClaims"])
