@@ -1288,10 +1288,14 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
       throw KsError(KS_ERR_PARSE, "update: unknown field " + kv.first);
   if (d.G) throw KsError(KS_ERR_UNSUPPORTED, "update: the cluster has topology groups");
   if (d.volAny) throw KsError(KS_ERR_UNSUPPORTED, "update: the cluster has volume limits");
-  if (c.uidIndex.empty())
+  if (c.uidIndex.empty()) {
+    c.uidIndex.reserve(h.pods.size());
     for (size_t i = 0; i < h.pods.size(); i++) c.uidIndex.emplace(h.pods[i].uid, (int)i);
-  if (c.nodeIndex.empty())
+  }
+  if (c.nodeIndex.empty()) {
+    c.nodeIndex.reserve(h.nodes.size());
     for (size_t i = 0; i < h.nodes.size(); i++) c.nodeIndex.emplace(h.nodes[i].name, (int)i);
+  }
   auto podOf = [&](const Value& v) {
     if (!v.is_str()) throw KsError(KS_ERR_PARSE, "update: pod uid is not a string");
     auto it = c.uidIndex.find(v.str());
