@@ -914,14 +914,19 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   c.L.lplan = make_plan(dd, d.G ? 64 * 1024 : 40 * 1024, true);
   if (c.L.lplan.lds > 80 * 1024 || c.L.lplan.KO < 1) c.L.lplan = make_plan(dd, 160 * 1024 - 256, true);
   if (c.L.lplan.lds > 160 * 1024 || c.L.lplan.KO < 1) throw KsError(KS_ERR_CAPACITY, "simulation state does not fit in LDS");
-  // KS_SIM_MW=1: simulations of at least 256 pods (the multi-node prefixes lead the plan) get 4-wave
-  // workgroups (KS_SIM_MW_MIN sets the pod threshold, for tests).  Off by default: the 4-wave runs are
-  // faster per step but the pass was measured slower (multi-wave simulations).
+  // Simulations of at least 256 pods (the multi-node prefixes lead the plan) get 4-wave workgroups in one
+  // mixed launch when the plan is chain-bound: its pods number at most kMwChainRatio times its longest
+  // simulation's (C5: a rank of world >= 4).  A throughput-bound plan (world 1 or 2) runs single-wave, which is
+  // faster there.  KS_SIM_MW=0 / 1 turns this off / on for every plan; KS_SIM_MW_MIN sets the pod
+  // threshold (tests).
+  constexpr int kMwChainRatio = 30;
   const char* mwEnv = std::getenv("KS_SIM_MW");
   const char* mwMinEnv = std::getenv("KS_SIM_MW_MIN");
   const int mwMin = mwMinEnv ? std::max(1, std::atoi(mwMinEnv)) : 256;
+  const bool mwAuto = ns > 0 && (int64_t)c.L.lnent <= (int64_t)kMwChainRatio * simP[0];
+  const bool mwWanted = mwEnv ? mwEnv[0] == '1' : mwAuto;
   c.L.lnmw = 0;
-  if (mwEnv && mwEnv[0] == '1' && sims_mw_supported(pb.dev, c.L.lplan))
+  if (mwWanted && sims_mw_supported(pb.dev, c.L.lplan))
     while (c.L.lnmw < ns && simP[(size_t)c.L.lnmw] >= mwMin) c.L.lnmw++;
   c.L.lrank = rank;
   c.L.lworld = world;

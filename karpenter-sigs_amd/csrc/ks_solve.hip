@@ -2562,820 +2562,41 @@ __device__ __forceinline__ void mw_helper(const KsDev& D, const KsWork& W, LU32 
 
 template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN, bool MW = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, MW ? 256 : 64))) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_solve(KsDev D, const KsWork* works, Plan pl) {
-  constexpr int RM = Solver<RT, TL, SIM, TOPO, LEAN>::RM;
-  // The loop's branch conditions are forced scalar (ub / uni): its control flow is wave-uniform by
-  // construction, and left to prove that itself the compiler falls back to exec-masked code for the whole
-  // commit loop, which costs time and, in one build of the requirement-carrying instantiation, lost a
-  // claim-state write-back (two reference Binpacking scenarios; device requests 0 for one NodeClaim).
-  // The LEAN Solve instantiation (resource-only pods, C1/C2) keeps the compiler's choice: there the
-  // scalar form's extra SGPR spills cost 15 % of C2, and its parity is pinned by the full-size digests.
-  constexpr bool FORCEU = SIM || !LEAN;
-  auto U = [](bool x) { return FORCEU ? ub(x) : x; };
-  auto UI = [](int x) { return FORCEU ? uni(x) : x; };
-  extern __shared__ __attribute__((aligned(16))) char smem_generic[];
+#define KS_BODY_WORK ((const KsWork KS_C*)works)[blockIdx.x]
+#define KS_BODY_SMEM_DECL                                             \
+  extern __shared__ __attribute__((aligned(16))) char smem_generic[]; \
   char KS_L* smem = (char KS_L*)smem_generic;
-  const KsWork KS_C& W = ((const KsWork KS_C*)works)[blockIdx.x];
-  const KsDims& d = D.d;
-  Solver<RT, TL, SIM, TOPO, LEAN> S(D, W, pl);
-  const int R = S.R();
-  char KS_L* sp = smem;
-  auto take = [&](size_t bytes) { char KS_L* r = sp; sp += (bytes + 15) & ~(size_t)15; return r; };
-  KeyMeta KS_L* s_keys = (KeyMeta KS_L*)take(sizeof(KeyMeta) * d.NK);
-  S.s_order = (LI32)take(4 * (size_t)pl.KO);
-  S.s_okey = (LI32)take(4 * (size_t)pl.KO);
-  S.s_ptpl = (LI32)take(4 * (size_t)pl.KO);
-  S.s_phead = (LI64)take(8 * (size_t)pl.KO * R);
-  S.lc.tpl = (LI32)take(4 * (size_t)pl.KL);
-  S.lc.req = (LI64)take(8 * (size_t)pl.KL * R);
-  S.lc.max = (LI64)take(8 * (size_t)pl.KL * R);
-  S.lc.rem = (LU32)take(4 * (size_t)pl.KL * d.TW);
-  S.lc.thr = (LI32)take(4 * (size_t)pl.KL * R);
-  S.lc.cnt = (LI32)take(4 * (size_t)pl.KL);
-  S.s_talloc = (LI64)take(TL ? 8 * (size_t)d.totalTplIts * R : 0);
-  S.s_tsa = (LI64)take(TL && pl.tsort ? 8 * (size_t)d.totalTplIts * R : 0);
-  S.s_tsp = (LI32)take(TL && pl.tsort ? 4 * (size_t)d.totalTplIts * R : 0);
-  S.s_tbeg = (LI32)take(4 * (size_t)(d.NTPL + 1));
-  S.s_pool = (LI64)take(8 * (size_t)(d.NPOOL + 1) * R);
-  S.s_rs = (LU32)take(4 * (size_t)d.RSW);
-  S.s_pin = (LU32)take(4 * (size_t)d.RSW);
-  S.s_rem = (LU32)take(4 * (size_t)d.TW + 8);
-  S.s_cand = (LU32)take(4 * (size_t)d.TW + 8);
-  S.s_fic = (LU32)take(4 * (size_t)d.TW + 8);
-  S.s_fof = (LU32)take(4 * (size_t)d.TW + 8);
-  S.s_firr = (LU32)take(4 * (size_t)d.TW + 8);
-  const int NWN = (d.N + 31) >> 5;
-  S.s_rmv = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
-  S.s_tch = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
-  S.s_tchr = (LU32)take(SIM || d.fnOn ? 4 * (size_t)NWN : 0);
-  S.s_tvol = (LU32)take(SIM ? 4 * (size_t)NWN : 0);
-  S.s_tgm = (LI32)take(4 * (size_t)d.G * TGM_WORDS);
-  S.s_tmin = (LI32)take(4 * (size_t)d.G);
-  S.s_trs0 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
-  S.s_trs1 = (LU32)take(d.G ? 4 * (size_t)d.RSW : 0);
-  S.s_tcs = (LI32)take(d.G ? 4 * (size_t)pl.tcl : 0);
-  const int NWC = SIM && d.G ? (d.tgCntWords - d.tgSmall + 31) >> 5 : 0;
-  S.s_tcd = (LU32)take(4 * (size_t)NWC);
-  S.s_gw = (LU64)take(TOPO && d.G && d.GMW > 1 ? 8 * (size_t)GS_N * d.GMW : 0);
-  // MW: waves 1..3 hold window blocks 1..3 and serve wave 0's window steps (mw_helper); the mailbox follows
-  // the plan's LDS
-  constexpr bool MWK = MW && SIM && LEAN && !TOPO && RT > 0;
-  const LU32 mb = (LU32)(smem + pl.lds);
-  if constexpr (MWK) {
+#include "ks_solve_body.inc"
+#undef KS_BODY_WORK
+#undef KS_BODY_SMEM_DECL
+}
+
+// The same body for one simulation of a mixed launch (k_sim_mixed): work item widx, LDS at smem_in.
+template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN, bool MW>
+__device__ __forceinline__ void solve_body(const KsDev& D, const KsWork* works, const Plan& pl, int widx,
+                                           char KS_L* smem_in) {
+#define KS_BODY_WORK ((const KsWork KS_C*)works)[widx]
+#define KS_BODY_SMEM_DECL char KS_L* smem = smem_in;
+#include "ks_solve_body.inc"
+#undef KS_BODY_WORK
+#undef KS_BODY_SMEM_DECL
+}
+
+// One launch for a consolidation pass with long simulations (MW): workgroups [0, nmw) run the long ones on
+// 4 waves, dispatched first; each later workgroup runs four short ones, one per wave, each in its own LDS
+// slice (stride bytes).  The two kinds overlap on the chip, which two launches on two streams did not.
+template <int RT>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256))) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_sim_mixed(
+    KsDev D, const KsWork* works, Plan pl, int nmw, int n, int stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem_mixed[];
+  char KS_L* base = (char KS_L*)smem_mixed;
+  if ((int)blockIdx.x < nmw) {
+    solve_body<RT, true, true, false, true, true>(D, works, pl, (int)blockIdx.x, base);
+  } else {
     const int wv = (int)(threadIdx.x >> 6);
-    if (wv > 0) {
-      mw_helper<RM>(D, W, S.s_rmv, mb, wv);
-      return;
-    }
+    const int s = nmw + ((int)blockIdx.x - nmw) * kMwWaves + wv;
+    if (s < n) solve_body<RT, true, true, false, true, false>(D, works, pl, s, base + (size_t)wv * stride);
   }
-  if constexpr (TOPO) {  // groups in t.topologies at the start: all but the late ones (topology.go:102-119)
-    S.t_active = ~D.tg_late[0];
-    for (int w = 1 + lane(); w < d.GMW; w += kWave) S.s_gw[GS_ACT * d.GMW + w] = ~D.tg_late[w];
-  }
-  if (d.G) lds_copy<8>(S.s_tcs, D.tg_cnt0, pl.tcl);
-  for (int i = lane(); i < NWC; i += kWave) S.s_tcd[i] = 0;
-  lds_copy<4>(S.s_tgm, D.tg_meta, d.G * TGM_WORDS);
-  S.gc.tpl = W.c_tpl;
-  S.gc.req = W.c_req;
-  S.gc.max = W.c_max;
-  S.gc.rem = W.c_rem;
-  S.gc.thr = W.c_thr;
-  S.gc.cnt = W.c_cnt;
-  for (int i = lane(); i < d.NK * (int)(sizeof(KeyMeta) / 4); i += kWave)
-    ((uint32_t KS_L*)s_keys)[i] = ((const uint32_t KS_G*)D.keys)[i];
-  for (int i = lane(); i <= d.NTPL; i += kWave) S.s_tbeg[i] = D.tpl_it_beg[i];
-  for (int i = lane(); i < d.NPOOL * R; i += kWave) S.s_pool[i] = SIM ? W.pool0[i] : D.pool_rem0[i];
-  const int P = SIM ? W.P : d.P;
-  if (!SIM && d.fnOn)
-    for (int i = lane(); i < NWN; i += kWave) S.s_tchr[i] = 0;
-  if constexpr (SIM) {
-    // the simulation's fresh Scheduler state (what k_init does for plain Solves): NewQueue order is
-    // the local order (pod_map is sorted), nothing placed, no staleness marks.  The per-pod queue arrays
-    // are written at the first push-back (sim_queue_init): until then nothing reads them.
-    for (int i = lane(); i < NWN; i += kWave) {
-      S.s_rmv[i] = 0;
-      S.s_tch[i] = 0;
-      S.s_tchr[i] = 0;
-      S.s_tvol[i] = 0;
-    }
-    if constexpr (TOPO) {
-      // NewTopology for this simulation: the shared counts minus the candidates' pods, which the
-      // simulation schedules and NewTopology therefore excludes (topology.go:72-75,262-265); a
-      // domain left with no pod and no other registration drops out of TopologyGroup.domains.
-      // (copy-on-write: only the words these entries touch get a private copy)
-      // placeholder counts: column 0 (the first fresh claim's); try_templates zeroes the next one per new claim
-      for (int g = lane(); g < d.G; g += kWave) W.tg_ccnt[(int64_t)g * W.ccs] = 0;
-      for (int i = lane(); i < d.G; i += kWave) W.tg_cpos[i] = 0;
-      wsync();
-      // offsets are distinct within one simulation; 4 entries per lane in flight (a long prefix has thousands)
-      for (int i0 = lane(); i0 < W.ntdel; i0 += 4 * kWave) {
-        int off[4], x[4], c0[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int i = i0 + u * kWave < W.ntdel ? i0 + u * kWave : i0;
-          off[u] = W.tdel[2 * i];
-          x[u] = W.tdel[2 * i + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) c0[u] = D.tg_cnt0[off[u]];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {  // (guarded stores, no per-lane break: DESIGN §3)
-          const bool live = i0 + u * kWave < W.ntdel;
-          const int c = c0[u] - (x[u] >> 1);
-          const int n = (c == 0 && (x[u] & 1)) ? -1 : c;
-          const bool small = off[u] < d.tgSmall;
-          if (live && small) S.s_tcs[off[u]] = n;
-          if (live && !small) {
-            W.tg_cnt[off[u]] = n;
-            const int b = off[u] - d.tgSmall;
-            __hip_atomic_fetch_or(S.s_tcd + (b >> 5), 1u << (b & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-          }
-        }
-      }
-      hbm_release();
-    }
-    wsync();
-    for (int i = lane(); i < W.nrm; i += kWave) {  // the removed candidates (a multi-node prefix: up to 101)
-      const int n = W.rm[i];
-      __hip_atomic_fetch_or(S.s_rmv + (n >> 5), 1u << (n & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
-    hbm_release();
-  }
-  if (TL) lds_copy<8>(S.s_talloc, D.tpl_alloc, d.totalTplIts * R);
-  if (TL && pl.tsort) {
-    lds_copy<8>(S.s_tsa, D.tsort_alloc, d.totalTplIts * R);
-    lds_copy<8>(S.s_tsp, D.tsort_pos, d.totalTplIts * R);
-  }
-  S.L.nkeys = d.NK;
-  S.L.W = d.W;
-  S.L.NB = d.NB;
-  S.L.HDR = d.HDR;
-  S.L.RSW = d.RSW;
-  S.L.keys = s_keys;
-  S.L.wordValid = D.wordValid;
-  S.L.vIsInt = D.vIsInt;
-  S.L.vInt = D.vInt;
-  wsync();
-
-  // Register window: the first NW*64 nodes of the first-fit order (where every scan starts) stay in
-  // VGPRs for the whole Solve — lane l holds nodes l, l+64, ...: taints, Available, requests and
-  // flags.  A pod that fits there costs no memory round trip; commits update the owner's registers.
-  constexpr int NW = RT > 0 ? 4 : 0;
-  constexpr int NWA = NW > 0 ? NW : 1;
-  // LEAN (no negative requests): the window keeps each node's free capacity Available - requests, so
-  // Fits(requests + pod, Available) is one compare per resource; a node that can never fit (negative
-  // Available, beyond N, removed by the simulation) holds INT64_MIN, which no request (>= 0) fits.
-  constexpr bool FREEW = LEAN && SIM;  // (the Solve instantiations keep Available + requests: measured faster there)
-  constexpr int NWQ = FREEW ? 1 : NWA;
-  uint64_t wtx[NWA], wty[NWA], whp[NWA];
-  int64_t wav[NWA][RM], wrq[NWQ][RM];  // FREEW: wav = free capacity, wrq unused
-  int wnf[NWA];
-  if constexpr (MWK) mw_barrier();  // B0a: the prologue's LDS (removed-node mask) is ready for the helpers
-  if constexpr (NW > 0) {
-    if (d.N > 0) {
-#pragma unroll
-      for (int k = 0; k < (MWK ? 1 : NW); k++) {
-        const int n = k * kWave + lane(), c = n < d.N ? n : d.N - 1;
-        wtx[k] = D.n_taint[2 * c];
-        wty[k] = D.n_taint[2 * c + 1];
-        bool never = n >= d.N;
-        if (SIM) never |= S.tbit(S.s_rmv, c);
-#pragma unroll
-        for (int r = 0; r < RM; r++) {
-          const int64_t a = D.n_avail[(int64_t)c * RM + r], q = D.n_req0[(int64_t)c * RM + r];
-          if constexpr (FREEW) {
-            never |= a < 0;
-            wav[k][r] = a - q;
-          } else {
-            wav[k][r] = a;
-            wrq[k][r] = q;
-          }
-        }
-        if constexpr (FREEW)
-#pragma unroll
-          for (int r = 0; r < RM; r++) wav[k][r] = never ? INT64_MIN : wav[k][r];
-        wnf[k] = SIM ? D.n_flags[c] : 0;
-        whp[k] = D.n_hp0[c];
-      }
-    }
-  }
-  bool winUnusable = false;  // some register-window node is NF_UNUSABLE (a run's placements check it)
-  if constexpr (MWK) {  // each wave's block ballot through the mailbox
-    mb_st64(mb, MB_UMASK, d.N > 0 ? wballot(wnf[0] & NF_UNUSABLE) : 0ull);  // wave-wide store of a uniform value
-    mw_barrier();  // B0b
-#pragma unroll
-    for (int q = 0; q < kMwWaves; q++) winUnusable |= mb_ld64(mb, MB_UMASK + 2 * q) != 0;
-    winUnusable = ub(winUnusable);
-  } else if constexpr (NW > 0) {
-    if (d.N > 0)
-#pragma unroll
-      for (int k = 0; k < NW; k++) winUnusable |= wballot(wnf[k] & NF_UNUSABLE) != 0;
-  }
-  int mwseq = 0;
-  // MW: post a window step to the helpers (wave-wide stores of uniform values), then B1
-  auto mw_post = [&](int cmd, int m, const int64_t* fpp, uint64_t ft0, uint64_t ft1, int fpf) {
-    mb[MB_M] = (uint32_t)m;
-    mb[MB_FPF] = (uint32_t)fpf;
-    mb_st64(mb, MB_FT0, ft0);
-    mb_st64(mb, MB_FT1, ft1);
-#pragma unroll
-    for (int r = 0; r < RM; r++) mb_st64(mb, MB_FP + 2 * r, (uint64_t)fpp[r]);
-    mb[MB_SEQ] = (uint32_t)++mwseq;
-    mb[MB_CMD] = (uint32_t)cmd;
-    mw_barrier();  // B1
-  };
-  // MW: block 0's first-fit ballot, then every block's (B2); returns the first block holding a fit
-  auto mw_fit = [&](const int64_t* fpp, uint64_t ft0, uint64_t ft1, uint64_t& mj) {
-    mw_post(MW_FIT, 0, fpp, ft0, ft1, 0);
-    bool ok = (((wtx[0] & ~ft0) | (wty[0] & ~ft1)) == 0);
-#pragma unroll
-    for (int r = 0; r < RM; r++) ok &= fpp[r] <= wav[0][r];
-    mb_st64(mb, MB_MASK, wballot(ok));
-    mw_barrier();  // B2
-    return mw_first_fit(mb, mj);
-  };
-  int nclaims = 0, nlog = 0, hostCtr = SIM ? 0 : d.hostnameSeed;
-  bool allSched = true;  // SIM: AllNonPendingPodsScheduled so far (pods placed on unusable nodes)
-  int nrs = 0;           // SIM: compact node-requirement slots in use
-  bool srt = true;      // s.newNodeClaims non-decreasing in len(Pods)
-  bool pushed = false;  // a failed pod was pushed back since the last window refill
-  bool ident = true;    // no pod was pushed back yet (refill reads the pods' first states directly)
-  uint32_t epoch = 1;
-  int qhead = 0, qlen = P;
-  int wn = 0, wi = 0;  // window size / next index
-  int64_t pops = 0, sorts = 0, slow = 0, exact = 0, windows = 0, fulls = 0, fullFails = 0, runs = 0, runPods = 0;
-  // Every pop either places a pod, relaxes it, or marks it stale; the reference's queue can cycle
-  // O(P^2) in adversarial inputs, far beyond any realistic batch.  Bound it so a logic error ends the
-  // kernel with KE_ITER_CAP instead of hanging the device.
-  const int64_t popCap = (int64_t)64 * (d.S + P) + 100000;
-  int err = KE_OK;
-  Window<RT> w;
-  int64_t pod[RM];
-  int64_t req[RM];
-  int nthr[RM];
-#ifdef KS_PHASE_STATS
-  uint64_t cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t tstart = __builtin_amdgcn_s_memtime();
-#endif
-
-  while (true) {
-    qlen = UI(qlen);
-    qhead = UI(qhead);
-    wi = UI(wi);
-    wn = UI(wn);
-    if (qlen <= 0) break;
-    PH_BEGIN(t0);
-    if (wi == wn) {
-      PH_BEGIN(tr);
-      S.refill(w, qhead, qlen, P, pushed, ident);
-      if (FREEW) SPHS_END(S, tr, 0);  // simulation fast path (stats build): window refills
-      pushed = false;
-      wn = qlen < kWave ? qlen : kWave;
-      wi = 0;
-      windows++;
-    }
-    if constexpr (FREEW && NW > 0) {
-      // Fast path of a simulation over resource-only pods (what consolidation re-schedules): while the
-      // next pops each fit a node of the register window, the step is Queue.Pop + the window's
-      // first-fit ballots + the commit to the owner lane's registers, with nothing else live.  A pod
-      // that fits no window node (or a stale queue) leaves it un-popped for the general step below.
-      // (A simulation's placements are not read back -- its record is -- so nothing is logged here.)
-      if (d.N > 0) {
-        while (wi < wn) {
-          const uint64_t fll = (uint64_t)rdl64((int64_t)w.ll, wi);
-          if ((uint32_t)(fll >> 32) == epoch && (uint32_t)fll == (uint32_t)qlen) break;
-          const uint64_t ft0 = (uint64_t)rdl64((int64_t)w.tol0, wi), ft1 = (uint64_t)rdl64((int64_t)w.tol1, wi);
-          const int fpf = rdl(w.pf, wi);
-          int64_t fp[RM];
-#pragma unroll
-          for (int r = 0; r < RM; r++) fp[r] = rdl64(w.req[r], wi);
-          // A run of identical pods (same requests, tolerations and provisionable flag, none stale when it is
-          // popped): pod after pod, first-fit fills the window's nodes in order, each taking as many as fit (min
-          // over resources of floor(free / request)), so the whole run is placed in one step -- per node its
-          // capacity for the run, an exclusive scan over the node order, each node's share.  While no pod was
-          // pushed back (ident) the queue is the NewQueue order and the run is k_sim_run_len's count at this
-          // position, which may reach past the window; otherwise the identical, non-stale pods that follow in
-          // the window.
-          int m;
-          if (ident) {
-            m = rdl(w.rl, wi);
-            m = m < qlen ? m : qlen;
-          } else {
-            bool inrun = false;
-            if (lane() >= wi && lane() < wn) {
-              bool same = w.tol0 == ft0 && w.tol1 == ft1 && ((w.pf ^ fpf) & PF_PROVISIONABLE) == 0;
-#pragma unroll
-              for (int r = 0; r < RM; r++) same &= w.req[r] == fp[r];
-              const uint32_t qx = (uint32_t)(qlen - (lane() - wi));
-              inrun = same && !((uint32_t)(w.ll >> 32) == epoch && (uint32_t)w.ll == qx);
-            }
-            const uint64_t nr = wballot(!inrun) & (~0ull << wi);
-            m = (nr ? ctz64(nr) : kWave) - wi;
-          }
-          m = uni(m);
-          if (m >= KS_RUN_MIN) {
-            PH_BEGIN(tb);
-            float rq[RM];
-#pragma unroll
-            for (int r = 0; r < RM; r++) rq[r] = run_rcp(fp[r]);
-            int placed = 0;
-            bool unusable = false;
-            int ab = 0;  // sum over the run's pods of their node's position + 1 (< 2^31 below 8M pods per run)
-            if constexpr (MWK) {
-              // block 0 here, blocks 1..3 on the helpers; the blocks' totals give each its base
-              mw_post(MW_RUN, m, fp, ft0, ft1, fpf);
-              const bool tol = (((wtx[0] & ~ft0) | (wty[0] & ~ft1)) == 0);
-              int cap = tol ? m : 0;
-#pragma unroll
-              for (int r = 0; r < RM; r++) {
-                const int c = run_cap(wav[0][r], fp[r], rq[r], m);
-                cap = c < cap ? c : cap;
-              }
-              const int incl = wscan_add(cap);
-              mb[MB_TOT] = (uint32_t)rdl(incl, kWave - 1);  // wave-wide store of a uniform value
-              mw_barrier();  // B2
-              int tot = 0;
-#pragma unroll
-              for (int q = 0; q < kMwWaves; q++) tot += (int)mb[MB_TOT + q];
-              tot = uni(tot);
-              placed = tot < m ? tot : m;
-              // (placed == 0: every block's capacity is 0, so every share below is 0)
-              const int p0 = incl - cap, room = m - p0;
-              const int tk0 = room <= 0 ? 0 : (cap < room ? cap : room);
-#pragma unroll
-              for (int r = 0; r < RM; r++) wav[0][r] -= (int64_t)tk0 * fp[r];
-              unusable = tk0 > 0 && (wnf[0] & NF_UNUSABLE);
-              ab = tk0 * (lane() + 1);
-              if (placed == 0) break;  // pod wi fits no window node: the general step
-            } else {
-              int tk[NWA];
-              int base = 0, nb = 0;  // nb: the window blocks the run reaches (the rest take nothing)
-#pragma unroll
-              for (int k = 0; k < NW; k++) {
-                tk[k] = 0;
-                if (base < m) {
-                  nb = k + 1;
-                  const bool tol = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
-                  int cap = tol ? m : 0;
-#pragma unroll
-                  for (int r = 0; r < RM; r++) {
-                    const int c = run_cap(wav[k][r], fp[r], rq[r], m);
-                    cap = c < cap ? c : cap;
-                  }
-                  const int incl = wscan_add(cap);
-                  const int p0 = base + incl - cap, room = m - p0;
-                  tk[k] = room <= 0 ? 0 : (cap < room ? cap : room);
-                  base += rdl(incl, kWave - 1);
-                }
-              }
-              placed = base < m ? base : m;
-              if (placed == 0) break;  // pod wi fits no window node: the general step
-              // commit: each node's share, in the blocks the run reached (branch-free per lane: tk = 0 leaves a
-              // node unchanged)
-#pragma unroll
-              for (int k = 0; k < NW; k++) {
-                if (k < nb) {
-#pragma unroll
-                  for (int r = 0; r < RM; r++) wav[k][r] -= (int64_t)tk[k] * fp[r];
-                  unusable = unusable || (tk[k] > 0 && (wnf[k] & NF_UNUSABLE));
-                  ab += tk[k] * (k * kWave + lane() + 1);
-                }
-              }
-            }
-            // AllNonPendingPodsScheduled: a non-provisionable pod on an unusable node (helpers.go:118-124)
-            if (winUnusable && !(fpf & PF_PROVISIONABLE) && wballot(unusable)) allSched = false;
-            // a run's pods within the window that had failed before (only after a push-back) are scheduled now
-            if (!ident && lane() >= wi && lane() < wi + placed && lane() < wn && w.st == ST_FAILED)
-              W.pod_status[w.p] = ST_SCHEDULED;
-            S.algbytes += (int64_t)rdl(wscan_add(ab), kWave - 1) * (16 * R + 16);
-            nlog += placed;
-            qhead += placed;
-            if (qhead >= P) qhead -= P;
-            qlen -= placed;
-            pops += placed;
-            wi += placed;
-            if (wi > wn) wi = wn;  // the run reached past the window: refill at the loop head
-            runs++;
-            runPods += placed;
-            SPHS_END(S, tb, 1);  // (stats build): runs placed in one step
-            if (placed < m) break;  // the next pod of the run fits no window node
-            continue;
-          }
-          int kj = -1;
-          uint64_t mj = 0;
-          if constexpr (MWK) {
-            kj = mw_fit(fp, ft0, ft1, mj);
-          } else {
-#pragma unroll
-            for (int k = 0; k < NW; k++) {
-              bool ok = (((wtx[k] & ~ft0) | (wty[k] & ~ft1)) == 0);
-#pragma unroll
-              for (int r = 0; r < RM; r++) ok &= fp[r] <= wav[k][r];
-              const uint64_t m = wballot(ok);
-              if (m) {
-                kj = k;
-                mj = m;
-                break;
-              }
-            }
-          }
-          if (kj < 0) break;
-          const int fpod = rdl(w.p, wi);
-          const int j = kj * kWave + ctz64(mj), owner = j & (kWave - 1);
-          int nfv = 0;
-          if constexpr (MWK) {  // block 0 commits here, the helper owning block kj commits there
-            const bool own = kj == 0 && lane() == owner;
-#pragma unroll
-            for (int r = 0; r < RM; r++) wav[0][r] -= own ? fp[r] : 0;
-            nfv = ((mb_ld64(mb, MB_UMASK + 2 * kj) >> owner) & 1ull) ? NF_UNUSABLE : 0;
-          } else {
-#pragma unroll
-            for (int k = 0; k < NW; k++)
-              if (k == kj) {
-                nfv = wnf[k];
-                if (lane() == owner)
-#pragma unroll
-                  for (int r = 0; r < RM; r++) wav[k][r] -= fp[r];
-              }
-          }
-          if ((rdl(nfv, owner) & NF_UNUSABLE) && !(fpf & PF_PROVISIONABLE)) allSched = false;
-          if (rdl(w.st, wi) == ST_FAILED) W.pod_status[fpod] = ST_SCHEDULED;  // (wave-wide, uniform)
-          nlog++;
-          S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
-          qhead = qhead + 1 == P ? 0 : qhead + 1;
-          qlen--;
-          pops++;
-          wi++;
-        }
-        if (wi == wn) continue;  // window drained: refill (or finish) at the loop head
-      }
-    }
-    // Queue.Pop (queue.go:46-61)
-    const int p = rdl(w.p, wi);
-    const int g = SIM ? rdl(w.g, wi) : p;
-    const int uid = rdl(w.uid, wi);
-    uint64_t ll = (uint64_t)rdl64((int64_t)w.ll, wi);
-    if (S.dupU()) {
-      hbm_release();
-      ll = uni64((int64_t)ld_sc1(W.last_len + uid));
-    }
-    if (U((uint32_t)(ll >> 32) == epoch && (uint32_t)ll == (uint32_t)qlen)) break;
-    qhead = qhead + 1 == P ? 0 : qhead + 1;
-    qlen--;
-    if (++pops > popCap) { err = KE_ITER_CAP; break; }
-    const int64_t abPop = S.algbytes;  // (claim runs: one pod's algorithmic bytes)
-    const int s = rdl(w.s, wi);
-    const int sflags = rdl(w.flags, wi);
-    const uint32_t toltpl = (uint32_t)rdl((int)w.toltpl, wi);
-    const uint64_t tol0 = (uint64_t)rdl64((int64_t)w.tol0, wi), tol1 = (uint64_t)rdl64((int64_t)w.tol1, wi);
-    if (S.hpA()) {
-      S.cur_hpc = (uint64_t)rdl64((int64_t)w.hpc, wi);
-      S.cur_hpu = (uint64_t)rdl64((int64_t)w.hpu, wi);
-      S.cur_hpo = (uint64_t)rdl64((int64_t)w.hpo, wi);
-    }
-    if (S.volA()) S.cur_vm = (uint64_t)rdl64((int64_t)w.vm, wi);
-    if (S.keys(sflags)) {  // the state's record, read by every check of this pop
-      S.copy_words(S.s_pin, D.st_rs + (int64_t)s * d.RSW, d.RSW);
-      S.fnp = d.fnOn ? D.st_fn + (int64_t)uni(D.st_fnrow[s]) * ((d.N + 31) >> 5) : nullptr;
-      wsync();
-    }
-    if (TOPO)
-      S.topo_pop(s, SIM ? rdl(w.g, wi) : rdl(w.p, wi), (uint64_t)rdl64((int64_t)w.tsel, wi),
-                 (uint64_t)rdl64((int64_t)w.tinv, wi), (uint64_t)rdl64((int64_t)w.town, wi),
-                 (uint64_t)rdl64((int64_t)w.trss, wi));
-#pragma unroll
-    for (int r = 0; r < RM; r++) {
-      if (RT == 0 && r >= R) break;
-      pod[r] = rdl64(w.req[r], wi);
-    }
-    wi++;
-    PH_END(t0, 0);
-    bool placed = false;
-    // 1) existing nodes in order (none can pass when a matching group admits no domain)
-    PH_BEGIN(t1);
-    // (unlabelled nodes choose their domain from their requirements: no shortcut then)
-    const bool skipNodes = TOPO && S.t_nonode && !d.tgUnlab;
-    int scanFrom = 0;
-    if constexpr (NW > 0) {
-      // (problems with unlabelled nodes scan every node through node_okK, which handles them)
-      if (d.N > 0 && !skipNodes && !(TOPO && d.tgUnlab)) {
-        int kj = -1;
-        uint64_t mj = 0;
-        asm volatile("; KS_MARK window_begin");
-        if constexpr (MWK) kj = mw_fit(pod, tol0, tol1, mj);  // (LEAN: no host ports, volumes, keys)
-#pragma unroll
-        for (int k = 0; k < (MWK ? 0 : NW); k++) {
-          const int n = k * kWave + lane();
-          bool ok = (((wtx[k] & ~tol0) | (wty[k] & ~tol1)) == 0);
-          if constexpr (FREEW) {
-#pragma unroll
-            for (int r = 0; r < RM; r++) ok &= pod[r] <= wav[k][r];
-          } else {
-            ok &= n < d.N;
-            if (SIM) ok &= !S.tbit(S.s_rmv, n < d.N ? n : 0);
-#pragma unroll
-            for (int r = 0; r < RM; r++) ok &= (wav[k][r] >= 0) & (wrq[k][r] + pod[r] <= wav[k][r]);
-          }
-          ok &= (whp[k] & S.cur_hpc) == 0;
-          if (S.volA() && S.cur_vm && ok) ok = S.vol_ok(n);
-          if (S.keys(sflags) && ok) ok = S.node_compat(n);
-          if (TOPO && S.t_any && ok) {  // every node is labelled here
-            int cn = n < d.N ? n : d.N - 1;
-            bool sl;
-            S.template topo_node_stateK<1>(&cn, &ok, &sl);
-          }
-          const uint64_t m = wballot(ok);
-          if (m) {
-            kj = k;
-            mj = m;
-            break;
-          }
-        }
-        asm volatile("; KS_MARK window_end");
-        if (U(kj >= 0)) {
-          const int j = kj * kWave + ctz64(mj), owner = j & (kWave - 1);
-          int nfv = 0;
-          if constexpr (MWK) {
-            const bool own = kj == 0 && lane() == owner;
-#pragma unroll
-            for (int r = 0; r < RM; r++) wav[0][r] -= own ? pod[r] : 0;
-            nfv = ((mb_ld64(mb, MB_UMASK + 2 * kj) >> owner) & 1ull) ? NF_UNUSABLE : 0;
-          }
-#pragma unroll
-          for (int k = 0; k < (MWK ? 0 : NW); k++)
-            if (k == kj) {
-              nfv = wnf[k];
-              if (lane() == owner) {
-#pragma unroll
-                for (int r = 0; r < RM; r++) {
-                  if constexpr (FREEW) wav[k][r] -= pod[r];
-                  else wrq[k][r] += pod[r];
-                }
-                whp[k] = (whp[k] & ~S.cur_hpo) | S.cur_hpu;
-                if (S.volA() && S.cur_vm) S.vol_commit(j);
-              }
-            }
-          PH_BEGIN(t7);
-          if constexpr (SIM) {
-            if (S.keys(sflags)) S.sim_node_commit(j, s, sflags, pod, pod, nrs, true);
-            if ((rdl(nfv, owner) & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
-          } else if (S.keys(sflags) && lane() == owner) {
-            rs_add(S.L, W.n_rs + (int64_t)j * d.RSW, S.s_pin);
-            S.node_rs_changed(j);
-          }
-          if (TOPO && S.t_rec) S.topo_record(S.node_rs(j), -1, j, 0, nlog);  // existingnode.go:121
-          S.log_commit(p, -(j + 1), nlog);
-          PH_END(t7, 7);
-          S.algbytes += (int64_t)(j + 1) * (16 * R + 16);
-          placed = true;
-        } else {
-          S.algbytes += (int64_t)min(NW * kWave, d.N) * (16 * R + 16);
-        }
-        scanFrom = NW * kWave;
-      }
-    }
-    for (int base = skipNodes ? d.N : scanFrom; U(base < d.N && !placed); base += KS_NODE_K * kWave) {
-      constexpr int KN = KS_NODE_K;
-      bool ok[KN], sl[KN];
-      int nf[KN];
-      int64_t q[KN][RM];
-      S.template node_okK<KN>(base + lane(), sflags, pod, tol0, tol1, ok, nf, q, sl);
-      uint64_t mk[KN];
-#pragma unroll
-      for (int i = 0; i < KN; i++) mk[i] = wballot(ok[i]);
-      int j = -1;
-      bool slowj = false;
-#pragma unroll
-      for (int i = KN - 1; i >= 0; i--)
-        if (mk[i]) j = base + i * kWave + ctz64(mk[i]);
-      if (TOPO && d.tgUnlab) {  // unlabelled nodes before the first fast fit are decided wave-wide, in order
-#pragma unroll
-        for (int i = 0; i < KN; i++) {
-          if (slowj) break;
-          uint64_t sm = wballot(sl[i]);
-          const uint64_t fm = mk[i];
-          if (fm) sm &= (fm & (~fm + 1)) - 1;  // only those before this block's first fast fit
-          for (; sm && !slowj; sm &= sm - 1) {
-            const int jj = base + i * kWave + ctz64(sm);
-            if (S.node_slow(jj, s, sflags)) {
-              j = jj;
-              slowj = true;
-            }
-          }
-          if (fm) break;
-        }
-      }
-      j = UI(j);
-      if (j >= 0) {
-        const int hi = (j - base) >> 6;  // the block of the step holding node j
-        S.algbytes += (int64_t)(j - base + 1) * (16 * R + 16);
-        PH_BEGIN(t7);
-        const int fl = slowj ? (sflags & ~SF_HAS_KEYS) : sflags;  // node_slow's record replaces rs_add
-        if constexpr (SIM) {
-          int64_t qs[RM];
-          int nfs = 0;
-#pragma unroll
-          for (int i = 0; i < KN; i++)
-            if (i == hi) {
-              nfs = nf[i];
-#pragma unroll
-              for (int r = 0; r < RM; r++) qs[r] = q[i][r];
-            }
-          S.sim_node_commit(j, s, fl, pod, qs, nrs, false);
-          const int nfj = rdl(nfs, j & (kWave - 1));
-          if ((nfj & NF_UNUSABLE) && !(rdl(w.pf, wi - 1) & PF_PROVISIONABLE)) allSched = false;
-        } else if (lane() == (j & (kWave - 1))) {
-          S.node_commit(j, s, fl, pod);  // the owner lane of node j
-        }
-        if (TOPO && slowj) {
-          S.node_store_rs(j, nrs);
-          if (S.t_rec) S.topo_record(S.s_rs, -1, -1, 0, nlog);  // existingnode.go:121
-        } else if (TOPO && S.t_rec) {
-          S.topo_record(S.node_rs(j), -1, j, 0, nlog);  // existingnode.go:121
-        }
-        S.log_commit(p, -(j + 1), nlog);
-        PH_END(t7, 7);
-        placed = true;
-      } else {
-        S.algbytes += (int64_t)min(KN * kWave, d.N - base) * (16 * R + 16);
-      }
-    }
-    PH_END(t1, 1);
-    // A simulation's pod one of whose (non-hostname) groups admits no domain at all (t_nonode) fails every
-    // NodeClaim too: the claims' domain choices are a subset of the domains topo_pop already found empty
-    // (nextDomainTopologySpread / Affinity / AntiAffinity over fewer values), and a failed topo_apply has no
-    // side effect.  Simulations render no messages, so only the NewNodeClaim calls are counted (the
-    // record's RF_HOSTINCR).  The claim re-sort of this add() still runs: s.newNodeClaims' order after the last
-    // add() is what NewNodeClaims[0] of the record reads.
-    const bool simNoClaim = SIM && TOPO && S.t_nonode && d.NTPL > 0;
-    // 2) in-flight NodeClaims, sorted by pod count
-    if (U(!placed && nclaims > 0)) {
-      PH_BEGIN(t2);
-      sorts++;
-      if (!U(srt)) {
-        exact += S.sort_claims(nclaims);
-        slow++;
-        srt = true;
-      }
-      PH_END(t2, 2);
-      for (int base = 0; U(base < nclaims && !placed && !simNoClaim); base += kWave) {
-        PH_BEGIN(t3);
-        const int j = base + lane();
-        const bool q = j < nclaims && S.claim_quick(j, s, sflags, toltpl, pod);
-        uint64_t m = wballot(q);
-        S.algbytes += (int64_t)min(kWave, nclaims - base) * (8 * R + 4);
-        PH_END(t3, 3);
-        while (U(m != 0 && !placed)) {
-          const int jj = base + ctz64(m);
-          m &= m - 1;
-          const int c = uni(S.s_order[jj]);
-          PH_BEGIN(t4);
-          const bool inl = c < pl.KL;
-          int ncnt = 0;
-          const bool ok = U(inl ? S.template claim_full<true>(c, s, sflags, pod, req, nthr, ncnt)
-                                 : S.template claim_full<false>(c, s, sflags, pod, req, nthr, ncnt));
-          fulls++;
-          PH_END(t4, 4);
-          PH_BEGIN(t5);
-          if (ok) {
-            srt = U(inl ? S.template commit_claim<true>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog)
-                         : S.template commit_claim<false>(c, jj, nclaims, p, sflags, pod, req, nthr, ncnt, nlog));
-            placed = true;
-            if constexpr (LEAN && !SIM && KS_CLAIM_RUNS) {
-              // the identical pods that follow land here too (claim_run_cap): placed in one step
-              if (srt && wi < wn) {
-                bool inrun = false;
-                if (lane() >= wi && lane() < wn) {
-                  bool same = (uint32_t)w.toltpl == toltpl && w.tol0 == tol0 && w.tol1 == tol1;
-#pragma unroll
-                  for (int r = 0; r < RM; r++) {
-                    if (RT == 0 && r >= R) break;
-                    same &= w.req[r] == pod[r];
-                  }
-                  const uint32_t qx = (uint32_t)(qlen - (lane() - wi));
-                  inrun = same && !((uint32_t)(w.ll >> 32) == epoch && (uint32_t)w.ll == qx);
-                }
-                const uint64_t nr = wballot(!inrun) & (~0ull << wi);
-                const int m = (nr ? ctz64(nr) : kWave) - wi;
-                if (m > 0) {
-                  const int cj = uni(S.s_okey[jj]);
-                  const int nx = jj + 1 < nclaims ? uni(S.s_okey[jj + 1]) : 0x3fffffff;
-                  const int M = m < nx - cj + 1 ? m : nx - cj + 1;
-                  const int k = inl ? S.template claim_run_cap<true>(c, pod, M) : S.template claim_run_cap<false>(c, pod, M);
-                  if (k > 0) {
-                    int64_t podk[RM];
-#pragma unroll
-                    for (int r = 0; r < RM; r++) podk[r] = (int64_t)k * pod[r];
-                    const int64_t ab0 = S.algbytes;
-                    int kcnt = 0;
-                    if (inl) (void)S.template claim_full<true>(c, s, sflags, podk, req, nthr, kcnt);
-                    else (void)S.template claim_full<false>(c, s, sflags, podk, req, nthr, kcnt);
-                    srt = inl ? S.template commit_bulk<true>(c, jj, nclaims, k, podk, req, nthr, kcnt)
-                              : S.template commit_bulk<false>(c, jj, nclaims, k, podk, req, nthr, kcnt);
-                    S.algbytes = ab0 + (int64_t)k * (ab0 - abPop);  // each pod scanned as the first one did
-                    const int src = wi + lane() < kWave ? wi + lane() : kWave - 1;
-                    S.log_batch(k, __shfl(w.p, src), c, nlog);
-                    qhead += k;
-                    if (qhead >= P) qhead -= P;
-                    qlen -= k;
-                    pops += k;
-                    wi += k;
-                    runs++;
-                    runPods += k;
-                  }
-                }
-              }
-            }
-          } else {
-            // the quick bound was stale: tighten it to the exact max over the current options
-            fullFails++;
-            const int t = inl ? uni(S.lc.tpl[c]) : uni(W.c_tpl[c]);
-            if (inl) S.template recompute_max<true>(c, S.lc.rem + (int64_t)c * d.TW, t, jj);
-            else S.template recompute_max<false>(c, S.gc.rem + (int64_t)c * d.TW, t, jj);
-          }
-          PH_END(t5, 5);
-        }
-      }
-    }
-    // 3) new NodeClaim per template
-    if (!U(placed)) {
-      PH_BEGIN(t6);
-      const int r = U(simNoClaim) ? S.sim_template_calls(hostCtr)
-                                  : UI(S.try_templates(p, s, sflags, toltpl, pod, nclaims, nlog, hostCtr, srt));
-      PH_END(t6, 6);
-      nclaims = UI(nclaims);
-      hostCtr = UI(hostCtr);
-      srt = U(srt);
-      if (r < 0) { err = KE_CLAIM_CAP; break; }
-      if (r == 1) placed = true;
-      if (r == 2) {  // no templates: add() returns a nil error
-        W.pod_status[p] = ST_SCHEDULED;  // wave-wide store of a uniform value
-        placed = true;
-      }
-    }
-    if (U(placed)) {
-      // SIM: the epilogue reads the final status; only a pod that failed before needs a store
-      if (SIM && rdl(w.st, wi - 1) == ST_FAILED) W.pod_status[p] = ST_SCHEDULED;  // (wave-wide, uniform)
-      continue;
-    }
-    // failure: Preferences.Relax (preferences.go:38) + Queue.Push (queue.go:64-71)
-    if (SIM && ident) S.sim_queue_init(P);  // the simulation's first push-back: its queue state, lazily
-    const int s0 = D.pod_state0[g], ns = D.pod_nstate[g];
-    const bool relaxed = U(s - s0 + 1 < ns);
-    W.pod_status[p] = ST_FAILED;  // wave-wide stores of uniform values
-    W.pod_fstate[p] = s;
-    if (relaxed) W.pod_state[p] = s + 1;
-    if (relaxed) epoch++;
-    if (TOPO && relaxed) S.topo_activate_state(s + 1, nclaims, hostCtr);  // Topology.Update (scheduler.go:160-170)
-    int tail = qhead + qlen;
-    if (tail >= P) tail -= P;
-    W.queue[tail] = p;  // wave-wide store of a uniform value
-    qlen++;
-    pushed = true;
-    ident = false;
-    if (!relaxed) W.last_len[uid] = ((uint64_t)epoch << 32) | (uint32_t)qlen;  // (wave-wide, uniform)
-  }
-  if constexpr (MWK) {  // the helpers' contributions, then they leave
-    mw_post(MW_EXIT, 0, pod, 0, 0, 0);
-    mw_barrier();  // B2
-    bool hall = true;
-    int64_t hab = 0;
-#pragma unroll
-    for (int q = 1; q < kMwWaves; q++) {
-      hall = hall && mb[MB_ALL + q] != 0;
-      hab += (int64_t)mb_ld64(mb, MB_AB + 2 * q);
-    }
-    allSched = allSched && ub(hall);
-    S.algbytes += uni64(hab);
-  }
-  S.log_flush(nlog);
-  // write back LDS-resident claim state for the host
-  for (int i = lane(); i < nclaims; i += kWave) W.order[i] = S.s_order[i];
-  const int kl = nclaims < pl.KL ? nclaims : pl.KL;
-  for (int i = lane(); i < kl * R; i += kWave) W.c_req[i] = S.lc.req[i];
-  for (int i = lane(); i < kl * d.TW; i += kWave) W.c_rem[i] = S.lc.rem[i];
-  if (lane() == 0) {
-    W.counters[CT_NCLAIMS] = nclaims;
-    W.counters[CT_NLOG] = nlog;
-    W.counters[CT_HOSTCTR] = hostCtr;
-    W.counters[CT_ERROR] = err;
-    W.counters[CT_POPS] = pops;
-    W.counters[CT_ALGBYTES] = S.algbytes;
-    W.counters[CT_SORTS] = sorts;
-    W.counters[CT_SORT_SLOW] = slow;
-    W.counters[CT_CLAIM_FULL] = fulls;
-    W.counters[CT_CLAIM_QUICK_FAIL] = fullFails;
-    W.counters[CT_WINDOWS] = windows;
-    W.counters[CT_RUNS] = runs;
-    W.counters[CT_RUN_PODS] = runPods;
-    W.counters[CT_SORT_EXACT] = exact;
-#ifdef KS_PHASE_STATS
-    for (int i = 0; i < 7; i++) W.counters[CT_CYC_POP + i] = (int64_t)cyc[i];
-    W.counters[CT_CYC_TOTAL] = (int64_t)(__builtin_amdgcn_s_memtime() - tstart);
-    W.counters[CT_CYC_NCOMMIT] = (int64_t)cyc[7];
-    for (int i = 0; i < 4; i++) W.counters[CT_CYC_SUB + i] = (int64_t)S.scyc[i];
-#endif
-  }
-  if constexpr (SIM) S.sim_record(P, nclaims, hostCtr, allSched, err, !ident);
 }
 
 // Every translation unit instantiates one k_solve family (KS_TU 0: Solve, 1: Solve + topology,
@@ -3403,6 +2624,7 @@ hipError_t launch_solve_topo(const KsDev& D, const KsWork* w, int n, const Plan&
 hipError_t launch_sims_plain(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
 hipError_t launch_sims_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
 hipError_t launch_sims_mw(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
+hipError_t launch_sims_mixed(const KsDev& D, const KsWork* w, int n, int nmw, const Plan& pl, hipStream_t st);
 
 #if KS_TU == 1
 hipError_t launch_solve_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
@@ -3411,6 +2633,22 @@ hipError_t launch_solve_topo(const KsDev& D, const KsWork* w, int n, const Plan&
 #elif KS_TU == 2
 hipError_t launch_sims_plain(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st) {
   return launch_family<true, false>(D, w, n, pl, st);
+}
+// One mixed launch (k_sim_mixed): the first nmw simulations on 4-wave workgroups, the rest four to a workgroup.
+// hipErrorNotSupported when four LDS slices do not fit a CU (the caller falls back to two launches).
+hipError_t launch_sims_mixed(const KsDev& D, const KsWork* w, int n, int nmw, const Plan& pl, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const size_t stride = (pl.lds + 15) & ~(size_t)15;
+  const size_t lds = std::max(pl.lds + kMwBytes, (size_t)kMwWaves * stride);
+  if (D.d.G || !D.d.lean || !pl.talloc || D.d.N <= 0 || lds > 160 * 1024) return hipErrorNotSupported;
+  const int grid = nmw + (n - nmw + kMwWaves - 1) / kMwWaves;
+  const dim3 blk(kMwWaves * kWave);
+  switch (D.d.R) {
+    case 3: hipLaunchKernelGGL((k_sim_mixed<3>), dim3(grid), blk, lds, st, D, w, pl, nmw, n, (int)stride); break;
+    case 4: hipLaunchKernelGGL((k_sim_mixed<4>), dim3(grid), blk, lds, st, D, w, pl, nmw, n, (int)stride); break;
+    default: return hipErrorNotSupported;
+  }
+  return hipGetLastError();
 }
 // The long simulations on 4-wave workgroups (MW): resource-only pods with the window in free-capacity form
 // (the LEAN instantiations); hipErrorNotSupported for other problems (the caller runs them single-wave).
@@ -3554,6 +2792,9 @@ hipError_t launch_sims_split(const KsDev& D, const KsWork* works_dev, int nsims,
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
   if (D.d.fmOn) launch_feasibility(D, st);
   if (D.d.fnOn) launch_feasibility_nodes(D, st);
+  // one launch when four simulations' LDS fit a workgroup: the long ones are dispatched first
+  const hipError_t em = launch_sims_mixed(D, works_dev, nsims, nmw, pl, st);
+  if (em != hipErrorNotSupported) return em;
   hipError_t e = hipEventRecord(fork, st);
   if (e == hipSuccess) e = hipStreamWaitEvent(st2, fork, 0);
   if (e == hipSuccess) e = launch_sims_mw(D, works_dev, nmw, pl, st2);
