@@ -48,7 +48,11 @@ def test_update_each_kind_alone():
               {"deletePods": [pend]},
               {"bindPods": [{"uid": pend, "node": node["name"]}]},
               {"removeNodes": [node["name"]]},
-              {"removeNodes": [snap["stateNodes"][0]["name"], snap["stateNodes"][-1]["name"]]}):
+              {"removeNodes": [snap["stateNodes"][0]["name"], snap["stateNodes"][-1]["name"]]},
+              # bound to a node that is removed in the same update: the pod leaves with it
+              {"bindPods": [{"uid": pend, "node": node["name"]}], "removeNodes": [node["name"]]},
+              # every pod of a node deleted: an empty candidate (cost 0) leads the order
+              {"deletePods": [p["metadata"]["uid"] for p in node["pods"]]}):
         got = inspect_consolidation_update(json.dumps(snap), d)
         want = inspect_consolidation_update(json.dumps(apply_delta(snap, d)))
         for k in ("candidates", "pendingPods", "nodeRows", "poolRemaining", "sims"):
