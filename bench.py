@@ -182,7 +182,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
             dist.all_gather_into_tensor(gathered, out)
             recs = gathered.cpu().numpy().tobytes()
         if world == 1:
-            doc = c.decide(recs, 1, candidates=False)
+            doc = c.decide(recs, 1, candidates=False, sims=False)
         else:
             # every rank holds the gathered records, so every rank knows which simulations' NodeClaim
             # requirements the decision needs; each is broadcast by the rank that ran it
@@ -196,7 +196,7 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
                     t.copy_(torch.frombuffer(bytearray(c.claim_requirements(s)), dtype=torch.int32))
                 dist.broadcast(t, src=owner)
                 table[s] = t.cpu().numpy().tobytes()
-            doc = c.decide(recs, world, fetch=table.__getitem__, candidates=False) if rank == 0 else None
+            doc = c.decide(recs, world, fetch=table.__getitem__, candidates=False, sims=False) if rank == 0 else None
         return ms, recs, doc
 
     t0 = time.perf_counter()

@@ -183,6 +183,7 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
  * and this handle's last ks_cons_run covered every simulation: the records are then read from that run. */
 #define KS_CONS_ALL_SIMS 1   /* flags: report every simulation */
 #define KS_CONS_CANDIDATES 2 /* flags: include the ordered candidate list */
+#define KS_CONS_NO_SIMS 4    /* flags: leave out the per-simulation "sims" lists (the commands are unchanged) */
 int ks_cons_requirement_words(const ks_cons* c);
 int ks_cons_needed_sims(const ks_cons* c, const void* records, int world, int flags, int32_t* out, int cap);
 int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out);

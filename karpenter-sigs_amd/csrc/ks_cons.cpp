@@ -958,7 +958,7 @@ using RsFn = std::function<const uint32_t*(int)>;
 // consults (MultiNodeConsolidation's 1 min, multinodeconsolidation.go:34,99-110; SingleNodeConsolidation's
 // 3 min, singlenodeconsolidation.go:29,58-65); null or sim_seconds 0: the clock never passes a timeout.
 std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool allSims, const RsFn& rsOf,
-                        bool withCandidates = true, const ks_cons_clock* clk = nullptr) {
+                        bool withCandidates = true, const ks_cons_clock* clk = nullptr, bool withSims = true) {
   const double simS = clk ? clk->sim_seconds : 0.0;
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
@@ -1120,7 +1120,8 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
     }
   }
   std::string multiSims;
-  for (int mid : multiRan) multiSims += (multiSims.empty() ? "" : ",") + simJSON(c.sim_of_multi(mid));
+  if (withSims)
+    for (int mid : multiRan) multiSims += (multiSims.empty() ? "" : ",") + simJSON(c.sim_of_multi(mid));
   // SingleNodeConsolidation.ComputeCommand: the first candidate whose simulation yields an action
   int singleSim = -1;
   std::string singleSims;
@@ -1135,7 +1136,7 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
     if (!timedOut) now += simS;
     const int sim = c.sim_of_single(i);
     run(sim);
-    singleSims += (i ? "," : "") + simJSON(sim);
+    if (withSims) singleSims += (i ? "," : "") + simJSON(sim);
     const int a = rec(sim)[RF_ACTION];
     if (singleSim >= 0 || timedOut || a == CA_ERROR || a == CA_NOOP) continue;
     singleSim = sim;
@@ -1786,7 +1787,9 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
       }
       return v.data();
     };
-    *json_out = strdup(decide_json(*c, recs, world, all_sims, fetch, (flags & KS_CONS_CANDIDATES) != 0, clock).c_str());
+    *json_out = strdup(decide_json(*c, recs, world, all_sims, fetch, (flags & KS_CONS_CANDIDATES) != 0, clock,
+                                   (flags & KS_CONS_NO_SIMS) == 0)
+                           .c_str());
     return KS_OK;
   }
   std::vector<int> need = needed_sims(*c, recs, world, all_sims);
@@ -1794,7 +1797,7 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
   std::map<int, const uint32_t*> table;
   for (size_t i = 0; i < need.size(); i++) table[need[i]] = rs_table + i * c->pb->host.dims.RSW;
   *json_out = strdup(decide_json(*c, recs, world, all_sims, [&](int sim) { return table.at(sim); },
-                                 (flags & KS_CONS_CANDIDATES) != 0, clock)
+                                 (flags & KS_CONS_CANDIDATES) != 0, clock, (flags & KS_CONS_NO_SIMS) == 0)
                          .c_str());
   return KS_OK;
   API_CATCH

@@ -495,10 +495,11 @@ class Consolidator:
         _check(l.ks_cons_claim_requirements(self._h, sim, out))
         return bytes(out)
 
-    def decide(self, records, world=1, all_sims=False, fetch=None, candidates=True, clock=None):
+    def decide(self, records, world=1, all_sims=False, fetch=None, candidates=True, clock=None, sims=True):
         """Sequential selection over the gathered records ([rank][slot] layout, bytes).  fetch(sim)
         returns the requirement record bytes of a needed simulation (default: this handle's run);
-        candidates=False leaves out the ordered candidate list (the commands are unchanged);
+        candidates=False leaves out the ordered candidate list and sims=False the per-simulation lists (the
+        commands are unchanged);
         clock=(multi_timeout_s, single_timeout_s, sim_seconds): the methods' timeouts on a virtual clock."""
         l = _cons_lib()
         if fetch is None and world == 1:
@@ -510,7 +511,7 @@ class Consolidator:
             tbuf = ctypes.create_string_buffer(table, max(len(table), 4))
         buf = None if records is None else _records_buffer(records)  # None: the handle's own records (run(keep=True))
         js = ctypes.c_void_p()
-        flags = (1 if all_sims else 0) | (2 if candidates else 0)
+        flags = (1 if all_sims else 0) | (2 if candidates else 0) | (0 if sims else 4)
         if clock is None:
             _check(l.ks_cons_decide(self._h, ctypes.cast(buf, ctypes.c_void_p), world, flags,
                                     None if tbuf is None else ctypes.cast(tbuf, ctypes.c_void_p), ctypes.byref(js)))

@@ -366,3 +366,15 @@ def test_records_kept_in_handle_gpu():
     assert none is None
     assert c.decide(None, 1, all_sims=True) == want
     assert c.alg_bytes(None) == wb
+
+
+def test_decide_without_sims_gpu():
+    """KS_CONS_NO_SIMS: the per-simulation lists are left out, the commands are those of the full output."""
+    snap = synth.cluster_snapshot(30, 6, n_its=40, seed=78, n_pending=2, spot_frac=0.4)
+    c = Consolidator(json.dumps(snap))
+    recs, _ = c.run(0, 1)
+    full = c.decide(recs, 1)
+    lean = c.decide(recs, 1, sims=False)
+    for m in ("multi", "single"):
+        assert lean[m]["command"] == full[m]["command"]
+        assert lean[m]["sims"] == []
