@@ -27,3 +27,14 @@ for _ in range(20):
 med = lambda i: sorted(r[i] for r in rows)[len(rows) // 2]  # noqa: E731
 print("run wall %.3f ms (kernel events %.3f ms) | needed_sims %.3f ms (%d sims) | decide %.3f ms (doc %d B)" % (
     med(0), med(1), med(2), rows[-1][4], med(3), rows[-1][5]))
+# the bench's pass (world 1): records kept in the handle's pinned buffer, decide without the per-simulation lists
+rows = []
+for _ in range(30):
+    t0 = time.perf_counter()
+    _, k = c.run(0, 1, keep=True)
+    t1 = time.perf_counter()
+    doc = c.decide(None, 1, candidates=False, sims=False)
+    t2 = time.perf_counter()
+    rows.append(((t1 - t0) * 1e3, k, (t2 - t1) * 1e3, len(json.dumps(doc))))
+print("bench pass: run(keep) wall %.3f ms (kernel events %.3f ms) | decide(sims=False) %.3f ms (doc %d B)" % (
+    med(0), med(1), med(2), rows[-1][3]))
