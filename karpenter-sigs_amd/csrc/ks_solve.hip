@@ -806,7 +806,7 @@ struct Solver {
   // false then).
   template <int KN>
   __device__ __forceinline__ void node_okK(int n0, int sflags, const int64_t* pod, uint64_t tol0, uint64_t tol1,
-                                           bool* ok, int* nf, int64_t (*q)[RM], bool* sl) const {
+                                           bool* ok, int* nf, int64_t (*q)[RM], bool* sl, bool* rk) const {
     int c[KN];
     uint64_t tx[KN], ty[KN], h[KN];
     int64_t a[KN][RM];
@@ -832,13 +832,15 @@ struct Solver {
     }
 #pragma unroll
     for (int i = 0; i < KN; i++) {
-      ok[i] = (n0 + i * kWave < d.N) & (((tx[i] & ~tol0) | (ty[i] & ~tol1)) == 0) & ((h[i] & cur_hpc) == 0);  // Taints.Tolerates
-      if (SIM) ok[i] &= !tbit(s_rmv, c[i]);  // the simulation removed these candidates
+      bool rr = n0 + i * kWave < d.N;
+      if (SIM) rr &= !tbit(s_rmv, c[i]);  // the simulation removed these candidates
 #pragma unroll
       for (int r = 0; r < RM; r++) {  // Fits(requests + pod, Available())
         if (RT == 0 && r >= d.R) break;
-        ok[i] &= (a[i][r] >= 0) & (q[i][r] + pod[r] <= a[i][r]);
+        rr &= (a[i][r] >= 0) & (q[i][r] + pod[r] <= a[i][r]);
       }
+      rk[i] = rr;  // (permanent for these requests: the caller's resource-failing prefix)
+      ok[i] = rr & (((tx[i] & ~tol0) | (ty[i] & ~tol1)) == 0) & ((h[i] & cur_hpc) == 0);  // Taints.Tolerates
       if (volA() && cur_vm && ok[i]) ok[i] = vol_ok(c[i]);
       if (keys(sflags) && ok[i]) ok[i] = node_compat(c[i]);  // strict Compatible
       sl[i] = false;
