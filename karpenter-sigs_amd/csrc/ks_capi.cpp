@@ -25,7 +25,7 @@ namespace {
 
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
-      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, n_vm, n_vc, tg_cnt,
+      log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, n_vc, vlog, vspec, tg_cnt,
       tg_ccnt, tg_cpos, fail_rs, log_hg, tg_act, total;
   int32_t ccs;  // tg_ccnt row stride
 };
@@ -60,8 +60,9 @@ WorkLayout work_layout(const KsDims& d) {
   w.counters = a.add(8 * CT_NCOUNTERS);
   w.n_hp = a.add(8 * N);
   w.c_hp = a.add(8 * K);
-  w.n_vm = a.add(d.volAny ? 8 * N : 8);
-  w.n_vc = a.add(d.volAny ? 4 * N * d.VD : 4);
+  w.n_vc = a.add(d.volAny ? 4 * N * std::max(d.VD, 1) : 4);
+  w.vlog = a.add(8 * (size_t)std::max(d.vLogCap, 1));
+  w.vspec = a.add(8 * (size_t)std::max(d.vLogCap, 1));
   w.tg_cnt = a.add(4 * std::max<size_t>(d.G ? (size_t)d.tgCntWords : 1, 1));
   w.tg_ccnt = a.add(4 * (size_t)std::max(d.G, 1) * (d.G ? K + 1 : 1));
   w.tg_cpos = a.add(4 * (size_t)std::max(d.G, 1));
@@ -99,8 +100,10 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.counters = (int64_t*)(base + w.counters);
   k.n_hp = (uint64_t*)(base + w.n_hp);
   k.c_hp = (uint64_t*)(base + w.c_hp);
-  k.n_vm = (uint64_t*)(base + w.n_vm);
   k.n_vc = (int32_t*)(base + w.n_vc);
+  k.n_vslot = nullptr;
+  k.vlog = (int32_t*)(base + w.vlog);
+  k.vspec = (int32_t*)(base + w.vspec);
   k.tg_cnt = (int32_t*)(base + w.tg_cnt);
   k.tg_ccnt = (int32_t*)(base + w.tg_ccnt);
   k.tg_cpos = (int32_t*)(base + w.tg_cpos);
@@ -240,9 +243,13 @@ void ks_upload(ks_problem* pb) {
   size_t o_phu = put(t.pod_hpu.data(), t.pod_hpu.size() * 8);
   size_t o_pho = put(t.pod_hpo.data(), t.pod_hpo.size() * 8);
   size_t o_nhp = put(t.n_hp0.data(), t.n_hp0.size() * 8);
-  size_t o_pvm = put(t.pod_vm.data(), t.pod_vm.size() * 8);
-  size_t o_vdm = put(t.vol_dm.data(), t.vol_dm.size() * 8);
-  size_t o_nvm = put(t.n_vm0.data(), t.n_vm0.size() * 8);
+  size_t o_vdb = put(t.pod_vdbeg.data(), t.pod_vdbeg.size() * 4);
+  size_t o_vd = put(t.pod_vd.data(), t.pod_vd.size() * 4);
+  size_t o_vsb = put(t.pod_vsbeg.data(), t.pod_vsbeg.size() * 4);
+  size_t o_vs = put(t.pod_vs.data(), t.pod_vs.size() * 4);
+  size_t o_vub = put(t.pod_vubeg.data(), t.pod_vubeg.size() * 4);
+  size_t o_vu = put(t.pod_vu.data(), t.pod_vu.size() * 4);
+  size_t o_vud = put(t.vol_udrv.data(), t.vol_udrv.size() * 4);
   size_t o_nvc = put(t.n_vc0.data(), t.n_vc0.size() * 4);
   size_t o_nvl = put(t.n_vlim.data(), t.n_vlim.size() * 4);
   size_t o_tgm = put(t.tg_meta.data(), t.tg_meta.size() * 4);
@@ -381,9 +388,13 @@ void ks_upload(ks_problem* pb) {
   D.pod_hpu = (const uint64_t*)(b + o_phu);
   D.pod_hpo = (const uint64_t*)(b + o_pho);
   D.n_hp0 = (const uint64_t*)(b + o_nhp);
-  D.pod_vm = (const uint64_t*)(b + o_pvm);
-  D.vol_dm = (const uint64_t*)(b + o_vdm);
-  D.n_vm0 = (const uint64_t*)(b + o_nvm);
+  D.pod_vdbeg = (const int32_t*)(b + o_vdb);
+  D.pod_vd = (const int32_t*)(b + o_vd);
+  D.pod_vsbeg = (const int32_t*)(b + o_vsb);
+  D.pod_vs = (const int32_t*)(b + o_vs);
+  D.pod_vubeg = (const int32_t*)(b + o_vub);
+  D.pod_vu = (const int32_t*)(b + o_vu);
+  D.vol_udrv = (const int32_t*)(b + o_vud);
   D.n_vc0 = (const int32_t*)(b + o_nvc);
   D.n_vlim = (const int32_t*)(b + o_nvl);
   D.tg_meta = (const int32_t*)(b + o_tgm);
@@ -473,6 +484,33 @@ static void replay_check(const Host& h, int nc, int nl, const std::vector<int32_
       if (q != h.tab.n_req0[(size_t)n * d.R + r] && !(a >= 0 && q <= a))
         fail("node " + std::to_string(n) + " over its Available for " + h.resNames[(size_t)r]);
     }
+  // VolumeUsage: every existing node that took pods keeps each limited driver's PVC union within its limit
+  // (ExceedsLimits held at each placement and the union only grows, volumeusage.go:202-219)
+  if (d.volAny) {
+    std::vector<std::map<std::string, std::set<std::string>>> use((size_t)d.N);
+    std::vector<char> took((size_t)d.N, 0);
+    for (int i = 0; i < nl; i++) {
+      const int p = logp[(size_t)i], t = logt[(size_t)i];
+      if (t >= 0) continue;
+      const int n = -t - 1;
+      if (!took[(size_t)n]) use[(size_t)n] = h.nodes[(size_t)n].volumes;
+      took[(size_t)n] = 1;
+      const PodH& ph = h.pods[(size_t)p];
+      if (h.tab.pod_flags[(size_t)p] & PF_VOLERR) fail("pod " + std::to_string(p) + " whose GetVolumes fails placed on a node");
+      for (auto& name : ph.pvcNames) {
+        auto dv = h.volumeDrivers.find(ph.ns + "/" + name);
+        if (dv != h.volumeDrivers.end() && !dv->second.empty()) use[(size_t)n][dv->second].insert(ph.ns + "/" + name);
+      }
+    }
+    for (int n = 0; n < d.N; n++) {
+      if (!took[(size_t)n]) continue;
+      for (auto& kv : h.nodes[(size_t)n].volumeLimits) {
+        auto u = use[(size_t)n].find(kv.first);
+        if (u != use[(size_t)n].end() && (int64_t)u->second.size() > kv.second)
+          fail("node " + std::to_string(n) + " over its volume limit for " + kv.first);
+      }
+    }
+  }
   std::vector<char> seen((size_t)nc, 0);
   for (int k = 0; k < nc; k++) {
     const int c = order[(size_t)k];
@@ -1029,6 +1067,15 @@ int ks_problem_inspect(const char* json, size_t len, char** out) {
   long long nlate = 0;
   for (uint64_t x : h.tab.tg_late) nlate += __builtin_popcountll(x);
   kv("lateGroups", nlate); kv("groupWords", d.GMW); kv("unlabelledNodes", d.tgUnlab);
+  long long nfail = 0, nshared = 0, nverr = 0;
+  for (char x : h.injectFailed) nfail += x ? 1 : 0;
+  for (int32_t f : h.tab.pod_flags) {
+    nshared += (f & PF_VSHARED) ? 1 : 0;
+    nverr += (f & PF_VOLERR) ? 1 : 0;
+  }
+  kv("volAny", d.volAny); kv("volDrivers", d.VD); kv("volPvcs", d.NVU); kv("volLogCap", d.vLogCap);
+  kv("volSharedPods", nshared); kv("volErrorPods", nverr); kv("injectFailed", nfail);
+  kv("volStaticMounts", (long long)(h.tab.pod_vsbeg.empty() ? 0 : h.tab.pod_vsbeg.back()));
   // LDS plans (ks_solve.hip make_plan) at the default and a few reduced budgets
   o += ",\"plans\":{";
   const size_t budgets[] = {160 * 1024 - 256, 6000, 9000, 14000, 24000, 40000};

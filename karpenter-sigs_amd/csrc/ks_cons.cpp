@@ -446,6 +446,10 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   const std::vector<PodH>& podH = h.pods;
   pt.mark("Host::build");
   if (h.dims.dupUids) throw KsError(KS_ERR_UNSUPPORTED, "consolidation snapshot has duplicate pod UIDs");
+  // a pod whose VolumeTopology.Inject fails stays out of every simulation's NewTopology pod list
+  // (provisioner.go:432-442), which the per-simulation count offsets do not model
+  if (h.dims.G && std::find(h.injectFailed.begin(), h.injectFailed.end(), 1) != h.injectFailed.end())
+    throw KsError(KS_ERR_UNSUPPORTED, "consolidation with topology groups: a pod's volume topology injection failed");
   c.hostnameSeed = h.hostnameSeed;
   std::map<std::string, int> hostNode;  // node name -> host.nodes index (sorted order)
   for (size_t i = 0; i < h.nodes.size(); i++) hostNode[h.nodes[i].name] = (int)i;
@@ -649,7 +653,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   struct Off {
     size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
         last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price, n_hp,
-        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, tdead, n_vm, n_vc;
+        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, tdead, n_vslot, n_vc, vlog, vspec;
   };
   std::vector<Off> offs(ns);
   std::vector<int> simP(ns), entBeg(ns + 1, 0);
@@ -700,9 +704,14 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     o.rm = ai.add(4 * std::max<size_t>(sm.cands.size(), 1));
     o.pool0 = ai.add(8 * (size_t)NP * R);
     o.st_price = sm.multi ? ai.add(8 * (size_t)std::max(d.T, 1)) : 0;
-    if (d.volAny) {  // indexed by node, written only where a pod with PVCs lands (copy-on-write)
-      o.n_vm = a.add(8 * (size_t)N);
-      o.n_vc = a.add(4 * (size_t)N * std::max(d.VD, 1));
+    if (d.volAny) {  // copy-on-write rows: a node's slot is taken the first time a pod with PVCs lands there
+      int64_t vcap = 0;  // the log: every PVC of the simulation's PF_VSHARED pods, at most once per placement
+      for (int p : pods)
+        if (h.tab.pod_flags[(size_t)p] & PF_VSHARED) vcap += h.tab.pod_vubeg[(size_t)p + 1] - h.tab.pod_vubeg[(size_t)p];
+      o.n_vslot = a.add(4 * (size_t)N);
+      o.n_vc = a.add(4 * P * std::max(d.VD, 1));
+      o.vlog = a.add(8 * (size_t)std::max<int64_t>(vcap, 1));
+      o.vspec = a.add(8 * (size_t)std::max<int64_t>(vcap, 1));
     }
     if (d.G) {
       o.tg_cnt = a.add(4 * (size_t)d.tgCntWords);
@@ -884,8 +893,10 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     w.cflags = cflags;
     w.ccs = simP[k] + 1;
     if (d.volAny) {
-      w.n_vm = (uint64_t*)(base + o.n_vm);
+      w.n_vslot = (int32_t*)(base + o.n_vslot);
       w.n_vc = (int32_t*)(base + o.n_vc);
+      w.vlog = (int32_t*)(base + o.vlog);
+      w.vspec = (int32_t*)(base + o.vspec);
     }
     if (d.G) {
       w.tg_cnt = (int32_t*)(base + o.tg_cnt);

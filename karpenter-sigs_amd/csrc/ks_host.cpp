@@ -11,6 +11,7 @@
 //   InstanceType.Allocatable        pkg/cloudprovider/types.go:100-110
 //   Taints.Tolerates / ToleratesTaint pkg/scheduling/taints.go:38-50 (k8s.io/api v0.28.4)
 #include "ks_host.h"
+#include "ks_volume.h"
 
 #include <arpa/inet.h>
 #include <cstring>
@@ -605,6 +606,27 @@ void Host::build(const Value& root) {
   else parsePods(root.get("pods"), pods);
   if (auto* v = root.get("volumeDrivers"))
     for (auto& kv : v->obj()) volumeDrivers[kv.first] = kv.second.str();
+  // Provisioner.NewScheduler's injectTopology (provisioner.go:283-284,432-442) and, without an explicit
+  // "volumeDrivers" map, GetVolumes' driver resolution, both from the snapshot's PVC / PV / StorageClass
+  // objects (ks_volume.cpp)
+  std::set<std::string> volErrKeys;
+  {
+    VolumeObjects vobj;
+    vobj.parse(root);
+    injectFailed.assign(pods.size(), 0);
+    if (vobj.present) {
+      parallel_for((int)pods.size(), 256, [&](int i) { injectFailed[(size_t)i] = vobj.inject(pods[(size_t)i], nullptr) ? 0 : 1; });
+      if (!root.get("volumeDrivers"))
+        for (auto& p : pods)
+          for (auto& name : p.pvcNames) {
+            const std::string key = p.ns + "/" + name;
+            if (volumeDrivers.count(key) || volErrKeys.count(key)) continue;
+            std::string drv;
+            if (!vobj.driver(key, drv)) volErrKeys.insert(key);
+            else if (vobj.pvcs.count(key)) volumeDrivers[key] = drv;
+          }
+    }
+  }
 
   pt.mark("parse pods");
   // --- universe of keys and values
@@ -1015,10 +1037,13 @@ void Host::build(const Value& root) {
   };
   dims.hpAny = hostPortUniverse.empty() ? 0 : 1;
   // --- volume limits (ExistingNode.Add: GetVolumes + VolumeUsage.ExceedsLimits, existingnode.go:70-78).
-  // GetVolumes skips PVCs the snapshot does not resolve (NotFound) and empty drivers.  Only drivers some
-  // node limits can fail the check; their pending-pod PVCs form the universe.  Per node and driver:
-  // |usage ∪ pod| = count + |pod PVCs not yet mounted|.  A node already over a limit rejects every pod
-  // (the union always holds its own set), which the encoder folds into an unsatisfiable Available().
+  // GetVolumes skips PVCs the snapshot does not resolve (NotFound) and empty drivers; it fails for a claim
+  // bound to a PV that does not exist (volErrKeys), and then ExistingNode.Add fails on every node
+  // (PF_VOLERR).  Only drivers some node limits can fail the check; the pods' PVCs of those drivers form the
+  // universe (ids u), any number of them.  Per node and driver: |usage ∪ pod| = count + |pod PVCs not yet
+  // mounted|, where "mounted" is asked only of the pod's own PVCs (KsDev, ks_problem.h).  A node already over a
+  // limit rejects every pod (the union always holds its own set), which the encoder folds into an
+  // unsatisfiable Available().
   std::set<std::string> limited;
   for (auto& n : nodes)
     for (auto& kv : n.volumeLimits) {
@@ -1026,34 +1051,49 @@ void Host::build(const Value& root) {
         throw KsError(-2, "node " + n.name + ": volume limit out of range for driver " + kv.first);
       limited.insert(kv.first);
     }
-  auto podVolumes = [&](const PodH& p) {  // GetVolumes (volumeusage.go:82-113)
-    std::vector<std::pair<std::string, std::string>> out;  // (driver, pvc key)
+  auto podVolumes = [&](const PodH& p) {  // GetVolumes (volumeusage.go:82-113): driver -> set of PVC keys
+    std::map<std::string, std::set<std::string>> out;
     for (auto& name : p.pvcNames) {
       auto it = volumeDrivers.find(p.ns + "/" + name);
       if (it == volumeDrivers.end() || it->second.empty()) continue;
-      out.push_back({it->second, p.ns + "/" + name});
+      out[it->second].insert(p.ns + "/" + name);
     }
     return out;
   };
-  std::map<std::string, int> volBit;
-  for (auto& p : pods)
-    for (auto& dv : podVolumes(p)) {
-      if (!limited.count(dv.first) || volBit.count(dv.second)) continue;
-      if (std::find(volDrivers.begin(), volDrivers.end(), dv.first) == volDrivers.end()) volDrivers.push_back(dv.first);
-      volBit[dv.second] = (int)volUniverse.size();
-      volUniverse.push_back(dv.second);
+  std::map<std::string, int> volBit, volDrv;  // PVC key -> u; driver -> v
+  volDrivers.clear();
+  volUniverse.clear();
+  std::vector<int32_t> udrv;
+  std::vector<std::vector<int>> podU(pods.size());  // per pod: its universe PVCs
+  std::vector<std::vector<std::pair<int, int>>> podVD(pods.size());  // per pod: (v, count)
+  std::vector<char> podVolErr(pods.size(), 0);
+  for (size_t i = 0; i < pods.size(); i++) {
+    for (auto& name : pods[i].pvcNames) podVolErr[i] |= volErrKeys.count(pods[i].ns + "/" + name) ? 1 : 0;
+    for (auto& dv : podVolumes(pods[i])) {
+      if (!limited.count(dv.first)) continue;
+      auto d = volDrv.find(dv.first);
+      if (d == volDrv.end()) {
+        d = volDrv.emplace(dv.first, (int)volDrivers.size()).first;
+        volDrivers.push_back(dv.first);
+      }
+      podVD[i].push_back({d->second, (int)dv.second.size()});
+      for (auto& key : dv.second) {
+        auto b = volBit.find(key);
+        if (b == volBit.end()) {
+          b = volBit.emplace(key, (int)volUniverse.size()).first;
+          volUniverse.push_back(key);
+          udrv.push_back(d->second);
+        }
+        podU[i].push_back(b->second);
+      }
     }
-  if (volUniverse.size() > 64) throw KsError(-3, "more than 64 distinct PVCs of limited drivers in the pending pods");
-  if (volDrivers.size() > (size_t)kMaxVD) throw KsError(-3, "more than 4 limited CSI drivers in the pending pods");
-  dims.volAny = volUniverse.empty() ? 0 : 1;
-  const int VD = (int)volDrivers.size();
+  }
+  const int VD = (int)volDrivers.size(), NVU = (int)volUniverse.size();
+  if ((int64_t)std::max(N, 1) * std::max(VD, 1) > INT32_MAX / 2) throw KsError(-3, "volume count table exceeds 2^30 entries");
   dims.VD = VD;
-  tab.vol_dm.assign(std::max(VD, 1), 0);
-  for (int v = 0; v < VD; v++)
-    for (auto& p : pods)
-      for (auto& dv : podVolumes(p))
-        if (dv.first == volDrivers[v]) tab.vol_dm[v] |= 1ull << volBit[dv.second];
-  tab.n_vm0.assign(std::max(N, 1), 0);
+  dims.NVU = NVU;
+  // the nodes mounting each universe PVC at NewScheduler time
+  std::vector<std::vector<int>> uNodes((size_t)NVU);
   tab.n_vc0.assign((size_t)std::max(N, 1) * std::max(VD, 1), 0);
   tab.n_vlim.assign((size_t)std::max(N, 1) * std::max(VD, 1), INT32_MAX);
   std::vector<char> volBlocked(std::max(N, 1), 0);
@@ -1069,19 +1109,54 @@ void Host::build(const Value& root) {
         tab.n_vc0[(size_t)i * VD + v] = (int32_t)u->second.size();
         for (auto& key : u->second) {
           auto b = volBit.find(key);
-          if (b != volBit.end()) tab.n_vm0[i] |= 1ull << b->second;
+          if (b != volBit.end() && udrv[(size_t)b->second] == v) uNodes[(size_t)b->second].push_back(i);
         }
       }
       auto l = n.volumeLimits.find(volDrivers[v]);
       if (l != n.volumeLimits.end()) tab.n_vlim[(size_t)i * VD + v] = (int32_t)l->second;
     }
   }
-  tab.pod_vm.assign(std::max((int)pods.size(), 1), 0);
-  for (size_t i = 0; i < pods.size(); i++)
-    for (auto& dv : podVolumes(pods[i])) {
-      auto b = volBit.find(dv.second);
-      if (b != volBit.end()) tab.pod_vm[i] |= 1ull << b->second;
+  // pods sharing a PVC with another pod being scheduled: their placements log the PVCs they mount
+  std::vector<int> uPods((size_t)NVU, 0);
+  for (auto& us : podU) for (int u : us) uPods[(size_t)u]++;
+  const int P0 = (int)pods.size();
+  tab.pod_vdbeg.assign((size_t)P0 + 1, 0);
+  tab.pod_vsbeg.assign((size_t)P0 + 1, 0);
+  tab.pod_vubeg.assign((size_t)P0 + 1, 0);
+  tab.pod_vd.clear();
+  tab.pod_vs.clear();
+  tab.pod_vu.clear();
+  std::vector<char> podShared(pods.size(), 0);
+  int64_t vlog = 0;
+  bool anyVol = false;
+  for (int i = 0; i < P0; i++) {
+    for (auto& e : podVD[(size_t)i]) {
+      tab.pod_vd.push_back(e.first);
+      tab.pod_vd.push_back(e.second);
     }
+    for (int u : podU[(size_t)i]) {
+      for (int n : uNodes[(size_t)u]) {
+        tab.pod_vs.push_back(n);
+        tab.pod_vs.push_back(u);
+      }
+      podShared[(size_t)i] |= uPods[(size_t)u] > 1 ? 1 : 0;
+    }
+    if (podShared[(size_t)i]) {
+      tab.pod_vu.insert(tab.pod_vu.end(), podU[(size_t)i].begin(), podU[(size_t)i].end());
+      vlog += (int64_t)podU[(size_t)i].size();
+    }
+    anyVol = anyVol || !podVD[(size_t)i].empty() || podVolErr[(size_t)i];
+    tab.pod_vdbeg[(size_t)i + 1] = (int32_t)(tab.pod_vd.size() / 2);
+    tab.pod_vsbeg[(size_t)i + 1] = (int32_t)(tab.pod_vs.size() / 2);
+    tab.pod_vubeg[(size_t)i + 1] = (int32_t)tab.pod_vu.size();
+  }
+  if (tab.pod_vs.size() > (size_t)INT32_MAX || vlog > INT32_MAX / 4) throw KsError(-3, "volume tables exceed 2^30 entries");
+  for (auto* v : {&tab.pod_vd, &tab.pod_vs}) if (v->empty()) v->assign(2, 0);
+  if (tab.pod_vu.empty()) tab.pod_vu.push_back(0);
+  tab.vol_udrv = udrv;
+  if (tab.vol_udrv.empty()) tab.vol_udrv.push_back(0);
+  dims.vLogCap = (int32_t)vlog;
+  dims.volAny = anyVol && N > 0 ? 1 : 0;
   for (int i = 0; i < N; i++) {
     Node& n = nodes[i];
     tab.n_flags[i] = (!n.initialized || !n.ready) ? NF_UNUSABLE : 0;
@@ -1162,7 +1237,8 @@ void Host::build(const Value& root) {
   tab.pod_hpu.assign(std::max(P, 1), 0);
   tab.pod_hpo.assign(std::max(P, 1), 0);
   for (int i = 0; i < P; i++) {
-    tab.pod_flags[i] = pods[i].provisionable ? PF_PROVISIONABLE : 0;
+    tab.pod_flags[i] = (pods[i].provisionable ? PF_PROVISIONABLE : 0) | (podShared[(size_t)i] ? PF_VSHARED : 0) |
+                       (podVolErr[(size_t)i] ? PF_VOLERR : 0);
     if (hostPortUniverse.empty()) continue;
     const std::string key = pods[i].ns + "/" + pods[i].name;
     for (size_t u = 0; u < hostPortUniverse.size(); u++)

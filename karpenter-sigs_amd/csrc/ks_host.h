@@ -121,7 +121,10 @@ struct Host {
   std::vector<HostPortH> hostPortUniverse;  // distinct (IP, port, protocol), bit i of the host-port masks
   std::vector<std::string> hostPortOwner;   // per element: "" or the key of the pod being scheduled whose initial entry it is
   std::map<std::string, std::string> volumeDrivers;  // "ns/pvc" -> resolved CSI driver (resolveDriver, volumeusage.go:115-172)
-  std::vector<std::string> volDrivers, volUniverse;  // limited drivers; the pending pods' PVC keys (bit i)
+  std::vector<std::string> volDrivers, volUniverse;  // limited drivers (id v); the pods' PVC keys of those drivers (id u)
+  // per pod: VolumeTopology.Inject failed (provisioner.go:432-442: the pod is left out of NewTopology's pod
+  // list -- not excluded from the counts, no Topology.Update -- and still scheduled, uninjected)
+  std::vector<char> injectFailed;
   // instance types
   struct Offer { std::string zone, ct; double price = 0; bool available = true; };
   struct IT { std::string name; std::vector<NSR> reqs; QList capacity, alloc; std::vector<std::pair<std::string, std::string>> offers;
@@ -185,7 +188,8 @@ struct Host {
     std::vector<double> off_price;
     std::vector<int32_t> n_flags, pod_flags;
     std::vector<uint64_t> pod_hpc, pod_hpu, pod_hpo, n_hp0;
-    std::vector<uint64_t> pod_vm, vol_dm, n_vm0;  // volume limits (volumeusage.go:183-227)
+    // volume limits (volumeusage.go:183-227), sparse over the pods' PVC universe (ks_problem.h KsDev)
+    std::vector<int32_t> pod_vdbeg, pod_vd, pod_vsbeg, pod_vs, pod_vubeg, pod_vu, vol_udrv;
     std::vector<int32_t> n_vc0, n_vlim;
     // topology groups (ks_topo.cpp)
     std::vector<int32_t> tg_meta;   // [G][TGM_WORDS]

@@ -28,7 +28,6 @@ namespace ks {
 constexpr int kMaxR = 16;         // resource names per problem
 constexpr int kMaxTpl = 32;       // NodeClaimTemplates (NodePools) per problem
 constexpr int kWave = 64;
-constexpr int kMaxVD = 4;        // CSI drivers with a volume limit that pending pods mount
 
 enum PodStatus : int32_t { ST_PENDING = 0, ST_SCHEDULED = 1, ST_FAILED = 2 };
 enum FailCode : uint32_t {
@@ -69,8 +68,10 @@ struct KsDims {
   int32_t tgCntWords;      // size of the count table
   int32_t tgSmall;         // count words [0, tgSmall): the non-hostname groups, LDS-resident in k_solve
   int32_t FSW;             // fail_rs words per (pod, template): RSW, or counts + registered bits if larger
-  int32_t volAny;          // some pending pod mounts a PVC of a driver an existing node limits
-  int32_t VD;              // limited drivers (<= kMaxVD); vol_dm[VD] partitions the pods' PVC universe
+  int32_t volAny;          // some pod mounts a PVC of a driver an existing node limits, or GetVolumes fails for it
+  int32_t VD;              // limited drivers the pods mount (n_vc0 / n_vlim columns)
+  int32_t NVU;             // the pods' PVCs of those drivers (universe ids u)
+  int32_t vLogCap;         // placements that can log a shared PVC: sum over PF_VSHARED pods of their PVC count
   int32_t tgUnlab;         // some existing node lacks the label of a topology group's key (k_solve node_slow)
   int32_t GMW;             // 64-bit words of a topology-group set (st_gown, pod_gsel, pod_ginv, tg_late, log_hg):
                            // ceil(G / 64), at least 1
@@ -144,12 +145,21 @@ struct KsDev {
   const uint64_t KS_G* pod_hpu;    // [P] host-port triples a pod reserves
   const uint64_t KS_G* pod_hpo;    // [P] elements of the pod's own initial entries on existing nodes
   const uint64_t KS_G* n_hp0;      // [N] host-port triples reserved on an existing node
-  // volume limits (volumeusage.go:183-227): the pending pods' PVCs of limited drivers are a <=64-bit
-  // universe; a node's usage per driver is a count (all its PVCs) plus the universe bits it mounts
-  const uint64_t KS_G* pod_vm;     // [P] universe PVCs the pod mounts (GetVolumes)
-  const uint64_t KS_G* vol_dm;     // [VD] universe PVCs resolved to driver v
-  const uint64_t KS_G* n_vm0;      // [N] universe PVCs mounted on the node
-  const int32_t KS_G* n_vc0;       // [N][VD] PVCs of driver v mounted on the node
+  // volume limits (volumeusage.go:183-227), sparse: any number of PVCs and drivers.  VolumeUsage.ExceedsLimits
+  // of a pod on node n is, per limited driver v the pod mounts, count(n, v) + (the pod's PVCs of v that n does
+  // not mount yet) <= limit(n, v); the other drivers cannot fail (a node over a limit before the Solve is
+  // folded into an unsatisfiable Available by the encoder, and commits keep every count within its limit).
+  // "Not mounted yet" needs membership only for the pod's own PVCs: those some node mounts at NewScheduler
+  // time (pod_vs), and -- for a pod sharing a PVC with another pod being scheduled (PF_VSHARED) -- those an
+  // earlier placement of this Solve mounted (the workspace log, KsWork::vlog).
+  const int32_t KS_G* pod_vdbeg;   // [P+1] CSR into pod_vd
+  const int32_t KS_G* pod_vd;      // [][2] (driver v, number of the pod's PVCs of v)
+  const int32_t KS_G* pod_vsbeg;   // [P+1] CSR into pod_vs
+  const int32_t KS_G* pod_vs;      // [][2] (node, PVC u): the pod's PVC u is mounted on the node at NewScheduler time
+  const int32_t KS_G* pod_vubeg;   // [P+1] CSR into pod_vu (PF_VSHARED pods only)
+  const int32_t KS_G* pod_vu;      // [] the pod's PVCs (universe ids)
+  const int32_t KS_G* vol_udrv;    // [NVU] driver of PVC u
+  const int32_t KS_G* n_vc0;       // [N][VD] PVCs of driver v mounted on the node (|VolumeUsage.volumes[v]|)
   const int32_t KS_G* n_vlim;      // [N][VD] the node's limit for driver v (INT32_MAX: none)
   // topology (topology.go; ks_topo.cpp)
   const int32_t KS_G* tg_meta;     // [G][TGM_WORDS]
@@ -184,7 +194,11 @@ enum TopoGroupType : int32_t { TG_SPREAD = 0, TG_AFFINITY = 1, TG_ANTI = 2 };
 enum TgMeta : int32_t {  // per topology group, int32 words
   TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST, TGM_WORDS = 12
 };
-enum PodFlag : int32_t { PF_PROVISIONABLE = 1 };
+enum PodFlag : int32_t {
+  PF_PROVISIONABLE = 1,
+  PF_VSHARED = 2,  // shares a PVC of a limited driver with another pod being scheduled (KsWork::vlog)
+  PF_VOLERR = 4,   // GetVolumes fails (a bound PV that does not exist): ExistingNode.Add always errors
+};
 enum ConsFlag : int32_t { CF_PRICE_ERR = 1, CF_ALL_SPOT = 2, CF_MULTI = 4 };
 enum ConsAction : int32_t { CA_NOOP = 0, CA_DELETE = 1, CA_REPLACE = 2, CA_ERROR = 3 };
 
@@ -236,8 +250,10 @@ struct KsWork {
   int64_t KS_G* counters;   // [16]
   uint64_t KS_G* n_hp;      // [N] host ports reserved per existing node (SIM: valid where s_tch is set)
   uint64_t KS_G* c_hp;      // [Kcap] host ports reserved per NodeClaim
-  uint64_t KS_G* n_vm;      // [N] volume usage per existing node (copies of n_vm0 / n_vc0)
-  int32_t KS_G* n_vc;       // [N][VD]
+  int32_t KS_G* n_vc;       // [N][VD] volume counts per existing node (copy of n_vc0); SIM: [P][VD] slots (n_vslot)
+  int32_t KS_G* n_vslot;    // SIM: [N] n_vc row of a node whose volume usage changed (valid where s_tvol is set)
+  int32_t KS_G* vlog;       // [vLogCap][2] (PVC u, node): PF_VSHARED pods' PVCs a placement mounted on a node
+  int32_t KS_G* vspec;      // [vLogCap][2] the popped pod's entries of vlog
   int32_t KS_G* tg_cnt;     // topology domain counts (copy of tg_cnt0)
   int32_t KS_G* tg_cpos;    // [G] NodeClaims whose placeholder domain has a positive count
   int32_t KS_G* tg_ccnt;    // [G][Kcap] counts of the NodeClaims' hostname-placeholder domains

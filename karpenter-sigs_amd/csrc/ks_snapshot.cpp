@@ -74,8 +74,8 @@ void io_rows(A& a, std::vector<uint32_t>& v, uint64_t width) {
 
 template <class A> void io_tables(A& a, Host::Tables& t, uint64_t rsw) {
   io_all(a, t.tsort_alloc, t.it_alloc, t.it_cap, t.tpl_daemon, t.pool_rem0, t.pod_req, t.pod_sortkey, t.n_avail, t.n_req0,
-         t.off_price, t.n_flags, t.pod_flags, t.pod_hpc, t.pod_hpu, t.pod_hpo, t.n_hp0, t.pod_vm, t.vol_dm, t.n_vm0, t.n_vc0,
-         t.n_vlim, t.tg_meta, t.tg_cnt0, t.tg_frs, t.st_gown, t.pod_gsel, t.pod_ginv, t.n_tdom, t.it_rs, t.tpl_rs, t.n_rs0,
+         t.off_price, t.n_flags, t.pod_flags, t.pod_hpc, t.pod_hpu, t.pod_hpo, t.n_hp0, t.pod_vdbeg, t.pod_vd, t.pod_vsbeg,
+         t.pod_vs, t.pod_vubeg, t.pod_vu, t.vol_udrv, t.n_vc0, t.n_vlim, t.tg_meta, t.tg_cnt0, t.tg_frs, t.st_gown, t.pod_gsel, t.pod_ginv, t.n_tdom, t.it_rs, t.tpl_rs, t.n_rs0,
          t.pool_mask, t.st_toltpl, t.tpl_taint, t.st_tol, t.n_taint, t.tsort_pos, t.it_off_beg, t.off_zone, t.off_ct,
          t.tpl_it_beg, t.tpl_its, t.tpl_pool, t.pod_state0, t.pod_nstate, t.pod_uid, t.st_flags, t.pod_rmask, t.tpl_rmask,
          t.pod_rfmt, t.tpl_rfmt, t.fk_words, t.fk_key_off, t.fk_tpl, t.tg_late);
@@ -137,7 +137,7 @@ void host_check(const Host& h) {
     if (want < 0 || (int64_t)have < want) bad(what);
   };
   if (d.R < 1 || d.R > kMaxR || d.NK < 0 || d.NK > 64 || d.NTPL < 0 || d.NTPL > kMaxTpl || d.T < 0 || d.N < 0 ||
-      d.P < 0 || d.S < 1 || d.NU < 1 || d.NPOOL < 0 || d.VD < 0 || d.VD > kMaxVD || d.TW < 1 || d.G < 0 ||
+      d.P < 0 || d.S < 1 || d.NU < 1 || d.NPOOL < 0 || d.VD < 0 || d.NVU < 0 || d.vLogCap < 0 || d.TW < 1 || d.G < 0 ||
       d.G1 < 0 || d.G1 > d.G || d.Kcap < 1)
     bad("dims");
   if (d.HDR != 8 + 4 * d.NB || d.RSW < d.HDR + d.W || d.W < 0 || d.NB < 0) bad("record layout");
@@ -175,7 +175,7 @@ void host_check(const Host& h) {
   need(t.pod_rfmt.size(), P1 * R, "pod_rfmt");
   need(t.pod_sortkey.size(), P1 * 4, "pod_sortkey");
   for (auto* v : {&t.pod_state0, &t.pod_nstate, &t.pod_uid, &t.pod_flags}) need(v->size(), P1, "per-pod table");
-  for (auto* v : {&t.pod_hpc, &t.pod_hpu, &t.pod_hpo, &t.pod_vm}) need(v->size(), P1, "per-pod mask");
+  for (auto* v : {&t.pod_hpc, &t.pod_hpu, &t.pod_hpo}) need(v->size(), P1, "per-pod mask");
   need(t.pod_rmask.size(), P1, "pod_rmask");
   need(t.st_rs.size(), S * RSW, "st_rs");
   need(t.st_tol.size(), S * 2, "st_tol");
@@ -190,10 +190,30 @@ void host_check(const Host& h) {
   need(t.n_taint.size(), N1 * 2, "n_taint");
   need(t.n_flags.size(), N1, "n_flags");
   need(t.n_hp0.size(), N1, "n_hp0");
-  need(t.n_vm0.size(), N1, "n_vm0");
   need(t.n_vc0.size(), N1 * VD1, "n_vc0");
   need(t.n_vlim.size(), N1 * VD1, "n_vlim");
-  need(t.vol_dm.size(), VD1, "vol_dm");
+  // the sparse volume tables: CSR offsets monotone and in range, every driver / node / PVC index inside its
+  // table, the shared pods' PVC lists within the log capacity
+  for (auto* b : {&t.pod_vdbeg, &t.pod_vsbeg, &t.pod_vubeg}) need(b->size(), (int64_t)d.P + 1, "volume CSR offsets");
+  need(t.vol_udrv.size(), std::max<int64_t>(d.NVU, 1), "vol_udrv");
+  auto csr = [&](const std::vector<int32_t>& beg, size_t entries, const char* what) {
+    if (beg[0] != 0) bad(what);
+    for (int64_t p = 0; p < d.P; p++)
+      if (beg[(size_t)p] > beg[(size_t)p + 1]) bad(what);
+    if ((size_t)beg[(size_t)d.P] > entries) bad(what);
+  };
+  csr(t.pod_vdbeg, t.pod_vd.size() / 2, "pod_vd");
+  csr(t.pod_vsbeg, t.pod_vs.size() / 2, "pod_vs");
+  csr(t.pod_vubeg, t.pod_vu.size(), "pod_vu");
+  for (size_t i = 0; i + 1 < t.pod_vd.size(); i += 2)
+    if (t.pod_vd[i] < 0 || (t.pod_vd[i] >= d.VD && d.P > 0 && t.pod_vdbeg[(size_t)d.P] > 0) || t.pod_vd[i + 1] < 0) bad("pod_vd entry");
+  for (size_t i = 0; i + 1 < t.pod_vs.size() && t.pod_vsbeg[(size_t)d.P] > 0; i += 2)
+    if (t.pod_vs[i] < 0 || t.pod_vs[i] >= d.N || t.pod_vs[i + 1] < 0 || t.pod_vs[i + 1] >= d.NVU) bad("pod_vs entry");
+  for (size_t i = 0; i < (size_t)t.pod_vubeg[(size_t)d.P]; i++)
+    if (t.pod_vu[i] < 0 || t.pod_vu[i] >= d.NVU) bad("pod_vu entry");
+  for (int64_t u = 0; u < d.NVU; u++)
+    if (t.vol_udrv[(size_t)u] < 0 || t.vol_udrv[(size_t)u] >= d.VD) bad("vol_udrv entry");
+  if (t.pod_vubeg[(size_t)d.P] > d.vLogCap) bad("volume log capacity");
   need(t.pod_gsel.size(), P1 * d.GMW, "pod_gsel");
   need(t.pod_ginv.size(), P1 * d.GMW, "pod_ginv");
   // CSR tables and the indices the kernels follow
@@ -249,7 +269,7 @@ template <class A> void host_io(A& a, Host& h) {
   PhaseTimer pt(A::reading ? "host_load" : "host_save");
   io_all(a, h.keyNames, h.keyId, h.values, h.valueId, h.keys, h.wordValid, h.vIsInt, h.vInt, h.hostKey, h.zoneKey, h.ctKey,
          h.hostPrivBit, h.allowWK, h.itKeys, h.wellKnown, h.resNames, h.resId, h.resShift, h.taints, h.hostPortUniverse,
-         h.hostPortOwner, h.volumeDrivers, h.volDrivers, h.volUniverse, h.its, h.tpls, h.pools, h.toleratePreferNoSchedule,
+         h.hostPortOwner, h.volumeDrivers, h.volDrivers, h.volUniverse, h.injectFailed, h.its, h.tpls, h.pools, h.toleratePreferNoSchedule,
          h.nodes, h.daemons);
   pt.mark("universe, types, templates, nodes");
   io_par(a, h.pods);
@@ -296,13 +316,13 @@ template <class A> void host_io(A& a, Host& h) {
 // Layout guards: adding a member to one of these types changes its size and stops the build here until the
 // member is listed above (sizes of this toolchain's libstdc++, x86-64).
 static_assert(sizeof(PodH) == 640, "PodH changed: update io(PodH) in ks_snapshot.cpp");
-static_assert(sizeof(Host::Tables) == 1368, "Host::Tables changed: update io(Host::Tables)");
+static_assert(sizeof(Host::Tables) == 1464, "Host::Tables changed: update io(Host::Tables)");
 static_assert(sizeof(Host::Node) == 456, "Host::Node changed: update io(Host::Node)");
 static_assert(sizeof(Host::Tpl) == 280, "Host::Tpl changed: update io(Host::Tpl)");
 static_assert(sizeof(Host::IT) == 224, "Host::IT changed: update io(Host::IT)");
 static_assert(sizeof(TopoGroup) == 256, "TopoGroup changed: update io(TopoGroup)");
 static_assert(sizeof(PodState) == 120, "PodState changed: update io(PodState)");
-static_assert(sizeof(Host) == 2864, "Host changed: update host_io");
+static_assert(sizeof(Host) == 2992, "Host changed: update host_io");
 static_assert(sizeof(HostPortH) == 88 && sizeof(AffTerm) == 128 && sizeof(SpreadC) == 104 && sizeof(LabelSel) == 32,
               "a pod-spec type changed: update its io()");
 

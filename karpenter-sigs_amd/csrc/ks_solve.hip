@@ -205,10 +205,8 @@ __global__ void k_init(KsDev D, const KsWork* works, int nrep, const int32_t* qo
     for (int64_t i = gtid; i < (int64_t)d.N * d.R; i += gsz) W.n_req[i] = D.n_req0[i];
     for (int64_t i = gtid; i < (int64_t)d.N * d.RSW; i += gsz) W.n_rs[i] = D.n_rs0[i];
     for (int64_t i = gtid; i < d.N; i += gsz) W.n_hp[i] = D.n_hp0[i];
-    if (d.volAny) {
-      for (int64_t i = gtid; i < d.N; i += gsz) W.n_vm[i] = D.n_vm0[i];
+    if (d.volAny)
       for (int64_t i = gtid; i < (int64_t)d.N * d.VD; i += gsz) W.n_vc[i] = D.n_vc0[i];
-    }
     if (d.G) {
       for (int64_t i = gtid; i < d.tgCntWords; i += gsz) W.tg_cnt[i] = D.tg_cnt0[i];
       for (int64_t i = gtid; i < (int64_t)d.G * (d.Kcap + 1); i += gsz) W.tg_ccnt[i] = 0;
@@ -241,7 +239,7 @@ template <int RT>
 struct Window {
   int p, g, uid, s, flags, toltpl, pf, st;
   int rl;  // SIM, nothing pushed back yet: identical pods from this queue position to the end of their run
-  uint64_t ll, tol0, tol1, hpc, hpu, hpo, vm;
+  uint64_t ll, tol0, tol1, hpc, hpu, hpo;
   uint64_t tsel, tinv, town, trss;  // TOPO: word 0 of the pod's selecting / inverse / owned group sets, st_rss keys
   int64_t req[RT > 0 ? RT : kMaxR];
 };
@@ -563,7 +561,7 @@ struct Solver {
   LU32 s_tch;           // SIM: [ceil(N/32)] nodes whose requests live in a W.n_req slot
   LU32 s_tchr;          // SIM: [ceil(N/32)] nodes whose requirements live in a W.n_rs slot; Solve (d.fnOn): nodes
                         // whose requirements a commit narrowed (k_feasibility_nodes's bits no longer apply)
-  LU32 s_tvol;          // SIM: [ceil(N/32)] nodes whose volume usage lives in W.n_vm / W.n_vc
+  LU32 s_tvol;          // SIM: [ceil(N/32)] nodes whose volume counts live in a W.n_vc slot (W.n_vslot)
   LI32 s_tgm;           // [G][TGM_WORDS] topology group metadata
   LI32 s_tmin;          // [G] domainMinCount of the popped pod, per spread group
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
@@ -588,7 +586,11 @@ struct Solver {
   bool rem_same = false;  // the last claim_full left the claim's options unchanged (commit skips the copy back)
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
   uint64_t cur_hpo = 0;               // its own initial entries on existing nodes (HostPortUsage.Add replaces them)
-  uint64_t cur_vm = 0;                // the popped pod's PVCs of limited drivers (Solve only; SIM refuses them)
+  // the popped pod's volumes (volA): driver entries [v_db, v_de) of D.pod_vd, NewScheduler-time mounts of its
+  // PVCs [v_sb, v_se) of D.pod_vs, this Solve's earlier mounts of them [0, v_nsp) of W.vspec (PF_VSHARED)
+  int v_db = 0, v_de = 0, v_sb = 0, v_se = 0, v_nsp = 0, v_ub = 0, v_ue = 0;
+  int v_nlog = 0;    // entries in W.vlog
+  int v_nslot = 0;   // SIM: W.n_vc slots in use
 #ifdef KS_PHASE_STATS
   uint64_t scyc[4] = {0, 0, 0, 0};  // claim_full sub-phases: requirements, thresholds, masks, apply
 #endif
@@ -772,29 +774,93 @@ struct Solver {
 
 
   // --- existing nodes (ExistingNode.Add, existingnode.go:64-124) -------------------------------
-  // VolumeUsage.ExceedsLimits (volumeusage.go:202-209) for the popped pod's PVCs: per limited driver,
-  // the node's count plus the pod's PVCs it does not mount yet.  Nodes over a limit before the Solve
-  // never fit (the encoder's Available()), so a pod without PVCs needs no check.
-  // SIM: a node's usage lives in W only once a pod of this simulation mounted something there
-  // (s_tvol, copy-on-write from the shared n_vm0 / n_vc0).
+  // Volumes (VolumeUsage, volumeusage.go:183-227; KsDev in ks_problem.h).  vol_pop loads the popped pod's
+  // entries (wave-uniform); for a pod sharing a PVC with other pods being scheduled it also collects the
+  // earlier placements' log entries of its PVCs (W.vlog -> W.vspec; every store here is a wave-wide store of
+  // a uniform value, so each lane later reads what it wrote itself).
+  __device__ __forceinline__ void vol_pop(int g, int pf) {
+    v_db = uni(D.pod_vdbeg[g]);
+    v_de = uni(D.pod_vdbeg[g + 1]);
+    v_sb = uni(D.pod_vsbeg[g]);
+    v_se = uni(D.pod_vsbeg[g + 1]);
+    v_ub = v_ue = v_nsp = 0;
+    if (!(pf & PF_VSHARED)) return;
+    v_ub = uni(D.pod_vubeg[g]);
+    v_ue = uni(D.pod_vubeg[g + 1]);
+    for (int i0 = 0; i0 < v_nlog; i0 += kWave) {
+      const int i = i0 + lane();
+      const int ic = i < v_nlog ? i : i0;
+      const int lu = W.vlog[2 * ic], ln = W.vlog[2 * ic + 1];
+      bool hit = false;
+      for (int k = v_ub; k < v_ue; k++) hit |= D.pod_vu[k] == lu;
+      for (uint64_t m = wballot(hit && i < v_nlog); m; m &= m - 1) {
+        const int l = ctz64(m);
+        const int u = rdl(lu, l), n = rdl(ln, l);
+        W.vspec[2 * v_nsp] = u;  // wave-wide stores of uniform values
+        W.vspec[2 * v_nsp + 1] = n;
+        v_nsp++;
+      }
+    }
+  }
+  __device__ __forceinline__ bool vol_any() const { return v_de > v_db; }
+  // The pod's PVCs of driver v that node n mounts already (at NewScheduler time, or by an earlier placement).
+  __device__ __forceinline__ int vol_mounted(int n, int v) const {
+    int c = 0;
+    for (int k = v_sb; k < v_se; k++) c += (D.pod_vs[2 * k] == n && D.vol_udrv[D.pod_vs[2 * k + 1]] == v) ? 1 : 0;
+    for (int k = 0; k < v_nsp; k++) c += (W.vspec[2 * k + 1] == n && D.vol_udrv[W.vspec[2 * k]] == v) ? 1 : 0;
+    return c;
+  }
+  __device__ __forceinline__ const int32_t KS_G* vol_row(int n) const {
+    if (!SIM) return W.n_vc + (int64_t)n * d.VD;
+    return tbit(s_tvol, n) ? W.n_vc + (int64_t)W.n_vslot[n] * d.VD : D.n_vc0 + (int64_t)n * d.VD;
+  }
+  // VolumeUsage.ExceedsLimits (volumeusage.go:202-209) of the popped pod on node n (per lane): per limited
+  // driver it mounts, the node's count plus its PVCs the node does not mount yet.
   __device__ __forceinline__ bool vol_ok(int n) const {
-    const bool own = !SIM || tbit(s_tvol, n);
-    const uint64_t add = cur_vm & ~(own ? W.n_vm[n] : D.n_vm0[n]);
-    const int32_t KS_G* vc = (own ? W.n_vc : D.n_vc0) + (int64_t)n * d.VD;
+    const int32_t KS_G* vc = vol_row(n);
     bool ok = true;
-    for (int v = 0; v < d.VD; v++) ok &= vc[v] + __popcll(add & D.vol_dm[v]) <= D.n_vlim[(int64_t)n * d.VD + v];
+    for (int j = v_db; j < v_de; j++) {
+      const int v = D.pod_vd[2 * j], c = D.pod_vd[2 * j + 1];
+      ok &= vc[v] + c - vol_mounted(n, v) <= D.n_vlim[(int64_t)n * d.VD + v];
+    }
     return ok;
   }
-  // VolumeUsage.Add (existingnode.go:122), by node n's owner lane.
-  __device__ __forceinline__ void vol_commit(int n) const {
-    if (SIM && !tbit(s_tvol, n)) {
-      W.n_vm[n] = D.n_vm0[n];
-      for (int v = 0; v < d.VD; v++) W.n_vc[(int64_t)n * d.VD + v] = D.n_vc0[(int64_t)n * d.VD + v];
-      s_tvol[n >> 5] |= 1u << (n & 31);
+  // VolumeUsage.Add (existingnode.go:122) of the popped pod on node n (wave-uniform n; wave-wide stores of
+  // uniform values).  SIM: the node's counts move to a W.n_vc slot at its first such placement.
+  __device__ __forceinline__ void vol_commit(int n) {
+    int32_t KS_G* vc;
+    if (SIM) {
+      if (!tbit(s_tvol, n)) {
+        const int slot = v_nslot++;
+        for (int v = 0; v < d.VD; v++) W.n_vc[(int64_t)slot * d.VD + v] = D.n_vc0[(int64_t)n * d.VD + v];
+        W.n_vslot[n] = slot;
+        __hip_atomic_fetch_or(s_tvol + (n >> 5), 1u << (n & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        wsync();
+        vc = W.n_vc + (int64_t)slot * d.VD;
+      } else {
+        vc = W.n_vc + (int64_t)uni(W.n_vslot[n]) * d.VD;
+      }
+    } else {
+      vc = W.n_vc + (int64_t)n * d.VD;
     }
-    const uint64_t add = cur_vm & ~W.n_vm[n];
-    for (int v = 0; v < d.VD; v++) W.n_vc[(int64_t)n * d.VD + v] += __popcll(add & D.vol_dm[v]);
-    W.n_vm[n] |= cur_vm;
+    for (int j = v_db; j < v_de; j++) {
+      const int v = D.pod_vd[2 * j], c = D.pod_vd[2 * j + 1];
+      const int add = uni(c - vol_mounted(n, v));
+      if (add) vc[v] = uni(vc[v]) + add;
+    }
+    // the shared pod's PVCs not yet on n join the log (each (PVC, node) pair once)
+    for (int k = v_ub; k < v_ue; k++) {
+      const int u = D.pod_vu[k];
+      bool on = false;
+      for (int q = v_sb; q < v_se; q++) on |= D.pod_vs[2 * q] == n && D.pod_vs[2 * q + 1] == u;
+      for (int q = 0; q < v_nsp; q++) on |= W.vspec[2 * q + 1] == n && W.vspec[2 * q] == u;
+      if (!ub(on)) {
+        W.vlog[2 * v_nlog] = u;
+        W.vlog[2 * v_nlog + 1] = n;
+        v_nlog++;
+      }
+    }
+    hbm_release();
   }
   // Lane (n & 63) is the only lane that ever reads or writes node n's mutable state.
   __device__ __forceinline__ bool tbit(LU32 m, int n) const { return (m[n >> 5] >> (n & 31)) & 1u; }
@@ -841,7 +907,7 @@ struct Solver {
       }
       rk[i] = rr;  // (permanent for these requests: the caller's resource-failing prefix)
       ok[i] = rr & (((tx[i] & ~tol0) | (ty[i] & ~tol1)) == 0) & ((h[i] & cur_hpc) == 0);  // Taints.Tolerates
-      if (volA() && cur_vm && ok[i]) ok[i] = vol_ok(c[i]);
+      if (volA() && vol_any() && ok[i]) ok[i] = vol_ok(c[i]);
       if (keys(sflags) && ok[i]) ok[i] = node_compat(c[i]);  // strict Compatible
       sl[i] = false;
     }
@@ -867,7 +933,6 @@ struct Solver {
   __device__ __forceinline__ void node_commit(int j, int s, int sflags, const int64_t* pod) {
     for (int r = 0; r < R(); r++) W.n_req[(int64_t)j * R() + r] += pod[r];
     if (hpA()) W.n_hp[j] = (W.n_hp[j] & ~cur_hpo) | cur_hpu;  // HostPortUsage.Add (hostportusage.go:70-72)
-    if (volA() && cur_vm) vol_commit(j);
     if (keys(sflags)) {
       rs_add(L, W.n_rs + (int64_t)j * d.RSW, s_pin);
       node_rs_changed(j);
@@ -891,7 +956,6 @@ struct Solver {
         W.n_req[(int64_t)j * R() + r] = q[r] + pod[r];
       }
       if (hpA()) W.n_hp[j] = ((fresh ? D.n_hp0[j] : W.n_hp[j]) & ~cur_hpo) | cur_hpu;
-      if (volA() && cur_vm) vol_commit(j);
       if (fresh) s_tch[j >> 5] |= 1u << (j & 31);
     }
     if (keys(sflags)) {
@@ -2384,12 +2448,11 @@ struct Solver {
         w.tol0 = D.st_tol[2 * w.s];
         w.tol1 = D.st_tol[2 * w.s + 1];
       }
-      w.pf = SIM ? D.pod_flags[w.g] : 0;
+      w.pf = SIM || !LEAN ? D.pod_flags[w.g] : 0;
       w.rl = SIM && LEAN && ident ? W.run_len[pos] : 1;
       w.hpc = D.pod_hpc[w.g];
       w.hpu = D.pod_hpu[w.g];
       w.hpo = D.pod_hpo[w.g];
-      w.vm = D.pod_vm[w.g];
       if (TOPO) {
         w.tsel = D.pod_gsel[(int64_t)w.g * d.GMW];
         w.tinv = D.pod_ginv[(int64_t)w.g * d.GMW];

@@ -102,6 +102,16 @@ void Host::buildTopology() {
     return;
   }
   PhaseTimer pt("buildTopology");
+  // A pod whose VolumeTopology.Inject failed is not in NewTopology's pod list (provisioner.go:432-442): its
+  // UID is not excluded from the counts and Topology.Update never ran for it, so its state 0 owns no group;
+  // a later relaxation's Update creates and owns its groups (the late groups below).  That Update would also
+  // create inverse anti-affinity groups mid-Solve, which the device does not model: refused.
+  auto injFailed = [&](int p) { return (size_t)p < injectFailed.size() && injectFailed[(size_t)p]; };
+  for (int p = 0; p < P; p++)
+    if (injFailed(p) && pods[(size_t)p].hasAffinity && pods[(size_t)p].hasPodAnti && !pods[(size_t)p].antiRequired.empty())
+      throw KsError(-2, "pod " + pods[(size_t)p].ns + "/" + pods[(size_t)p].name +
+                            ": volume topology injection failed and the pod has required pod anti-affinity (its "
+                            "inverse groups would be created mid-Solve)");
   // --- domain universe (provisioner.go:229-283)
   std::map<std::string, std::set<std::string>> dom;
   auto valuesOf = [&](const std::vector<uint32_t>& rec, int k) {  // Requirement.Values(): the raw set
@@ -132,7 +142,9 @@ void Host::buildTopology() {
   // --- groups
   std::set<std::string> excluded;
   if (topoExcluded) excluded = *topoExcluded;
-  else for (auto& p : pods) excluded.insert(p.uid);
+  else
+    for (int p = 0; p < P; p++)
+      if (!injFailed(p)) excluded.insert(pods[(size_t)p].uid);
   topoContrib.clear();
   topoInvOwner.clear();
   // (group index, domain) per counted cluster pod, resolved to value ids once the groups are final
@@ -304,7 +316,7 @@ void Host::buildTopology() {
   std::vector<char> podHasAnti((size_t)P, 0);
   parallel_for(P, 64, [&](int p) {
     const std::shared_ptr<PodH>& sp = states[(size_t)p][0].spec;
-    if (!sp) return;
+    if (!sp || injFailed(p)) return;
     if (sp->hasAffinity && sp->hasPodAnti && (!sp->antiRequired.empty() || !sp->antiPreferred.empty())) {
       podHasAnti[(size_t)p] = 1;
       podAnti[(size_t)p] = antiGroups(*sp);
@@ -315,7 +327,7 @@ void Host::buildTopology() {
   std::vector<std::vector<int32_t>> invOwned(P);
   for (int p = 0; p < P; p++) {  // NewTopology: Update(pod) for every pod, in order
     const std::shared_ptr<PodH>& sp = states[(size_t)p][0].spec;
-    if (!sp) continue;
+    if (!sp || injFailed(p)) continue;
     if (podHasAnti[(size_t)p]) invOwned[(size_t)p] = inverseAnti(*sp, std::move(podAnti[(size_t)p]), nullptr, false);
     std::vector<int32_t> gown;
     for (auto& g : podOwn[(size_t)p]) {

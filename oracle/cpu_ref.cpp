@@ -638,19 +638,18 @@ struct Problem {
   map<string, map<string, string>> nodeLabels;
   vector<std::pair<string, map<string, string>>> namespaces;  // the cluster's Namespace list (name, labels)
   map<string, string> volumeDrivers;  // "ns/pvc" -> resolved CSI driver (resolveDriver, volumeusage.go:115-172)
+  bool hasVolumeDrivers = false;      // the snapshot gave volumeDrivers (else resolved from the objects below)
+  // the cluster's PersistentVolumeClaim / PersistentVolume / StorageClass objects (volumes.inc)
+  bool volObjects = false;
+  struct PVCObj { string volumeName, storageClass; };
+  struct PVObj { string csiDriver; bool awsEBS = false, required = false; vector<vector<NSR>> terms; };
+  struct SCObj { string provisioner; vector<vector<NSR>> allowedTopologies; };
+  map<string, PVCObj> pvcs;  // "namespace/name"
+  map<string, PVObj> pvs;
+  map<string, SCObj> scs;
 };
 
-// GetVolumes (volumeusage.go:82-113): PVCs the snapshot does not list are NotFound (skipped); an empty
-// driver (unbound PVC without a storage class) is skipped too.
-static Volumes GetVolumes(const Problem& pb, const Pod& p) {
-  Volumes v;
-  for (auto& name : p.pvcNames) {
-    auto d = pb.volumeDrivers.find(p.ns + "/" + name);
-    if (d == pb.volumeDrivers.end() || d->second.empty()) continue;
-    v[d->second].insert(p.ns + "/" + name);
-  }
-  return v;
-}
+#include "volumes.inc"
 
 // ---------------------------------------------------------------------------------------------
 // JSON -> model
@@ -962,8 +961,11 @@ static Problem parseProblem(const ojson::Value& root) {
   if (auto* ps = root.get("pods")) for (auto& v : ps->arr()) pb.pods.push_back(parsePod(v));
   if (auto* hs = root.get("hostnameSeed")) pb.hostnameSeed = hs->i64();
   if (auto* et = root.get("emptyTopology")) pb.emptyTopology = et->boolean();
-  if (auto* vd = root.get("volumeDrivers"))
+  if (auto* vd = root.get("volumeDrivers")) {
+    pb.hasVolumeDrivers = true;
     for (auto& kv : vd->obj()) pb.volumeDrivers[kv.first] = kv.second.str();
+  }
+  parseVolumeObjects(root, pb);
   if (auto* cps = root.get("clusterPods")) for (auto& v : cps->arr()) pb.clusterPods.push_back(parsePod(v));
   if (auto* nss = root.get("namespaces"))
     for (auto& v : nss->arr()) {
@@ -1041,6 +1043,9 @@ class Scheduler {
  public:
   explicit Scheduler(Problem& pb) : pb_(pb) {
     nodeID_ = pb.hostnameSeed;
+    // Provisioner.NewScheduler: injectTopology before NewTopology (provisioner.go:283-287, 432-442)
+    injectFailed_.assign(pb.pods.size(), false);
+    for (size_t i = 0; i < pb.pods.size(); i++) injectFailed_[i] = !VolumeTopologyInject(pb, pb.pods[i]);
     buildTopology();
     initAlgBytes();
     // NewScheduler (scheduler.go:49-83)
@@ -1144,7 +1149,9 @@ class Scheduler {
     topo_.clusterPods = &pb_.clusterPods;
     topo_.nodes = &pb_.nodeLabels;
     topo_.namespaceList = &pb_.namespaces;
-    for (auto& p : pb_.pods) topo_.excluded.insert(p.uid);
+    // the pods NewTopology receives: those whose volume topology injection succeeded
+    for (size_t i = 0; i < pb_.pods.size(); i++)
+      if (!injectFailed_[i]) topo_.excluded.insert(pb_.pods[i].uid);
     for (auto& cp : pb_.clusterPods) {  // updateInverseAffinities via ForPodsWithAntiAffinity
       if (!(cp.hasAffinity && cp.hasPodAnti && !cp.antiRequired.empty())) continue;
       if (cp.nodeName.empty()) continue;
@@ -1153,8 +1160,10 @@ class Scheduler {
       if (topo_.excluded.count(cp.uid)) continue;
       topo_.inverseAnti(cp, &n->second);
     }
-    for (auto& p : pb_.pods) topo_.Update(p);
+    for (size_t i = 0; i < pb_.pods.size(); i++)
+      if (!injectFailed_[i]) topo_.Update(pb_.pods[i]);
   }
+  vector<bool> injectFailed_;
   int64_t nodeID_ = 0;
   bool toleratePreferNoSchedule_ = false;
   vector<ResourceList> daemonOverhead_;
@@ -1307,7 +1316,9 @@ class Scheduler {
     if (!Tolerates(sn.taints, pod).empty()) return false;
     vector<HostPort> hp = GetHostPorts(pod);
     string key = pod.ns + "/" + pod.name;
-    Volumes vols = GetVolumes(pb_, pod);
+    bool volErr = false;
+    Volumes vols = GetVolumes(pb_, pod, &volErr);
+    if (volErr) return false;                         // existingnode.go:70-73
     if (n.volumes.ExceedsLimits(vols)) return false;  // existingnode.go:76-78
     if (n.hostPorts.Conflicts(key, hp)) return false;
     ResourceList podReq = RequestsForPods({&pod});

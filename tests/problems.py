@@ -164,6 +164,148 @@ def add_volumes(rng, pods, nodes):
     return drivers
 
 
+OBJ_DRIVERS = ["ebs.csi.aws.com", "fake.csi.provider", "pd.csi.storage.gke.io", "disk.csi.azure.com",
+               "efs.csi.aws.com", "d5.csi", "d6.csi", "unlimited.csi"]
+IN_TREE = {"ebs.csi.aws.com": "kubernetes.io/aws-ebs", "pd.csi.storage.gke.io": "kubernetes.io/gce-pd",
+           "disk.csi.azure.com": "kubernetes.io/azure-disk"}
+
+
+def _resolve(claim, pvs, scs):
+    """resolveDriver (volumeusage.go:119-155), for the generator's node usage lists only."""
+    vn = claim["spec"].get("volumeName", "")
+    if vn:
+        pv = pvs.get(vn)
+        if pv is None:
+            return None
+        src = pv["spec"]
+        if src.get("csi"):
+            return src["csi"]["driver"] or None
+        if src.get("awsElasticBlockStore"):
+            return "ebs.csi.aws.com"
+    sc = scs.get(claim["spec"].get("storageClassName") or "")
+    if sc is None:
+        return None
+    inv = {v: k for k, v in IN_TREE.items()}
+    return inv.get(sc["provisioner"], sc["provisioner"])
+
+
+def add_volume_objects(rng, pods, nodes, n_claims=300, share=0.1, zonal=0.5, broken=0.02, n_drivers=8,
+                       own_usage=None, limit_range=(0, 8), mount_frac=0.6):
+    """PersistentVolumeClaim / PersistentVolume / StorageClass objects instead of a volumeDrivers map: the
+    library resolves drivers (resolveDriver, volumeusage.go:119-182, incl. the in-tree names of
+    csi-translation-lib) and runs VolumeTopology.Inject (volumetopology.go:41-140) itself.  Pods mount 0-3
+    claims, mostly their own (a StatefulSet's), a `share` fraction from a small pool (RWX); claims are bound to
+    PVs (CSI, in-tree EBS or no CSI source, some with one or two zonal node-affinity terms) or unbound with a
+    storage class (provisioner in-tree or CSI, zonal allowedTopologies or none, "" or missing); `broken` of the
+    pods mount a missing claim or a claim bound to a missing PV (Inject fails; GetVolumes fails for the
+    latter).  Nodes carry CSINode limits for most drivers and a usage list: `own_usage` maps node name ->
+    pods bound there (their claims are mounted), plus some random claims.  Returns the three object lists."""
+    drivers = OBJ_DRIVERS[:n_drivers]
+    scs = {}
+    for i, d in enumerate(drivers):
+        for z in range(2):
+            name = "sc-%d-%d" % (i, z)
+            prov = IN_TREE[d] if d in IN_TREE and rng.random() < 0.5 else d
+            sc = {"metadata": {"name": name}, "provisioner": prov}
+            if z == 1 and rng.random() < zonal:
+                zs = sorted(set(_pick(rng, ZONES) for _ in range(int(rng.integers(1, 3)))))
+                sc["allowedTopologies"] = [{"matchLabelExpressions": [{"key": synth.ZONE, "values": zs}]}]
+            scs[name] = sc
+    pvs, pvcs = {}, {}
+
+    def make_claim(ns, name):
+        c = {"metadata": {"name": name, "namespace": ns}, "spec": {}}
+        u = rng.random()
+        if u < 0.5:
+            pvname = "pv-%s-%s" % (ns, name)
+            c["spec"]["volumeName"] = pvname
+            c["spec"]["storageClassName"] = _pick(rng, sorted(scs)) if rng.random() < 0.7 else ""
+            v = rng.random()
+            spec = {}
+            if v < 0.7:
+                spec["csi"] = {"driver": _pick(rng, drivers), "volumeHandle": "h"}
+            elif v < 0.85:
+                spec["awsElasticBlockStore"] = {"volumeID": "vol-1", "fsType": "ext4"}
+            if rng.random() < zonal:
+                terms = [{"matchExpressions": [{"key": synth.ZONE, "operator": "In",
+                                                "values": sorted(set(_pick(rng, ZONES) for _ in range(2)))}]}]
+                if rng.random() < 0.2:
+                    terms.append({"matchExpressions": [{"key": synth.ZONE, "operator": "In", "values": [_pick(rng, ZONES)]}]})
+                spec["nodeAffinity"] = {"required": {"nodeSelectorTerms": terms}}
+            pvs[pvname] = {"metadata": {"name": pvname}, "spec": spec}
+        elif u < 0.96:
+            c["spec"]["storageClassName"] = _pick(rng, sorted(scs))
+        else:
+            c["spec"]["storageClassName"] = ""
+        pvcs[(ns, name)] = c
+        return c
+
+    pool = ["shared-%03d" % i for i in range(max(4, n_claims // 20))]
+    next_claim = [0]
+
+    def own(ns):
+        next_claim[0] += 1
+        return "claim-%05d" % next_claim[0]
+
+    def anti_required(p):
+        return bool(p["spec"].get("affinity", {}).get("podAntiAffinity", {}).get("requiredDuringSchedulingIgnoredDuringExecution"))
+
+    for p in pods:
+        ns = p["metadata"]["namespace"]
+        if rng.random() >= mount_frac:
+            continue
+        vols = []
+        for k in range(int(rng.integers(1, 4))):
+            if rng.random() < 0.1:
+                vols.append({"name": "eph%d" % k, "ephemeral": {"volumeClaimTemplate": {"spec": {}}}})
+                make_claim(ns, "%s-eph%d" % (p["metadata"]["name"], k))
+                continue
+            name = _pick(rng, pool) if rng.random() < share else own(ns)
+            if (ns, name) not in pvcs:
+                make_claim(ns, name)
+            vols.append({"name": "v%d" % k, "persistentVolumeClaim": {"claimName": name}})
+        if rng.random() < broken and not anti_required(p):
+            u = rng.random()
+            if u < 0.3:
+                vols.append({"name": "missing", "persistentVolumeClaim": {"claimName": "no-such-claim"}})
+            elif u < 0.6:
+                name = own(ns)
+                pvcs[(ns, name)] = {"metadata": {"name": name, "namespace": ns},
+                                    "spec": {"storageClassName": "missing-class"}}
+                vols.append({"name": "noclass", "persistentVolumeClaim": {"claimName": name}})
+            else:
+                name = own(ns)
+                pvcs[(ns, name)] = {"metadata": {"name": name, "namespace": ns}, "spec": {"volumeName": "no-such-pv"}}
+                vols.append({"name": "gone", "persistentVolumeClaim": {"claimName": name}})
+        p["spec"]["volumes"] = vols
+    lo, hi = limit_range
+    for n in nodes:
+        lim = {d: int(rng.integers(lo, hi)) for d in drivers[:-1] if rng.random() < 0.8}
+        usage = {}
+        mounted = []
+        for bp in (own_usage or {}).get(n["name"], []):
+            for v in bp["spec"].get("volumes", []):
+                name = v["persistentVolumeClaim"]["claimName"] if "persistentVolumeClaim" in v else \
+                    "%s-%s" % (bp["metadata"]["name"], v["name"])
+                mounted.append((bp["metadata"]["namespace"], name))
+        keys = list(pvcs)
+        for _ in range(int(rng.integers(0, 3))):
+            if keys:
+                mounted.append(keys[int(rng.integers(len(keys)))])
+        for key in mounted:
+            c = pvcs.get(key)
+            if c is None:
+                continue
+            d = _resolve(c, pvs, scs)
+            if d:
+                usage.setdefault(d, set()).add("%s/%s" % key)
+        for i in range(int(rng.integers(0, 3))):
+            usage.setdefault(_pick(rng, drivers), set()).add("default/bound-%s-%d" % (n["name"], i))
+        n["volumeLimits"] = lim
+        n["volumeUsage"] = {d: sorted(v) for d, v in usage.items()}
+    return list(pvcs.values()), list(pvs.values()), list(scs.values())
+
+
 TOPO_KEYS = [synth.ZONE, synth.HOSTNAME, synth.CT]
 
 
@@ -318,7 +460,7 @@ def special_nsr(rng):
 
 def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, host_ports=False, topology=False,
                    affinity=False, volumes=False, namespaces=False, same_pod_ports=False, or_terms=False,
-                   special=False):
+                   special=False, volume_objects=None):
     """same_pod_ports: existing nodes' HostPortUsage also holds entries keyed by pods being scheduled
     (their own ports, or others), the case HostPortUsage.Conflicts skips and Add replaces
     (hostportusage.go:70-85).  special: NodePool and pod terms on the 'special' key (special_nsr)."""
@@ -408,9 +550,13 @@ def random_problem(seed, n_pods=120, n_its=40, n_nodes=None, n_templates=None, h
     cluster = add_topology(rng, pods, nodes, affinity, or_terms) if topology else []
     nss = add_namespaces(rng, pods, cluster) if namespaces else []
     vdrivers = add_volumes(rng, pods, nodes) if volumes else {}
+    vobj = {}
+    if volume_objects is not None:  # dict of add_volume_objects keyword arguments
+        pvcs, pvs, scs = add_volume_objects(rng, pods, nodes, **volume_objects)
+        vobj = {"persistentVolumeClaims": pvcs, "persistentVolumes": pvs, "storageClasses": scs}
     return {
         **({"namespaces": nss} if namespaces else {}),
-        "volumeDrivers": vdrivers,
+        **({"volumeDrivers": vdrivers} if volume_objects is None else vobj),
         "wellKnownLabels": synth.FAKE_WELL_KNOWN,
         "instanceTypes": its,
         "instanceTypesByNodePool": by_pool,

@@ -1,0 +1,152 @@
+"""Volume topology injection and an unbounded volume universe.
+
+The snapshot carries the cluster's PersistentVolumeClaims, PersistentVolumes and StorageClasses; the library
+runs VolumeTopology.Inject (volumetopology.go:41-140, called by Provisioner.NewScheduler before NewTopology,
+provisioner.go:283-287,432-442) and GetVolumes' driver resolution (volumeusage.go:82-182) itself, and
+encodes any number of PVCs and CSI drivers (sparse per-pod / per-node volume tables, ks_problem.h KsDev).
+
+CPU: the oracle (oracle/volumes.inc) reproduces the 17 transcribed suite_test.go scenarios; the injection is
+what decides their zones; the host encoder takes hundreds of PVCs and 7 drivers, and the binary snapshot
+round-trips them.  GPU: the HIP Solve and consolidation equal the oracle on the scenarios, on random
+problems with 300-2000 claims (shared RWX claims, zonal PVs and classes, missing objects), and on a
+consolidation cluster whose nodes mount over 1000 limited-driver PVCs."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import problems
+from karpenter_amd import Consolidator, Scheduler, inspect, snapshot_check, synth
+from oracle import bridge
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import make_volume_topology_fixtures as mvt  # noqa: E402
+
+FIXTURES = json.load(open(os.path.join(HERE, "golden", "volume_topology_scenarios.json")))
+SCENARIOS = {s["name"]: s for s in mvt.scenarios()}
+
+
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
+def test_oracle_volume_topology_scenarios(fx):
+    scn = SCENARIOS[fx["name"]]
+    assert scn["expect"] == fx["expect"] and scn["dropped"] == fx["dropped"]
+    res, _ = bridge.solve(json.dumps(scn["snapshot"]))
+    bad = mvt.check(scn, res)
+    assert not bad, bad
+
+
+def test_injection_is_what_picks_the_zone():
+    """Without the PV the same pod is not restricted to test-zone-3: the scenario pins Inject."""
+    scn = json.loads(json.dumps(SCENARIOS["volume-zones-bound"]))
+    res, _ = bridge.solve(json.dumps(scn["snapshot"]))
+    assert not mvt.check(scn, res)
+    scn["snapshot"]["persistentVolumes"][0]["spec"].pop("nodeAffinity")
+    res, _ = bridge.solve(json.dumps(scn["snapshot"]))
+    assert mvt.check(scn, res)
+
+
+def _random(seed, n_pods=300, n_claims=300, topology=False, affinity=False, n_nodes=20, **kw):
+    return problems.random_problem(seed, n_pods=n_pods, n_nodes=n_nodes, topology=topology, affinity=affinity,
+                                   volume_objects=dict(n_claims=n_claims, **kw))
+
+
+def test_host_encodes_hundreds_of_pvcs_and_drivers():
+    snap = _random(931, n_pods=600, n_claims=600)
+    d = inspect(json.dumps(snap))
+    assert d["volAny"] == 1 and d["volPvcs"] > 400 and d["volDrivers"] >= 5, d
+    assert d["volSharedPods"] > 0 and d["volStaticMounts"] > 0 and d["injectFailed"] > 0, d
+    assert snapshot_check(json.dumps(snap)) > 0
+
+
+def _volume_cluster(seed, n_nodes=60, ppn=20, topology=0):
+    """Every pod (bound or pending) mounts 1-3 claims, mostly its own; each node's VolumeUsage holds its own
+    pods' claims and its CSINode limit is 20-40 per driver: a StatefulSet-heavy cluster."""
+    snap = synth.cluster_snapshot(n_nodes, ppn, n_its=40, it_range=(4, 20), seed=seed, n_pending=4, topology=topology)
+    rng = np.random.default_rng(seed)
+    pods = snap["pendingPods"] + [p for n in snap["stateNodes"] for p in n["pods"]]
+    own = {n["name"]: n["pods"] for n in snap["stateNodes"]}
+    pvcs, pvs, scs = problems.add_volume_objects(rng, pods, snap["stateNodes"], n_claims=len(pods), share=0.05,
+                                                 broken=0.0 if topology else 0.01, own_usage=own,
+                                                 limit_range=(20, 40), mount_frac=0.9)
+    snap.update({"persistentVolumeClaims": pvcs, "persistentVolumes": pvs, "storageClasses": scs})
+    return snap
+
+
+def test_cluster_with_over_a_thousand_pvcs_encodes():
+    """The consolidation handle encodes every pod any simulation schedules (pending + all nodes' pods)."""
+    snap = _volume_cluster(71)
+    union = dict(snap, pods=snap["pendingPods"] + [p for n in snap["stateNodes"] for p in n["pods"]])
+    d = inspect(json.dumps(union))
+    assert d["volAny"] == 1 and d["volPvcs"] > 1000 and d["volStaticMounts"] > 1000, d
+    assert snapshot_check(json.dumps(union)) > 0
+    total = len({(c["metadata"]["namespace"], c["metadata"]["name"]) for c in snap["persistentVolumeClaims"]})
+    assert total > 1000, total
+
+
+# ------------------------------------------------------------------------------------------- GPU
+
+
+def _solve_both(snap):
+    s = json.dumps(snap)
+    want, _ = bridge.solve(s)
+    want.pop("stats", None)
+    got = Scheduler(s).solve()
+    return problems.canonical(want), got.canonical()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
+def test_volume_topology_scenarios_gpu(fx):
+    scn = SCENARIOS[fx["name"]]
+    want, got = _solve_both(scn["snapshot"])
+    assert got == want
+    bad = mvt.check(scn, got)
+    assert not bad, bad
+
+
+RANDOM_CASES = [(901, 300, False, False), (902, 300, True, False), (903, 600, False, False), (904, 600, True, True),
+                (905, 2000, False, False), (906, 1200, True, False)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,claims,topo,aff", RANDOM_CASES, ids=["r%d" % c[0] for c in RANDOM_CASES])
+def test_random_volume_objects_parity(seed, claims, topo, aff):
+    """Solve over PVC / PV / StorageClass objects: injected zonal terms (ANDed into every term, so relaxation
+    keeps them), resolved drivers (CSI, in-tree EBS, class provisioners through the CSI migration names),
+    shared claims (the placement log), claims already mounted on nodes, missing PVCs / classes (Inject fails:
+    no NewTopology ownership) and missing PVs (GetVolumes fails: no existing node)."""
+    snap = _random(seed, n_pods=max(300, claims // 2), n_claims=claims, topology=topo, affinity=aff)
+    want, got = _solve_both(snap)
+    assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [921, 922, 923])
+def test_shared_claims_and_tight_limits(seed):
+    """Many pods share a small claim pool (RWX) onto nodes with limits 0-3: the placement log decides which
+    claims a node already mounts."""
+    snap = _random(seed, n_pods=400, n_claims=80, share=0.6, limit_range=(0, 4), n_nodes=40)
+    want, got = _solve_both(snap)
+    assert got == want
+
+
+def _cons_both(snap):
+    s = json.dumps(snap)
+    want, _ = bridge.consolidate(s, all_sims=True)
+    got = Consolidator(s).consolidate(all_sims=True)
+    got.pop("kernel_ms")
+    return want, got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,topo", [(71, 0), (72, 0), (73, 6)])
+def test_consolidation_with_over_a_thousand_pvcs(seed, topo):
+    """Consolidation of a cluster whose nodes mount >1000 limited-driver PVCs: every simulation's volume
+    counts are copy-on-write slots over the shared table, GPU == oracle on every simulation record and
+    decision."""
+    snap = _volume_cluster(seed, topology=topo)
+    want, got = _cons_both(snap)
+    assert got == want
