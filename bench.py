@@ -90,35 +90,40 @@ def _traffic(tag):
 
 
 def _roofline(kernel, k_ms, kernel_bytes, ref_bytes, traffic_tag, per_gpu_div=1, extra=None):
-    """The dominant kernel's roofline (every field follows its definition).
+    """The dominant kernel's roofline.  `frac` is always a physical fraction of the 8 TB/s HBM peak (<= 1):
     achieved / frac: SURVEY.md §8d algorithmic bytes -- the reference's scan, counted by the oracle on this exact
-    workload (tests/golden/full_size_digests.json) -- per launch, over the HIP-event launch duration, against the
-    8 TB/s HBM peak.  Where the oracle has no count for the workload, the kernel's own scan count stands in and
-    algorithmic_bytes_source says so.  A frac above 1 is not bandwidth: the kernel skips scans the reference
-    makes (identical-pod runs placed in one step, the infeasible-topology shortcut), so the reference-scan
-    bytes it stands for exceed what HBM could move in that time; `note` says so.
-    hbm_achieved / hbm_frac: the rocprofv3 PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, the committed
-    profile in traffic_source) over the same duration: what the kernel really moves.
-    kernel_scan_bytes / kernel_scan_frac: the kernel's own count (each pod of an identical-pod run credited
-    with the first pod's scan), a bookkeeping figure kept beside the two physical ones."""
+    workload (tests/golden/full_size_digests.json) -- per launch, over the HIP-event launch duration, when that
+    rate is one HBM could deliver (the Solve lines).  Where it is not (the consolidation passes: the kernel
+    skips scans the reference makes -- identical-pod runs placed in one step, the infeasible-topology
+    shortcut -- so the reference-scan bytes it stands for exceed what HBM could move in that time), achieved /
+    frac are the rocprofv3 PMC bytes per launch (FETCH_SIZE + WRITE_SIZE of the committed profile in
+    traffic_source) over the same duration, i.e. what the kernel really moves, and `frac_basis` says so.
+    reference_scan_achieved / reference_scan_frac: the §8d ratio itself, kept beside it on every line.
+    hbm_achieved / hbm_frac: the PMC rate on every line that has a committed profile.
+    kernel_scan_bytes / kernel_scan_frac: the kernel's own scan count (each pod of an identical-pod run
+    credited with the first pod's scan), a bookkeeping figure."""
     traffic, src = _traffic(traffic_tag)
     sec = k_ms / 1000.0
     alg, asrc = (ref_bytes, "SURVEY 8d reference scan, oracle count (tests/golden/full_size_digests.json)") if ref_bytes \
         else (kernel_bytes, "kernel-counted scan (no oracle count for this workload)")
-    achieved = alg / sec / 1e9 / per_gpu_div
-    r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
-         "algorithmic_bytes_per_launch": alg, "algorithmic_bytes_source": asrc, "kernel_ms": round(k_ms, 3),
-         "hbm_achieved": None, "hbm_frac": None,
+    ref_achieved = alg / sec / 1e9 / per_gpu_div
+    r = {"bound": "hbm", "kernel": kernel, "achieved": round(ref_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": ref_achieved / HBM_PEAK_GBS, "frac_basis": "algorithmic bytes (%s)" % asrc, "traffic": traffic,
+         "traffic_source": src, "algorithmic_bytes_per_launch": alg, "algorithmic_bytes_source": asrc,
+         "kernel_ms": round(k_ms, 3), "reference_scan_achieved": round(ref_achieved, 3),
+         "reference_scan_frac": ref_achieved / HBM_PEAK_GBS, "hbm_achieved": None, "hbm_frac": None,
          "kernel_scan_bytes": kernel_bytes,
          "kernel_scan_frac": kernel_bytes / sec / 1e9 / per_gpu_div / HBM_PEAK_GBS}
     if traffic:
         ha = traffic / sec / 1e9 / per_gpu_div
         r["hbm_achieved"] = round(ha, 3)
         r["hbm_frac"] = ha / HBM_PEAK_GBS
-    if r["frac"] > 1:
-        r["note"] = ("reference-scan equivalent, kernel skips scans (identical-pod runs, infeasible-topology "
-                     "shortcut): not HBM bandwidth; hbm_frac is the physical fraction")
+    if r["reference_scan_frac"] > 1:
+        # not a bandwidth: report the physical PMC rate as the roofline (null without a committed profile)
+        r["achieved"] = r["hbm_achieved"]
+        r["frac"] = r["hbm_frac"]
+        r["frac_basis"] = ("rocprofv3 PMC HBM bytes per launch (%s): the §8d reference-scan rate (reference_scan_frac) "
+                           "exceeds the HBM peak because the kernel skips scans the reference makes" % src)
     if extra:
         r.update(extra)
     return r

@@ -5,6 +5,7 @@
 // as a length followed by their elements.  A snapshot starts with a magic, a format version and the sizes
 // of the device-facing structs, so a blob from another build is refused rather than misread.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -73,17 +74,27 @@ template <class A, class T>
 void io(A& a, std::vector<T>& v) {
   uint64_t n = v.size();
   io_len(a, n);
+  constexpr bool raw = std::is_trivially_copyable<T>::value && !std::is_same<T, bool>::value;
   if constexpr (A::reading) {
-    // every element takes at least one byte (raw elements exactly sizeof(T))
-    constexpr bool raw = std::is_trivially_copyable<T>::value && !std::is_same<T, bool>::value;
-    a.need(raw ? n * sizeof(T) : n);
-    v.resize(n);
-  }
-  if constexpr (std::is_trivially_copyable<T>::value && !std::is_same<T, bool>::value) {
-    if (n) {
-      if constexpr (A::reading) a.raw(v.data(), n * sizeof(T));
-      else a.raw(v.data(), n * sizeof(T));
+    if constexpr (raw) {
+      a.need(n * sizeof(T));  // raw elements take exactly sizeof(T): the bytes must be there before the allocation
+      v.resize(n);
+      if (n) a.raw(v.data(), n * sizeof(T));
+    } else {
+      // an element's encoded size is not bounded below by its in-memory size (an empty PodH is a few bytes,
+      // 640 in memory): the vector grows only with elements actually decoded, so a corrupt count runs out of
+      // input (ArchiveError) before it can force a large allocation
+      a.need(n);
+      v.clear();
+      v.reserve((size_t)std::min<uint64_t>(n, 1u << 12));
+      for (uint64_t i = 0; i < n; i++) {
+        T x{};
+        io(a, x);
+        v.push_back(std::move(x));
+      }
     }
+  } else if constexpr (raw) {
+    if (n) a.raw(v.data(), n * sizeof(T));
   } else {
     for (auto& x : v) io(a, x);
   }

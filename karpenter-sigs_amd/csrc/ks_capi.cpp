@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -162,6 +163,10 @@ struct ks_results {
     }
   };
   ks_problem* pb = nullptr;  // a reference on the problem the lazy rendering reads (ks_problem_free defers)
+  // First-use rendering writes the claims' caches: serialised, so two threads reading one Results (ctypes
+  // and cgo release the interpreter / scheduler around the call) render once; what a call hands out is
+  // never rebuilt afterwards.
+  mutable std::mutex render;
   ~ks_results() {
     if (pb && --pb->refs == 0) delete pb;
   }
@@ -930,7 +935,9 @@ int ks_problem_create(const char* json, size_t len, ks_problem** out) {
 // --- binary snapshot (ks_archive.h, ks_snapshot.cpp) ----------------------------------------------------
 extern "C++" {
 namespace {
-constexpr char kProblemMagic[8] = {'K', 'S', 'P', 'R', 'O', 'B', '0', '1'};
+// the format version: 03 = round 5 (sparse volume tables, injectFailed); 02 = round 4 (group sets);
+// 01 = round 3.  A blob of another version is refused with a version error (snapshot_check_header).
+constexpr char kProblemMagic[8] = {'K', 'S', 'P', 'R', 'O', 'B', '0', '3'};
 }  // namespace
 
 void snapshot_header(ArOut& a, const char magic[8]) {
@@ -943,6 +950,9 @@ void snapshot_check_header(ArIn& a, const char magic[8]) {
   uint32_t v[4];
   a.raw(m, 8);
   a.raw(v, sizeof(v));
+  if (memcmp(m, magic, 6) == 0 && memcmp(m, magic, 8) != 0)  // the same kind, another format version
+    throw KsError(KS_ERR_PARSE, "binary snapshot format version " + std::string(m + 6, 2) + ", this build reads version " +
+                                    std::string(magic + 6, 2));
   if (memcmp(m, magic, 8) != 0) throw KsError(KS_ERR_PARSE, "not a binary snapshot of this kind");
   if (v[0] != 1u || v[1] != sizeof(KsDims) || v[2] != sizeof(KeyMeta) || v[3] != sizeof(Host))
     throw KsError(KS_ERR_PARSE, "binary snapshot from another build of the library");
@@ -1141,7 +1151,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   // caller pays both launches, so the reported times are their sums (the re-plan is remembered).
   float ms = 0, setup = 0, fms = 0, fnms = 0;
   int feasLaunches = 0, attempts = 0;
-  for (int attempt = 0; attempt < 2; attempt++) {
+  for (int attempt = 0; attempt < 3; attempt++) {
     attempts++;
     HIPCHK(hipEventRecord(e0, pb->stream));
     HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp,
@@ -1165,6 +1175,11 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
     fms += f;
     int64_t err = 0;
     HIPCHK(hipMemcpy(&err, w0.counters + CT_ERROR, 8, hipMemcpyDeviceToHost));
+    if (err == KE_LEAN_EXIT && pb->dev.d.lean) {
+      // shared UIDs and a push-back: the non-LEAN instantiation (remembered for later Solves of this problem)
+      pb->dev.d.lean = 0;
+      continue;
+    }
     if (err != KE_CLAIM_CAP || pb->wideKO) break;
     // more NodeClaims than the default plan holds: re-plan with claim positions filling the LDS
     // (remembered for later Solves of this problem) and solve again
@@ -1205,6 +1220,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
 int ks_results_json(const ks_results* r, char** json_out) {
   API_TRY
   std::string o = "{\"newNodeClaims\":[";
+  std::lock_guard<std::mutex> lk(r->render);
   for (size_t i = 0; i < r->claims.size(); i++) {
     finish_json(r->pb->host, r->claims[i]);
     o += (i ? "," : "") + r->claims[i].json;
@@ -1261,7 +1277,10 @@ int ks_results_nodeclaim_requests(const ks_results* r, int i, int* n, const char
 int ks_results_nodeclaim_requirements(const ks_results* r, int i, int* n, const ks_requirement** reqs) {
   if (!r || i < 0 || i >= (int)r->claims.size()) return KS_ERR_ARG;
   const auto& c = r->claims[(size_t)i];
-  finish_reqs(r->pb->host, c);
+  {
+    std::lock_guard<std::mutex> lk(r->render);
+    finish_reqs(r->pb->host, c);
+  }
   if (n) *n = (int)c.reqC.size();
   if (reqs) *reqs = c.reqC.data();
   return KS_OK;

@@ -191,6 +191,12 @@ struct ks_cons {
     bool multi = false;
   };
   std::unique_ptr<ks_problem> pb;
+  // An update whose device upload failed left the host model ahead of HBM: the handle refuses every later
+  // call (KS_ERR_HIP) instead of simulating a mix of the two (rebuild it with ks_cons_create).
+  std::string broken;
+  void check_usable() const {
+    if (!broken.empty()) throw KsError(KS_ERR_HIP, "consolidation handle unusable after a failed update upload (" + broken + ")");
+  }
   // [0, nPass): the pass's candidates in disruption-cost order; [nPass, size): nodes only
   // Validation.ShouldDisrupt admits (their pool has consolidateAfter Never), for validation's mapping
   std::vector<Cand> cands;
@@ -1439,6 +1445,7 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   // builds its plan into the previous plan's buffers
   c.invalidate_launch();
   KsDev& D = pb.dev;
+  try {
   if (!rows.empty() || !rm.empty())
     HIPCHK(hipMemcpyAsync((void*)D.n_avail, h.tab.n_avail.data(), 8 * h.tab.n_avail.size(), hipMemcpyHostToDevice,
                           pb.stream));
@@ -1449,6 +1456,10 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     HIPCHK(hipMemcpyAsync((void*)D.pool_rem0, h.tab.pool_rem0.data(), 8 * h.tab.pool_rem0.size(),
                           hipMemcpyHostToDevice, pb.stream));
   HIPCHK(hipStreamSynchronize(pb.stream));
+  } catch (const std::exception& e) {
+    c.broken = e.what();
+    throw;
+  }
   pt.mark("upload rows");
 }
 
@@ -1566,7 +1577,8 @@ template <class A> void io(A& a, ks_cons::Sim& x) { io_all(a, x.cands, x.multi);
 template <class A> void io(A& a, ks_cons::CandIn& x) { io_all(a, x.k, x.remaining, x.passOk); }
 }  // namespace ks
 namespace {
-constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '2'};
+// 03 = round 5 (the embedded problem's format, KSPROB03); 02 = round 4
+constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '3'};
 template <class A> void cons_io(A& a, ks_cons& c) {
   io_all(a, c.cands, c.nPass, c.sims, c.multiHi, c.pending, c.deleting, c.nominated, c.hostnameSeed, c.recWords,
          c.candIn, c.nodePods, c.podNode, c.podBlock, c.podCost, c.nodeGone, c.updates);
@@ -1580,7 +1592,7 @@ void cons_check(const ks_cons& c) {
   if (c.recWords != rec_words(h.dims.TW)) bad("record width");
   if ((int)c.sims.size() != c.multiHi + c.nPass) bad("simulation plan");
   for (auto& cd : c.cands) {
-    if (cd.node < 0 || cd.node >= N || cd.it >= h.dims.T) bad("candidate node");
+    if (cd.node < 0 || cd.node >= N || cd.it < 0 || cd.it >= h.dims.T) bad("candidate node");
     for (int p : cd.pods)
       if (p < 0 || p >= P) bad("candidate pod");
   }
@@ -1680,6 +1692,7 @@ int ks_cons_inspect_update(const char* json, size_t len, const char* update_json
 int ks_cons_update(ks_cons* c, const char* update_json, size_t len) {
   API_TRY
   if (!c || !update_json) throw KsError(KS_ERR_ARG, "null argument");
+  c->check_usable();
   DeviceGuard guard(c->pb->device, nullptr);
   const ksjson::Value delta = ksjson::Parser(update_json, len ? len : strlen(update_json)).parse();
   apply_update(*c, delta, true);
@@ -1707,6 +1720,7 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
   API_TRY
   if (!c || (!records && (records_on_device || world != 1)) || world < 1 || rank < 0 || rank >= world)
     throw KsError(KS_ERR_ARG, "bad argument");
+  c->check_usable();
   DeviceGuard guard(c->pb->device, opts);
   const double ms = run_sims(*c, rank, world, records, records_on_device != 0);
   if (kernel_ms) *kernel_ms = ms;
@@ -1717,6 +1731,7 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
 int ks_cons_validate(ks_cons* c, const char* command_json, size_t len, const ks_solve_opts* opts, char** json_out) {
   API_TRY
   if (!c || !command_json || !json_out) throw KsError(KS_ERR_ARG, "null argument");
+  c->check_usable();
   DeviceGuard guard(c->pb->device, opts);
   ksjson::Value cmd = ksjson::Parser(command_json, len ? len : strlen(command_json)).parse();
   if (!cmd.is_obj()) throw KsError(KS_ERR_PARSE, "command is not an object");

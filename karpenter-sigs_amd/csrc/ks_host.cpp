@@ -1424,7 +1424,10 @@ void Host::build(const Value& root) {
   dims.Kcap = std::max(1, std::min(P, 16384));
   bool anyKeys = false;
   for (int32_t f : tab.st_flags) anyKeys |= (f & SF_HAS_KEYS) != 0;
-  dims.lean = !dims.hpAny && !dims.volAny && !dims.dupUids && !dims.negReq && groups.empty() && !anyKeys ? 1 : 0;
+  // Shared UIDs (BenchmarkScheduling's literal pods all have UID "") matter only once a pod is pushed back
+  // (Queue.Pop's lastLen is keyed by UID, queue.go:54-69): the LEAN Solve takes them and leaves at the first
+  // push-back (KE_LEAN_EXIT), after which the host re-runs the Solve non-LEAN.
+  dims.lean = !dims.hpAny && !dims.volAny && !dims.negReq && groups.empty() && !anyKeys ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------------

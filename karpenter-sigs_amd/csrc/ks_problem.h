@@ -77,8 +77,8 @@ struct KsDims {
                            // ceil(G / 64), at least 1
   uint64_t fkMulti;        // keys some instance type constrains with more than one value (feas_masks)
   int32_t fmOn;            // st_fm is computed (k_feasibility) and k_solve reads it
-  int32_t lean;            // none of host ports, limited volumes, pod label requirements, shared UIDs,
-                           // negative requests, topology: k_solve's LEAN instantiation applies
+  int32_t lean;            // none of host ports, limited volumes, pod label requirements, negative requests,
+                           // topology: k_solve's LEAN instantiation applies (with shared UIDs until a push-back)
   int32_t fnOn;            // st_fn is computed (k_feasibility_nodes) and k_solve reads it
   int32_t FNR;             // rows of st_fn: the relaxation states with label requirements
 };
@@ -295,6 +295,7 @@ enum Counter {
   CT_SORT_EXACT,   // claim re-sorts that ran the lane-0 pdqsort (not the wave-parallel partialInsertionSort)
   CT_NCOUNTERS = 27
 };
-enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3 };
+// KE_LEAN_EXIT: a LEAN Solve of pods sharing a UID met its first push-back (the host re-runs it non-LEAN)
+enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3, KE_LEAN_EXIT = 4 };
 
 }  // namespace ks

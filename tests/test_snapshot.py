@@ -166,3 +166,31 @@ def test_create_binary_rejects_flipped_dims():
     with pytest.raises(KsError) as e:
         Scheduler.from_binary(bytes(bad))
     assert e.value.code == KS_ERR_PARSE
+
+
+def test_binary_snapshot_version_mismatch_is_named():
+    """a blob of an older format version (KSPROB01 / 02) is refused as a version mismatch, not as
+    an inconsistent table."""
+    blob = encode_binary(json.dumps(problems.random_problem(3)))
+    assert blob[:8] == b"KSPROB03"
+    for old in (b"KSPROB01", b"KSPROB02"):
+        with pytest.raises(KsError) as e:
+            check_binary(old + blob[8:])
+        assert e.value.code == KS_ERR_PARSE and "format version" in str(e.value), str(e.value)
+
+
+def test_corrupt_element_count_does_not_allocate():
+    """a vector of non-trivial elements (pods, nodes) whose count is corrupt grows only with the
+    elements actually decoded, so the blob runs out of input (a parse error) instead of forcing a huge
+    allocation; here the node list's count is raised to 2^28 in a small blob."""
+    snap = problems.random_problem(5, n_nodes=6)
+    blob = encode_binary(json.dumps(snap))
+    name = snap["stateNodes"][0]["name"]
+    enc = struct.pack("<Q", len(name)) + name.encode()
+    at = blob.find(struct.pack("<Q", 6) + enc)
+    assert at >= 0
+    bad = bytearray(blob)
+    struct.pack_into("<Q", bad, at, 1 << 28)
+    with pytest.raises(KsError) as e:
+        check_binary(bytes(bad))
+    assert e.value.code == KS_ERR_PARSE

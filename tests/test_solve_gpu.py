@@ -195,6 +195,28 @@ def test_config1_literal_benchmark_pods():
     assert d is None, d
 
 
+@pytest.mark.parametrize("seed", [440, 441, 442, 443])
+def test_lean_shared_uids_with_push_backs(seed):
+    """Resource-only pods sharing UID "" (BenchmarkScheduling's literal pods) run the LEAN Solve; a pod that
+    fails (too large for every instance type, or past a NodePool limit) is pushed back, and the Solve leaves
+    the LEAN kernel there (KE_LEAN_EXIT) and re-runs non-LEAN, where Queue.Pop re-reads the shared staleness
+    entry (queue.go:54-69).  Seed 440 has no failure (stays LEAN)."""
+    snap = synth.benchmark_snapshot(600, 60, seed, diverse=False, literal=True)
+    if seed in (441, 443):
+        for k in range(3):
+            big = synth.pod(900000 + k, cpu="1000", mem="1Gi")
+            big["metadata"].pop("uid", None)
+            snap["pods"].insert(100 * (k + 1), big)
+    if seed in (442, 443):
+        pool = synth.node_pool("default-pool", limits={"cpu": "150"})
+        snap["nodePools"] = [pool]
+    want, got = _solve_both(snap)
+    d = _diff(want, got)
+    assert d is None, d
+    if seed != 440:
+        assert want["podErrors"], "the case must push pods back"
+
+
 @pytest.mark.parametrize("seed", list(range(400, 412)))
 def test_queue_ties_parity(seed):
     """Random problems whose pods share UIDs and timestamps in groups, so NewQueue's order of equal
