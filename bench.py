@@ -194,13 +194,15 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
             need = c.needed_sims(recs, world)
             rsw = c.requirement_words
             table = {}
-            for s in need:
-                owner = s % world
-                t = torch.zeros(rsw, dtype=torch.int32, device=dev)
-                if rank == owner:
-                    t.copy_(torch.frombuffer(bytearray(c.claim_requirements(s)), dtype=torch.int32))
-                dist.broadcast(t, src=owner)
-                table[s] = t.cpu().numpy().tobytes()
+            if need:  # one collective: each owner fills its rows, zeros elsewhere, summed over the ranks
+                t = torch.zeros(len(need) * rsw, dtype=torch.int32, device=dev)
+                for i, s in enumerate(need):
+                    if s % world == rank:
+                        t[i * rsw:(i + 1) * rsw].copy_(torch.frombuffer(bytearray(c.claim_requirements(s)),
+                                                                        dtype=torch.int32))
+                dist.all_reduce(t)
+                host = t.cpu().numpy()
+                table = {s: host[i * rsw:(i + 1) * rsw].tobytes() for i, s in enumerate(need)}
             doc = c.decide(recs, world, fetch=table.__getitem__, candidates=False, sims=False) if rank == 0 else None
         return ms, recs, doc
 

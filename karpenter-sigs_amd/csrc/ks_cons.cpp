@@ -240,6 +240,12 @@ struct ks_cons {
     KsWork* lworks = nullptr;
     int32_t* lrec = nullptr;
     int32_t* hrec = nullptr;  // pinned host staging of the records (one DMA per pass, no pageable bounce)
+    // A world-1 pass whose records stay in the handle (ks_cons_run with records NULL) downloads only their
+    // headers (k_rec_headers: RF_HDR words per simulation, + 2 status words the device's record checks fill);
+    // the decision fetches the option words of the few records it renders from lrec (RecView)
+    int32_t* lhdr = nullptr;
+    int32_t* hhdr = nullptr;
+    bool hdrOnly = false;
     int32_t* lentries = nullptr;
     int32_t* lentrySim = nullptr;
     int32_t* lpodmap = nullptr;
@@ -255,12 +261,13 @@ struct ks_cons {
     Plan lplan{};
     std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
     // allocation capacities: a new plan (another rank / world, an update) reuses the buffers that fit
-    size_t capBuf = 0, capWorks = 0, capRec = 0, capHrec = 0, capEnt = 0, capRunw = 0, capTemp = 0;
+    size_t capBuf = 0, capWorks = 0, capRec = 0, capHrec = 0, capEnt = 0, capRunw = 0, capTemp = 0, capHdr = 0, capHhdr = 0;
     void release() {
       for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
-                      (void*)lrunlen, (void*)lrunw, (void*)lkeys, (void*)lvals, ltemp})
+                      (void*)lrunlen, (void*)lrunw, (void*)lkeys, (void*)lvals, ltemp, (void*)lhdr})
         if (p) (void)hipFree(p);
       if (hrec) (void)hipHostFree(hrec);
+      if (hhdr) (void)hipHostFree(hhdr);
       *this = Launch{};  // stale lookups (claim requirements, counters) now fail cleanly
     }
     // drop the plan, keep the allocations
@@ -270,6 +277,7 @@ struct ks_cons {
       lhost.clear();
       lnent = lrbits = lsbits = lnmw = 0;
       lsorted = false;
+      hdrOnly = false;
       lplan = Plan{};
     }
   };
@@ -745,6 +753,14 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   char* ibase = base + inBase;
   grow(c.L.lworks, c.L.capWorks, sizeof(KsWork) * nsz);
   grow(c.L.lrec, c.L.capRec, 4 * (size_t)c.recWords * nsz);
+  const size_t hdrBytes = 4 * (size_t)RF_HDR * nsz + 16;  // headers + the two u64 status words
+  grow(c.L.lhdr, c.L.capHdr, hdrBytes);
+  if (!c.L.hhdr || hdrBytes > c.L.capHhdr) {
+    if (c.L.hhdr) HIPCHK(hipHostFree(c.L.hhdr));
+    c.L.hhdr = nullptr;
+    HIPCHK(hipHostMalloc((void**)&c.L.hhdr, hdrBytes, hipHostMallocDefault));
+    c.L.capHhdr = hdrBytes;
+  }
   if (!c.L.hrec || 4 * (size_t)c.recWords * nsz > c.L.capHrec) {
     if (c.L.hrec) HIPCHK(hipHostFree(c.L.hrec));
     c.L.hrec = nullptr;
@@ -974,24 +990,62 @@ using RsFn = std::function<const uint32_t*(int)>;
 // clk: the methods' timeouts on a virtual clock that advances clk->sim_seconds per simulation the replay
 // consults (MultiNodeConsolidation's 1 min, multinodeconsolidation.go:34,99-110; SingleNodeConsolidation's
 // 3 min, singlenodeconsolidation.go:29,58-65); null or sim_seconds 0: the clock never passes a timeout.
-std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool allSims, const RsFn& rsOf,
+// The simulation records a decision reads: the gathered records ([rank][slot] layout), or -- after a world-1
+// ks_cons_run that kept them in the handle -- their headers (k_rec_headers, already checked on the device),
+// the option words of the few records the output renders fetched from the device on first use.
+struct RecView {
+  const ks_cons& c;
+  int world = 1;
+  const int32_t* full_ = nullptr;
+  const int32_t* hdr_ = nullptr;
+  mutable std::map<int, std::vector<int32_t>> fetched;
+  const int32_t* head(int sim) const {
+    if (full_) return full_ + ((size_t)(sim % world) * c.per_rank(world) + (size_t)(sim / world)) * c.recWords;
+    return hdr_ + (size_t)sim * RF_HDR;
+  }
+  const int32_t* full(int sim) const {
+    if (full_) return head(sim);
+    std::vector<int32_t>& v = fetched[sim];
+    if (v.empty()) {
+      v.resize((size_t)c.recWords);
+      HIPCHK(hipMemcpy(v.data(), c.L.lrec + (size_t)sim * c.recWords, 4 * (size_t)c.recWords, hipMemcpyDeviceToHost));
+    }
+    return v.data();
+  }
+};
+
+std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool allSims, const RsFn& rsOf,
                         bool withCandidates = true, const ks_cons_clock* clk = nullptr, bool withSims = true) {
   const double simS = clk ? clk->sim_seconds : 0.0;
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
-  const int per = c.per_rank(world);
-  auto rec = [&](int sim) -> const int32_t* {
-    return recs + ((size_t)(sim % world) * per + (size_t)(sim / world)) * c.recWords;
-  };
-  for (size_t s = 0; s < c.sims.size(); s++)
+  auto rec = [&](int sim) -> const int32_t* { return rv.head(sim); };
+  static const char* checkName[] = {"", "action out of range", "NodeClaim counts", "Delete with NodeClaims",
+                                    "Replace without exactly one NodeClaim", "template out of range",
+                                    "options beyond the template's list", "price filter output not a subset of its input",
+                                    "option count", "price-filter counts"};
+  if (!rv.full_) {  // headers: k_rec_headers checked every record on the device
+    const uint64_t* status = (const uint64_t*)(rv.hdr_ + (size_t)RF_HDR * c.sims.size());
+    if (status[1] != ~0ull) {
+      const int s = (int)(status[1] >> 32), e = (int)(uint32_t)status[1];
+      throw KsError(e == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
+                    "simulation " + std::to_string(s) + " reported kernel error " + std::to_string(e));
+    }
+    if (status[0] != ~0ull) {
+      const unsigned k = (unsigned)(uint32_t)status[0];
+      throw KsError(KS_ERR_INTERNAL, "simulation " + std::to_string(status[0] >> 32) + " record check (device): " +
+                                         (k < 10 ? checkName[k] : "?"));
+    }
+  }
+  for (size_t s = 0; s < c.sims.size() && rv.full_; s++)
     if (rec((int)s)[RF_ERROR] != KE_OK)
       throw KsError(rec((int)s)[RF_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
                     "simulation " + std::to_string(s) + " reported kernel error " + std::to_string(rec((int)s)[RF_ERROR]));
   // Record invariants (a lost or stale device store becomes a loud error, not a wrong decision): the action
   // agrees with the NodeClaim count (computeConsolidation, consolidation.go:113-194: Delete = none, Replace =
   // exactly one); NewNodeClaims[0]'s options lie in its template's list and number RF_NOPT; filterByPrice's
-  // and filterOutSameType's outputs are subsets of their inputs.
-  for (size_t s = 0; s < c.sims.size(); s++) {
+  // and filterOutSameType's outputs are subsets of their inputs.  (Headers only: checked on the device.)
+  for (size_t s = 0; s < c.sims.size() && rv.full_; s++) {
     const int32_t* r = rec((int)s);
     auto bad = [&](const char* what) {
       throw KsError(KS_ERR_INTERNAL, "simulation " + std::to_string(s) + " record check: " + what);
@@ -1042,7 +1096,7 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
     if (r[RF_NCLAIMS] > 0) {
       o += ",\"claim0\":{\"nodePoolName\":";
       ksjson::quote(o, h.tpls[(size_t)r[RF_TPL]].pool);
-      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR));
+      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], rv.full(sim) + RF_HDR));
       o += ",\"requirementsString\":";
       ksjson::quote(o, h.reqsString(rsOf(sim), before.at(sim) + r[RF_HOST]));
       o += "}";
@@ -1052,9 +1106,9 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
     static const char* sact[] = {"no-op", "delete", "replace", "error"};
     o += std::string(",\"action\":\"") + sact[r[RF_ACTION]] + "\"";
     if (r[RF_ACTION] == CA_REPLACE) {
-      o += ",\"priceOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR + d.TW));
+      o += ",\"priceOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], rv.full(sim) + RF_HDR + d.TW));
       if (c.sims[(size_t)sim].multi)
-        o += ",\"sameTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR + 2 * d.TW));
+        o += ",\"sameTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], rv.full(sim) + RF_HDR + 2 * d.TW));
     }
     return o + "}";
   };
@@ -1076,7 +1130,7 @@ std::string decide_json(const ks_cons& c, const int32_t* recs, int world, bool a
       }
       o += ",\"replacement\":{\"nodePoolName\":";
       ksjson::quote(o, h.tpls[(size_t)r[RF_TPL]].pool);
-      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], r + RF_HDR + (multi ? 2 : 1) * d.TW));
+      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], rv.full(sim) + RF_HDR + (multi ? 2 : 1) * d.TW));
       o += ",\"requirements\":[";
       const uint64_t pr = rs_present(rs.data());
       bool first = true;
@@ -1203,10 +1257,16 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
   if (onDevice) {
     if (all > bytes) HIPCHK(hipMemsetAsync((char*)records + bytes, 0, all - bytes, pb.stream));
     if (bytes) HIPCHK(hipMemcpyAsync(records, c.L.lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
+  } else if (!records && world == 1) {  // the records stay in the handle: headers + device checks only
+    unsigned long long* status = (unsigned long long*)(c.L.lhdr + (size_t)RF_HDR * ns);
+    HIPCHK(rec_headers(c.L.lrec, ns, c.recWords, pb.host.dims.TW, pb.dev.tpl_it_beg, pb.host.dims.NTPL, c.L.lhdr, status,
+                       pb.stream));
+    HIPCHK(hipMemcpyAsync(c.L.hhdr, c.L.lhdr, 4 * (size_t)RF_HDR * ns + 16, hipMemcpyDeviceToHost, pb.stream));
   } else if (bytes) {
     HIPCHK(hipMemcpyAsync(c.L.hrec, c.L.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
   }
   HIPCHK(hipStreamSynchronize(pb.stream));
+  c.L.hdrOnly = !onDevice && !records && world == 1;
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, c.ev[0], c.ev[1]));
   if (!onDevice && records) {  // (records == NULL: they stay in the handle's pinned buffer, host_records)
@@ -1707,12 +1767,18 @@ int ks_cons_num_sims(const ks_cons* c) { return c ? (int)c->sims.size() : 0; }
 int ks_cons_record_bytes(const ks_cons* c) { return c ? 4 * c->recWords : 0; }
 int ks_cons_records_per_rank(const ks_cons* c, int world) { return c && world > 0 ? c->per_rank(world) : 0; }
 
-// The gathered records: the caller's, or (NULL) those a world-1 ks_cons_run left in the handle's pinned buffer.
-static const int32_t* host_records(const ks_cons* c, const void* records, int world) {
-  if (records) return (const int32_t*)records;
-  if (world != 1 || c->L.lworld != 1 || !c->L.hrec || c->L.lsims.size() != c->sims.size())
+// The gathered records: the caller's, or (NULL) those a world-1 ks_cons_run left in the handle (their headers in
+// its pinned buffer).
+static RecView host_records(const ks_cons* c, const void* records, int world) {
+  RecView v{*c, world};
+  if (records) {
+    v.full_ = (const int32_t*)records;
+    return v;
+  }
+  if (world != 1 || c->L.lworld != 1 || !c->L.hdrOnly || c->L.lsims.size() != c->sims.size())
     throw KsError(KS_ERR_ARG, "records NULL without a world-1 run of every simulation on this handle");
-  return c->L.hrec;
+  v.hdr_ = c->L.hhdr;
+  return v;
 }
 
 int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void* records, int records_on_device,
@@ -1742,7 +1808,7 @@ int ks_cons_validate(ks_cons* c, const char* command_json, size_t len, const ks_
 
 // The simulations whose NewNodeClaims[0] requirement record the decision output needs, in the order
 // ks_cons_decide consumes them (a dry run of the replay that records every lookup).
-static std::vector<int> needed_sims(const ks_cons& c, const int32_t* recs, int world, bool allSims) {
+static std::vector<int> needed_sims(const ks_cons& c, const RecView& recs, int world, bool allSims) {
   std::vector<int> need;
   std::set<int> seen;
   std::vector<uint32_t> zero(std::max(c.pb->host.dims.RSW, 1), 0);
@@ -1794,7 +1860,7 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
                          const ks_cons_clock* clock, char** json_out) {
   API_TRY
   if (!c || !json_out || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
-  const int32_t* recs = host_records(c, records, world);
+  const RecView recs = host_records(c, records, world);
   const bool all_sims = (flags & KS_CONS_ALL_SIMS) != 0;
   if (!rs_table && world == 1 && c->L.lworld == 1) {
     // One rank ran every simulation: the requirement records the output needs are read from this handle's
@@ -1804,7 +1870,7 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
     auto fetch = [&](int sim) -> const uint32_t* {
       std::vector<uint32_t>& v = cache[sim];
       if (v.empty()) {
-        const int32_t claim = recs[(size_t)sim * c->recWords + RF_CLAIM];
+        const int32_t claim = recs.head(sim)[RF_CLAIM];
         if (sim < 0 || sim >= (int)c->L.lhost.size() || claim < 0)
           throw KsError(KS_ERR_INTERNAL, "simulation " + std::to_string(sim) + " has no NodeClaim record");
         v.resize((size_t)RSW);
@@ -1850,11 +1916,14 @@ int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n) {
 }
 
 double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world) {
-  if (!c || world < 1 || (!records && !(world == 1 && c->L.lworld == 1 && c->L.hrec))) return 0;
-  const int32_t* r = records ? (const int32_t*)records : c->L.hrec;
+  if (!c || world < 1 || (!records && !(world == 1 && c->L.lworld == 1 && c->L.hdrOnly))) return 0;
+  // (headers: RF_HDR words per simulation, the algorithmic-byte words among them)
+  const int32_t* r = records ? (const int32_t*)records : c->L.hhdr;
+  const size_t stride = records ? (size_t)c->recWords : (size_t)RF_HDR;
+  const size_t n = records ? (size_t)c->per_rank(world) * world : c->sims.size();
   double sum = 0;
-  for (size_t i = 0; i < (size_t)c->per_rank(world) * world; i++) {
-    const int32_t* x = r + i * c->recWords;
+  for (size_t i = 0; i < n; i++) {
+    const int32_t* x = r + i * stride;
     sum += (double)(((uint64_t)(uint32_t)x[RF_ALGB_HI] << 32) | (uint32_t)x[RF_ALGB_LO]);
   }
   return sum;

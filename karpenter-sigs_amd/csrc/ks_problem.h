@@ -192,7 +192,9 @@ struct KsDev {
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };
 enum TopoGroupType : int32_t { TG_SPREAD = 0, TG_AFFINITY = 1, TG_ANTI = 2 };
 enum TgMeta : int32_t {  // per topology group, int32 words
-  TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST, TGM_WORDS = 12
+  TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST,
+  TGM_LATE,  // created by a relaxation mid-Solve (tg_late): its existing nodes start unregistered
+  TGM_WORDS = 12
 };
 enum PodFlag : int32_t {
   PF_PROVISIONABLE = 1,

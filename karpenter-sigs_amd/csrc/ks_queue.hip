@@ -146,3 +146,64 @@ hipError_t sim_run_lengths(const int32_t* podmap, const int32_t* entry_sim, cons
 }
 
 }  // namespace ks
+
+namespace ks {
+
+// Consolidation record headers (ks_cons.cpp RecView): per simulation the first RF_HDR words of its record,
+// compacted for the host (a world-1 pass downloads these instead of every record's option words), and the
+// record invariants the host replay would otherwise read every record for (a lost or stale device store
+// becomes a loud error, not a wrong decision): computeConsolidation's action against the NodeClaim count
+// (consolidation.go:113-194), NewNodeClaims[0]'s options inside its template's list and numbering RF_NOPT,
+// filterByPrice's and filterOutSameType's outputs subsets of their inputs with the recorded counts.
+// status[0] = min over failing simulations of (sim << 32 | check), status[1] = min of (sim << 32 | kernel
+// error) over simulations reporting one; ~0 when none (the caller sets them before the launch).
+__global__ void k_rec_headers(const int32_t* recs, int ns, int recWords, int TW, const int32_t* tplBeg, int ntpl,
+                              int32_t* hdr, unsigned long long* status) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= ns) return;
+  const int32_t* r = recs + (size_t)s * recWords;
+  int32_t h[RF_HDR];
+  for (int i = 0; i < RF_HDR; i++) {
+    h[i] = r[i];
+    hdr[(size_t)s * RF_HDR + i] = h[i];
+  }
+  int bad = 0;
+  if (h[RF_ACTION] < CA_NOOP || h[RF_ACTION] > CA_ERROR) bad = 1;
+  else if (h[RF_NCLAIMS] < 0 || h[RF_HOSTINCR] < h[RF_NCLAIMS]) bad = 2;
+  else if (h[RF_ACTION] == CA_DELETE && h[RF_NCLAIMS] != 0) bad = 3;
+  else if (h[RF_ACTION] == CA_REPLACE && h[RF_NCLAIMS] != 1) bad = 4;
+  else if (h[RF_NCLAIMS] > 0) {
+    if (h[RF_TPL] < 0 || h[RF_TPL] >= ntpl) {
+      bad = 5;
+    } else {
+      const int nIT = tplBeg[h[RF_TPL] + 1] - tplBeg[h[RF_TPL]];
+      const uint32_t* o = (const uint32_t*)r + RF_HDR;
+      int nopt = 0, nprice = 0, nsame = 0;
+      for (int w = 0; w < TW; w++) {
+        const int lo = w * 32;
+        const uint32_t valid = nIT >= lo + 32 ? ~0u : nIT > lo ? (1u << (nIT - lo)) - 1u : 0u;
+        const uint32_t a = o[w], b = o[TW + w], c = o[2 * TW + w];
+        if (a & ~valid) bad = 6;
+        if ((b & ~a) || (c & ~b)) bad = bad ? bad : 7;
+        nopt += __popc(a);
+        nprice += __popc(b);
+        nsame += __popc(c);
+      }
+      if (!bad && (nopt != h[RF_NOPT] || nopt == 0)) bad = 8;
+      if (!bad && (nprice != h[RF_NPRICE] || nsame != h[RF_NSAME])) bad = 9;
+    }
+  }
+  if (bad) atomicMin(status, ((unsigned long long)s << 32) | (unsigned)bad);
+  if (h[RF_ERROR] != KE_OK) atomicMin(status + 1, ((unsigned long long)s << 32) | (unsigned)h[RF_ERROR]);
+}
+
+hipError_t rec_headers(const int32_t* recs, int ns, int recWords, int TW, const int32_t* tplBeg, int ntpl, int32_t* hdr,
+                       unsigned long long* status, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(status, 0xff, 2 * sizeof(unsigned long long), st);
+  if (e != hipSuccess || ns <= 0) return e;
+  hipLaunchKernelGGL(k_rec_headers, dim3((ns + 255) / 256), dim3(256), 0, st, recs, ns, recWords, TW, tplBeg, ntpl, hdr,
+                     status);
+  return hipGetLastError();
+}
+
+}  // namespace ks

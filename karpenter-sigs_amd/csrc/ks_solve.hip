@@ -564,6 +564,13 @@ struct Solver {
   LU32 s_tvol;          // SIM: [ceil(N/32)] nodes whose volume counts live in a W.n_vc slot (W.n_vslot)
   LI32 s_tgm;           // [G][TGM_WORDS] topology group metadata
   LI32 s_tmin;          // [G] domainMinCount of the popped pod, per spread group
+  // [G][2] per hostname spread / anti-affinity group (not late): the first existing node whose count is within
+  // the group's threshold for a pod that is not (0) / is (1) selected by it (anti-affinity: 0 pods; spread:
+  // maxSkew - self, the hostname domainMinCount being 0).  Counts only grow after the prologue and every node
+  // is registered, so the nodes below it fail topo_node_state1 for every later pod matching the group: a dead
+  // prefix the scan skips (topo_skip_advance keeps it, t_skip is the popped pod's largest).
+  LI32 s_tptr;
+  int t_skip = 0;
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
   LU32 s_trs1;          // [RSW] one group's domains as a single-key record
   LI32 s_tcs;           // [pl.tcl] the count table's LDS-resident prefix: the small-key groups (a Solve: the
@@ -1070,9 +1077,14 @@ struct Solver {
     t_any = anyM;
     t_rec = anyR;
     t_nonode = false;
+    t_skip = 0;
     for (int w = 0; w < GMW; w++)
       for (uint64_t m = gword(GS_MASK, w, t_mask); m; m &= m - 1) {
         const int g = 64 * w + ctz64(m);
+        if (tg(g, TGM_HOST) && !tg(g, TGM_LATE) && tg(g, TGM_TYPE) != TG_AFFINITY) {
+          const int p = s_tptr[2 * g + (tg(g, TGM_TYPE) == TG_SPREAD && sel_has(g) ? 1 : 0)];
+          t_skip = p > t_skip ? p : t_skip;
+        }
         if (tg(g, TGM_TYPE) == TG_AFFINITY) {
           const int nv = tg(g, TGM_NV);
           bool pos = false, reg = false;
@@ -1352,6 +1364,7 @@ struct Solver {
             rec = v >= 0;
           }
           if (!SIM && tg(g, TGM_HOST) && rdl(rec, 0)) hg |= 1ull << (g & 63);
+          if (tg(g, TGM_HOST) && !tg(g, TGM_LATE) && tg(g, TGM_TYPE) != TG_AFFINITY) topo_skip_advance(g, node);
           continue;
         }
         const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
@@ -1388,6 +1401,38 @@ struct Solver {
     }
     hbm_release();
     wsync();
+  }
+
+  // The dead prefix of hostname group g (s_tptr) after a pod was recorded on node `node`: a pointer at that node
+  // moves past every node whose count now exceeds its threshold (or that the simulation removed), wave-wide.
+  __device__ __forceinline__ void topo_skip_advance(int g, int node) {
+    const bool anti = tg(g, TGM_TYPE) == TG_ANTI;
+    for (int i = 0; i < 2; i++) {
+      int p = s_tptr[2 * g + i];
+      if (p != node) continue;
+      hbm_release();  // the count lane 0 just wrote
+      wsync();
+      const int thr = anti ? 0 : tg(g, TGM_SKEW) - i;
+      const int32_t KS_G* dom = D.n_tdom + (int64_t)g * d.N;
+      while (true) {
+        const int n = p + lane();
+        bool dead = false;
+        if (n < d.N) {
+          const int v = dom[n];
+          const int c = v >= 0 ? tcnt(g, v) : -1;
+          dead = c > thr || c < 0;
+          if (SIM) dead = dead || tbit(s_rmv, n);
+        }
+        const uint64_t alive = wballot(!dead);  // (lanes past the last node count as alive: p stops at N)
+        if (alive) {
+          p += ctz64(alive);
+          break;
+        }
+        p += kWave;
+      }
+      s_tptr[2 * g + i] = p;  // wave-wide store of a uniform value
+      wsync();
+    }
   }
 
   // Topology.Update for relaxation state s1 (topology.go:102-119), wave-wide: the late groups it owns that do not
@@ -2750,7 +2795,8 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
                        2 * r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 +
                        (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : d.fnOn ? r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
-                       (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) +
+                       (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + r16(8 * (size_t)d.G) +
+                                  2 * r16(4 * (size_t)d.RSW) +
                                   (d.GMW > 1 ? r16(8 * (size_t)GS_N * d.GMW) : 0) +
                                   (sim ? r16(4 * (size_t)((d.tgCntWords - d.tgSmall + 31) / 32)) : 0)
                               : 0);
