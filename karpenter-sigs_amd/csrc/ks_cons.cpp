@@ -246,6 +246,7 @@ struct ks_cons {
     int32_t* lhdr = nullptr;
     int32_t* hhdr = nullptr;
     bool hdrOnly = false;
+    bool keptFull = false;  // a world-1 run kept the records with KS_CONS_FULL_RECORDS set (full download)
     int32_t* lentries = nullptr;
     int32_t* lentrySim = nullptr;
     int32_t* lpodmap = nullptr;
@@ -277,7 +278,7 @@ struct ks_cons {
       lhost.clear();
       lnent = lrbits = lsbits = lnmw = 0;
       lsorted = false;
-      hdrOnly = false;
+      hdrOnly = keptFull = false;
       lplan = Plan{};
     }
   };
@@ -1224,6 +1225,7 @@ namespace {
 // The queue sort + simulation kernel over this rank's simulations; records to host or device memory.
 // Returns the HIP-event time of both launches on the stream they ran on.
 double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
+  PhaseTimer pt("run_sims");
   prepare_launch(c, rank, world);
   ks_problem& pb = *c.pb;
   const int ns = (int)c.L.lsims.size();
@@ -1252,12 +1254,13 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
   }
   HIPCHK(launch_sims_split(pb.dev, c.L.lworks, ns, c.L.lnmw, c.L.lplan, pb.stream, c.st2, c.evFork, c.evJoin));
   HIPCHK(hipEventRecord(c.ev[1], pb.stream));
+  pt.mark("launches enqueued");
   // the records follow on the same stream; one synchronisation covers both
   const size_t bytes = 4 * (size_t)c.recWords * ns, all = 4 * (size_t)c.recWords * c.per_rank(world);
   if (onDevice) {
     if (all > bytes) HIPCHK(hipMemsetAsync((char*)records + bytes, 0, all - bytes, pb.stream));
     if (bytes) HIPCHK(hipMemcpyAsync(records, c.L.lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
-  } else if (!records && world == 1) {  // the records stay in the handle: headers + device checks only
+  } else if (!records && world == 1 && !std::getenv("KS_CONS_FULL_RECORDS")) {  // records stay in the handle: headers only
     unsigned long long* status = (unsigned long long*)(c.L.lhdr + (size_t)RF_HDR * ns);
     HIPCHK(rec_headers(c.L.lrec, ns, c.recWords, pb.host.dims.TW, pb.dev.tpl_it_beg, pb.host.dims.NTPL, c.L.lhdr, status,
                        pb.stream));
@@ -1265,8 +1268,11 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
   } else if (bytes) {
     HIPCHK(hipMemcpyAsync(c.L.hrec, c.L.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
   }
+  pt.mark("record copies enqueued");
   HIPCHK(hipStreamSynchronize(pb.stream));
-  c.L.hdrOnly = !onDevice && !records && world == 1;
+  pt.mark("synchronized");
+  c.L.hdrOnly = !onDevice && !records && world == 1 && !std::getenv("KS_CONS_FULL_RECORDS");
+  c.L.keptFull = !onDevice && !records && world == 1 && !c.L.hdrOnly;
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, c.ev[0], c.ev[1]));
   if (!onDevice && records) {  // (records == NULL: they stay in the handle's pinned buffer, host_records)
@@ -1775,9 +1781,10 @@ static RecView host_records(const ks_cons* c, const void* records, int world) {
     v.full_ = (const int32_t*)records;
     return v;
   }
-  if (world != 1 || c->L.lworld != 1 || !c->L.hdrOnly || c->L.lsims.size() != c->sims.size())
+  if (world != 1 || c->L.lworld != 1 || !(c->L.hdrOnly || c->L.keptFull) || c->L.lsims.size() != c->sims.size())
     throw KsError(KS_ERR_ARG, "records NULL without a world-1 run of every simulation on this handle");
-  v.hdr_ = c->L.hhdr;
+  if (c->L.keptFull) v.full_ = c->L.hrec;  // (KS_CONS_FULL_RECORDS: the whole records were downloaded)
+  else v.hdr_ = c->L.hhdr;
   return v;
 }
 
@@ -1916,8 +1923,9 @@ int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n) {
 }
 
 double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world) {
-  if (!c || world < 1 || (!records && !(world == 1 && c->L.lworld == 1 && c->L.hdrOnly))) return 0;
+  if (!c || world < 1 || (!records && !(world == 1 && c->L.lworld == 1 && (c->L.hdrOnly || c->L.keptFull)))) return 0;
   // (headers: RF_HDR words per simulation, the algorithmic-byte words among them)
+  if (!records && c->L.keptFull) records = c->L.hrec;
   const int32_t* r = records ? (const int32_t*)records : c->L.hhdr;
   const size_t stride = records ? (size_t)c->recWords : (size_t)RF_HDR;
   const size_t n = records ? (size_t)c->per_rank(world) * world : c->sims.size();

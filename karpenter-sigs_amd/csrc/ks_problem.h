@@ -145,22 +145,6 @@ struct KsDev {
   const uint64_t KS_G* pod_hpu;    // [P] host-port triples a pod reserves
   const uint64_t KS_G* pod_hpo;    // [P] elements of the pod's own initial entries on existing nodes
   const uint64_t KS_G* n_hp0;      // [N] host-port triples reserved on an existing node
-  // volume limits (volumeusage.go:183-227), sparse: any number of PVCs and drivers.  VolumeUsage.ExceedsLimits
-  // of a pod on node n is, per limited driver v the pod mounts, count(n, v) + (the pod's PVCs of v that n does
-  // not mount yet) <= limit(n, v); the other drivers cannot fail (a node over a limit before the Solve is
-  // folded into an unsatisfiable Available by the encoder, and commits keep every count within its limit).
-  // "Not mounted yet" needs membership only for the pod's own PVCs: those some node mounts at NewScheduler
-  // time (pod_vs), and -- for a pod sharing a PVC with another pod being scheduled (PF_VSHARED) -- those an
-  // earlier placement of this Solve mounted (the workspace log, KsWork::vlog).
-  const int32_t KS_G* pod_vdbeg;   // [P+1] CSR into pod_vd
-  const int32_t KS_G* pod_vd;      // [][2] (driver v, number of the pod's PVCs of v)
-  const int32_t KS_G* pod_vsbeg;   // [P+1] CSR into pod_vs
-  const int32_t KS_G* pod_vs;      // [][2] (node, PVC u): the pod's PVC u is mounted on the node at NewScheduler time
-  const int32_t KS_G* pod_vubeg;   // [P+1] CSR into pod_vu (PF_VSHARED pods only)
-  const int32_t KS_G* pod_vu;      // [] the pod's PVCs (universe ids)
-  const int32_t KS_G* vol_udrv;    // [NVU] driver of PVC u
-  const int32_t KS_G* n_vc0;       // [N][VD] PVCs of driver v mounted on the node (|VolumeUsage.volumes[v]|)
-  const int32_t KS_G* n_vlim;      // [N][VD] the node's limit for driver v (INT32_MAX: none)
   // topology (topology.go; ks_topo.cpp)
   const int32_t KS_G* tg_meta;     // [G][TGM_WORDS]
   const int32_t KS_G* tg_cnt0;     // per group: domain counts over its key's values, -1 = not registered (NewTopology state)
@@ -187,14 +171,28 @@ struct KsDev {
   const int32_t KS_G* st_fnrow;
   const int32_t KS_G* fn_state;
   uint32_t KS_G* st_fn;
+  // volume limits (volumeusage.go:183-227), sparse: any number of PVCs and drivers.  VolumeUsage.ExceedsLimits
+  // of a pod on node n is, per limited driver v the pod mounts, count(n, v) + (the pod's PVCs of v that n does
+  // not mount yet) <= limit(n, v); the other drivers cannot fail (a node over a limit before the Solve is
+  // folded into an unsatisfiable Available by the encoder, and commits keep every count within its limit).
+  // "Not mounted yet" needs membership only for the pod's own PVCs: those some node mounts at NewScheduler
+  // time (pod_vs), and -- for a pod sharing a PVC with another pod being scheduled (PF_VSHARED) -- those an
+  // earlier placement of this Solve mounted (the workspace log, KsWork::vlog).
+  const int32_t KS_G* pod_vdbeg;   // [P+1] CSR into pod_vd
+  const int32_t KS_G* pod_vd;      // [][2] (driver v, number of the pod's PVCs of v)
+  const int32_t KS_G* pod_vsbeg;   // [P+1] CSR into pod_vs
+  const int32_t KS_G* pod_vs;      // [][2] (node, PVC u): the pod's PVC u is mounted on the node at NewScheduler time
+  const int32_t KS_G* pod_vubeg;   // [P+1] CSR into pod_vu (PF_VSHARED pods only)
+  const int32_t KS_G* pod_vu;      // [] the pod's PVCs (universe ids)
+  const int32_t KS_G* vol_udrv;    // [NVU] driver of PVC u
+  const int32_t KS_G* n_vc0;       // [N][VD] PVCs of driver v mounted on the node (|VolumeUsage.volumes[v]|)
+  const int32_t KS_G* n_vlim;      // [N][VD] the node's limit for driver v (INT32_MAX: none)
 };
 
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };
 enum TopoGroupType : int32_t { TG_SPREAD = 0, TG_AFFINITY = 1, TG_ANTI = 2 };
 enum TgMeta : int32_t {  // per topology group, int32 words
-  TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST,
-  TGM_LATE,  // created by a relaxation mid-Solve (tg_late): its existing nodes start unregistered
-  TGM_WORDS = 12
+  TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST, TGM_WORDS = 12
 };
 enum PodFlag : int32_t {
   PF_PROVISIONABLE = 1,
@@ -253,9 +251,6 @@ struct KsWork {
   uint64_t KS_G* n_hp;      // [N] host ports reserved per existing node (SIM: valid where s_tch is set)
   uint64_t KS_G* c_hp;      // [Kcap] host ports reserved per NodeClaim
   int32_t KS_G* n_vc;       // [N][VD] volume counts per existing node (copy of n_vc0); SIM: [P][VD] slots (n_vslot)
-  int32_t KS_G* n_vslot;    // SIM: [N] n_vc row of a node whose volume usage changed (valid where s_tvol is set)
-  int32_t KS_G* vlog;       // [vLogCap][2] (PVC u, node): PF_VSHARED pods' PVCs a placement mounted on a node
-  int32_t KS_G* vspec;      // [vLogCap][2] the popped pod's entries of vlog
   int32_t KS_G* tg_cnt;     // topology domain counts (copy of tg_cnt0)
   int32_t KS_G* tg_cpos;    // [G] NodeClaims whose placeholder domain has a positive count
   int32_t KS_G* tg_ccnt;    // [G][Kcap] counts of the NodeClaims' hostname-placeholder domains
@@ -282,6 +277,10 @@ struct KsWork {
   const int32_t KS_G* tdel;     // [ntdel][2]: tg_cnt offset, (pods removed << 1) | unregister-if-zero
   int32_t ntdel;
   const uint64_t KS_G* tdead;   // [GMW] inverse groups none of whose owners exist in this simulation
+  // volumes (volA)
+  int32_t KS_G* n_vslot;    // SIM: [N] n_vc row of a node whose volume usage changed (valid where s_tvol is set)
+  int32_t KS_G* vlog;       // [vLogCap][2] (PVC u, node): PF_VSHARED pods' PVCs a placement mounted on a node
+  int32_t KS_G* vspec;      // [vLogCap][2] the popped pod's entries of vlog
 };
 
 enum Counter {

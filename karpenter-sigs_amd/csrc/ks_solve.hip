@@ -564,13 +564,6 @@ struct Solver {
   LU32 s_tvol;          // SIM: [ceil(N/32)] nodes whose volume counts live in a W.n_vc slot (W.n_vslot)
   LI32 s_tgm;           // [G][TGM_WORDS] topology group metadata
   LI32 s_tmin;          // [G] domainMinCount of the popped pod, per spread group
-  // [G][2] per hostname spread / anti-affinity group (not late): the first existing node whose count is within
-  // the group's threshold for a pod that is not (0) / is (1) selected by it (anti-affinity: 0 pods; spread:
-  // maxSkew - self, the hostname domainMinCount being 0).  Counts only grow after the prologue and every node
-  // is registered, so the nodes below it fail topo_node_state1 for every later pod matching the group: a dead
-  // prefix the scan skips (topo_skip_advance keeps it, t_skip is the popped pod's largest).
-  LI32 s_tptr;
-  int t_skip = 0;
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
   LU32 s_trs1;          // [RSW] one group's domains as a single-key record
   LI32 s_tcs;           // [pl.tcl] the count table's LDS-resident prefix: the small-key groups (a Solve: the
@@ -593,11 +586,12 @@ struct Solver {
   bool rem_same = false;  // the last claim_full left the claim's options unchanged (commit skips the copy back)
   uint64_t cur_hpc = 0, cur_hpu = 0;  // the popped pod's host-port conflict / reservation masks
   uint64_t cur_hpo = 0;               // its own initial entries on existing nodes (HostPortUsage.Add replaces them)
-  // the popped pod's volumes (volA): driver entries [v_db, v_de) of D.pod_vd, NewScheduler-time mounts of its
-  // PVCs [v_sb, v_se) of D.pod_vs, this Solve's earlier mounts of them [0, v_nsp) of W.vspec (PF_VSHARED)
-  int v_db = 0, v_de = 0, v_sb = 0, v_se = 0, v_nsp = 0, v_ub = 0, v_ue = 0;
-  int v_nlog = 0;    // entries in W.vlog
-  int v_nslot = 0;   // SIM: W.n_vc slots in use
+  // the popped pod's volumes (volA), in LDS (SGPRs are the scarce resource of the non-LEAN loop): driver
+  // entries [VO_DB, VO_DE) of D.pod_vd, NewScheduler-time mounts of its PVCs [VO_SB, VO_SE) of D.pod_vs, this
+  // Solve's earlier mounts of them [0, VO_NSP) of W.vspec (PF_VSHARED pods: its PVCs [VO_UB, VO_UE) of
+  // D.pod_vu); VO_NLOG entries in W.vlog; SIM: VO_NSLOT W.n_vc slots in use
+  enum : int { VO_DB = 0, VO_DE, VO_SB, VO_SE, VO_NSP, VO_UB, VO_UE, VO_NLOG, VO_NSLOT, VO_WORDS };
+  LI32 s_vol;
 #ifdef KS_PHASE_STATS
   uint64_t scyc[4] = {0, 0, 0, 0};  // claim_full sub-phases: requirements, thresholds, masks, apply
 #endif
@@ -785,36 +779,43 @@ struct Solver {
   // entries (wave-uniform); for a pod sharing a PVC with other pods being scheduled it also collects the
   // earlier placements' log entries of its PVCs (W.vlog -> W.vspec; every store here is a wave-wide store of
   // a uniform value, so each lane later reads what it wrote itself).
+  __device__ __forceinline__ int vo(int f) const { return uni(s_vol[f]); }
+  __device__ __forceinline__ void vo_set(int f, int v) const { s_vol[f] = v; }  // wave-wide store of a uniform value
   __device__ __forceinline__ void vol_pop(int g, int pf) {
-    v_db = uni(D.pod_vdbeg[g]);
-    v_de = uni(D.pod_vdbeg[g + 1]);
-    v_sb = uni(D.pod_vsbeg[g]);
-    v_se = uni(D.pod_vsbeg[g + 1]);
-    v_ub = v_ue = v_nsp = 0;
-    if (!(pf & PF_VSHARED)) return;
-    v_ub = uni(D.pod_vubeg[g]);
-    v_ue = uni(D.pod_vubeg[g + 1]);
-    for (int i0 = 0; i0 < v_nlog; i0 += kWave) {
-      const int i = i0 + lane();
-      const int ic = i < v_nlog ? i : i0;
-      const int lu = W.vlog[2 * ic], ln = W.vlog[2 * ic + 1];
-      bool hit = false;
-      for (int k = v_ub; k < v_ue; k++) hit |= D.pod_vu[k] == lu;
-      for (uint64_t m = wballot(hit && i < v_nlog); m; m &= m - 1) {
-        const int l = ctz64(m);
-        const int u = rdl(lu, l), n = rdl(ln, l);
-        W.vspec[2 * v_nsp] = u;  // wave-wide stores of uniform values
-        W.vspec[2 * v_nsp + 1] = n;
-        v_nsp++;
+    vo_set(VO_DB, D.pod_vdbeg[g]);
+    vo_set(VO_DE, D.pod_vdbeg[g + 1]);
+    vo_set(VO_SB, D.pod_vsbeg[g]);
+    vo_set(VO_SE, D.pod_vsbeg[g + 1]);
+    int ub = 0, ue = 0, nsp = 0;
+    if (pf & PF_VSHARED) {
+      ub = uni(D.pod_vubeg[g]);
+      ue = uni(D.pod_vubeg[g + 1]);
+      const int nlog = vo(VO_NLOG);
+      for (int i0 = 0; i0 < nlog; i0 += kWave) {
+        const int i = i0 + lane();
+        const int ic = i < nlog ? i : i0;
+        const int lu = W.vlog[2 * ic], ln = W.vlog[2 * ic + 1];
+        bool hit = false;
+        for (int k = ub; k < ue; k++) hit |= D.pod_vu[k] == lu;
+        for (uint64_t m = wballot(hit && i < nlog); m; m &= m - 1) {
+          const int l = ctz64(m);
+          W.vspec[2 * nsp] = rdl(lu, l);  // wave-wide stores of uniform values
+          W.vspec[2 * nsp + 1] = rdl(ln, l);
+          nsp++;
+        }
       }
     }
+    vo_set(VO_UB, ub);
+    vo_set(VO_UE, ue);
+    vo_set(VO_NSP, nsp);
+    wsync();
   }
-  __device__ __forceinline__ bool vol_any() const { return v_de > v_db; }
+  __device__ __forceinline__ bool vol_any() const { return vo(VO_DE) > vo(VO_DB); }
   // The pod's PVCs of driver v that node n mounts already (at NewScheduler time, or by an earlier placement).
   __device__ __forceinline__ int vol_mounted(int n, int v) const {
     int c = 0;
-    for (int k = v_sb; k < v_se; k++) c += (D.pod_vs[2 * k] == n && D.vol_udrv[D.pod_vs[2 * k + 1]] == v) ? 1 : 0;
-    for (int k = 0; k < v_nsp; k++) c += (W.vspec[2 * k + 1] == n && D.vol_udrv[W.vspec[2 * k]] == v) ? 1 : 0;
+    for (int k = vo(VO_SB), e = vo(VO_SE); k < e; k++) c += (D.pod_vs[2 * k] == n && D.vol_udrv[D.pod_vs[2 * k + 1]] == v) ? 1 : 0;
+    for (int k = 0, e = vo(VO_NSP); k < e; k++) c += (W.vspec[2 * k + 1] == n && D.vol_udrv[W.vspec[2 * k]] == v) ? 1 : 0;
     return c;
   }
   __device__ __forceinline__ const int32_t KS_G* vol_row(int n) const {
@@ -826,7 +827,7 @@ struct Solver {
   __device__ __forceinline__ bool vol_ok(int n) const {
     const int32_t KS_G* vc = vol_row(n);
     bool ok = true;
-    for (int j = v_db; j < v_de; j++) {
+    for (int j = vo(VO_DB), e = vo(VO_DE); j < e; j++) {
       const int v = D.pod_vd[2 * j], c = D.pod_vd[2 * j + 1];
       ok &= vc[v] + c - vol_mounted(n, v) <= D.n_vlim[(int64_t)n * d.VD + v];
     }
@@ -838,9 +839,10 @@ struct Solver {
     int32_t KS_G* vc;
     if (SIM) {
       if (!tbit(s_tvol, n)) {
-        const int slot = v_nslot++;
+        const int slot = vo(VO_NSLOT);
         for (int v = 0; v < d.VD; v++) W.n_vc[(int64_t)slot * d.VD + v] = D.n_vc0[(int64_t)n * d.VD + v];
         W.n_vslot[n] = slot;
+        vo_set(VO_NSLOT, slot + 1);
         __hip_atomic_fetch_or(s_tvol + (n >> 5), 1u << (n & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         wsync();
         vc = W.n_vc + (int64_t)slot * d.VD;
@@ -850,24 +852,27 @@ struct Solver {
     } else {
       vc = W.n_vc + (int64_t)n * d.VD;
     }
-    for (int j = v_db; j < v_de; j++) {
+    for (int j = vo(VO_DB), e = vo(VO_DE); j < e; j++) {
       const int v = D.pod_vd[2 * j], c = D.pod_vd[2 * j + 1];
       const int add = uni(c - vol_mounted(n, v));
       if (add) vc[v] = uni(vc[v]) + add;
     }
     // the shared pod's PVCs not yet on n join the log (each (PVC, node) pair once)
-    for (int k = v_ub; k < v_ue; k++) {
+    int nlog = vo(VO_NLOG);
+    for (int k = vo(VO_UB), e = vo(VO_UE); k < e; k++) {
       const int u = D.pod_vu[k];
       bool on = false;
-      for (int q = v_sb; q < v_se; q++) on |= D.pod_vs[2 * q] == n && D.pod_vs[2 * q + 1] == u;
-      for (int q = 0; q < v_nsp; q++) on |= W.vspec[2 * q + 1] == n && W.vspec[2 * q] == u;
+      for (int q = vo(VO_SB), qe = vo(VO_SE); q < qe; q++) on |= D.pod_vs[2 * q] == n && D.pod_vs[2 * q + 1] == u;
+      for (int q = 0, qe = vo(VO_NSP); q < qe; q++) on |= W.vspec[2 * q + 1] == n && W.vspec[2 * q] == u;
       if (!ub(on)) {
-        W.vlog[2 * v_nlog] = u;
-        W.vlog[2 * v_nlog + 1] = n;
-        v_nlog++;
+        W.vlog[2 * nlog] = u;
+        W.vlog[2 * nlog + 1] = n;
+        nlog++;
       }
     }
+    vo_set(VO_NLOG, nlog);
     hbm_release();
+    wsync();
   }
   // Lane (n & 63) is the only lane that ever reads or writes node n's mutable state.
   __device__ __forceinline__ bool tbit(LU32 m, int n) const { return (m[n >> 5] >> (n & 31)) & 1u; }
@@ -1077,14 +1082,9 @@ struct Solver {
     t_any = anyM;
     t_rec = anyR;
     t_nonode = false;
-    t_skip = 0;
     for (int w = 0; w < GMW; w++)
       for (uint64_t m = gword(GS_MASK, w, t_mask); m; m &= m - 1) {
         const int g = 64 * w + ctz64(m);
-        if (tg(g, TGM_HOST) && !tg(g, TGM_LATE) && tg(g, TGM_TYPE) != TG_AFFINITY) {
-          const int p = s_tptr[2 * g + (tg(g, TGM_TYPE) == TG_SPREAD && sel_has(g) ? 1 : 0)];
-          t_skip = p > t_skip ? p : t_skip;
-        }
         if (tg(g, TGM_TYPE) == TG_AFFINITY) {
           const int nv = tg(g, TGM_NV);
           bool pos = false, reg = false;
@@ -1364,7 +1364,6 @@ struct Solver {
             rec = v >= 0;
           }
           if (!SIM && tg(g, TGM_HOST) && rdl(rec, 0)) hg |= 1ull << (g & 63);
-          if (tg(g, TGM_HOST) && !tg(g, TGM_LATE) && tg(g, TGM_TYPE) != TG_AFFINITY) topo_skip_advance(g, node);
           continue;
         }
         const int k = tg(g, TGM_KEY), nv = tg(g, TGM_NV);
@@ -1401,38 +1400,6 @@ struct Solver {
     }
     hbm_release();
     wsync();
-  }
-
-  // The dead prefix of hostname group g (s_tptr) after a pod was recorded on node `node`: a pointer at that node
-  // moves past every node whose count now exceeds its threshold (or that the simulation removed), wave-wide.
-  __device__ __forceinline__ void topo_skip_advance(int g, int node) {
-    const bool anti = tg(g, TGM_TYPE) == TG_ANTI;
-    for (int i = 0; i < 2; i++) {
-      int p = s_tptr[2 * g + i];
-      if (p != node) continue;
-      hbm_release();  // the count lane 0 just wrote
-      wsync();
-      const int thr = anti ? 0 : tg(g, TGM_SKEW) - i;
-      const int32_t KS_G* dom = D.n_tdom + (int64_t)g * d.N;
-      while (true) {
-        const int n = p + lane();
-        bool dead = false;
-        if (n < d.N) {
-          const int v = dom[n];
-          const int c = v >= 0 ? tcnt(g, v) : -1;
-          dead = c > thr || c < 0;
-          if (SIM) dead = dead || tbit(s_rmv, n);
-        }
-        const uint64_t alive = wballot(!dead);  // (lanes past the last node count as alive: p stops at N)
-        if (alive) {
-          p += ctz64(alive);
-          break;
-        }
-        p += kWave;
-      }
-      s_tptr[2 * g + i] = p;  // wave-wide store of a uniform value
-      wsync();
-    }
   }
 
   // Topology.Update for relaxation state s1 (topology.go:102-119), wave-wide: the late groups it owns that do not
@@ -2493,7 +2460,7 @@ struct Solver {
         w.tol0 = D.st_tol[2 * w.s];
         w.tol1 = D.st_tol[2 * w.s + 1];
       }
-      w.pf = SIM || !LEAN ? D.pod_flags[w.g] : 0;
+      w.pf = SIM || (!LEAN && d.volAny) ? D.pod_flags[w.g] : 0;
       w.rl = SIM && LEAN && ident ? W.run_len[pos] : 1;
       w.hpc = D.pod_hpc[w.g];
       w.hpu = D.pod_hpu[w.g];
@@ -2793,10 +2760,9 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   Plan pl{};
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
   const size_t fixed = r16(sizeof(KeyMeta) * d.NK) + r16(4 * (size_t)(d.NTPL + 1)) + r16(8 * (size_t)(d.NPOOL + 1) * R) +
-                       2 * r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 +
+                       2 * r16(4 * (size_t)d.RSW) + 5 * r16(4 * TW + 8) + 16 * 16 + (d.volAny ? 48 : 0) +
                        (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : d.fnOn ? r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
-                       (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + r16(8 * (size_t)d.G) +
-                                  2 * r16(4 * (size_t)d.RSW) +
+                       (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) +
                                   (d.GMW > 1 ? r16(8 * (size_t)GS_N * d.GMW) : 0) +
                                   (sim ? r16(4 * (size_t)((d.tgCntWords - d.tgSmall + 31) / 32)) : 0)
                               : 0);

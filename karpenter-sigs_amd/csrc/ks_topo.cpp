@@ -437,7 +437,6 @@ void Host::buildTopology() {
     m[TGM_NV] = nv;
     m[TGM_FBEG] = (int32_t)(tab.tg_frs.size() / dims.RSW);
     m[TGM_HOST] = tg.key == kHostnameKey ? 1 : 0;
-    m[TGM_LATE] = tg.late ? 1 : 0;
     std::vector<int32_t> cnt(std::max(nv, 1), -1);  // -1: domain not registered (absent from the map)
     for (auto& kv : tg.domains) {
       auto vi = valueId[(size_t)tg.keyId].find(kv.first);
