@@ -268,9 +268,11 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
     name = "C5" if not topology else "C5 + topology (%d apps: spread, pod affinity, anti-affinity)" % topology
     pass_ms = elapsed * 1000.0 / args.cons_steps
     # Incremental update between passes (ks_cons_update): 10 pods deleted on one node and one node removed,
-    # then the next pass (new plan: pod lists, queue sort, run lengths; simulations; decide), 5 times.
+    # then the next pass (new plan: pod lists, queue sort, run lengths; simulations; decide), 5 times.  On a
+    # topology cluster the update also moves the shared NewTopology counts and the pass re-derives every
+    # simulation's count offsets.
     update = None
-    if world == 1 and not topology:
+    if world == 1:
         nodes = json.loads(snap)["stateNodes"]
         ums, pms = [], []
         for i in range(5):

@@ -1375,7 +1375,6 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   for (const auto& kv : delta.obj())
     if (kv.first != "deletePods" && kv.first != "bindPods" && kv.first != "removeNodes")
       throw KsError(KS_ERR_PARSE, "update: unknown field " + kv.first);
-  if (d.G) throw KsError(KS_ERR_UNSUPPORTED, "update: the cluster has topology groups");
   if (d.volAny) throw KsError(KS_ERR_UNSUPPORTED, "update: the cluster has volume limits");
   if (c.uidIndex.empty()) {
     c.uidIndex.reserve(h.pods.size());
@@ -1425,6 +1424,45 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     const int n = nodeOf(&v);
     if (!seenNode.insert(n).second) throw KsError(KS_ERR_ARG, "update: node " + v.str() + " removed twice");
     rm.push_back(n);
+  }
+
+  // Topology clusters: the shared NewTopology counts (tg_cnt0, topology.go:61-85) follow the events -- a
+  // deleted cluster pod's countDomains and inverse anti-affinity contributions leave, a bound pod's join (it
+  // is no longer one every simulation schedules), a removed node's pods leave and its hostname is no longer
+  // registered by NewExistingNode.  Groups stay: one no remaining pod owns is never evaluated (only owned
+  // groups are checked; an inverse group without owners is dead in every simulation, sim_topology).
+  std::vector<std::vector<std::pair<int, int>>> bindContrib(bind.size());
+  std::vector<std::vector<int32_t>> bindInv(bind.size());
+  if (d.G) {
+    for (size_t i = 0; i < bind.size(); i++) {
+      PodH cp = h.pods[(size_t)bind[i]];
+      cp.nodeName = h.nodes[(size_t)bindNode[i]].name;
+      cp.phase = "Running";
+      if (!h.topoClusterPod(cp, bindContrib[i], bindInv[i]))
+        throw KsError(KS_ERR_UNSUPPORTED, "update: bound pod " + cp.uid +
+                                              " counts in a topology domain or inverse group the handle does not hold");
+    }
+    // A group that a leaving pod's first state creates and that remaining pods own only in later relaxation
+    // states would be a late group (created mid-Solve, ks_topo.cpp) in a fresh build: refused.
+    std::vector<char> gone(h.pods.size(), 0);
+    std::set<int> rmSet(rm.begin(), rm.end());
+    for (int p : del) gone[(size_t)p] = 1;
+    for (size_t i = 0; i < bind.size(); i++)
+      if (rmSet.count(bindNode[i])) gone[(size_t)bind[i]] = 1;
+    for (size_t p = 0; p < c.podNode.size(); p++)
+      if (c.podNode[p] >= 0 && rmSet.count(c.podNode[p])) gone[p] = 1;
+    std::set<int32_t> lost;
+    for (size_t p = 0; p < gone.size(); p++)
+      if (gone[p]) lost.insert(h.states[p][0].gown.begin(), h.states[p][0].gown.end());
+    auto remaining = [&](size_t p) { return !gone[p] && c.podNode[p] != ks_cons::PN_GONE; };
+    for (size_t p = 0; p < h.pods.size() && !lost.empty(); p++)
+      if (remaining(p)) for (int32_t g : h.states[p][0].gown) lost.erase(g);
+    for (size_t p = 0; p < h.pods.size() && !lost.empty(); p++)
+      for (size_t k = 1; remaining(p) && k < h.states[p].size(); k++)
+        for (int32_t g : h.states[p][k].gown)
+          if (lost.count(g))
+            throw KsError(KS_ERR_UNSUPPORTED, "update: topology group " + std::to_string(g) +
+                                                  " would only be created by a relaxation (rebuild the handle)");
   }
 
   pt.mark("validate");
@@ -1494,6 +1532,74 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     int64_t* row = &h.tab.n_avail[(size_t)n * R];
     row[0] = -1;  // Fits fails on any negative total: no pod lands on a removed node
   }
+  if (d.G) {
+    const int hostKey = h.keyId.count("kubernetes.io/hostname") ? h.keyId.at("kubernetes.io/hostname") : -1;
+    auto cnt = [&](int g, int v) -> int32_t& {
+      return h.tab.tg_cnt0[(size_t)h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_CNT] + (size_t)v];
+    };
+    auto keep = [&](int g, int v) {  // registered with no pod: as sim_topology
+      return h.topoUniverse[(size_t)g][(size_t)v] ||
+             (h.groups[(size_t)g].keyId == hostKey && !h.groups[(size_t)g].late && h.activeHost(v));
+    };
+    auto leave = [&](const std::string& uid) {
+      auto ct = h.topoContrib.find(uid);
+      if (ct != h.topoContrib.end()) {
+        for (auto& gv : ct->second) {
+          int32_t& x = cnt(gv.first, gv.second);
+          if (x <= 0) throw KsError(KS_ERR_INTERNAL, "update: topology count below zero");
+          if (--x == 0 && !keep(gv.first, gv.second)) x = -1;
+        }
+        h.topoContrib.erase(ct);
+      }
+      auto io = h.topoInvOwner.find(uid);
+      if (io != h.topoInvOwner.end()) {
+        for (int32_t g : io->second) h.topoInvOwners[(size_t)g]--;
+        h.topoInvOwner.erase(io);
+      }
+    };
+    auto dropCluster = [&](auto pred) {  // the cluster pod listing loses these pods (and their counts)
+      auto& cps = h.clusterPods;
+      size_t o = 0;
+      for (size_t i = 0; i < cps.size(); i++) {
+        if (pred(cps[i])) {
+          leave(cps[i].uid);
+          continue;
+        }
+        if (o != i) cps[o] = std::move(cps[i]);
+        o++;
+      }
+      cps.resize(o);
+    };
+    std::set<std::string> delUids;
+    for (int p : del) delUids.insert(h.pods[(size_t)p].uid);
+    for (const std::string& u : delUids) leave(u);  // (counted pods are listed; leave is idempotent)
+    dropCluster([&](const PodH& cp) { return delUids.count(cp.uid) != 0; });
+    for (size_t i = 0; i < bind.size(); i++) {
+      const PodH& ph = h.pods[(size_t)bind[i]];
+      dropCluster([&](const PodH& cp) { return cp.uid == ph.uid; });
+      for (auto& gv : bindContrib[i]) {
+        int32_t& x = cnt(gv.first, gv.second);
+        x = x < 0 ? 1 : x + 1;
+      }
+      if (!bindContrib[i].empty()) h.topoContrib[ph.uid] = bindContrib[i];
+      if (!bindInv[i].empty()) {
+        for (int32_t g : bindInv[i]) h.topoInvOwners[(size_t)g]++;
+        h.topoInvOwner[ph.uid] = bindInv[i];
+      }
+      h.clusterPods.push_back(ph);
+    }
+    for (int n : rm) {
+      const Host::Node& hn = h.nodes[(size_t)n];
+      dropCluster([&](const PodH& cp) { return cp.nodeName == hn.name; });
+      if (hostKey < 0) continue;
+      auto hv = h.valueId[(size_t)hostKey].find(hn.hostName);
+      if (hv == h.valueId[(size_t)hostKey].end()) continue;
+      h.topoHostActive.erase(hv->second);
+      for (int g = 0; g < d.G; g++)
+        if (h.groups[(size_t)g].keyId == hostKey && cnt(g, hv->second) == 0 && !keep(g, hv->second))
+          cnt(g, hv->second) = -1;
+    }
+  }
   for (int n : rows) {
     int64_t* row = &h.tab.n_avail[(size_t)n * R];
     for (int r = 0; r < R; r++) row[r] = 0;
@@ -1518,6 +1624,9 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   if (!bind.empty())
     HIPCHK(hipMemcpyAsync((void*)D.pod_flags, h.tab.pod_flags.data(), 4 * h.tab.pod_flags.size(),
                           hipMemcpyHostToDevice, pb.stream));
+  if (d.G && (!del.empty() || !bind.empty() || !rm.empty()))
+    HIPCHK(hipMemcpyAsync((void*)D.tg_cnt0, h.tab.tg_cnt0.data(), 4 * h.tab.tg_cnt0.size(), hipMemcpyHostToDevice,
+                          pb.stream));
   if (pools)
     HIPCHK(hipMemcpyAsync((void*)D.pool_rem0, h.tab.pool_rem0.data(), 8 * h.tab.pool_rem0.size(),
                           hipMemcpyHostToDevice, pb.stream));
@@ -1527,6 +1636,48 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     throw;
   }
   pt.mark("upload rows");
+}
+
+// The shared NewTopology state of a topology cluster, keyed by group identity (an FNV-1a digest of the
+// group's Hash): per group the registered domains' counts, whether it is late, and whether any pod in the
+// simulations' union or any cluster pod owns it (an unowned group is never evaluated).  ks_cons_update
+// tests compare the owned groups with a from-scratch build.
+std::string topology_json(const ks_cons& c) {
+  const Host& h = c.pb->host;
+  const KsDims& d = h.dims;
+  std::vector<char> owned((size_t)d.G, 0);
+  for (size_t p = 0; p < h.pods.size(); p++) {
+    if (c.podNode[p] == ks_cons::PN_GONE) continue;
+    for (auto& st : h.states[p])
+      for (int32_t g : st.gown) owned[(size_t)g] = 1;
+    for (int g = d.G1; g < d.G; g++)
+      if (gtest(h.tab.pod_ginv, p, d.GMW, g)) owned[(size_t)g] = 1;
+  }
+  for (int g = d.G1; g < d.G; g++)
+    if (h.topoInvOwners[(size_t)g] > 0) owned[(size_t)g] = 1;
+  std::string o = "{";
+  for (int g = 0; g < d.G; g++) {
+    const TopoGroup& tg = h.groups[(size_t)g];
+    uint64_t f = 1469598103934665603ull;
+    for (unsigned char ch : tg.hash) f = (f ^ ch) * 1099511628211ull;
+    f = (f ^ (unsigned)(g >= d.G1)) * 1099511628211ull;  // (an inverse group and an owned one may share a Hash)
+    char buf[40];
+    snprintf(buf, sizeof buf, "%s\"%016llx\":{", g ? "," : "", (unsigned long long)f);
+    o += buf;
+    o += std::string("\"late\":") + (tg.late ? "true" : "false") + ",\"owned\":" + (owned[(size_t)g] ? "true" : "false") +
+         ",\"counts\":{";
+    const int32_t* cnt = &h.tab.tg_cnt0[(size_t)h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_CNT]];
+    bool first = true;
+    for (int v = 0; v < h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_NV]; v++) {
+      if (cnt[v] < 0) continue;
+      o += first ? "" : ",";
+      first = false;
+      ksjson::quote(o, h.values[(size_t)tg.keyId][(size_t)v]);
+      o += ":" + std::to_string(cnt[v]);
+    }
+    o += "}}";
+  }
+  return o + "}";
 }
 
 // Host-only description of a handle: the pass's candidates, the pending pods, the simulation plan and the
@@ -1580,6 +1731,7 @@ std::string inspect_json(const ks_cons& c, bool nodes) {
     o += "},\"poolRemaining\":[";
     for (size_t i = 0; i < h.tab.pool_rem0.size(); i++) o += (i ? "," : "") + std::to_string(h.tab.pool_rem0[i]);
     o += "]";
+    if (h.dims.G) o += ",\"topology\":" + topology_json(c);
   }
   o += ",\"sims\":" + std::to_string(c.sims.size()) + ",\"multiPrefixes\":" + std::to_string(c.multiHi) +
        ",\"recordBytes\":" + std::to_string(4 * c.recWords) + ",\"pods\":" + std::to_string(h.dims.P) +

@@ -215,6 +215,7 @@ struct Host {
 
   void build(const ksjson::Value& root);
   void buildTopology();  // ks_topo.cpp: after the pods' relaxation chains
+  bool topoClusterPod(const PodH& cp, std::vector<std::pair<int, int>>& contrib, std::vector<int32_t>& inv) const;
 
   // encoded algebra helpers
   std::vector<uint32_t> emptyRec() const { return std::vector<uint32_t>(dims.RSW, 0); }

@@ -77,6 +77,76 @@ std::string sel_key(const LabelSel& s) {  // Hash identity (hashstructure with S
   return o;
 }
 
+// NewTopologyGroup (topologygroup.go:70-91) + its Hash (topologygroup.go:142-158)
+TopoGroup make_group(const Host& h, int type, const std::string& key, const PodH& p, const std::set<std::string>& ns,
+                     const LabelSel& sel, int32_t maxSkew, int32_t minDomains) {
+  TopoGroup g;
+  g.type = type;
+  g.key = key;
+  g.keyId = h.keyId.at(key);
+  g.namespaces = ns;
+  g.sel = sel;
+  g.maxSkew = maxSkew;
+  g.minDomains = minDomains;
+  g.filterNil = type != TG_SPREAD;
+  if (type == TG_SPREAD) {  // MakeTopologyNodeFilter (topologynodefilter.go:33-51)
+    std::vector<uint32_t> sel0 = h.emptyRec();
+    h.addLabels(sel0, p.nodeSelector);
+    if (p.hasAffinity && p.hasNodeAffinity && p.hasRequired) {
+      for (auto& term : p.requiredTerms) {
+        std::vector<uint32_t> r = sel0;
+        for (auto& n : term) h.addNSR(r, n.key, n.op, n.values);
+        g.filter.push_back(r);
+      }
+    } else {
+      g.filter.push_back(sel0);
+    }
+  }
+  g.hash = key + "#" + std::to_string(type) + "#";
+  for (auto& n : ns) g.hash += n + ",";
+  g.hash += "#" + sel_key(sel) + "#" + std::to_string(maxSkew) + "#";
+  if (g.filterNil) g.hash += "nil";
+  for (auto& f : g.filter) {  // the filter records' words, as bytes (an exact key, not a printable one)
+    g.hash.append(reinterpret_cast<const char*>(f.data()), f.size() * sizeof(uint32_t));
+    g.hash += "|";
+  }
+  return g;
+}
+
+// buildNamespaceList (topology.go:339-362): the pod's namespace when neither is set, else the listed
+// namespaces plus the namespaces whose labels the selector matches (empty selector: all of them)
+std::set<std::string> term_ns(const Host& h, const PodH& p, const AffTerm& t) {
+  if (t.namespaces.empty() && !t.nsSelector) return std::set<std::string>{p.ns};
+  std::set<std::string> out(t.namespaces.begin(), t.namespaces.end());
+  if (!t.nsSelector) return out;
+  if (!sel_valid(t.nsSel))
+    throw KsError(-1, "pod " + p.ns + "/" + p.name + ": tracking topology counts, parsing selector: invalid namespaceSelector");
+  for (auto& ns : h.namespaceList) {
+    bool ok = true;
+    for (auto& r : t.nsSel.reqs) ok = ok && sel_req_matches(r, ns.second);
+    if (ok) out.insert(ns.first);
+  }
+  return out;
+}
+
+std::vector<TopoGroup> anti_groups(const Host& h, const PodH& p) {
+  std::vector<TopoGroup> gs;
+  for (auto& t : p.antiRequired) gs.push_back(make_group(h, TG_ANTI, t.key, p, term_ns(h, p, t), t.sel, INT32_MAX, -1));
+  return gs;
+}
+
+// TopologyNodeFilter.Matches (topologynodefilter.go:55-70) against a node's label record
+template <class Rec>
+bool filter_matches(const Host& h, const TopoGroup& g, Rec nodeRec) {
+  if (g.filterNil || g.filter.empty()) return true;
+  for (auto& f : g.filter)
+    if (rs_present(f.data()) == 0) return true;  // an empty term is Compatible with every record
+  const std::vector<uint32_t>& rec = nodeRec();
+  for (auto& f : g.filter)
+    if (rs_compatible(h.L, rec.data(), f.data(), 0)) return true;
+  return false;
+}
+
 }  // namespace
 
 void Host::buildTopology() {
@@ -164,17 +234,8 @@ void Host::buildTopology() {
     }
     nodeRecsBuilt = true;
   };
-  auto nodeRec = [&](const std::string& name, const std::map<std::string, std::string>&)
-      -> const std::vector<uint32_t>& { return nodeRecs.at(name); };
-  auto filterMatches = [&](const TopoGroup& g, const std::string& name, const std::map<std::string, std::string>& labels,
-                           uint64_t allow) {
-    if (g.filterNil || g.filter.empty()) return true;
-    for (auto& f : g.filter)
-      if (rs_present(f.data()) == 0) return true;  // an empty term is Compatible with every record
-    const std::vector<uint32_t>& rec = nodeRec(name, labels);
-    for (auto& f : g.filter)
-      if (rs_compatible(L, rec.data(), f.data(), allow)) return true;
-    return false;
+  auto filterMatches = [&](const TopoGroup& g, const std::string& name) {
+    return filter_matches(*this, g, [&]() -> const std::vector<uint32_t>& { return nodeRecs.at(name); });
   };
   // TopologyGroup.domains starts with the universe's values of the key (NewTopologyGroup); seeded only
   // for groups that are new (a pod whose group exists already shares it)
@@ -184,53 +245,9 @@ void Host::buildTopology() {
   };
   auto makeGroup = [&](int type, const std::string& key, const PodH& p, const std::set<std::string>& ns,
                        const LabelSel& sel, int32_t maxSkew, int32_t minDomains) {
-    TopoGroup g;  // NewTopologyGroup (topologygroup.go:70-91)
-    g.type = type;
-    g.key = key;
-    g.keyId = keyId.at(key);
-    g.namespaces = ns;
-    g.sel = sel;
-    g.maxSkew = maxSkew;
-    g.minDomains = minDomains;
-    g.filterNil = type != TG_SPREAD;
-    if (type == TG_SPREAD) {  // MakeTopologyNodeFilter (topologynodefilter.go:33-51)
-      std::vector<uint32_t> sel0 = emptyRec();
-      addLabels(sel0, p.nodeSelector);
-      if (p.hasAffinity && p.hasNodeAffinity && p.hasRequired) {
-        for (auto& term : p.requiredTerms) {
-          std::vector<uint32_t> r = sel0;
-          for (auto& n : term) addNSR(r, n.key, n.op, n.values);
-          g.filter.push_back(r);
-        }
-      } else {
-        g.filter.push_back(sel0);
-      }
-    }
-    g.hash = key + "#" + std::to_string(type) + "#";
-    for (auto& n : ns) g.hash += n + ",";
-    g.hash += "#" + sel_key(sel) + "#" + std::to_string(maxSkew) + "#";
-    if (g.filterNil) g.hash += "nil";
-    for (auto& f : g.filter) {  // the filter records' words, as bytes (an exact key, not a printable one)
-      g.hash.append(reinterpret_cast<const char*>(f.data()), f.size() * sizeof(uint32_t));
-      g.hash += "|";
-    }
-    return g;
+    return make_group(*this, type, key, p, ns, sel, maxSkew, minDomains);
   };
-  // buildNamespaceList (topology.go:339-362): the pod's namespace when neither is set, else the listed
-  // namespaces plus the namespaces whose labels the selector matches (empty selector: all of them)
-  auto termNs = [&](const PodH& p, const AffTerm& t) {
-    if (t.namespaces.empty() && !t.nsSelector) return std::set<std::string>{p.ns};
-    std::set<std::string> out(t.namespaces.begin(), t.namespaces.end());
-    if (!t.nsSelector) return out;
-    if (!sel_valid(t.nsSel))
-      throw KsError(-1, "pod " + p.ns + "/" + p.name + ": tracking topology counts, parsing selector: invalid namespaceSelector");
-    for (auto& ns : namespaceList) {
-      bool ok = true;
-      for (auto& r : t.nsSel.reqs) ok = ok && sel_req_matches(r, ns.second);
-      if (ok) out.insert(ns.first);
-    }
-    return out;
-  };
+  auto termNs = [&](const PodH& p, const AffTerm& t) { return term_ns(*this, p, t); };
   auto countDomains = [&](TopoGroup& g, int gidx) {  // topology.go:238-291
     if (!g.filterNil && !g.filter.empty()) buildNodeRecs();
     // each cluster pod's domain (or none), on worker threads; counted in pod order
@@ -248,7 +265,7 @@ void Host::buildTopology() {
       if (l != n->second.end()) d = &l->second;
       else if (g.key == kHostnameKey) d = &n->first;
       else return;
-      if (!filterMatches(g, n->first, n->second, 0)) return;
+      if (!filterMatches(g, n->first)) return;
       dsel[(size_t)i] = d;
     });
     for (int i = 0; i < NC; i++) {
@@ -257,11 +274,7 @@ void Host::buildTopology() {
       if (topoExcluded) contrib[clusterPods[(size_t)i].uid].push_back({gidx, *dsel[(size_t)i]});
     }
   };
-  auto antiGroups = [&](const PodH& p) {
-    std::vector<TopoGroup> gs;
-    for (auto& t : p.antiRequired) gs.push_back(makeGroup(TG_ANTI, t.key, p, termNs(p, t), t.sel, INT32_MAX, -1));
-    return gs;
-  };
+  auto antiGroups = [&](const PodH& p) { return anti_groups(*this, p); };
   auto inverseAnti = [&](const PodH& p, std::vector<TopoGroup> gs, const std::map<std::string, std::string>* labels,
                          bool cluster) {
     std::vector<int32_t> owned;  // updateInverseAntiAffinity (topology.go:207-232): inverse group indices
@@ -518,6 +531,65 @@ void Host::buildTopology() {
     }
   dims.tgCntWords = (int32_t)tab.tg_cnt0.size();
   pt.mark("consolidation contributions");
+}
+
+// ks_cons_update's bindPods in a topology cluster: what countDomains (topology.go:238-291) and
+// ForPodsWithAntiAffinity's inverse counts (topology.go:190-203) take from one more bound cluster pod under
+// the groups the build made: (group, value) contributions and the inverse groups it owns.  False when a
+// domain or an inverse group it needs is outside the build's universe (the caller refuses the update).
+bool Host::topoClusterPod(const PodH& cp, std::vector<std::pair<int, int>>& contrib, std::vector<int32_t>& inv) const {
+  contrib.clear();
+  inv.clear();
+  if (cp.nodeName.empty()) return true;
+  auto n = nodeLabelsByName.find(cp.nodeName);
+  if (n == nodeLabelsByName.end()) return true;
+  std::vector<uint32_t> rec;
+  auto nodeRec = [&]() -> const std::vector<uint32_t>& {
+    if (rec.empty()) {
+      rec = emptyRec();
+      addNodeLabels(rec, n->second);
+    }
+    return rec;
+  };
+  auto domainOf = [&](const TopoGroup& g, int* v) {
+    auto l = n->second.find(g.key);
+    const std::string* d;
+    if (l != n->second.end()) d = &l->second;
+    else if (g.key == kHostnameKey) d = &n->first;
+    else return 0;  // no domain: not counted
+    auto it = valueId[(size_t)g.keyId].find(*d);
+    if (it == valueId[(size_t)g.keyId].end()) return -1;
+    *v = it->second;
+    return 1;
+  };
+  const int G1 = dims.G1, G = dims.G;
+  if (!(cp.phase == "Failed" || cp.phase == "Succeeded" || cp.deleting))
+    for (int g = 0; g < G1; g++) {
+      const TopoGroup& tg = groups[(size_t)g];
+      if (!tg.namespaces.count(cp.ns) || !sel_lists(tg.sel, cp.labels)) continue;
+      int v = 0;
+      const int k = domainOf(tg, &v);
+      if (k < 0) return false;
+      if (k == 0 || !filter_matches(*this, tg, nodeRec)) continue;
+      contrib.push_back({g, v});
+    }
+  if (!cp.antiRequired.empty())
+    for (const TopoGroup& ag : anti_groups(*this, cp)) {
+      int idx = -1;
+      for (int g = G1; g < G && idx < 0; g++)
+        if (groups[(size_t)g].hash == ag.hash) idx = g;
+      if (idx < 0) return false;
+      auto d = n->second.find(groups[(size_t)idx].key);  // (the inverse count reads the label only)
+      if (d != n->second.end()) {
+        auto it = valueId[(size_t)groups[(size_t)idx].keyId].find(d->second);
+        if (it == valueId[(size_t)groups[(size_t)idx].keyId].end()) return false;
+        contrib.push_back({idx, it->second});
+      }
+      inv.push_back(idx);
+    }
+  std::sort(inv.begin(), inv.end());
+  inv.erase(std::unique(inv.begin(), inv.end()), inv.end());
+  return true;
 }
 
 }  // namespace ks

@@ -3,7 +3,9 @@ would report after the events, state/cluster.go:220-512) and draw random ones.
 
 apply_delta is written independently of the C++ update: it edits the snapshot JSON (pods move between
 "pendingPods" and the nodes' "pods", StateNode "available" strings follow the pod requests, removed nodes
-leave "stateNodes" and "candidates"), and the oracle then consolidates the edited snapshot from scratch.
+leave "stateNodes" and "candidates"; in a topology snapshot the "clusterPods" listing NewTopology counts
+loses deleted pods and the removed nodes' pods and gains bound ones), and the oracle then consolidates the
+edited snapshot from scratch.
 """
 import copy
 import random
@@ -60,7 +62,14 @@ def apply_delta(snap, delta):
     """The snapshot after ks_cons_update's delta (deletePods, then bindPods, then removeNodes)."""
     s = copy.deepcopy(snap)
     nodes = {n["name"]: n for n in s["stateNodes"]}
+    listed = "clusterPods" in s
+
+    def unlist(pred):
+        if listed:
+            s["clusterPods"] = [p for p in s["clusterPods"] if not pred(p)]
+
     for uid in delta.get("deletePods", []):
+        unlist(lambda p: p["metadata"]["uid"] == uid)
         pend = [p for p in s.get("pendingPods", []) if p["metadata"]["uid"] == uid]
         if pend:
             s["pendingPods"].remove(pend[0])
@@ -81,7 +90,11 @@ def apply_delta(snap, delta):
         node = nodes[b["node"]]
         node.setdefault("pods", []).append(pod)
         _move(node, pod, -1)
+        unlist(lambda p: p["metadata"]["uid"] == b["uid"])
+        if listed:
+            s["clusterPods"].append(pod)
     for name in delta.get("removeNodes", []):
+        unlist(lambda p: p.get("spec", {}).get("nodeName") == name)
         s["stateNodes"] = [n for n in s["stateNodes"] if n["name"] != name]
         s["candidates"] = [c for c in s.get("candidates", []) if c != name]
     return s

@@ -93,10 +93,43 @@ def test_invalid_updates_are_refused(bad, code):
         inspect_consolidation_update(json.dumps(snap), [{"deletePods": ["pod-uid-000001"]}, bad])
 
 
-def test_topology_cluster_refused():
-    snap = synth.cluster_snapshot(n_nodes=10, pods_per_node=4, n_its=40, seed=3, n_pending=2, topology=3)
-    with pytest.raises(KsError):
-        inspect_consolidation_update(json.dumps(snap), {"deletePods": [snap["stateNodes"][0]["pods"][0]["metadata"]["uid"]]})
+def _topo_snap(seed, apps=8):
+    return synth.cluster_snapshot(n_nodes=30, pods_per_node=5, n_its=40, seed=seed, n_pending=6, topology=apps)
+
+
+def _owned_topology(doc):
+    return {k: (v["late"], v["counts"]) for k, v in doc["topology"].items() if v["owned"]}
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_topology_update_host_state(seed):
+    """Topology clusters: after a delta sequence the shared NewTopology counts of every group a remaining pod
+    owns equal a from-scratch build's (registered domains and counts, late flag); groups only the updated
+    handle holds are owned by no pod."""
+    snap = _topo_snap(seed)
+    deltas, final = delta_sequence(seed, snap, steps=4, n_del=4, n_bind=3)
+    got = inspect_consolidation_update(json.dumps(snap), deltas)
+    want = inspect_consolidation_update(json.dumps(final))
+    for k in ("candidates", "pendingPods", "nodeRows", "poolRemaining", "sims"):
+        assert got[k] == want[k], k
+    assert _owned_topology(got) == _owned_topology(want)
+    before = inspect_consolidation_update(json.dumps(snap))
+    assert _owned_topology(before) != _owned_topology(got)
+
+
+def test_topology_update_each_kind_alone():
+    snap = _topo_snap(24)
+    node = snap["stateNodes"][2]
+    pend = snap["pendingPods"][0]["metadata"]["uid"]
+    for d in ({"deletePods": [node["pods"][0]["metadata"]["uid"]]},
+              {"bindPods": [{"uid": pend, "node": node["name"]}]},
+              {"removeNodes": [node["name"]]},
+              {"bindPods": [{"uid": pend, "node": node["name"]}], "removeNodes": [node["name"]]},
+              {"deletePods": [p["metadata"]["uid"] for p in node["pods"]]}):
+        got = inspect_consolidation_update(json.dumps(snap), d)
+        want = inspect_consolidation_update(json.dumps(apply_delta(snap, d)))
+        assert _owned_topology(got) == _owned_topology(want), d
+        assert got["sims"] == want["sims"] and got["candidates"] == want["candidates"], d
 
 
 @pytest.mark.gpu
@@ -129,6 +162,28 @@ def test_update_sequence_gpu_parity(seed):
     d, _ = delta_sequence(seed + 100, cur, steps=1)
     c2.update(d[0])
     want, _ = bridge.consolidate(json.dumps(apply_delta(cur, d[0])), all_sims=True)
+    got = c2.consolidate(all_sims=True)
+    got.pop("kernel_ms")
+    assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [31, 32, 33])
+def test_topology_update_sequence_gpu_parity(seed):
+    """a topology cluster's handle follows deltas (shared counts re-uploaded); every pass
+    equals the oracle's consolidation of the edited snapshot."""
+    snap = _topo_snap(seed)
+    deltas, _ = delta_sequence(seed, snap, steps=3, n_del=4, n_bind=3)
+    c = Consolidator(json.dumps(snap))
+    cur = snap
+    for i, d in enumerate(deltas):
+        c.update(d)
+        cur = apply_delta(cur, d)
+        want, _ = bridge.consolidate(json.dumps(cur), all_sims=True)
+        got = c.consolidate(all_sims=True)
+        got.pop("kernel_ms")
+        assert got == want, (seed, i)
+    c2 = Consolidator.from_binary(c.save())
     got = c2.consolidate(all_sims=True)
     got.pop("kernel_ms")
     assert got == want
