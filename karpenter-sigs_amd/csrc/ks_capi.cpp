@@ -228,13 +228,14 @@ void ks_upload(ks_problem* pb) {
   size_t o_sr = put(t.st_rs.data(), t.st_rs.size() * 4);
   size_t o_st = put(t.st_tol.data(), t.st_tol.size() * 8);
   size_t o_sf = put(t.st_flags.data(), t.st_flags.size() * 4);
-  size_t o_stt = put(t.st_toltpl.data(), t.st_toltpl.size() * 4);
-  std::vector<uint64_t> ps0((size_t)std::max(h.dims.P, 1) * 3, 0);
+  size_t o_stt = put(t.st_toltpl.data(), t.st_toltpl.size() * 8);
+  std::vector<uint64_t> ps0((size_t)std::max(h.dims.P, 1) * 4, 0);
   for (int p = 0; p < h.dims.P; p++) {
     const int s0 = t.pod_state0[(size_t)p];
-    ps0[(size_t)p * 3] = t.st_tol[(size_t)s0 * 2];
-    ps0[(size_t)p * 3 + 1] = t.st_tol[(size_t)s0 * 2 + 1];
-    ps0[(size_t)p * 3 + 2] = ((uint64_t)t.st_toltpl[(size_t)s0] << 32) | (uint32_t)t.st_flags[(size_t)s0];
+    ps0[(size_t)p * 4] = t.st_tol[(size_t)s0 * 2];
+    ps0[(size_t)p * 4 + 1] = t.st_tol[(size_t)s0 * 2 + 1];
+    ps0[(size_t)p * 4 + 2] = t.st_toltpl[(size_t)s0];
+    ps0[(size_t)p * 4 + 3] = (uint32_t)t.st_flags[(size_t)s0];
   }
   size_t o_ps0i = put(ps0.data(), ps0.size() * 8);
   size_t o_na = put(t.n_avail.data(), t.n_avail.size() * 8);
@@ -381,7 +382,7 @@ void ks_upload(ks_problem* pb) {
   D.st_rs = (const uint32_t*)(b + o_sr);
   D.st_tol = (const uint64_t*)(b + o_st);
   D.st_flags = (const int32_t*)(b + o_sf);
-  D.st_toltpl = (const uint32_t*)(b + o_stt);
+  D.st_toltpl = (const uint64_t*)(b + o_stt);
   D.n_avail = (const int64_t*)(b + o_na);
   D.n_req0 = (const int64_t*)(b + o_nr);
   D.n_rs0 = (const uint32_t*)(b + o_nrs);

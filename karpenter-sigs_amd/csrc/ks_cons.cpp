@@ -1603,10 +1603,13 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   for (int n : rows) {
     int64_t* row = &h.tab.n_avail[(size_t)n * R];
     for (int r = 0; r < R; r++) row[r] = 0;
+    bool never = false;  // a negative total outside the resource universe (ks_host.cpp neverFits)
     for (const auto& kv : h.nodes[(size_t)n].available) {
       auto id = h.resId.find(kv.first);
       if (id != h.resId.end()) row[id->second] = h.toDev(id->second, kv.second);
+      else never = never || kv.second.n < 0;
     }
+    if (never) row[0] = -1;
   }
   pt.mark("apply");
   order_candidates(c);

@@ -437,14 +437,13 @@ std::vector<uint32_t> Host::podRequirements(PodH& p, bool all) const {
   return r;
 }
 
-uint64_t Host::tolMask(const std::vector<TolH>& tols, uint64_t out[2]) const {
+void Host::tolMask(const std::vector<TolH>& tols, const std::vector<int>& cls, uint64_t out[2]) const {
   out[0] = out[1] = 0;
   for (size_t i = 0; i < taints.size(); i++) {
     bool ok = false;
     for (auto& t : tols) ok = ok || toleratesTaint(t, taints[i]);
-    if (ok) out[i >> 6] |= 1ull << (i & 63);
+    if (ok) out[cls[i] >> 6] |= 1ull << (cls[i] & 63);  // (every taint of a class is tolerated alike)
   }
-  return out[0];
 }
 
 int64_t Host::toDev(int r, const Qty& q) const {
@@ -757,14 +756,25 @@ void Host::build(const Value& root) {
 
   pt.mark("universe");
   // --- resources
+  // The resource universe is the names some request list (pods, daemons) or NodePool limit holds: Fits reads
+  // the candidate's names only (resources.go:162-175), and the limits test the names the limits list.  Any
+  // other name (an instance type's or node's extra capacity nobody requests) decides only through Fits'
+  // negative-total rule, which the encoder folds into the entity (neverFits below).
+  std::set<std::string> live;
+  for (auto& p : pods) for (auto& kv : p.requests) live.insert(kv.first);
+  for (auto& p : daemons) for (auto& kv : p.requests) live.insert(kv.first);
+  for (auto& p : pools) for (auto& kv : p.remaining) live.insert(kv.first);
   std::map<std::string, std::vector<__int128>> seen;
-  auto visitQ = [&](const QList& q) { for (auto& kv : q) seen[kv.first].push_back(kv.second.n); };
+  auto visitQ = [&](const QList& q) {
+    for (auto& kv : q) if (live.empty() || live.count(kv.first)) seen[kv.first].push_back(kv.second.n);
+  };
   for (auto& it : its) { visitQ(it.capacity); visitQ(it.alloc); }
   for (auto& p : pods) visitQ(p.requests);
   for (auto& p : daemons) visitQ(p.requests);
   for (auto& n : nodes) { visitQ(n.available); visitQ(n.capacity); visitQ(n.dsRequests); }
   for (auto& p : pools) visitQ(p.remaining);
-  if (seen.size() > (size_t)kMaxR) throw KsError(-3, "more than 16 resource names");
+  if (seen.size() > (size_t)kMaxR)
+    throw KsError(-3, "more than 16 resource names in the pods' / daemons' requests and the NodePool limits");
   for (auto& kv : seen) {
     int shift = 9;
     for (__int128 x : kv.second) {
@@ -790,7 +800,15 @@ void Host::build(const Value& root) {
   dims.R = R;
   auto vec = [&](const QList& q, int64_t* out) {
     for (int r = 0; r < R; r++) out[r] = 0;
-    for (auto& kv : q) out[resId.at(kv.first)] = toDev(resId.at(kv.first), kv.second);
+    for (auto& kv : q) {
+      auto id = resId.find(kv.first);
+      if (id != resId.end()) out[id->second] = toDev(id->second, kv.second);
+    }
+  };
+  // Fits fails on any negative total (resources.go:166-170), outside the universe too: such an entity never fits
+  auto neverFits = [&](const QList& q, int64_t* out) {
+    for (auto& kv : q)
+      if (!resId.count(kv.first) && kv.second.n < 0) out[0] = -1;
   };
   auto qmeta = [&](const QList& q, uint32_t& mask, uint8_t* fmt) {  // names present + formats
     mask = 0;
@@ -808,13 +826,17 @@ void Host::build(const Value& root) {
   };
   for (auto& t : tpls) for (auto& x : t.taints) internTaint(x);
   for (auto& n : nodes) for (auto& x : n.taints) internTaint(x);
-  if (taints.size() > 128) throw KsError(-3, "more than 128 distinct taints");
+  // The device's taint masks are two words over taint CLASSES: taints that exactly the same toleration lists
+  // tolerate are interchangeable in every Taints.Tolerates test the device makes (a node's or a template's
+  // taints against a relaxation state's tolerations, taints.go), so they share a bit.  The classes are formed
+  // once the relaxation chains' toleration lists are final (below); the masks are filled there.
+  std::vector<int> taintClass;
   auto taintMask = [&](const std::vector<TaintH>& ts, uint64_t* out) {
     out[0] = out[1] = 0;
     for (auto& t : ts)
       for (size_t i = 0; i < taints.size(); i++)
         if (taints[i].key == t.key && taints[i].value == t.value && taints[i].effect == t.effect)
-          out[i >> 6] |= 1ull << (i & 63);
+          out[taintClass[i] >> 6] |= 1ull << (taintClass[i] & 63);
   };
 
   // --- instance types
@@ -826,6 +848,7 @@ void Host::build(const Value& root) {
   tab.it_off_beg.assign(T + 1, 0);
   for (int i = 0; i < T; i++) {
     vec(its[i].alloc, &tab.it_alloc[(size_t)i * R]);
+    neverFits(its[i].alloc, &tab.it_alloc[(size_t)i * R]);
     vec(its[i].capacity, &tab.it_cap[(size_t)i * R]);
     std::vector<uint32_t> rs = emptyRec();
     for (auto& n : its[i].reqs) addNSR(rs, n.key, n.op, n.values);
@@ -871,7 +894,6 @@ void Host::build(const Value& root) {
       rs_add(L, withHost.data(), h.data());
     }
     std::copy(withHost.begin(), withHost.end(), tab.tpl_rs.begin() + (size_t)t * dims.RSW);
-    taintMask(tp.taints, &tab.tpl_taint[(size_t)t * 2]);
     QList overhead;
     int nd = 0;
     for (size_t i = 0; i < daemons.size(); i++) {
@@ -1029,11 +1051,14 @@ void Host::build(const Value& root) {
     if (podKeyCount[key] > 1 && (!p.ports.empty() || ownerKeys.count(key)))
       throw KsError(-2, "pods being scheduled share the key " + key + " and host ports");
   }
-  if (hostPortUniverse.size() > 64) throw KsError(-3, "more than 64 distinct host ports");
-  auto hpMask = [&](const std::vector<std::pair<std::string, HostPortH>>& v) {
-    uint64_t m = 0;
-    for (auto& e : v) m |= 1ull << internHP(e.second, podKeyCount.count(e.first) ? e.first : "");
-    return m;
+  // The device masks are one word over element CLASSES: elements that every pod being scheduled treats alike
+  // (in its conflict set, its reservations and its own initial entries, or in none of them) evolve alike
+  // under Conflicts / Add on every node and NodeClaim, so they share a bit; a node's entries that no pod
+  // matches collapse into one class.  Classes are formed with the pods' masks (below).
+  std::vector<std::vector<int>> nodeHP((size_t)N);
+  auto hpMask = [&](const std::vector<std::pair<std::string, HostPortH>>& v, std::vector<int>& out) {
+    for (auto& e : v) out.push_back(internHP(e.second, podKeyCount.count(e.first) ? e.first : ""));
+    return 0ull;
   };
   dims.hpAny = hostPortUniverse.empty() ? 0 : 1;
   // --- volume limits (ExistingNode.Add: GetVolumes + VolumeUsage.ExceedsLimits, existingnode.go:70-78).
@@ -1160,7 +1185,7 @@ void Host::build(const Value& root) {
   for (int i = 0; i < N; i++) {
     Node& n = nodes[i];
     tab.n_flags[i] = (!n.initialized || !n.ready) ? NF_UNUSABLE : 0;
-    tab.n_hp0[i] = hpMask(n.hostPorts);
+    tab.n_hp0[i] = hpMask(n.hostPorts, nodeHP[(size_t)i]);
     std::vector<uint32_t> lab = emptyRec();
     addNodeLabels(lab, n.labels);  // the keys of the universe only (see the universe build)
     QList dreq;
@@ -1187,11 +1212,11 @@ void Host::build(const Value& root) {
       if (kv.second.n < 0) kv.second.n = 0;
     }
     vec(n.available, &tab.n_avail[(size_t)i * R]);
+    neverFits(n.available, &tab.n_avail[(size_t)i * R]);
     if (volBlocked[i]) tab.n_avail[(size_t)i * R] = -1;  // Fits fails on any negative total (resources.go:166-170)
     vec(n.req0, &tab.n_req0[(size_t)i * R]);
     addNSR(lab, kHostname, "In", {n.hostName});
     std::copy(lab.begin(), lab.end(), tab.n_rs0.begin() + (size_t)i * dims.RSW);
-    taintMask(n.taints, &tab.n_taint[(size_t)i * 2]);
   }
   pt.mark("nodes+hostports+volumes");
   // --- limits: remaining = Limits - capacity of existing nodes in the pool
@@ -1236,21 +1261,43 @@ void Host::build(const Value& root) {
   tab.pod_hpc.assign(std::max(P, 1), 0);
   tab.pod_hpu.assign(std::max(P, 1), 0);
   tab.pod_hpo.assign(std::max(P, 1), 0);
+  const size_t NUH = hostPortUniverse.size();
+  // per element, the pods that have it in their conflict / reservation / own-entry sets (pod order)
+  std::vector<std::vector<int32_t>> hpSig(NUH);
   for (int i = 0; i < P; i++) {
     tab.pod_flags[i] = (pods[i].provisionable ? PF_PROVISIONABLE : 0) | (podShared[(size_t)i] ? PF_VSHARED : 0) |
                        (podVolErr[(size_t)i] ? PF_VOLERR : 0);
-    if (hostPortUniverse.empty()) continue;
+    if (NUH == 0 || (pods[i].ports.empty() && !ownerKeys.count(pods[i].ns + "/" + pods[i].name))) continue;
     const std::string key = pods[i].ns + "/" + pods[i].name;
-    for (size_t u = 0; u < hostPortUniverse.size(); u++)
-      if (hostPortOwner[u] == key) tab.pod_hpo[i] |= 1ull << u;  // its own entries: never a conflict, replaced by Add
-    for (auto& h : pods[i].ports) {
-      for (size_t u = 0; u < hostPortUniverse.size(); u++) {
-        if (hostPortUniverse[u].ip == h.ip && hostPortUniverse[u].port == h.port && hostPortUniverse[u].proto == h.proto &&
-            hostPortOwner[u].empty())
-          tab.pod_hpu[i] |= 1ull << u;
-        if (h.matches(hostPortUniverse[u]) && hostPortOwner[u] != key) tab.pod_hpc[i] |= 1ull << u;
+    for (size_t u = 0; u < NUH; u++) {
+      bool hpc = false, hpu = false;
+      const bool hpo = hostPortOwner[u] == key;  // its own entries: never a conflict, replaced by Add
+      for (auto& h : pods[i].ports) {
+        hpu = hpu || (hostPortUniverse[u].ip == h.ip && hostPortUniverse[u].port == h.port &&
+                      hostPortUniverse[u].proto == h.proto && hostPortOwner[u].empty());
+        hpc = hpc || (h.matches(hostPortUniverse[u]) && hostPortOwner[u] != key);
       }
+      const int code = (hpc ? 1 : 0) | (hpu ? 2 : 0) | (hpo ? 4 : 0);
+      if (code) hpSig[u].push_back(i * 8 + code);
     }
+  }
+  if (NUH) {
+    std::map<std::vector<int32_t>, int> cls;
+    std::vector<int> hpClass(NUH);
+    for (size_t u = 0; u < NUH; u++) hpClass[u] = cls.emplace(hpSig[u], (int)cls.size()).first->second;
+    if (cls.size() > 64)
+      throw KsError(-3, "more than 64 host-port classes (" + std::to_string(NUH) +
+                            " (IP, port, protocol) entries that the pods being scheduled tell apart)");
+    for (size_t u = 0; u < NUH; u++)
+      for (int32_t e : hpSig[u]) {
+        const int i = e >> 3, code = e & 7;
+        const uint64_t b = 1ull << hpClass[u];
+        if (code & 1) tab.pod_hpc[(size_t)i] |= b;
+        if (code & 2) tab.pod_hpu[(size_t)i] |= b;
+        if (code & 4) tab.pod_hpo[(size_t)i] |= b;
+      }
+    for (int i = 0; i < N; i++)
+      for (int u : nodeHP[(size_t)i]) tab.n_hp0[(size_t)i] |= 1ull << hpClass[(size_t)u];
   }
   std::map<std::string, int> uids;
   for (auto& p : pods) uids[p.uid] = 0;
@@ -1386,6 +1433,33 @@ void Host::build(const Value& root) {
   // the per-pod relaxation states here do not model.
   if (dims.dupUids && !groups.empty())
     throw KsError(-2, "pods sharing a UID own topology groups (TopologyGroup owners are keyed by UID)");
+  {  // taint classes: the distinct toleration lists of every relaxation state, then one class per distinct
+     // "tolerated by which lists" signature
+    std::map<std::vector<std::string>, int> lists;
+    std::vector<const std::vector<TolH>*> tl;
+    for (auto& chain : states)
+      for (auto& st : chain) {
+        std::vector<std::string> k;
+        for (auto& t : st.tols) k.push_back(t.key + '\x1f' + t.op + '\x1f' + t.value + '\x1f' + t.effect);
+        if (lists.emplace(std::move(k), (int)tl.size()).second) tl.push_back(&st.tols);
+      }
+    std::map<std::vector<uint64_t>, int> sig;
+    taintClass.assign(taints.size(), 0);
+    for (size_t i = 0; i < taints.size(); i++) {
+      std::vector<uint64_t> b((tl.size() + 63) / 64, 0);
+      for (size_t j = 0; j < tl.size(); j++) {
+        bool ok = false;
+        for (auto& t : *tl[j]) ok = ok || toleratesTaint(t, taints[i]);
+        if (ok) b[j >> 6] |= 1ull << (j & 63);
+      }
+      taintClass[i] = sig.emplace(std::move(b), (int)sig.size()).first->second;
+    }
+    if (sig.size() > 128)
+      throw KsError(-3, "more than 128 taint classes (" + std::to_string(taints.size()) +
+                            " taints that the pods' toleration lists tell apart)");
+    for (int t = 0; t < NT; t++) taintMask(tpls[(size_t)t].taints, &tab.tpl_taint[(size_t)t * 2]);
+    for (int i = 0; i < N; i++) taintMask(nodes[(size_t)i].taints, &tab.n_taint[(size_t)i * 2]);
+  }
   tab.st_rs.assign((size_t)dims.S * dims.RSW, 0);
   tab.st_tol.assign((size_t)dims.S * 2, 0);
   tab.st_flags.assign(dims.S, 0);
@@ -1397,13 +1471,13 @@ void Host::build(const Value& root) {
     for (auto& st : chain) {
       std::copy(st.rsAll.begin(), st.rsAll.end(), tab.st_rs.begin() + (size_t)s * dims.RSW);
       uint64_t m[2];
-      tolMask(st.tols, m);
+      tolMask(st.tols, taintClass, m);
       tab.st_tol[(size_t)s * 2] = m[0];
       tab.st_tol[(size_t)s * 2 + 1] = m[1];
       uint64_t pres = rs_present(st.rsAll.data());
-      uint32_t tt = 0;
+      uint64_t tt = 0;
       for (int t = 0; t < dims.NTPL; t++)
-        if (((tab.tpl_taint[(size_t)t * 2] & ~m[0]) | (tab.tpl_taint[(size_t)t * 2 + 1] & ~m[1])) == 0) tt |= 1u << t;
+        if (((tab.tpl_taint[(size_t)t * 2] & ~m[0]) | (tab.tpl_taint[(size_t)t * 2 + 1] & ~m[1])) == 0) tt |= 1ull << t;
       tab.st_toltpl[s] = tt;
       if (!groups.empty()) {
         for (int32_t g : st.gown) gset(tab.st_gown, (size_t)s, dims.GMW, g);

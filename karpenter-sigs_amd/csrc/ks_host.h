@@ -199,7 +199,8 @@ struct Host {
     std::vector<uint64_t> tg_late;                      // [GMW] groups a relaxation creates mid-Solve
     std::vector<uint32_t> st_rss;   // [S][RSW] strict pod requirements (NewStrictPodRequirements)
     std::vector<int32_t> n_tdom;    // [G][N] value index of the node's label for the group's key (-1: none)
-    std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask, st_toltpl;
+    std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask;
+    std::vector<uint64_t> st_toltpl;
     std::vector<uint64_t> tpl_taint, st_tol, n_taint;
     std::vector<int32_t> tsort_pos, it_off_beg, off_zone, off_ct, tpl_it_beg, tpl_its, tpl_pool, pod_state0, pod_nstate, pod_uid,
         st_flags;
@@ -225,7 +226,7 @@ struct Host {
   // an existing node's labels, restricted to the universe's keys (node-only keys are not interned: build)
   void addNodeLabels(std::vector<uint32_t>& rec, const std::map<std::string, std::string>& labels) const;
   std::vector<uint32_t> podRequirements(PodH& p, bool all) const;
-  uint64_t tolMask(const std::vector<TolH>& tols, uint64_t out[2]) const;
+  void tolMask(const std::vector<TolH>& tols, const std::vector<int>& cls, uint64_t out[2]) const;
   int64_t toDev(int r, const Qty& q) const;
   Qty fromDev(int r, int64_t v) const;
 

@@ -26,7 +26,7 @@
 namespace ks {
 
 constexpr int kMaxR = 16;         // resource names per problem
-constexpr int kMaxTpl = 32;       // NodeClaimTemplates (NodePools) per problem
+constexpr int kMaxTpl = 64;       // NodeClaimTemplates (NodePools) per problem (st_toltpl is one 64-bit mask)
 constexpr int kWave = 64;
 
 enum PodStatus : int32_t { ST_PENDING = 0, ST_SCHEDULED = 1, ST_FAILED = 2 };
@@ -126,13 +126,13 @@ struct KsDev {
   const int32_t KS_G* pod_nstate;  // [P]
   const int32_t KS_G* pod_uid;     // [P] interned UID (queue staleness key, queue.go:54-69)
   const int64_t KS_G* pod_sortkey; // [P][4] cpu, memory, creation second, uid rank (queue.go:83-112)
-  const uint64_t KS_G* pod_s0;     // [P][3] the pod's first relaxation state: st_tol[0..1], st_toltpl << 32 | st_flags
+  const uint64_t KS_G* pod_s0;     // [P][4] the pod's first relaxation state: st_tol[0..1], st_toltpl, st_flags
                                    // (queue window refills before any Queue.Push read these, one level fewer)
   // relaxation states (preferences.go:38-147 applied 0..n times)
   const uint32_t KS_G* st_rs;      // [S][RSW] NewPodRequirements
   const uint64_t KS_G* st_tol;     // [S][2] tolerated-taint masks
   const int32_t KS_G* st_flags;    // [S]
-  const uint32_t KS_G* st_toltpl;  // [S] bit t: the state tolerates template t's taints
+  const uint64_t KS_G* st_toltpl;  // [S] bit t: the state tolerates template t's taints
   // existing nodes, in calculateExistingNodeClaims order (scheduler.go:313-321)
   const int64_t KS_G* n_avail;     // [N][R] StateNode.Available()
   const int64_t KS_G* n_req0;      // [N][R] remaining daemon requests (existingnode.go:43-52)

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void k_sim_run_breaks(const int32_t* podmap, c
   bool brk = true;
   if (i < n && i > 0 && entry_sim[i] == entry_sim[i - 1]) {
     const int p = podmap[i], q = podmap[i - 1];
-    bool same = pod_s0[3 * (int64_t)p] == pod_s0[3 * (int64_t)q] && pod_s0[3 * (int64_t)p + 1] == pod_s0[3 * (int64_t)q + 1] &&
+    bool same = pod_s0[4 * (int64_t)p] == pod_s0[4 * (int64_t)q] && pod_s0[4 * (int64_t)p + 1] == pod_s0[4 * (int64_t)q + 1] &&
                 ((pod_flags[p] ^ pod_flags[q]) & PF_PROVISIONABLE) == 0;
     for (int r = 0; r < R; r++) same = same && pod_req[(int64_t)p * R + r] == pod_req[(int64_t)q * R + r];
     brk = !same;

@@ -237,9 +237,9 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 // One queue entry per lane (the 64-pod window), read wave-uniformly with readlane.
 template <int RT>
 struct Window {
-  int p, g, uid, s, flags, toltpl, pf, st;
+  int p, g, uid, s, flags, pf, st;
   int rl;  // SIM, nothing pushed back yet: identical pods from this queue position to the end of their run
-  uint64_t ll, tol0, tol1, hpc, hpu, hpo;
+  uint64_t ll, tol0, tol1, toltpl, hpc, hpu, hpo;
   uint64_t tsel, tinv, town, trss;  // TOPO: word 0 of the pod's selecting / inverse / owned group sets, st_rss keys
   int64_t req[RT > 0 ? RT : kMaxR];
 };
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void k_feasibility(KsDev D) {
     const int rr = live ? row : rows - 1;
     const int s = rr / d.NTPL, t = rr - s * d.NTPL;
     uint32_t KS_G* out = D.st_fm + (int64_t)rr * d.TW;
-    if (!((D.st_toltpl[s] >> t) & 1u)) {  // the state does not tolerate the template's taints
+    if (!((D.st_toltpl[s] >> t) & 1ull)) {  // the state does not tolerate the template's taints
       for (int w = sub; w < d.TW; w += GW)
         if (live) out[w] = 0;
       continue;
@@ -1426,8 +1426,8 @@ struct Solver {
   }
 
   // --- NodeClaim quick reject at sorted position j: necessary conditions of NodeClaim.Add ------
-  __device__ __forceinline__ bool claim_quick(int j, int s, int sflags, uint32_t toltpl, const int64_t* pod) const {
-    if (!((toltpl >> s_ptpl[j]) & 1u)) return false;  // Taints.Tolerates (nodeclaim.go:68-71)
+  __device__ __forceinline__ bool claim_quick(int j, int s, int sflags, uint64_t toltpl, const int64_t* pod) const {
+    if (!((toltpl >> s_ptpl[j]) & 1ull)) return false;  // Taints.Tolerates (nodeclaim.go:68-71)
     if (hpA() && (W.c_hp[s_order[j]] & cur_hpc)) return false;  // host port conflicts (:72-75)
     bool ok = true;
 #pragma unroll
@@ -1743,7 +1743,7 @@ struct Solver {
 
   // --- new NodeClaim from each template in order (scheduler.go:258-283) -----------------------
   // Returns 1 placed, 0 failed (fail codes recorded), 2 no templates (add() returns nil), -1 cap.
-  __device__ __forceinline__ int try_templates(int p, int s, int sflags, uint32_t toltpl, const int64_t* pod,
+  __device__ __forceinline__ int try_templates(int p, int s, int sflags, uint64_t toltpl, const int64_t* pod,
                                                int& nclaims, int& nlog, int& hostCtr, bool& srt) {
     if (d.NTPL == 0) return 2;
     for (int t = 0; t < d.NTPL; t++) {
@@ -1771,7 +1771,7 @@ struct Solver {
         code = FC_LIMITS;
       } else {
         hostid = ++hostCtr;  // NewNodeClaim: atomic.AddInt64(&nodeID, 1) (nodeclaim.go:48)
-        if (!((toltpl >> t) & 1u)) {
+        if (!((toltpl >> t) & 1ull)) {
           code = FC_TAINTS;
         } else {
           copy_words(s_rs, D.tpl_rs + (int64_t)t * d.RSW, d.RSW);
@@ -2444,12 +2444,11 @@ struct Solver {
       if (ident) {
         w.s = D.pod_state0[w.g];
         w.ll = 0;
-        const uint64_t KS_G* s0 = D.pod_s0 + 3 * (int64_t)w.g;
+        const uint64_t KS_G* s0 = D.pod_s0 + 4 * (int64_t)w.g;
         w.tol0 = s0[0];
         w.tol1 = s0[1];
-        const uint64_t tf = s0[2];
-        w.toltpl = (int)(uint32_t)(tf >> 32);
-        w.flags = (int)(uint32_t)tf;
+        w.toltpl = s0[2];
+        w.flags = (int)(uint32_t)s0[3];
         w.st = ST_PENDING;
       } else {
         w.s = ld_sc1(W.pod_state + w.p);

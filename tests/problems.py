@@ -693,3 +693,106 @@ def many_groups_problem(seed, n_apps=150, n_pods=600, n_nodes=30, n_its=40):
             cluster.append(cp)
     snap["clusterPods"] = cluster
     return snap
+
+
+def caps_problem(seed, kind, n_pods=300):
+    """A random problem past one of the round-4 encoding caps, at about twice the cap:
+
+    pools:     64 NodePools (templates), most tainted with a key of their own that few pods tolerate, so the
+               pods spread over templates past the 32nd (st_toltpl is one 64-bit mask);
+    taints:    ~280 distinct taints (40 keys x 7 values) on nodes and templates, tolerated by key (Exists) or by
+               one value (Equal): more than 128 taints, at most ~90 toleration classes (ks_host.cpp);
+    ports:     ~140 distinct (IP, port, protocol) entries in the nodes' HostPortUsage, the pods' ports a
+               20-port subset that overlaps them: more than 64 triples, few classes;
+    resources: ~34 resource names in the instance types' and nodes' capacity (and a node whose extra resource is
+               overcommitted, an instance type whose overhead exceeds an extra resource), the pods requesting
+               cpu / memory and a few extended names, NodePool limits on one: more than 16 names, fewer live."""
+    rng = np.random.default_rng(seed)
+    if kind == "pools":
+        snap = random_problem(seed, n_pods=n_pods, n_templates=64, n_nodes=int(rng.integers(4, 12)))
+        for t, tpl in enumerate(snap["nodeClaimTemplates"]):
+            if t < 56:
+                tpl["spec"]["template"]["spec"]["taints"] = [{"key": "pool-only-%d" % t, "value": "x",
+                                                              "effect": "NoSchedule"}]
+        for p in snap["pods"]:
+            tols = p["spec"].setdefault("tolerations", [])
+            for t in rng.choice(64, size=int(rng.integers(0, 4)), replace=False):
+                tols.append({"key": "pool-only-%d" % int(t), "operator": "Exists"})
+            if not tols:
+                p["spec"].pop("tolerations")
+        return snap
+    snap = random_problem(seed, n_pods=n_pods, n_nodes=int(rng.integers(20, 40)), host_ports=(kind == "ports"))
+    if kind == "taints":
+        keys = ["taint-key-%02d" % k for k in range(40)]
+        vals = ["v%d" % v for v in range(7)]
+        for n in snap["stateNodes"]:
+            n["taints"] = [{"key": keys[int(rng.integers(40))], "value": vals[int(rng.integers(7))],
+                            "effect": _pick(rng, ["NoSchedule", "NoExecute"])} for _ in range(int(rng.integers(0, 4)))]
+        all_taints = [{"key": k, "value": v, "effect": "NoSchedule"} for k in keys for v in vals]
+        for i, tpl in enumerate(snap["nodeClaimTemplates"]):
+            picks = rng.choice(len(all_taints), size=int(rng.integers(0, 3)), replace=False)
+            tpl["spec"]["template"]["spec"]["taints"] = [all_taints[int(j)] for j in picks]
+        # every (key, value) pair appears somewhere: 280 distinct taints
+        extra = {"name": "taint-carrier", "hostName": "taint-carrier",
+                 "labels": dict(snap["stateNodes"][0]["labels"], **{synth.HOSTNAME: "taint-carrier"}),
+                 "taints": all_taints, "available": {"cpu": "4", "memory": "8Gi", "pods": "20"},
+                 "capacity": {"cpu": "4", "memory": "8Gi", "pods": "110"}, "daemonSetRequests": {}, "initialized": True}
+        snap["stateNodes"].append(extra)
+        for p in snap["pods"]:
+            if rng.random() < 0.6:
+                tols = []
+                for k in rng.choice(40, size=int(rng.integers(1, 12)), replace=False):
+                    if rng.random() < 0.7:
+                        tols.append({"key": keys[int(k)], "operator": "Exists"})
+                    else:
+                        tols.append({"key": keys[int(k)], "operator": "Equal", "value": "v0"})
+                p["spec"]["tolerations"] = tols
+        return snap
+    if kind == "ports":
+        ports = [("", 30000 + i, "TCP") for i in range(60)] + [("10.0.%d.1" % (i % 4), 31000 + i, "TCP") for i in range(50)] + \
+                [("", 32000 + i, "UDP") for i in range(40)]
+        for i, n in enumerate(snap["stateNodes"]):
+            use = n.setdefault("hostPortUsage", {})
+            for j in range(int(rng.integers(2, 8))):
+                ip, port, proto = ports[int(rng.integers(len(ports)))]
+                use["default/bound-%d-%d" % (i, j)] = [{"ip": ip or "0.0.0.0", "port": port, "protocol": proto}]
+        if snap["stateNodes"]:  # every entry on some node: 150 distinct triples
+            snap["stateNodes"][0]["hostPortUsage"]["default/port-carrier"] = [
+                {"ip": ip or "0.0.0.0", "port": port, "protocol": proto} for ip, port, proto in ports]
+        hot = [ports[int(i)] for i in rng.choice(len(ports), size=20, replace=False)]
+        for p in snap["pods"]:
+            if rng.random() < 0.3:
+                e = []
+                for _ in range(int(rng.integers(1, 3))):
+                    ip, port, proto = hot[int(rng.integers(len(hot)))]
+                    x = {"containerPort": port, "hostPort": port, "protocol": proto}
+                    if ip:
+                        x["hostIP"] = ip
+                    e.append(x)
+                p["spec"]["containers"][0]["ports"] = e
+        return snap
+    assert kind == "resources", kind
+    names = ["example.com/res-%02d" % k for k in range(30)]
+    for it in snap["instanceTypes"]:
+        for k in rng.choice(30, size=int(rng.integers(10, 30)), replace=False):
+            it["capacity"][names[int(k)]] = str(int(rng.integers(1, 9)))
+    it = snap["instanceTypes"][int(rng.integers(len(snap["instanceTypes"])))]
+    it["capacity"][names[29]] = "1"
+    it["overhead"]["kubeReserved"][names[29]] = "2"  # allocatable -1 of a name no pod requests: never fits
+    for n in snap["stateNodes"]:
+        for k in rng.choice(30, size=int(rng.integers(5, 30)), replace=False):
+            n["capacity"][names[int(k)]] = "8"
+            n["available"][names[int(k)]] = str(int(rng.integers(0, 9)))
+    if snap["stateNodes"]:
+        snap["stateNodes"][0]["available"][names[28]] = "-1"  # overcommitted, not requested: never fits
+    for p in snap["pods"]:
+        if rng.random() < 0.3:
+            req = p["spec"]["containers"][0]["resources"]["requests"]
+            for k in rng.choice(6, size=int(rng.integers(1, 3)), replace=False):
+                req[names[int(k)]] = str(int(rng.integers(1, 3)))
+    pool = snap["nodeClaimTemplates"][0]
+    pool["spec"].setdefault("limits", {})[names[7]] = "1000"
+    for np_obj in snap["nodePools"]:
+        if np_obj["metadata"]["name"] == pool["metadata"]["name"]:
+            np_obj["spec"]["limits"] = dict(pool["spec"]["limits"])
+    return snap
