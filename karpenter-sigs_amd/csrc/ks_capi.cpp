@@ -440,7 +440,7 @@ static std::string hostnameCounts(const Host& h, int g, int seq, int64_t ord, in
     if (logt[(size_t)i] >= 0) {
       ph[chost[(size_t)logt[(size_t)i]]] += 1;
     } else {
-      const int v = h.tab.n_tdom[(size_t)g * d.N + (size_t)(-logt[(size_t)i] - 1)];
+      const int v = h.tab.n_tdom[(size_t)gm[TGM_KSLOT] * d.N + (size_t)(-logt[(size_t)i] - 1)];
       if (v < 0 || v >= nv) throw KsError(KS_ERR_INTERNAL, "hostname record on a node without a hostname domain");
       cnt[(size_t)v] = cnt[(size_t)v] < 0 ? 1 : cnt[(size_t)v] + 1;
     }
@@ -938,7 +938,7 @@ extern "C++" {
 namespace {
 // the format version: 03 = round 5 (sparse volume tables, injectFailed); 02 = round 4 (group sets);
 // 01 = round 3.  A blob of another version is refused with a version error (snapshot_check_header).
-constexpr char kProblemMagic[8] = {'K', 'S', 'P', 'R', 'O', 'B', '0', '3'};
+constexpr char kProblemMagic[8] = {'K', 'S', 'P', 'R', 'O', 'B', '0', '4'};
 }  // namespace
 
 void snapshot_header(ArOut& a, const char magic[8]) {

@@ -1799,7 +1799,7 @@ template <class A> void io(A& a, ks_cons::CandIn& x) { io_all(a, x.k, x.remainin
 }  // namespace ks
 namespace {
 // 03 = round 5 (the embedded problem's format, KSPROB03); 02 = round 4
-constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '3'};
+constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '4'};
 template <class A> void cons_io(A& a, ks_cons& c) {
   io_all(a, c.cands, c.nPass, c.sims, c.multiHi, c.pending, c.deleting, c.nominated, c.hostnameSeed, c.recWords,
          c.candIn, c.nodePods, c.podNode, c.podBlock, c.podCost, c.nodeGone, c.updates);

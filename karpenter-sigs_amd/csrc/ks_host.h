@@ -198,7 +198,7 @@ struct Host {
     std::vector<uint64_t> st_gown, pod_gsel, pod_ginv;  // [S][GMW], [P][GMW], [P][GMW] group sets
     std::vector<uint64_t> tg_late;                      // [GMW] groups a relaxation creates mid-Solve
     std::vector<uint32_t> st_rss;   // [S][RSW] strict pod requirements (NewStrictPodRequirements)
-    std::vector<int32_t> n_tdom;    // [G][N] value index of the node's label for the group's key (-1: none)
+    std::vector<int32_t> n_tdom;    // [TK][N] value index of the node's label for each topology key (-1: none)
     std::vector<uint32_t> it_rs, tpl_rs, st_rs, n_rs0, pool_mask;
     std::vector<uint64_t> st_toltpl;
     std::vector<uint64_t> tpl_taint, st_tol, n_taint;

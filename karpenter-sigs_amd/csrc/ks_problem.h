@@ -81,6 +81,7 @@ struct KsDims {
                            // topology: k_solve's LEAN instantiation applies (with shared UIDs until a push-back)
   int32_t fnOn;            // st_fn is computed (k_feasibility_nodes) and k_solve reads it
   int32_t FNR;             // rows of st_fn: the relaxation states with label requirements
+  int32_t TK;              // distinct topology keys (rows of n_tdom)
 };
 
 // Per-launch LDS plan (ks_solve.hip): capacities of the LDS-resident claim state.
@@ -90,6 +91,7 @@ struct Plan {
   int32_t talloc;  // 1: template instance-type Allocatable tables are LDS-resident
   int32_t tsort;   // 1: the sorted Allocatable lists (tsort_*) are LDS-resident
   int32_t tcl;     // topology count words [0, tcl) are LDS-resident (>= KsDims::tgSmall)
+  int32_t tdl;     // node domain words [0, tdl) of n_tdom are LDS-resident (0 or TK * N)
   uint64_t lds;    // dynamic LDS bytes
 };
 
@@ -155,7 +157,7 @@ struct KsDev {
   const uint64_t KS_G* pod_ginv;   // [P][GMW] inverse groups the pod owns
   const uint64_t KS_G* tg_late;    // [GMW] groups a relaxed state creates mid-Solve: inactive until that relaxation
   const uint32_t KS_G* st_rss;     // [S][RSW] strict pod requirements (podDomains)
-  const int32_t KS_G* n_tdom;      // [G][N] value of the node's label for the group's key, -1 none
+  const int32_t KS_G* n_tdom;      // [TK][N] value of the node's label for each topology key (TGM_KSLOT), -1 none
   // feasibility tables (ks_host.cpp; k_solve feas_masks): per template, position bitsets per (key, value)
   const uint32_t KS_G* fk_words;
   const int32_t KS_G* fk_key_off;  // [NTPL][NK]
@@ -192,7 +194,9 @@ struct KsDev {
 enum NodeFlag : int32_t { NF_UNUSABLE = 1 };
 enum TopoGroupType : int32_t { TG_SPREAD = 0, TG_AFFINITY = 1, TG_ANTI = 2 };
 enum TgMeta : int32_t {  // per topology group, int32 words
-  TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST, TGM_WORDS = 12
+  TGM_TYPE = 0, TGM_KEY, TGM_SKEW, TGM_MIND, TGM_CNT, TGM_NV, TGM_FBEG, TGM_FEND, TGM_HOST,
+  TGM_KSLOT,  // the group's key among the topology keys: its row of n_tdom
+  TGM_WORDS = 12
 };
 enum PodFlag : int32_t {
   PF_PROVISIONABLE = 1,

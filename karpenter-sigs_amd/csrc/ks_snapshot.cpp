@@ -248,14 +248,15 @@ void host_check(const Host& h) {
   // topology
   if (d.G) {
     need(t.tg_meta.size(), (int64_t)d.G * TGM_WORDS, "tg_meta");
-    need(t.n_tdom.size(), (int64_t)d.G * N1, "n_tdom");
+    need(t.n_tdom.size(), (int64_t)std::max(d.TK, 1) * N1, "n_tdom");
     need(t.st_rss.size(), S * RSW, "st_rss");
     if (d.tgCntWords != (int32_t)t.tg_cnt0.size() || d.tgSmall < 0 || d.tgSmall > d.tgCntWords) bad("count table");
     for (int g = 0; g < d.G; g++) {
       const int32_t* m = &t.tg_meta[(size_t)g * TGM_WORDS];
       if (m[TGM_KEY] < 0 || m[TGM_KEY] >= d.NK || m[TGM_NV] < 0 || m[TGM_NV] > h.keys[(size_t)m[TGM_KEY]].nv ||
           m[TGM_CNT] < 0 || (int64_t)m[TGM_CNT] + std::max(m[TGM_NV], 1) > d.tgCntWords || m[TGM_FBEG] < 0 ||
-          m[TGM_FBEG] > m[TGM_FEND] || (int64_t)m[TGM_FEND] * RSW > (int64_t)t.tg_frs.size())
+          m[TGM_FBEG] > m[TGM_FEND] || (int64_t)m[TGM_FEND] * RSW > (int64_t)t.tg_frs.size() || m[TGM_KSLOT] < 0 ||
+          m[TGM_KSLOT] >= d.TK)
         bad("topology group");
     }
     for (int32_t v : t.n_tdom)
@@ -322,7 +323,7 @@ static_assert(sizeof(Host::Tpl) == 280, "Host::Tpl changed: update io(Host::Tpl)
 static_assert(sizeof(Host::IT) == 224, "Host::IT changed: update io(Host::IT)");
 static_assert(sizeof(TopoGroup) == 256, "TopoGroup changed: update io(TopoGroup)");
 static_assert(sizeof(PodState) == 120, "PodState changed: update io(PodState)");
-static_assert(sizeof(Host) == 2992, "Host changed: update host_io");
+static_assert(sizeof(Host) == 3000, "Host changed: update host_io");
 static_assert(sizeof(HostPortH) == 88 && sizeof(AffTerm) == 128 && sizeof(SpreadC) == 104 && sizeof(LabelSel) == 32,
               "a pod-spec type changed: update its io()");
 

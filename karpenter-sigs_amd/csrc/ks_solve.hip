@@ -566,6 +566,7 @@ struct Solver {
   LI32 s_tmin;          // [G] domainMinCount of the popped pod, per spread group
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
   LU32 s_trs1;          // [RSW] one group's domains as a single-key record
+  LI32 s_tdom;          // [pl.tdl] the node domain table (a Solve whose table fits)
   LI32 s_tcs;           // [pl.tcl] the count table's LDS-resident prefix: the small-key groups (a Solve: the
                         // whole table when it fits, make_plan)
   LU32 s_tcd;           // SIM: dirty bits over count words [tgSmall, tgCntWords): set once W.tg_cnt holds the word
@@ -1009,6 +1010,11 @@ struct Solver {
     return ld_sc1(W.tg_cnt + off);
   }
   __device__ __forceinline__ int tcnt(int g, int v) const { return tcnt_at(tg(g, TGM_CNT) + v); }
+  // node n's domain of group g's key (-1: the node lacks the label): LDS in a Solve whose table fits
+  __device__ __forceinline__ int tdom(int g, int n) const {
+    const int off = tg(g, TGM_KSLOT) * d.N + n;
+    return off < pl.tdl ? s_tdom[off] : D.n_tdom[off];
+  }
   // Topology.Record's count increment of word `off` (recording registers the domain), by one lane;
   // concurrent callers touch distinct words.
   __device__ __forceinline__ void tcnt_inc(int off) const {
@@ -1147,7 +1153,7 @@ struct Solver {
     for (int w = 0; w < d.GMW; w++)
       for (uint64_t m = gword(GS_MASK, w, t_mask); m; m &= m - 1) {
         const int g = 64 * w + ctz64(m);
-        const int v = D.n_tdom[(int64_t)g * d.N + n];
+        const int v = tdom(g, n);
         if (v < 0) {
           st = 2;
           continue;
@@ -1359,7 +1365,7 @@ struct Solver {
         if (node >= 0) {
           int rec = 0;
           if (lane() == 0) {
-            const int v = D.n_tdom[(int64_t)g * d.N + node];
+            const int v = tdom(g, node);
             if (v >= 0) tcnt_inc(tg(g, TGM_CNT) + v);  // recording registers the domain
             rec = v >= 0;
           }
@@ -2778,6 +2784,11 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   if (d.G && !sim && 4 * (size_t)d.tgCntWords <= avail / 4) pl.tcl = d.tgCntWords;
   const size_t tclB = r16(4 * (size_t)pl.tcl);
   avail = avail > tclB ? avail - tclB : 0;
+  // the node domain table likewise (a Solve's first-fit scan reads it for every node and matching group)
+  const size_t tdWords = (size_t)d.TK * (size_t)d.N;
+  pl.tdl = d.G && !sim && tdWords > 0 && 4 * tdWords <= avail / 4 ? (int32_t)tdWords : 0;
+  const size_t tdlB = r16(4 * (size_t)pl.tdl);
+  avail = avail > tdlB ? avail - tdlB : 0;
   // The threshold filter needs the sorted lists only without negative requests.
   const size_t tablesB = tallocB + (d.negReq ? 0 : tsortB);
   pl.talloc = (!wideKO && tablesB + 64 * (posB + clmB) <= avail) ? 1 : 0;
@@ -2796,7 +2807,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   }
   pl.KO = (int)ko;
   pl.KL = (int)kl;
-  pl.lds = fixed + tclB + 3 * r16(4 * ko) + r16(8 * ko * R) + 2 * r16(4 * kl) + 2 * r16(8 * kl * R) + r16(4 * kl * TW) +
+  pl.lds = fixed + tclB + tdlB + 3 * r16(4 * ko) + r16(8 * ko * R) + 2 * r16(4 * kl) + 2 * r16(8 * kl * R) + r16(4 * kl * TW) +
            r16(4 * kl * R) + (pl.tsort ? tsortB : 0) + (pl.talloc ? tallocB : 0);
   return pl;
 }

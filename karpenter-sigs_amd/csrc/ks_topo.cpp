@@ -169,6 +169,7 @@ void Host::buildTopology() {
     tab.tg_cnt0.assign(1, 0);
     tab.tg_frs.assign(dims.RSW, 0);
     tab.n_tdom.assign(1, -1);
+    dims.TK = 0;
     return;
   }
   PhaseTimer pt("buildTopology");
@@ -471,19 +472,31 @@ void Host::buildTopology() {
     tab.tg_cnt0.insert(tab.tg_cnt0.end(), cnts[(size_t)g].begin(), cnts[(size_t)g].end());
     if (isSmall[(size_t)g]) dims.tgSmall = (int32_t)tab.tg_cnt0.size();
   }
-  tab.n_tdom.assign((size_t)std::max(N, 1) * G, -1);  // [G][N]: a wave reads 64 nodes of one group
+  // A node's domain depends on the key only: one row per distinct topology key ([TK][N]; a wave reads 64
+  // nodes of one key), small enough for a Solve to keep in LDS.
+  std::vector<int> slotKey, slotOf(keyNames.size(), -1);
+  for (int g = 0; g < G; g++) {
+    const int k = groups[(size_t)g].keyId;
+    if (slotOf[(size_t)k] < 0) {
+      slotOf[(size_t)k] = (int)slotKey.size();
+      slotKey.push_back(k);
+    }
+    tab.tg_meta[(size_t)g * TGM_WORDS + TGM_KSLOT] = slotOf[(size_t)k];
+  }
+  dims.TK = (int32_t)slotKey.size();
+  tab.n_tdom.assign((size_t)std::max(N, 1) * std::max(dims.TK, 1), -1);
   for (int n = 0; n < N; n++)
-    for (int g = 0; g < G; g++) {
-      const TopoGroup& tg = groups[(size_t)g];
+    for (int k = 0; k < dims.TK; k++) {
+      const std::string& key = keyNames[(size_t)slotKey[(size_t)k]];
       std::string d;
-      if (tg.key == kHostnameKey) {
+      if (key == kHostnameKey) {
         d = nodes[(size_t)n].hostName;
       } else {
-        auto l = nodes[(size_t)n].labels.find(tg.key);
+        auto l = nodes[(size_t)n].labels.find(key);
         if (l == nodes[(size_t)n].labels.end()) continue;
         d = l->second;
       }
-      tab.n_tdom[(size_t)g * N + n] = valueId[(size_t)tg.keyId].at(d);
+      tab.n_tdom[(size_t)k * N + n] = valueId[(size_t)slotKey[(size_t)k]].at(d);
     }
   // A node without a group's label takes that key only from a pod's NotIn requirement
   // (existingnode.go:97-115: the strict Compatible admits nothing else), after which the topology
