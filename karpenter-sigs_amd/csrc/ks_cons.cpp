@@ -244,7 +244,9 @@ struct ks_cons {
     // headers (k_rec_headers: RF_HDR words per simulation, + 2 status words the device's record checks fill);
     // the decision fetches the option words of the few records it renders from lrec (RecView)
     int32_t* lhdr = nullptr;
-    int32_t* hhdr = nullptr;
+    int32_t* hhdr = nullptr;  // host-mapped pinned: k_rec_headers writes it directly (dhdr: its device address)
+    int32_t* dhdr = nullptr;
+    unsigned long long* lst = nullptr;  // device: the two status words + the block counter (persist, see k_rec_headers)
     bool hdrOnly = false;
     bool keptFull = false;  // a world-1 run kept the records with KS_CONS_FULL_RECORDS set (full download)
     int32_t* lentries = nullptr;
@@ -265,7 +267,7 @@ struct ks_cons {
     size_t capBuf = 0, capWorks = 0, capRec = 0, capHrec = 0, capEnt = 0, capRunw = 0, capTemp = 0, capHdr = 0, capHhdr = 0;
     void release() {
       for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
-                      (void*)lrunlen, (void*)lrunw, (void*)lkeys, (void*)lvals, ltemp, (void*)lhdr})
+                      (void*)lrunlen, (void*)lrunw, (void*)lkeys, (void*)lvals, ltemp, (void*)lhdr, (void*)lst})
         if (p) (void)hipFree(p);
       if (hrec) (void)hipHostFree(hrec);
       if (hhdr) (void)hipHostFree(hhdr);
@@ -759,8 +761,14 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   if (!c.L.hhdr || hdrBytes > c.L.capHhdr) {
     if (c.L.hhdr) HIPCHK(hipHostFree(c.L.hhdr));
     c.L.hhdr = nullptr;
-    HIPCHK(hipHostMalloc((void**)&c.L.hhdr, hdrBytes, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c.L.hhdr, hdrBytes, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void**)&c.L.dhdr, c.L.hhdr, 0));
     c.L.capHhdr = hdrBytes;
+  }
+  if (!c.L.lst) {  // status words ~0, block counter 0: k_rec_headers leaves them so after every pass
+    HIPCHK(hipMalloc((void**)&c.L.lst, 32));
+    HIPCHK(hipMemset(c.L.lst, 0xff, 16));
+    HIPCHK(hipMemset(c.L.lst + 2, 0, 16));
   }
   if (!c.L.hrec || 4 * (size_t)c.recWords * nsz > c.L.capHrec) {
     if (c.L.hrec) HIPCHK(hipHostFree(c.L.hrec));
@@ -1261,10 +1269,20 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
     if (all > bytes) HIPCHK(hipMemsetAsync((char*)records + bytes, 0, all - bytes, pb.stream));
     if (bytes) HIPCHK(hipMemcpyAsync(records, c.L.lrec, bytes, hipMemcpyDeviceToDevice, pb.stream));
   } else if (!records && world == 1 && !std::getenv("KS_CONS_FULL_RECORDS")) {  // records stay in the handle: headers only
-    unsigned long long* status = (unsigned long long*)(c.L.lhdr + (size_t)RF_HDR * ns);
-    HIPCHK(rec_headers(c.L.lrec, ns, c.recWords, pb.host.dims.TW, pb.dev.tpl_it_beg, pb.host.dims.NTPL, c.L.lhdr, status,
-                       pb.stream));
-    HIPCHK(hipMemcpyAsync(c.L.hhdr, c.L.lhdr, 4 * (size_t)RF_HDR * ns + 16, hipMemcpyDeviceToHost, pb.stream));
+    // the headers and status go straight to the host-mapped buffer (no copy); KS_CONS_HDR_COPY stages them in
+    // device memory and copies (A/B)
+    const bool copy = std::getenv("KS_CONS_HDR_COPY") != nullptr;
+    int32_t* out = copy ? c.L.lhdr : c.L.dhdr;
+    unsigned long long* sout = (unsigned long long*)(out + (size_t)RF_HDR * ns);
+    if (ns == 0) {
+      unsigned long long* hs = (unsigned long long*)(c.L.hhdr + (size_t)RF_HDR * ns);
+      hs[0] = hs[1] = ~0ull;
+    } else {
+      HIPCHK(rec_headers(c.L.lrec, ns, c.recWords, pb.host.dims.TW, pb.dev.tpl_it_beg, pb.host.dims.NTPL, out, c.L.lst,
+                         (unsigned*)(c.L.lst + 2), sout, pb.stream));
+      if (copy)
+        HIPCHK(hipMemcpyAsync(c.L.hhdr, c.L.lhdr, 4 * (size_t)RF_HDR * ns + 16, hipMemcpyDeviceToHost, pb.stream));
+    }
   } else if (bytes) {
     HIPCHK(hipMemcpyAsync(c.L.hrec, c.L.lrec, bytes, hipMemcpyDeviceToHost, pb.stream));
   }

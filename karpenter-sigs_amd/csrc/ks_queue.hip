@@ -156,53 +156,75 @@ namespace ks {
 // (consolidation.go:113-194), NewNodeClaims[0]'s options inside its template's list and numbering RF_NOPT,
 // filterByPrice's and filterOutSameType's outputs subsets of their inputs with the recorded counts.
 // status[0] = min over failing simulations of (sim << 32 | check), status[1] = min of (sim << 32 | kernel
-// error) over simulations reporting one; ~0 when none (the caller sets them before the launch).
-__global__ void k_rec_headers(const int32_t* recs, int ns, int recWords, int TW, const int32_t* tplBeg, int ntpl,
-                              int32_t* hdr, unsigned long long* status) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= ns) return;
-  const int32_t* r = recs + (size_t)s * recWords;
-  int32_t h[RF_HDR];
-  for (int i = 0; i < RF_HDR; i++) {
-    h[i] = r[i];
-    hdr[(size_t)s * RF_HDR + i] = h[i];
-  }
-  int bad = 0;
-  if (h[RF_ACTION] < CA_NOOP || h[RF_ACTION] > CA_ERROR) bad = 1;
-  else if (h[RF_NCLAIMS] < 0 || h[RF_HOSTINCR] < h[RF_NCLAIMS]) bad = 2;
-  else if (h[RF_ACTION] == CA_DELETE && h[RF_NCLAIMS] != 0) bad = 3;
-  else if (h[RF_ACTION] == CA_REPLACE && h[RF_NCLAIMS] != 1) bad = 4;
-  else if (h[RF_NCLAIMS] > 0) {
-    if (h[RF_TPL] < 0 || h[RF_TPL] >= ntpl) {
-      bad = 5;
-    } else {
-      const int nIT = tplBeg[h[RF_TPL] + 1] - tplBeg[h[RF_TPL]];
-      const uint32_t* o = (const uint32_t*)r + RF_HDR;
-      int nopt = 0, nprice = 0, nsame = 0;
-      for (int w = 0; w < TW; w++) {
-        const int lo = w * 32;
-        const uint32_t valid = nIT >= lo + 32 ? ~0u : nIT > lo ? (1u << (nIT - lo)) - 1u : 0u;
-        const uint32_t a = o[w], b = o[TW + w], c = o[2 * TW + w];
-        if (a & ~valid) bad = 6;
-        if ((b & ~a) || (c & ~b)) bad = bad ? bad : 7;
-        nopt += __popc(a);
-        nprice += __popc(b);
-        nsame += __popc(c);
-      }
-      if (!bad && (nopt != h[RF_NOPT] || nopt == 0)) bad = 8;
-      if (!bad && (nprice != h[RF_NPRICE] || nsame != h[RF_NSAME])) bad = 9;
+// error) over simulations reporting one; ~0 when none.  The device-side status words and the block counter
+// persist between passes (set once at allocation): the last block to finish publishes the status to
+// `statusOut` and resets both, so a pass needs no memset.  `hdr` / `statusOut` may be host-mapped pinned
+// memory (the pass then needs no copy either): each block stages its headers in LDS and writes them out
+// coalesced.
+__global__ __launch_bounds__(256) void k_rec_headers(const int32_t* recs, int ns, int recWords, int TW,
+                                                     const int32_t* tplBeg, int ntpl, int32_t* hdr,
+                                                     unsigned long long* status, unsigned* counter,
+                                                     unsigned long long* statusOut) {
+  __shared__ int32_t tile[256 * (RF_HDR + 1)];
+  __shared__ unsigned last;
+  const int s0 = blockIdx.x * blockDim.x, s = s0 + threadIdx.x;
+  if (s < ns) {
+    const int32_t* r = recs + (size_t)s * recWords;
+    int32_t h[RF_HDR];
+    for (int i = 0; i < RF_HDR; i++) {
+      h[i] = r[i];
+      tile[threadIdx.x * (RF_HDR + 1) + i] = h[i];
     }
+    int bad = 0;
+    if (h[RF_ACTION] < CA_NOOP || h[RF_ACTION] > CA_ERROR) bad = 1;
+    else if (h[RF_NCLAIMS] < 0 || h[RF_HOSTINCR] < h[RF_NCLAIMS]) bad = 2;
+    else if (h[RF_ACTION] == CA_DELETE && h[RF_NCLAIMS] != 0) bad = 3;
+    else if (h[RF_ACTION] == CA_REPLACE && h[RF_NCLAIMS] != 1) bad = 4;
+    else if (h[RF_NCLAIMS] > 0) {
+      if (h[RF_TPL] < 0 || h[RF_TPL] >= ntpl) {
+        bad = 5;
+      } else {
+        const int nIT = tplBeg[h[RF_TPL] + 1] - tplBeg[h[RF_TPL]];
+        const uint32_t* o = (const uint32_t*)r + RF_HDR;
+        int nopt = 0, nprice = 0, nsame = 0;
+        for (int w = 0; w < TW; w++) {
+          const int lo = w * 32;
+          const uint32_t valid = nIT >= lo + 32 ? ~0u : nIT > lo ? (1u << (nIT - lo)) - 1u : 0u;
+          const uint32_t a = o[w], b = o[TW + w], c = o[2 * TW + w];
+          if (a & ~valid) bad = 6;
+          if ((b & ~a) || (c & ~b)) bad = bad ? bad : 7;
+          nopt += __popc(a);
+          nprice += __popc(b);
+          nsame += __popc(c);
+        }
+        if (!bad && (nopt != h[RF_NOPT] || nopt == 0)) bad = 8;
+        if (!bad && (nprice != h[RF_NPRICE] || nsame != h[RF_NSAME])) bad = 9;
+      }
+    }
+    if (bad) atomicMin(status, ((unsigned long long)s << 32) | (unsigned)bad);
+    if (h[RF_ERROR] != KE_OK) atomicMin(status + 1, ((unsigned long long)s << 32) | (unsigned)h[RF_ERROR]);
   }
-  if (bad) atomicMin(status, ((unsigned long long)s << 32) | (unsigned)bad);
-  if (h[RF_ERROR] != KE_OK) atomicMin(status + 1, ((unsigned long long)s << 32) | (unsigned)h[RF_ERROR]);
+  __syncthreads();
+  const int nb = ns - s0 < (int)blockDim.x ? ns - s0 : (int)blockDim.x;
+  for (int w = threadIdx.x; w < nb * RF_HDR; w += blockDim.x)
+    hdr[(size_t)s0 * RF_HDR + w] = tile[(w / RF_HDR) * (RF_HDR + 1) + w % RF_HDR];
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (last && threadIdx.x < 2) {  // every block's status atomics are done: publish and reset
+    __threadfence();
+    statusOut[threadIdx.x] = atomicExch(status + threadIdx.x, ~0ull);
+    if (threadIdx.x == 0) atomicExch(counter, 0u);
+    __threadfence_system();
+  }
 }
 
 hipError_t rec_headers(const int32_t* recs, int ns, int recWords, int TW, const int32_t* tplBeg, int ntpl, int32_t* hdr,
-                       unsigned long long* status, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(status, 0xff, 2 * sizeof(unsigned long long), st);
-  if (e != hipSuccess || ns <= 0) return e;
+                       unsigned long long* status, unsigned* counter, unsigned long long* statusOut, hipStream_t st) {
+  if (ns <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_rec_headers, dim3((ns + 255) / 256), dim3(256), 0, st, recs, ns, recWords, TW, tplBeg, ntpl, hdr,
-                     status);
+                     status, counter, statusOut);
   return hipGetLastError();
 }
 

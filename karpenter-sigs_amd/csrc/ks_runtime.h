@@ -27,7 +27,7 @@ hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp,
 hipError_t rank_from_order(const int32_t* order, int32_t* rank, int n, hipStream_t st);
 // consolidation record headers + device-side record invariants (ks_queue.hip k_rec_headers)
 hipError_t rec_headers(const int32_t* recs, int ns, int recWords, int TW, const int32_t* tplBeg, int ntpl, int32_t* hdr,
-                       unsigned long long* status, hipStream_t st);
+                       unsigned long long* status, unsigned* counter, unsigned long long* statusOut, hipStream_t st);
 hipError_t sim_run_lengths(const int32_t* podmap, const int32_t* entry_sim, const int64_t* pod_req, const uint64_t* pod_s0,
                            const int32_t* pod_flags, int R, int n, uint64_t* words, int32_t* run_len, hipStream_t st);
 hipError_t sim_queue_sort(const int32_t* rank, const int32_t* entries, const int32_t* entry_sim, int n, int rbits,
