@@ -92,6 +92,7 @@ struct Plan {
   int32_t tsort;   // 1: the sorted Allocatable lists (tsort_*) are LDS-resident
   int32_t tcl;     // topology count words [0, tcl) are LDS-resident (>= KsDims::tgSmall)
   int32_t tdl;     // node domain words [0, tdl) of n_tdom are LDS-resident (0 or TK * N)
+  int32_t livl;    // a Solve's live node list (LDS words; 0: the scan walks every node)
   uint64_t lds;    // dynamic LDS bytes
 };
 

@@ -67,6 +67,7 @@ enum GroupSet : int { GS_MASK = 0, GS_SEL, GS_INV, GS_ACT, GS_N };
 __device__ __forceinline__ int lane() { return (int)threadIdx.x & (kWave - 1); }
 __device__ __forceinline__ uint64_t wballot(bool p) { return __ballot(p ? 1 : 0); }
 __device__ __forceinline__ int ctz64(uint64_t m) { return __builtin_ctzll(m); }
+__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 // A wave-uniform branch condition.  The commit chain's control flow is uniform by construction, but
 // the compiler cannot prove it for values that pass through LDS atomics or lane-indexed loads; a
@@ -567,6 +568,7 @@ struct Solver {
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
   LU32 s_trs1;          // [RSW] one group's domains as a single-key record
   LI32 s_tdom;          // [pl.tdl] the node domain table (a Solve whose table fits)
+  LI32 s_live;          // [pl.livl] a Solve's live node list (ks_solve_body.inc)
   LI32 s_tcs;           // [pl.tcl] the count table's LDS-resident prefix: the small-key groups (a Solve: the
                         // whole table when it fits, make_plan)
   LU32 s_tcd;           // SIM: dirty bits over count words [tgSmall, tgCntWords): set once W.tg_cnt holds the word
@@ -883,16 +885,19 @@ struct Solver {
   // clamped for the loads and masked.  nf: NodeFlag bits.  sl[i]: the node passed every check but lacks
   // the label of a matching group's key, so only the wave-cooperative node_slow can decide it (ok is
   // false then).
-  template <int KN>
+  // LIST: lane l of block i tests node nl[i] (the Solve's live list; -1: none) instead of n0 + 64 i + l; stay[i]:
+  // the node still passes Fits for these requests once the pod is committed to it (the list keeps it).
+  template <int KN, bool LIST = false>
   __device__ __forceinline__ void node_okK(int n0, int sflags, const int64_t* pod, uint64_t tol0, uint64_t tol1,
-                                           bool* ok, int* nf, int64_t (*q)[RM], bool* sl, bool* rk) const {
+                                           bool* ok, int* nf, int64_t (*q)[RM], bool* sl, bool* rk,
+                                           const int* nl = nullptr, bool* stay = nullptr) const {
     int c[KN];
     uint64_t tx[KN], ty[KN], h[KN];
     int64_t a[KN][RM];
 #pragma unroll
     for (int i = 0; i < KN; i++) {
-      const int n = n0 + i * kWave;
-      c[i] = n < d.N ? n : d.N - 1;
+      const int n = LIST ? nl[i] : n0 + i * kWave;
+      c[i] = LIST ? (n >= 0 ? n : 0) : n < d.N ? n : d.N - 1;
       const bool own = !SIM || tbit(s_tch, c[i]);
       const uint64_t KS_G* tp = D.n_taint + 2 * c[i];
       const int64_t KS_G* ap = D.n_avail + (int64_t)c[i] * R();
@@ -911,13 +916,16 @@ struct Solver {
     }
 #pragma unroll
     for (int i = 0; i < KN; i++) {
-      bool rr = n0 + i * kWave < d.N;
+      bool rr = LIST ? nl[i] >= 0 : n0 + i * kWave < d.N;
       if (SIM) rr &= !tbit(s_rmv, c[i]);  // the simulation removed these candidates
+      bool st = true;
 #pragma unroll
       for (int r = 0; r < RM; r++) {  // Fits(requests + pod, Available())
         if (RT == 0 && r >= d.R) break;
         rr &= (a[i][r] >= 0) & (q[i][r] + pod[r] <= a[i][r]);
+        if (LIST) st &= q[i][r] + 2 * pod[r] <= a[i][r];
       }
+      if (LIST) stay[i] = st;
       rk[i] = rr;  // (permanent for these requests: the caller's resource-failing prefix)
       ok[i] = rr & (((tx[i] & ~tol0) | (ty[i] & ~tol1)) == 0) & ((h[i] & cur_hpc) == 0);  // Taints.Tolerates
       if (volA() && vol_any() && ok[i]) ok[i] = vol_ok(c[i]);
@@ -2789,6 +2797,11 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   pl.tdl = d.G && !sim && tdWords > 0 && 4 * tdWords <= avail / 4 ? (int32_t)tdWords : 0;
   const size_t tdlB = r16(4 * (size_t)pl.tdl);
   avail = avail > tdlB ? avail - tdlB : 0;
+  // a Solve's live node list: the existing nodes past the register window passing Fits for the current
+  // request vector (ks_solve_body.inc)
+  pl.livl = !sim && d.N > 0 && !d.negReq && !d.tgUnlab && 4 * (size_t)d.N <= avail / 4 ? d.N : 0;
+  const size_t livB = r16(4 * (size_t)pl.livl);
+  avail = avail > livB ? avail - livB : 0;
   // The threshold filter needs the sorted lists only without negative requests.
   const size_t tablesB = tallocB + (d.negReq ? 0 : tsortB);
   pl.talloc = (!wideKO && tablesB + 64 * (posB + clmB) <= avail) ? 1 : 0;
@@ -2807,7 +2820,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   }
   pl.KO = (int)ko;
   pl.KL = (int)kl;
-  pl.lds = fixed + tclB + tdlB + 3 * r16(4 * ko) + r16(8 * ko * R) + 2 * r16(4 * kl) + 2 * r16(8 * kl * R) + r16(4 * kl * TW) +
+  pl.lds = fixed + tclB + tdlB + livB + 3 * r16(4 * ko) + r16(8 * ko * R) + 2 * r16(4 * kl) + 2 * r16(8 * kl * R) + r16(4 * kl * TW) +
            r16(4 * kl * R) + (pl.tsort ? tsortB : 0) + (pl.talloc ? tallocB : 0);
   return pl;
 }
