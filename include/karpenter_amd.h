@@ -148,11 +148,13 @@ int ks_cons_inspect(const char* snapshot_json, size_t len, char** out_json);
  * provisioner.go:204-296).  update_json: {"deletePods":[uid], "bindPods":[{"uid","node"}],
  * "removeNodes":[name]}, applied in that order: a deleted pod frees its node's requests; a bound pod
  * (pending until now) is Running on an active node and takes its requests; a removed node takes its pods
- * with it and returns its capacity to its NodePool's limits.  Candidates, their costs and order, and
- * the simulations are re-derived; the next ks_cons_run sees the new state.  All or nothing:
- * KS_ERR_ARG for unknown / already-deleted / not-pending pods or unknown nodes, KS_ERR_UNSUPPORTED
- * for clusters with topology groups or volume limits and pods with host ports (rebuild with
- * ks_cons_create there). */
+ * with it and returns its capacity to its NodePool's limits.  In a topology cluster the shared NewTopology
+ * counts follow (topology.go:61-85,190-230; the snapshot's clusterPods lose deleted / removed-node pods and
+ * gain bound ones).  Candidates, their costs and order, and the simulations are re-derived; the next
+ * ks_cons_run sees the new state.  All or nothing: KS_ERR_ARG for unknown / already-deleted / not-pending
+ * pods or unknown nodes, KS_ERR_UNSUPPORTED for clusters with volume limits, pods with host ports, and a
+ * topology update that would turn a group into one only a relaxation creates (rebuild with ks_cons_create
+ * there). */
 int ks_cons_update(ks_cons* c, const char* update_json, size_t len);
 /* Host-only: the snapshot with update_json applied ("{}" for none, an array for a sequence), as ks_cons_inspect plus
  * "nodeRows" {name: {available (device units), pods}} for every active node and "poolRemaining". */
