@@ -596,7 +596,7 @@ struct Solver {
   enum : int { VO_DB = 0, VO_DE, VO_SB, VO_SE, VO_NSP, VO_UB, VO_UE, VO_NLOG, VO_NSLOT, VO_WORDS };
   LI32 s_vol;
 #ifdef KS_PHASE_STATS
-  uint64_t scyc[4] = {0, 0, 0, 0};  // claim_full sub-phases: requirements, thresholds, masks, apply
+  mutable uint64_t scyc[4] = {0, 0, 0, 0};  // claim_full sub-phases: requirements, thresholds, masks, apply
 #endif
 
   __device__ Solver(const KsDev& D_, const KsWork KS_C& W_, const Plan& p_) : D(D_), d(D_.d), W(W_), pl(p_) {}
@@ -894,6 +894,7 @@ struct Solver {
     int c[KN];
     uint64_t tx[KN], ty[KN], h[KN];
     int64_t a[KN][RM];
+    PH_BEGIN(tok);
 #pragma unroll
     for (int i = 0; i < KN; i++) {
       const int n = LIST ? nl[i] : n0 + i * kWave;
@@ -932,7 +933,10 @@ struct Solver {
       if (keys(sflags) && ok[i]) ok[i] = node_compat(c[i]);  // strict Compatible
       sl[i] = false;
     }
+    if (LIST) PHS_END(tok, 0);  // stats build: a live-list step's loads and non-topology tests
+    PH_BEGIN(ttp);
     if (TOPO && t_any) topo_node_stateK<KN>(c, ok, sl);  // topology (existingnode.go:106-114)
+    if (LIST) PHS_END(ttp, 1);  // stats build: its topology tests
   }
   __device__ __forceinline__ const uint32_t KS_G* node_rs(int n) const {
     if (!SIM) return W.n_rs + (int64_t)n * d.RSW;
