@@ -1185,14 +1185,48 @@ struct Solver {
       }
     return st;
   }
+  // KN nodes per lane, group by group: the KN domain and count loads of one group are issued together
+  // (topo_node_state1's tests, state updated branch-free; KS_TOPO_SEQ: one node after the other).
   template <int KN>
   __device__ __forceinline__ void topo_node_stateK(const int* c, bool* ok, bool* sl) const {
+#ifdef KS_TOPO_SEQ
 #pragma unroll
     for (int i = 0; i < KN; i++) {
       const int st = ok[i] ? topo_node_state1(c[i]) : 0;
       ok[i] = st == 1;
       sl[i] = st == 2;
     }
+#else
+    int st[KN];
+#pragma unroll
+    for (int i = 0; i < KN; i++) st[i] = ok[i] ? 1 : 0;
+    for (int w = 0; w < d.GMW; w++)
+      for (uint64_t m = gword(GS_MASK, w, t_mask); m; m &= m - 1) {
+        const int g = 64 * w + ctz64(m);
+        int v[KN], cn[KN];
+#pragma unroll
+        for (int i = 0; i < KN; i++) v[i] = st[i] ? tdom(g, c[i]) : -1;
+#pragma unroll
+        for (int i = 0; i < KN; i++) cn[i] = v[i] >= 0 ? tcnt(g, v[i]) : 0;
+        const int type = tg(g, TGM_TYPE), self = sel_has(g) ? 1 : 0, skew = tg(g, TGM_SKEW), mn = s_tmin[g];
+#pragma unroll
+        for (int i = 0; i < KN; i++) {
+          const int vv = v[i] < 0 ? 0 : v[i];  // (v < 0 decides below; no out-of-range member test)
+          bool pass;
+          if (type == TG_SPREAD) pass = (int64_t)cn[i] + self - mn <= skew;
+          else if (type == TG_AFFINITY) pass = tpod_has(g, vv) && (mn ? cn[i] != 0 : self != 0);
+          else pass = cn[i] == 0 && tpod_has(g, vv);
+          pass = pass && cn[i] >= 0;  // unregistered: Get never returns it
+          const int nx = v[i] < 0 ? 2 : pass ? st[i] : 0;
+          st[i] = st[i] == 0 ? 0 : nx;
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < KN; i++) {
+      ok[i] = st[i] == 1;
+      sl[i] = st[i] == 2;
+    }
+#endif
   }
   // ExistingNode.Add's requirement and topology steps for node j, wave-wide, for a node lacking the
   // label of a matching group's key (existingnode.go:91-115): nodeRequirements = the node's requirements
