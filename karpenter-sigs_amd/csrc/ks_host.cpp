@@ -760,13 +760,13 @@ void Host::build(const Value& root) {
   // the candidate's names only (resources.go:162-175), and the limits test the names the limits list.  Any
   // other name (an instance type's or node's extra capacity nobody requests) decides only through Fits'
   // negative-total rule, which the encoder folds into the entity (neverFits below).
-  std::set<std::string> live;
+  std::set<std::string> live = {"pods"};  // (every template's daemon overhead names it, getDaemonOverhead)
   for (auto& p : pods) for (auto& kv : p.requests) live.insert(kv.first);
   for (auto& p : daemons) for (auto& kv : p.requests) live.insert(kv.first);
   for (auto& p : pools) for (auto& kv : p.remaining) live.insert(kv.first);
   std::map<std::string, std::vector<__int128>> seen;
   auto visitQ = [&](const QList& q) {
-    for (auto& kv : q) if (live.empty() || live.count(kv.first)) seen[kv.first].push_back(kv.second.n);
+    for (auto& kv : q) if (live.count(kv.first)) seen[kv.first].push_back(kv.second.n);
   };
   for (auto& it : its) { visitQ(it.capacity); visitQ(it.alloc); }
   for (auto& p : pods) visitQ(p.requests);
