@@ -17,6 +17,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <ctime>
@@ -33,6 +34,7 @@
 #include "ks_gosort.h"
 #include "ks_archive.h"
 #include "ks_host.h"
+#include "ks_parallel.h"
 #include "ks_runtime.h"
 
 using namespace ks;
@@ -224,6 +226,13 @@ struct ks_cons {
   std::vector<double> podCost;             // [pod] GetPodEvictionCost
   std::vector<uint8_t> nodeGone;           // [host node] removed by an update
   std::unordered_map<std::string, int> uidIndex, nodeIndex;  // built at the first update
+  // topology clusters, built at the first update (from the host state, so also after a binary load):
+  // clusterPods position per UID and UIDs per node name; per owned group, the remaining pods owning it in
+  // their first state / only in later states (a pod counted once per group)
+  std::unordered_map<std::string, int> cpIndex;
+  std::unordered_map<std::string, std::vector<std::string>> cpByNode;
+  std::vector<int> gOwn0, gOwnLate;
+  bool topoIndexed = false;
   int64_t updates = 0;
   // per host node, for the per-simulation limits (prepare_launch): the NodePools it counts against and its
   // capacity in device units (static for the handle; built on first use)
@@ -596,32 +605,68 @@ bool offering_price(const Host::IT& it, const std::string& ct, const std::string
 // 262-265), and the candidates' hostnames are no longer registered by NewExistingNode
 // (existingnode.go:60).  Returns (tg_cnt offset, (pods removed << 1) | unregister-if-zero) pairs,
 // one per touched domain; `dead` gets the inverse groups none of whose owners is in the simulation.
+void late_only_groups(const Host& h, int p, std::vector<int32_t>& out);
+void topo_index(ks_cons& c);
+
+// Per pod of the handle: its cluster contributions and owned inverse groups (the UID-keyed maps resolved once
+// per launch plan, so the simulations' sim_topology calls -- run in parallel -- do no string lookups).
+struct PodTopo {
+  std::vector<const std::vector<std::pair<int, int>>*> contrib;
+  std::vector<const std::vector<int32_t>*> inv;
+};
+PodTopo pod_topo(const Host& h) {
+  PodTopo t;
+  const int P = (int)h.pods.size();
+  t.contrib.assign((size_t)P, nullptr);
+  t.inv.assign((size_t)P, nullptr);
+  parallel_for(P, 1024, [&](int p) {
+    const std::string& uid = h.pods[(size_t)p].uid;
+    auto ct = h.topoContrib.find(uid);
+    if (ct != h.topoContrib.end()) t.contrib[(size_t)p] = &ct->second;
+    auto io = h.topoInvOwner.find(uid);
+    if (io != h.topoInvOwner.end()) t.inv[(size_t)p] = &io->second;
+  });
+  return t;
+}
+
 std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, const std::vector<int>& simPods,
-                                  std::vector<uint64_t>& dead) {
+                                  const PodTopo& pt, std::vector<uint64_t>& dead) {
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
   const int hostKey = h.keyId.count("kubernetes.io/hostname") ? h.keyId.at("kubernetes.io/hostname") : -1;
-  std::map<std::pair<int, int>, int> dec;  // (group, value) -> pods removed
+  std::vector<std::pair<int, int>> touched;  // (group, value) per removed pod's contribution (sorted below)
   std::vector<int> ownersGone((size_t)d.G, 0);
   std::set<int> goneHosts;  // hostname value ids of the removed candidates
   for (int ci : sm.cands) {
     const ks_cons::Cand& k = c.cands[(size_t)ci];
     for (int p : k.pods) {
-      const std::string& uid = h.pods[(size_t)p].uid;
-      auto ct = h.topoContrib.find(uid);
-      if (ct != h.topoContrib.end())
-        for (auto& gv : ct->second) dec[gv]++;
-      auto io = h.topoInvOwner.find(uid);
-      if (io != h.topoInvOwner.end())
-        for (int32_t g : io->second) ownersGone[(size_t)g]++;
+      if (const auto* ct = pt.contrib[(size_t)p]) touched.insert(touched.end(), ct->begin(), ct->end());
+      if (const auto* io = pt.inv[(size_t)p])
+        for (int32_t g : *io) ownersGone[(size_t)g]++;
     }
     auto hv = hostKey >= 0 ? h.valueId[(size_t)hostKey].find(h.nodes[(size_t)k.node].hostName)
                            : h.valueId[0].end();
-    if (hostKey >= 0 && hv != h.valueId[(size_t)hostKey].end()) {
-      const int v = hv->second;
-      goneHosts.insert(v);
-      for (int g = 0; g < d.G; g++)
-        if (h.groups[(size_t)g].keyId == hostKey) dec[{g, v}] += 0;
+    if (hostKey >= 0 && hv != h.valueId[(size_t)hostKey].end()) goneHosts.insert(hv->second);
+  }
+  std::sort(touched.begin(), touched.end());
+  std::vector<std::pair<std::pair<int, int>, int>> dec;  // (group, value) -> pods removed, in (group, value) order
+  for (size_t i = 0; i < touched.size();) {
+    size_t j = i;
+    while (j < touched.size() && touched[j] == touched[i]) j++;
+    dec.push_back({touched[i], (int)(j - i)});
+    i = j;
+  }
+  if (!goneHosts.empty()) {  // the removed candidates' hostname domains, touched or not (0 pods removed)
+    std::vector<std::pair<std::pair<int, int>, int>> hostOnly;
+    for (int g = 0; g < d.G; g++)
+      if (h.groups[(size_t)g].keyId == hostKey)
+        for (int v : goneHosts) {
+          auto it = std::lower_bound(dec.begin(), dec.end(), std::make_pair(std::make_pair(g, v), INT_MIN));
+          if (it == dec.end() || it->first != std::make_pair(g, v)) hostOnly.push_back({{g, v}, 0});
+        }
+    if (!hostOnly.empty()) {
+      dec.insert(dec.end(), hostOnly.begin(), hostOnly.end());
+      std::sort(dec.begin(), dec.end());
     }
   }
   std::vector<int32_t> out;
@@ -678,13 +723,24 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   std::vector<std::vector<int32_t>> tdel(ns);
   std::vector<std::vector<uint64_t>> tdead(ns);
   std::vector<std::vector<int>> simPods(ns);
-  int maxP = 1;
-  for (int k = 0; k < ns; k++) {
+  parallel_for(ns, 16, [&](int k) {
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
     std::vector<int>& pods = simPods[k];
     pods = c.pending;
     for (int ci : sm.cands) pods.insert(pods.end(), c.cands[(size_t)ci].pods.begin(), c.cands[(size_t)ci].pods.end());
     pods.insert(pods.end(), c.deleting.begin(), c.deleting.end());
+  });
+  if (d.G) {  // every simulation's NewTopology deltas, independent per simulation
+    const PodTopo ptopo = pod_topo(h);
+    parallel_for(ns, 4, [&](int k) {
+      tdel[k] = sim_topology(c, c.sims[(size_t)mine[(size_t)k]], simPods[k], ptopo, tdead[k]);
+    });
+  }
+  pt.mark("simulation pod lists + topology deltas");
+  int maxP = 1;
+  for (int k = 0; k < ns; k++) {
+    const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
+    std::vector<int>& pods = simPods[k];
     simP[k] = (int)pods.size();
     maxP = std::max(maxP, simP[k]);
     for (int p : pods) {
@@ -734,7 +790,6 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       o.tg_cnt = a.add(4 * (size_t)d.tgCntWords);
       o.tg_ccnt = a.add(4 * (size_t)d.G * (P + 1));
       o.tg_cpos = a.add(4 * (size_t)d.G);
-      tdel[k] = sim_topology(c, sm, simPods[k], tdead[k]);
       o.tdel = ai.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
       o.tdead = ai.add(8 * (size_t)d.GMW);
     }
@@ -1451,6 +1506,7 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   // groups are checked; an inverse group without owners is dead in every simulation, sim_topology).
   std::vector<std::vector<std::pair<int, int>>> bindContrib(bind.size());
   std::vector<std::vector<int32_t>> bindInv(bind.size());
+  std::map<int32_t, int> topoLeave, topoLeaveLate;  // owner counts to take away once the update applies
   if (d.G) {
     for (size_t i = 0; i < bind.size(); i++) {
       PodH cp = h.pods[(size_t)bind[i]];
@@ -1461,26 +1517,38 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
                                               " counts in a topology domain or inverse group the handle does not hold");
     }
     // A group that a leaving pod's first state creates and that remaining pods own only in later relaxation
-    // states would be a late group (created mid-Solve, ks_topo.cpp) in a fresh build: refused.
-    std::vector<char> gone(h.pods.size(), 0);
+    // states would be a late group (created mid-Solve, ks_topo.cpp) in a fresh build: refused.  Per-group
+    // owner counts over the remaining pods (built once) make the test proportional to the leaving pods.
+    auto lateOnly = [&](int p, std::vector<int32_t>& out) { late_only_groups(h, p, out); };
+    if (!c.topoIndexed) topo_index(c);
     std::set<int> rmSet(rm.begin(), rm.end());
-    for (int p : del) gone[(size_t)p] = 1;
+    std::set<int> leaving(del.begin(), del.end());
     for (size_t i = 0; i < bind.size(); i++)
-      if (rmSet.count(bindNode[i])) gone[(size_t)bind[i]] = 1;
-    for (size_t p = 0; p < c.podNode.size(); p++)
-      if (c.podNode[p] >= 0 && rmSet.count(c.podNode[p])) gone[p] = 1;
-    std::set<int32_t> lost;
-    for (size_t p = 0; p < gone.size(); p++)
-      if (gone[p]) lost.insert(h.states[p][0].gown.begin(), h.states[p][0].gown.end());
-    auto remaining = [&](size_t p) { return !gone[p] && c.podNode[p] != ks_cons::PN_GONE; };
-    for (size_t p = 0; p < h.pods.size() && !lost.empty(); p++)
-      if (remaining(p)) for (int32_t g : h.states[p][0].gown) lost.erase(g);
-    for (size_t p = 0; p < h.pods.size() && !lost.empty(); p++)
-      for (size_t k = 1; remaining(p) && k < h.states[p].size(); k++)
-        for (int32_t g : h.states[p][k].gown)
-          if (lost.count(g))
-            throw KsError(KS_ERR_UNSUPPORTED, "update: topology group " + std::to_string(g) +
-                                                  " would only be created by a relaxation (rebuild the handle)");
+      if (rmSet.count(bindNode[i])) leaving.insert(bind[i]);
+    for (int n : rm)
+      for (int p : c.nodePods[(size_t)n]) leaving.insert(p);
+    for (size_t p = 0; p < c.podNode.size() && !rm.empty(); p++)  // (bound pods GetNodePods leaves out)
+      if (c.podNode[p] >= 0 && rmSet.count(c.podNode[p])) leaving.insert((int)p);
+    std::map<int32_t, int> d0, dl;  // owner counts the leaving pods take away
+    std::vector<int32_t> tmp;
+    for (int p : leaving) {
+      if (c.podNode[(size_t)p] == ks_cons::PN_GONE) continue;
+      std::vector<int32_t> s0 = h.states[(size_t)p][0].gown;
+      std::sort(s0.begin(), s0.end());
+      s0.erase(std::unique(s0.begin(), s0.end()), s0.end());
+      for (int32_t g : s0) d0[g]++;
+      lateOnly(p, tmp);
+      for (int32_t g : tmp) dl[g]++;
+    }
+    for (auto& e : d0) {
+      const int g = e.first;
+      const int own0 = c.gOwn0[(size_t)g] - e.second, late = c.gOwnLate[(size_t)g] - (dl.count(g) ? dl[g] : 0);
+      if (own0 <= 0 && late > 0)
+        throw KsError(KS_ERR_UNSUPPORTED, "update: topology group " + std::to_string(g) +
+                                              " would only be created by a relaxation (rebuild the handle)");
+    }
+    topoLeave.swap(d0);
+    topoLeaveLate.swap(dl);
   }
 
   pt.mark("validate");
@@ -1559,6 +1627,8 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
       return h.topoUniverse[(size_t)g][(size_t)v] ||
              (h.groups[(size_t)g].keyId == hostKey && !h.groups[(size_t)g].late && h.activeHost(v));
     };
+    for (auto& e : topoLeave) c.gOwn0[(size_t)e.first] -= e.second;
+    for (auto& e : topoLeaveLate) c.gOwnLate[(size_t)e.first] -= e.second;
     auto leave = [&](const std::string& uid) {
       auto ct = h.topoContrib.find(uid);
       if (ct != h.topoContrib.end()) {
@@ -1575,26 +1645,34 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
         h.topoInvOwner.erase(io);
       }
     };
-    auto dropCluster = [&](auto pred) {  // the cluster pod listing loses these pods (and their counts)
-      auto& cps = h.clusterPods;
-      size_t o = 0;
-      for (size_t i = 0; i < cps.size(); i++) {
-        if (pred(cps[i])) {
-          leave(cps[i].uid);
-          continue;
+    auto unlist = [&](const std::string& uid) {  // the cluster pod listing loses this pod (swap-remove)
+      leave(uid);
+      auto it = c.cpIndex.find(uid);
+      if (it == c.cpIndex.end()) return;
+      const size_t i = (size_t)it->second, last = h.clusterPods.size() - 1;
+      const std::string node = h.clusterPods[i].nodeName;
+      if (!node.empty()) {
+        auto bn = c.cpByNode.find(node);
+        if (bn != c.cpByNode.end()) {
+          auto& v = bn->second;
+          auto f = std::find(v.begin(), v.end(), uid);
+          if (f != v.end()) {
+            *f = v.back();
+            v.pop_back();
+          }
         }
-        if (o != i) cps[o] = std::move(cps[i]);
-        o++;
       }
-      cps.resize(o);
+      c.cpIndex.erase(it);
+      if (i != last) {
+        h.clusterPods[i] = std::move(h.clusterPods[last]);
+        c.cpIndex[h.clusterPods[i].uid] = (int)i;
+      }
+      h.clusterPods.pop_back();
     };
-    std::set<std::string> delUids;
-    for (int p : del) delUids.insert(h.pods[(size_t)p].uid);
-    for (const std::string& u : delUids) leave(u);  // (counted pods are listed; leave is idempotent)
-    dropCluster([&](const PodH& cp) { return delUids.count(cp.uid) != 0; });
+    for (int p : del) unlist(h.pods[(size_t)p].uid);  // (leave is idempotent for unlisted UIDs)
     for (size_t i = 0; i < bind.size(); i++) {
       const PodH& ph = h.pods[(size_t)bind[i]];
-      dropCluster([&](const PodH& cp) { return cp.uid == ph.uid; });
+      unlist(ph.uid);
       for (auto& gv : bindContrib[i]) {
         int32_t& x = cnt(gv.first, gv.second);
         x = x < 0 ? 1 : x + 1;
@@ -1604,11 +1682,18 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
         for (int32_t g : bindInv[i]) h.topoInvOwners[(size_t)g]++;
         h.topoInvOwner[ph.uid] = bindInv[i];
       }
+      c.cpIndex[ph.uid] = (int)h.clusterPods.size();
+      c.cpByNode[ph.nodeName].push_back(ph.uid);
       h.clusterPods.push_back(ph);
     }
     for (int n : rm) {
       const Host::Node& hn = h.nodes[(size_t)n];
-      dropCluster([&](const PodH& cp) { return cp.nodeName == hn.name; });
+      auto bn = c.cpByNode.find(hn.name);
+      if (bn != c.cpByNode.end()) {
+        const std::vector<std::string> uids = bn->second;
+        for (const std::string& u : uids) unlist(u);
+        c.cpByNode.erase(hn.name);
+      }
       if (hostKey < 0) continue;
       auto hv = h.valueId[(size_t)hostKey].find(hn.hostName);
       if (hv == h.valueId[(size_t)hostKey].end()) continue;
@@ -1699,6 +1784,51 @@ std::string topology_json(const ks_cons& c) {
     o += "}}";
   }
   return o + "}";
+}
+
+// Groups pod p owns in later relaxation states only (once each; ks_cons_update's late-group test).
+void late_only_groups(const Host& h, int p, std::vector<int32_t>& out) {
+  out.clear();
+  const auto& st = h.states[(size_t)p];
+  if (st.size() < 2) return;
+  for (size_t k = 1; k < st.size(); k++)
+    for (int32_t g : st[k].gown) out.push_back(g);
+  std::sort(out.begin(), out.end());
+  out.erase(std::unique(out.begin(), out.end()), out.end());
+  std::vector<int32_t> s0 = st[0].gown;
+  std::sort(s0.begin(), s0.end());
+  std::vector<int32_t> o2;
+  std::set_difference(out.begin(), out.end(), s0.begin(), s0.end(), std::back_inserter(o2));
+  out.swap(o2);
+}
+
+// The topology update indexes (ks_cons::cpIndex / cpByNode / gOwn0 / gOwnLate), from the host state: at the end
+// of build_cons, or at the first update after a binary load.
+void topo_index(ks_cons& c) {
+  const Host& h = c.pb->host;
+  const int G = h.dims.G;
+  c.gOwn0.assign((size_t)G, 0);
+  c.gOwnLate.assign((size_t)G, 0);
+  std::vector<int32_t> tmp, s0;
+  for (size_t p = 0; p < h.pods.size(); p++) {
+    if (c.podNode[p] == ks_cons::PN_GONE) continue;
+    s0 = h.states[p][0].gown;
+    if (s0.size() > 1) {
+      std::sort(s0.begin(), s0.end());
+      s0.erase(std::unique(s0.begin(), s0.end()), s0.end());
+    }
+    for (int32_t g : s0) c.gOwn0[(size_t)g]++;
+    late_only_groups(h, (int)p, tmp);
+    for (int32_t g : tmp) c.gOwnLate[(size_t)g]++;
+  }
+  c.cpIndex.clear();
+  c.cpByNode.clear();
+  c.cpIndex.reserve(h.clusterPods.size());
+  for (size_t i = 0; i < h.clusterPods.size(); i++) {
+    c.cpIndex.emplace(h.clusterPods[i].uid, (int)i);
+    if (!h.clusterPods[i].nodeName.empty()) c.cpByNode[h.clusterPods[i].nodeName].push_back(h.clusterPods[i].uid);
+  }
+  c.topoIndexed = true;
 }
 
 // Host-only description of a handle: the pass's candidates, the pending pods, the simulation plan and the
