@@ -233,6 +233,9 @@ struct ks_cons {
   std::unordered_map<std::string, std::vector<std::string>> cpByNode;
   std::vector<int> gOwn0, gOwnLate;
   bool topoIndexed = false;
+  // per pod: its topoContrib / topoInvOwner entry (resolved once, kept current by ks_cons_update)
+  std::vector<const std::vector<std::pair<int, int>>*> podContrib;
+  std::vector<const std::vector<int32_t>*> podInv;
   int64_t updates = 0;
   // per host node, for the per-simulation limits (prepare_launch): the NodePools it counts against and its
   // capacity in device units (static for the handle; built on first use)
@@ -327,10 +330,13 @@ namespace {
 // summed in GetNodePods order) x lifetimeRemaining, filterCandidates, sort.Slice by cost, then the multi-node
 // prefixes and the singles.  Run by build_cons and after every ks_cons_update.
 void order_candidates(ks_cons& c) {
+  PhaseTimer pt("order_candidates");
   c.cands.clear();
   c.sims.clear();
+  pt.mark("clear");
   c.multiHi = 0;
   std::vector<ks_cons::Cand> cands, valOnly;
+  cands.reserve(c.candIn.size());
   for (const ks_cons::CandIn& ci : c.candIn) {
     if (c.nodeGone[(size_t)ci.k.node]) continue;
     const std::vector<int>& pods = c.nodePods[(size_t)ci.k.node];
@@ -346,6 +352,7 @@ void order_candidates(ks_cons& c) {
     k.cost = cost * ci.remaining;
     (ci.passOk ? cands : valOnly).push_back(std::move(k));
   }
+  pt.mark("costs");
   // sort.Slice(candidates, disruptionCost <): pdqsort only observes less(), so the costs' dense ranks
   // reproduce its swap sequence exactly.
   {
@@ -360,8 +367,10 @@ void order_candidates(ks_cons& c) {
     }
     GoSortExact g{GoSort{key.data(), idx.data()}};
     g.run(n);
+    c.cands.reserve((size_t)n + valOnly.size());
     for (int i = 0; i < n; i++) c.cands.push_back(std::move(cands[(size_t)idx[i]]));
   }
+  pt.mark("sort");
   c.nPass = (int)c.cands.size();
   for (auto& k : valOnly) c.cands.push_back(std::move(k));
   // the simulations: multi-node prefixes (firstNConsolidationOption's search space) and single nodes
@@ -371,16 +380,18 @@ void order_candidates(ks_cons& c) {
     if (n <= hi) hi = n - 1;
     c.multiHi = hi;
   }
+  c.sims.reserve((size_t)c.multiHi + (size_t)n);
   for (int mid = c.multiHi; mid >= 1; mid--) {
     ks_cons::Sim s;
     s.multi = true;
-    for (int i = 0; i <= mid; i++) s.cands.push_back(i);
-    c.sims.push_back(s);
+    s.cands.resize((size_t)mid + 1);
+    for (int i = 0; i <= mid; i++) s.cands[(size_t)i] = i;
+    c.sims.push_back(std::move(s));
   }
   for (int i = 0; i < n; i++) {
     ks_cons::Sim s;
-    s.cands.push_back(i);
-    c.sims.push_back(s);
+    s.cands.assign(1, i);
+    c.sims.push_back(std::move(s));
   }
 }
 
@@ -731,10 +742,19 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     pods.insert(pods.end(), c.deleting.begin(), c.deleting.end());
   });
   if (d.G) {  // every simulation's NewTopology deltas, independent per simulation
-    const PodTopo ptopo = pod_topo(h);
+    if (c.podContrib.size() != h.pods.size()) {
+      PodTopo t = pod_topo(h);
+      c.podContrib.swap(t.contrib);
+      c.podInv.swap(t.inv);
+    }
+    PodTopo ptopo;
+    ptopo.contrib.swap(c.podContrib);
+    ptopo.inv.swap(c.podInv);
     parallel_for(ns, 4, [&](int k) {
       tdel[k] = sim_topology(c, c.sims[(size_t)mine[(size_t)k]], simPods[k], ptopo, tdead[k]);
     });
+    c.podContrib.swap(ptopo.contrib);
+    c.podInv.swap(ptopo.inv);
   }
   pt.mark("simulation pod lists + topology deltas");
   int maxP = 1;
@@ -864,8 +884,6 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     std::map<std::string, int> ids;
     for (int t = 0; t < d.T; t++) itName[(size_t)t] = ids.emplace(h.its[(size_t)t].name, (int)ids.size()).first->second;
   }
-  std::vector<char> nameSeen(itName.size(), 0), nameHas(itName.size(), 0);
-  std::vector<double> nameBest(itName.size(), 0.0);
   // per candidate: its offering's price (Offerings.Get(ct, zone), first match) and capacity type
   std::vector<double> candPrice(c.cands.size(), 0.0);
   std::vector<char> candPriceOk(c.cands.size(), 0), candSpot(c.cands.size(), 0);
@@ -885,7 +903,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     }
   }
   std::vector<KsWork> works(ns);
-  for (int k = 0; k < ns; k++) {
+  parallel_for(ns, 64, [&](int k) {  // independent per simulation (each writes its own stage slices and work)
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
     const Off& o = offs[k];
     std::vector<int32_t> rm;
@@ -915,7 +933,9 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     if (sm.multi) {
       cflags |= CF_MULTI;
       // filterOutSameType: the cheapest candidate offering per candidate instance type (by name); names as
-      // dense ids (itName), the per-name state reset through the touched list
+      // dense ids (itName)
+      std::vector<char> nameSeen(itName.size(), 0), nameHas(itName.size(), 0);
+      std::vector<double> nameBest(itName.size(), 0.0);
       std::vector<int> touched;
       for (int ci : sm.cands) {
         const ks_cons::Cand& k = c.cands[(size_t)ci];
@@ -939,7 +959,6 @@ void prepare_launch(ks_cons& c, int rank, int world) {
         st[t] = id >= 0 && nameSeen[(size_t)id] ? (nameHas[(size_t)id] ? nameBest[(size_t)id] : 0.0)
                                                : std::numeric_limits<double>::quiet_NaN();
       }
-      for (int id : touched) nameSeen[(size_t)id] = nameHas[(size_t)id] = 0;
       w.st_price = (const double*)(ibase + o.st_price);
     }
     w.c_tpl = (int32_t*)(base + o.c_tpl);
@@ -995,7 +1014,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       w.tdead = (const uint64_t*)(ibase + o.tdead);
     }
     works[k] = w;
-  }
+  });
   // The workspaces (~120 KB per simulation on C5, mostly the node-indexed copy-on-write request slots)
   // are zeroed on the device; only the inputs cross PCIe.
   pt.mark("per-simulation inputs");
@@ -1630,6 +1649,13 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     for (auto& e : topoLeave) c.gOwn0[(size_t)e.first] -= e.second;
     for (auto& e : topoLeaveLate) c.gOwnLate[(size_t)e.first] -= e.second;
     auto leave = [&](const std::string& uid) {
+      if (!c.podContrib.empty()) {  // the per-pod cache must not point at erased entries
+        auto pi = c.uidIndex.find(uid);
+        if (pi != c.uidIndex.end()) {
+          c.podContrib[(size_t)pi->second] = nullptr;
+          c.podInv[(size_t)pi->second] = nullptr;
+        }
+      }
       auto ct = h.topoContrib.find(uid);
       if (ct != h.topoContrib.end()) {
         for (auto& gv : ct->second) {
@@ -1681,6 +1707,12 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
       if (!bindInv[i].empty()) {
         for (int32_t g : bindInv[i]) h.topoInvOwners[(size_t)g]++;
         h.topoInvOwner[ph.uid] = bindInv[i];
+      }
+      if (!c.podContrib.empty()) {
+        auto ct = h.topoContrib.find(ph.uid);
+        auto io = h.topoInvOwner.find(ph.uid);
+        c.podContrib[(size_t)bind[i]] = ct != h.topoContrib.end() ? &ct->second : nullptr;
+        c.podInv[(size_t)bind[i]] = io != h.topoInvOwner.end() ? &io->second : nullptr;
       }
       c.cpIndex[ph.uid] = (int)h.clusterPods.size();
       c.cpByNode[ph.nodeName].push_back(ph.uid);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Where an incremental update + pass spends its time on C5 (ks_cons_update, then run + decide).
 
-Usage: KS_HOST_TIMING=1 python scripts/cons_update_profile.py [nodes]   (phase lines go to stderr)
+Usage: KS_HOST_TIMING=1 python scripts/cons_update_profile.py [nodes] [topology apps]   (phase lines go to stderr)
 Prints per update: update ms, run ms (plan + kernel + record copy), kernel ms, decide ms.
 """
 import json
@@ -17,7 +17,8 @@ from karpenter_amd import Consolidator, synth  # noqa: E402
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
-    snap = synth.config5(n)
+    apps = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    snap = synth.config5(n) if not apps else synth.cluster_snapshot(n, 20, 400, seed=4205, topology=apps)
     c = Consolidator(json.dumps(snap))
     for _ in range(3):
         recs, _ = c.run(0, 1)
