@@ -330,68 +330,79 @@ namespace {
 // summed in GetNodePods order) x lifetimeRemaining, filterCandidates, sort.Slice by cost, then the multi-node
 // prefixes and the singles.  Run by build_cons and after every ks_cons_update.
 void order_candidates(ks_cons& c) {
+  // (the candidate and simulation vectors are rewritten in place: an update re-orders every pass, and
+  // freeing / re-allocating 5000 candidates' and simulations' storage cost more than the rest)
   PhaseTimer pt("order_candidates");
-  c.cands.clear();
-  c.sims.clear();
-  pt.mark("clear");
-  c.multiHi = 0;
-  std::vector<ks_cons::Cand> cands, valOnly;
-  cands.reserve(c.candIn.size());
-  for (const ks_cons::CandIn& ci : c.candIn) {
+  std::vector<int> pass, valOnly;  // candIn indices
+  std::vector<double> cost(c.candIn.size(), 0.0);
+  pass.reserve(c.candIn.size());
+  for (size_t i = 0; i < c.candIn.size(); i++) {
+    const ks_cons::CandIn& ci = c.candIn[i];
     if (c.nodeGone[(size_t)ci.k.node]) continue;
-    const std::vector<int>& pods = c.nodePods[(size_t)ci.k.node];
-    double cost = 0;
+    double sum = 0;
     bool blocked = false;
-    for (int p : pods) {
-      cost += c.podCost[(size_t)p];
+    for (int p : c.nodePods[(size_t)ci.k.node]) {
+      sum += c.podCost[(size_t)p];
       blocked = blocked || (c.podBlock[(size_t)p] & 1);
     }
     if (blocked) continue;
-    ks_cons::Cand k = ci.k;
-    k.pods = pods;
-    k.cost = cost * ci.remaining;
-    (ci.passOk ? cands : valOnly).push_back(std::move(k));
+    cost[i] = sum * ci.remaining;
+    (ci.passOk ? pass : valOnly).push_back((int)i);
   }
   pt.mark("costs");
   // sort.Slice(candidates, disruptionCost <): pdqsort only observes less(), so the costs' dense ranks
   // reproduce its swap sequence exactly.
+  const int n = (int)pass.size();
+  std::vector<int32_t> idx(n);
   {
-    const int n = (int)cands.size();
-    std::vector<double> vals;
-    for (auto& k : cands) vals.push_back(k.cost);
+    std::vector<double> vals(n);
+    for (int i = 0; i < n; i++) vals[(size_t)i] = cost[(size_t)pass[(size_t)i]];
     std::sort(vals.begin(), vals.end());
-    std::vector<int32_t> key(n), idx(n);
+    std::vector<int32_t> key(n);
     for (int i = 0; i < n; i++) {
-      key[i] = (int32_t)(std::lower_bound(vals.begin(), vals.end(), cands[i].cost) - vals.begin());
+      key[i] = (int32_t)(std::lower_bound(vals.begin(), vals.end(), cost[(size_t)pass[(size_t)i]]) - vals.begin());
       idx[i] = i;
     }
     GoSortExact g{GoSort{key.data(), idx.data()}};
     g.run(n);
-    c.cands.reserve((size_t)n + valOnly.size());
-    for (int i = 0; i < n; i++) c.cands.push_back(std::move(cands[(size_t)idx[i]]));
   }
   pt.mark("sort");
-  c.nPass = (int)c.cands.size();
-  for (auto& k : valOnly) c.cands.push_back(std::move(k));
+  c.cands.resize((size_t)n + valOnly.size());
+  auto put = [&](size_t at, int ii) {
+    const ks_cons::CandIn& ci = c.candIn[(size_t)ii];
+    ks_cons::Cand& k = c.cands[at];
+    k.node = ci.k.node;
+    k.name = ci.k.name;
+    k.pool = ci.k.pool;
+    k.ct = ci.k.ct;
+    k.zone = ci.k.zone;
+    k.it = ci.k.it;
+    k.cost = cost[(size_t)ii];
+    k.pods = c.nodePods[(size_t)ci.k.node];
+  };
+  for (int i = 0; i < n; i++) put((size_t)i, pass[(size_t)idx[i]]);
+  for (size_t i = 0; i < valOnly.size(); i++) put((size_t)n + i, valOnly[i]);
+  c.nPass = n;
+  pt.mark("candidates");
   // the simulations: multi-node prefixes (firstNConsolidationOption's search space) and single nodes
-  const int n = c.nPass;
+  c.multiHi = 0;
   if (n >= 2) {
     int hi = std::min(n, 100);
     if (n <= hi) hi = n - 1;
     c.multiHi = hi;
   }
-  c.sims.reserve((size_t)c.multiHi + (size_t)n);
-  for (int mid = c.multiHi; mid >= 1; mid--) {
-    ks_cons::Sim s;
+  c.sims.resize((size_t)c.multiHi + (size_t)n);
+  size_t at = 0;
+  for (int mid = c.multiHi; mid >= 1; mid--, at++) {
+    ks_cons::Sim& s = c.sims[at];
     s.multi = true;
     s.cands.resize((size_t)mid + 1);
     for (int i = 0; i <= mid; i++) s.cands[(size_t)i] = i;
-    c.sims.push_back(std::move(s));
   }
-  for (int i = 0; i < n; i++) {
-    ks_cons::Sim s;
+  for (int i = 0; i < n; i++, at++) {
+    ks_cons::Sim& s = c.sims[at];
+    s.multi = false;
     s.cands.assign(1, i);
-    c.sims.push_back(std::move(s));
   }
 }
 
