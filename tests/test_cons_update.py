@@ -210,3 +210,31 @@ def test_update_then_validate_gpu(seed):
         want = bridge.validate(cur, cmd)
         got = c.validate(cmd)
         assert got == want, cmd
+
+
+def test_topology_update_refuses_a_group_only_a_relaxation_would_create():
+    """Pod A's first state owns a zonal spread group whose node filter is term T2; pod B's first state has
+    required node-affinity terms [T1, T2] (another group), and its relaxation (removeRequiredNodeAffinityTerm,
+    preferences.go) leaves [T2]: A's group.  Deleting A leaves that group owned only by B's relaxed state, a
+    group a fresh build would create mid-Solve (late): the update is refused whole; deleting B is fine."""
+    snap = synth.cluster_snapshot(n_nodes=6, pods_per_node=3, n_its=40, seed=5, n_pending=2)
+    t1 = {"matchExpressions": [{"key": "kubernetes.io/arch", "operator": "In", "values": ["arm64"]}]}
+    t2 = {"matchExpressions": [{"key": "kubernetes.io/os", "operator": "In", "values": ["linux"]}]}
+    spread = [{"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "DoNotSchedule",
+               "labelSelector": {"matchLabels": {"app": "x"}}}]
+    a, b = snap["stateNodes"][0]["pods"][0], snap["stateNodes"][1]["pods"][0]
+    for p, terms in ((a, [t2]), (b, [t1, t2])):
+        p["metadata"]["labels"]["app"] = "x"
+        p["spec"]["topologySpreadConstraints"] = spread
+        p["spec"]["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+            "nodeSelectorTerms": terms}}}
+    snap["clusterPods"] = [p for n in snap["stateNodes"] for p in n["pods"]]
+    base = inspect_consolidation_update(json.dumps(snap))
+    assert base["groups"] >= 2
+    with pytest.raises(KsError) as e:
+        inspect_consolidation_update(json.dumps(snap), {"deletePods": [a["metadata"]["uid"]]})
+    assert "KS_ERR_UNSUPPORTED" in str(e.value) and "relaxation" in str(e.value)
+    d = {"deletePods": [b["metadata"]["uid"]]}
+    got = inspect_consolidation_update(json.dumps(snap), d)
+    want = inspect_consolidation_update(json.dumps(apply_delta(snap, d)))
+    assert _owned_topology(got) == _owned_topology(want)
