@@ -933,7 +933,6 @@ struct Solver {
       if (keys(sflags) && ok[i]) ok[i] = node_compat(c[i]);  // strict Compatible
       sl[i] = false;
     }
-    if (LIST) PHS_END(tok, 0);  // stats build: a live-list step's loads and non-topology tests
     PH_BEGIN(ttp);
     if (TOPO && t_any) topo_node_stateK<KN>(c, ok, sl);  // topology (existingnode.go:106-114)
     if (LIST) PHS_END(ttp, 1);  // stats build: its topology tests
@@ -1394,6 +1393,33 @@ struct Solver {
   __device__ __forceinline__ void topo_record(PR F, int claim, int node, uint64_t allow, int logAt) {
     hbm_release();
     const int GMW = d.GMW;
+    if (node >= 0) {  // an existing node: one domain per group (its label); group 64 w + l in lane l
+      for (int w = 0; w < GMW; w++) {
+        const uint64_t sel = gword(GS_SEL, w, t_sel), inv = gword(GS_INV, w, t_inv), act = gword(GS_ACT, w, t_active);
+        const uint64_t m = (sel & bits_below(d.G1, w) & act) | inv;
+        if (!m) continue;
+        bool mine = ((m >> lane()) & 1ull) != 0;
+        const int g = mine ? 64 * w + lane() : 0;
+        // a spread group over a filtered node set counts the pod only where the filter admits the node
+        const bool filt = mine && g < d.G1 && tg(g, TGM_TYPE) == TG_SPREAD && tg(g, TGM_FEND) > tg(g, TGM_FBEG);
+        for (uint64_t fm = wballot(filt); fm; fm &= fm - 1) {
+          const int gf = 64 * w + ctz64(fm);
+          int match = 0;
+          if (lane() == 0)
+            for (int f = tg(gf, TGM_FBEG); f < tg(gf, TGM_FEND) && !match; f++)
+              match = rs_compatible(L, F, D.tg_frs + (int64_t)f * d.RSW, allow) ? 1 : 0;
+          const bool keep = rdl(match, 0) != 0;
+          mine = lane() == (gf & 63) ? (mine && keep) : mine;
+        }
+        const int v = mine ? tdom(g, node) : -1;
+        if (v >= 0) tcnt_inc(tg(g, TGM_CNT) + v);  // recording registers the domain (distinct words per lane)
+        const uint64_t hg = wballot(v >= 0 && tg(g, TGM_HOST) != 0);
+        if (!SIM && logAt >= 0 && hg) W.log_hg[(int64_t)logAt * GMW + w] = hg;  // wave-wide store of a uniform value
+      }
+      hbm_release();
+      wsync();
+      return;
+    }
     const uint64_t pres = rs_present(F), compl_ = rs_compl(F);
     for (int w = 0; w < GMW; w++) {
       uint64_t hg = 0;
