@@ -187,9 +187,9 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
 #define KS_CONS_CANDIDATES 2 /* flags: include the ordered candidate list */
 #define KS_CONS_NO_SIMS 4    /* flags: leave out the per-simulation "sims" lists (the commands are unchanged) */
 int ks_cons_requirement_words(const ks_cons* c);
-int ks_cons_needed_sims(const ks_cons* c, const void* records, int world, int flags, int32_t* out, int cap);
+int ks_cons_needed_sims(ks_cons* c, const void* records, int world, int flags, int32_t* out, int cap);
 int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out);
-int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
+int ks_cons_decide(ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
                    char** json_out);
 /* The methods' timeouts (MultiNodeConsolidationTimeoutDuration = 1 min, multinodeconsolidation.go:34,99-110;
  * SingleNodeConsolidationTimeoutDuration = 3 min, singlenodeconsolidation.go:29,58-65) on a virtual clock
@@ -202,7 +202,7 @@ typedef struct ks_cons_clock {
   double single_timeout_s;
   double sim_seconds;
 } ks_cons_clock;
-int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
+int ks_cons_decide_clock(ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
                          const ks_cons_clock* clock, char** json_out);
 /* Validation.IsValid after its wait + ValidateCommand (disruption/validation.go:68-180): the handle
  * holds the current cluster snapshot (stateNodes may carry "nominated": Cluster.IsNodeNominated);
@@ -220,6 +220,11 @@ int ks_cons_sim_counters(ks_cons* c, int sim, int64_t* out24);
  * re-sorts); n larger than the build's count copies that count. Returns the number copied or a negative
  * KS_ERR_* code. */
 int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n);
+/* Multi-node probes the last ks_cons_decide / ks_cons_needed_sims ran on this handle's GPU (-1: none resolved).
+ * The reference's binary search hands each probe the pod objects the earlier probes relaxed in place
+ * (multinodeconsolidation.go:111-114, helpers.go:102-104, preferences.go:60-147): a probe holding such a pod is
+ * re-simulated from the carried relaxation states, one launch per probe (typically none). */
+int ks_cons_last_reruns(const ks_cons* c);
 /* Algorithmic bytes the gathered simulations scanned, summed from their records. */
 double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world);
 

@@ -75,7 +75,7 @@ WorkLayout work_layout(const KsDims& d) {
 }
 
 KsWork work_ptrs(char* base, const WorkLayout& w) {
-  KsWork k;
+  KsWork k{};
   k.c_tpl = (int32_t*)(base + w.c_tpl);
   k.c_cnt = (int32_t*)(base + w.c_cnt);
   k.c_thr = (int32_t*)(base + w.c_thr);
@@ -936,8 +936,9 @@ int ks_problem_create(const char* json, size_t len, ks_problem** out) {
 // --- binary snapshot (ks_archive.h, ks_snapshot.cpp) ----------------------------------------------------
 extern "C++" {
 namespace {
-// the format version: 03 = round 5 (sparse volume tables, injectFailed); 02 = round 4 (group sets);
-// 01 = round 3.  A blob of another version is refused with a version error (snapshot_check_header).
+// the format version: 04 = round 5's final layout (taint and host-port classes, live resource names, sparse
+// volume tables, injectFailed); 03 = round 5's first (sparse volume tables, injectFailed); 02 = round 4 (group
+// sets); 01 = round 3.  A blob of another version is refused with a version error (snapshot_check_header).
 constexpr char kProblemMagic[8] = {'K', 'S', 'P', 'R', 'O', 'B', '0', '4'};
 }  // namespace
 

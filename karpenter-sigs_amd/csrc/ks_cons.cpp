@@ -193,11 +193,12 @@ struct ks_cons {
     bool multi = false;
   };
   std::unique_ptr<ks_problem> pb;
-  // An update whose device upload failed left the host model ahead of HBM: the handle refuses every later
-  // call (KS_ERR_HIP) instead of simulating a mix of the two (rebuild it with ks_cons_create).
+  // An update that failed after it started editing the host model (an internal inconsistency, or the device
+  // upload) left it half-applied or ahead of HBM: the handle refuses every later call (KS_ERR_HIP) instead of
+  // simulating a mix (rebuild it with ks_cons_create).
   std::string broken;
   void check_usable() const {
-    if (!broken.empty()) throw KsError(KS_ERR_HIP, "consolidation handle unusable after a failed update upload (" + broken + ")");
+    if (!broken.empty()) throw KsError(KS_ERR_HIP, "consolidation handle unusable after a failed update (" + broken + ")");
   }
   // [0, nPass): the pass's candidates in disruption-cost order; [nPass, size): nodes only
   // Validation.ShouldDisrupt admits (their pool has consolidateAfter Never), for validation's mapping
@@ -301,6 +302,32 @@ struct ks_cons {
   hipStream_t st2 = nullptr;               // the multi-wave launch's stream (launch_sims_split)
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   int32_t* rank = nullptr;  // global NewQueue rank of every pod
+  // carry_walk: a probe re-run's starting relaxation state per pod (prepare_launch uploads it with the plan)
+  const std::vector<int32_t>* carryStart = nullptr;
+  // firstNConsolidationOption's binary search (multinodeconsolidation.go:101-135) as carry_walk resolved it for
+  // the last decision: the probes in search order, each the pass's simulation of its prefix or a re-run from
+  // the pod objects earlier probes relaxed
+  struct Probe {
+    int mid = 0;
+    bool carried = false;       // re-run from carried relaxation states
+    int sim = -1;               // the pass's simulation of the prefix
+    std::vector<int32_t> rec;   // carried: the re-run's record
+    std::vector<uint32_t> rs;   // carried: its NewNodeClaims[0] requirements (when it has a NodeClaim)
+  };
+  struct Walk {
+    bool valid = false;
+    uint64_t pass = 0;
+    int world = 0;
+    bool hasClock = false;
+    double clock[3] = {0, 0, 0};
+    std::vector<Probe> probes;
+    int chosen = -1;   // the probe whose command is lastSavedCommand (-1: none)
+    bool err = false;  // a probe's getCandidatePrices failed (ComputeCommand returns the error)
+    int reruns = 0;    // launches on this GPU: carried probes, and probes whose relaxed states another rank holds
+  };
+  Walk walk;
+  uint64_t passId = 0;  // ks_cons_run calls (a walk is valid for the pass it was computed on)
+  Launch LR;            // the re-runs' launch (its buffers are kept between re-runs)
 
   int sim_of_multi(int mid) const { return multiHi - mid; }  // mid in [1, multiHi]
   int sim_of_single(int i) const { return multiHi + i; }
@@ -314,6 +341,7 @@ struct ks_cons {
     // would leave a sticky error for the caller's next launch)
     if (pb && pb->device >= 0 && hipGetDevice(&prev) == hipSuccess) (void)hipSetDevice(pb->device);
     free_launch();
+    LR.release();
     if (rank) (void)hipFree(rank);
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -651,11 +679,34 @@ PodTopo pod_topo(const Host& h) {
   return t;
 }
 
+// `start` (null: every pod's first state): the relaxation state each pod starts the simulation in (a probe re-run
+// from carried pod objects, carry_walk).  `act` gets the groups in t.topologies when the simulation starts: those
+// Topology.Update creates for its pods' starting states (topology.go:91-122), every inverse group.  The others
+// join when a relaxation's Update creates them (k_solve topo_activate_state), with a late group's NewTopology
+// state: the existing nodes' hostnames not registered (NewExistingNode ran before it existed, existingnode.go:60).
+// The shared count table holds each group in the form the whole problem's build gave it (ks_topo.cpp: late = no
+// pod's first state creates it); a hostname group this simulation creates in the other form gets per-node
+// entries that register (or unregister) those hostnames -- only for groups some relaxation in the simulation can
+// still create, the others are never read.
 std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, const std::vector<int>& simPods,
-                                  const PodTopo& pt, std::vector<uint64_t>& dead) {
+                                  const PodTopo& pt, std::vector<uint64_t>& dead, std::vector<uint64_t>& act,
+                                  const std::vector<int32_t>* start) {
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
+  const int GMW = d.GMW;
   const int hostKey = h.keyId.count("kubernetes.io/hostname") ? h.keyId.at("kubernetes.io/hostname") : -1;
+  // the owned groups at the start (act) and those a later relaxation state of a simulation pod owns (later)
+  std::vector<uint64_t> later((size_t)GMW, 0);
+  act.assign((size_t)GMW, 0);
+  for (int p : simPods) {
+    const int s0 = h.tab.pod_state0[(size_t)p], sEnd = s0 + h.tab.pod_nstate[(size_t)p];
+    const int s = start ? (*start)[(size_t)p] : s0;
+    for (int w = 0; w < GMW; w++) act[(size_t)w] |= h.tab.st_gown[(size_t)s * GMW + w];
+    for (int k = s + 1; k < sEnd; k++)
+      for (int w = 0; w < GMW; w++) later[(size_t)w] |= h.tab.st_gown[(size_t)k * GMW + w];
+  }
+  for (int g = d.G1; g < 64 * GMW; g++) act[(size_t)(g >> 6)] |= 1ull << (g & 63);  // inverse groups (and unused bits)
+  auto simLate = [&](int g) { return g < d.G1 && !((act[(size_t)(g >> 6)] >> (g & 63)) & 1ull); };
   std::vector<std::pair<int, int>> touched;  // (group, value) per removed pod's contribution (sorted below)
   std::vector<int> ownersGone((size_t)d.G, 0);
   std::set<int> goneHosts;  // hostname value ids of the removed candidates
@@ -678,39 +729,67 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
     dec.push_back({touched[i], (int)(j - i)});
     i = j;
   }
-  if (!goneHosts.empty()) {  // the removed candidates' hostname domains, touched or not (0 pods removed)
+  // hostname groups this simulation can create in the other late / initial form than the shared table's
+  std::vector<int> flip;
+  if (hostKey >= 0)
+    for (int g = 0; g < d.G1; g++)
+      if (h.groups[(size_t)g].keyId == hostKey && simLate(g) != h.groups[(size_t)g].late &&
+          ((later[(size_t)(g >> 6)] >> (g & 63)) & 1ull))
+        flip.push_back(g);
+  if (!goneHosts.empty() || !flip.empty()) {  // the removed candidates' hostname domains, touched or not (0 pods removed)
     std::vector<std::pair<std::pair<int, int>, int>> hostOnly;
+    auto has = [&](int g, int v) {
+      auto it = std::lower_bound(dec.begin(), dec.end(), std::make_pair(std::make_pair(g, v), INT_MIN));
+      return it != dec.end() && it->first == std::make_pair(g, v);
+    };
     for (int g = 0; g < d.G; g++)
       if (h.groups[(size_t)g].keyId == hostKey)
-        for (int v : goneHosts) {
-          auto it = std::lower_bound(dec.begin(), dec.end(), std::make_pair(std::make_pair(g, v), INT_MIN));
-          if (it == dec.end() || it->first != std::make_pair(g, v)) hostOnly.push_back({{g, v}, 0});
-        }
+        for (int v : goneHosts)
+          if (!has(g, v)) hostOnly.push_back({{g, v}, 0});
+    // (INT_MIN marks a flip entry: its value is derived below)
+    for (int g : flip)
+      for (const Host::Node& n : h.nodes) {
+        auto hv = h.valueId[(size_t)hostKey].find(n.hostName);
+        if (hv == h.valueId[(size_t)hostKey].end() || goneHosts.count(hv->second) || has(g, hv->second)) continue;
+        hostOnly.push_back({{g, hv->second}, INT_MIN});
+      }
     if (!hostOnly.empty()) {
       dec.insert(dec.end(), hostOnly.begin(), hostOnly.end());
       std::sort(dec.begin(), dec.end());
+      dec.erase(std::unique(dec.begin(), dec.end(), [](const auto& x, const auto& y) { return x.first == y.first; }),
+                dec.end());
     }
   }
   std::vector<int32_t> out;
   for (auto& e : dec) {
     const int g = e.first.first, v = e.first.second;
     const bool host = h.groups[(size_t)g].keyId == hostKey;
-    // still registered with no pod: a universe domain, or the hostname of a node the simulation keeps
-    // (a late group never registered the nodes' hostnames: it was created after NewExistingNode)
-    const bool keep = h.topoUniverse[(size_t)g][(size_t)v] ||
-                      (host && !h.groups[(size_t)g].late && h.activeHost(v) && !goneHosts.count(v));
     if (v < 0 || v >= h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_NV])
       throw KsError(KS_ERR_CAPACITY, "topology domain outside its group's value range");
-    out.push_back(h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_CNT] + v);
+    const int32_t off = h.tab.tg_meta[(size_t)g * TGM_WORDS + TGM_CNT] + v;
+    if (e.second == INT_MIN) {  // a node's hostname in a flipped group: registered (0) unless the group is late here
+      const int32_t c0 = h.tab.tg_cnt0[(size_t)off];
+      const bool uni = h.topoUniverse[(size_t)g][(size_t)v];
+      const int32_t want = c0 > 0 ? c0 : (simLate(g) && !uni ? -1 : 0);
+      if (want == c0) continue;
+      // the prologue stores c0 - (x >> 1), or -1 for a zero with bit 0 set
+      out.push_back(off);
+      out.push_back(want < 0 ? (c0 << 1) | 1 : (c0 - want) * 2);
+      continue;
+    }
+    // still registered with no pod: a universe domain, or the hostname of a node the simulation keeps
+    // (a late group never registered the nodes' hostnames: it was created after NewExistingNode)
+    const bool keep = h.topoUniverse[(size_t)g][(size_t)v] || (host && !simLate(g) && h.activeHost(v) && !goneHosts.count(v));
+    out.push_back(off);
     out.push_back((e.second << 1) | (keep ? 0 : 1));
   }
   // inverse groups a simulation pod owns (Topology.Update, topology.go:91-122)
-  std::vector<uint64_t> simOwn((size_t)d.GMW, 0);
+  std::vector<uint64_t> simOwn((size_t)GMW, 0);
   for (int p : simPods)
-    for (int w = 0; w < d.GMW; w++) simOwn[(size_t)w] |= h.tab.pod_ginv[(size_t)p * d.GMW + w];
-  dead.assign((size_t)d.GMW, 0);
+    for (int w = 0; w < GMW; w++) simOwn[(size_t)w] |= h.tab.pod_ginv[(size_t)p * GMW + w];
+  dead.assign((size_t)GMW, 0);
   for (int g = d.G1; g < d.G; g++)
-    if (h.topoInvOwners[(size_t)g] - ownersGone[(size_t)g] <= 0 && !gtest(simOwn, 0, d.GMW, g)) gset(dead, 0, d.GMW, g);
+    if (h.topoInvOwners[(size_t)g] - ownersGone[(size_t)g] <= 0 && !gtest(simOwn, 0, GMW, g)) gset(dead, 0, GMW, g);
   return out;
 }
 
@@ -737,13 +816,13 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   struct Off {
     size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
         last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price, n_hp,
-        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, tdead, n_vslot, n_vc, vlog, vspec;
+        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, tdead, tact, sstart, n_vslot, n_vc, vlog, vspec;
   };
   std::vector<Off> offs(ns);
   std::vector<int> simP(ns), entBeg(ns + 1, 0);
   std::vector<int32_t> entries, entrySim;
   std::vector<std::vector<int32_t>> tdel(ns);
-  std::vector<std::vector<uint64_t>> tdead(ns);
+  std::vector<std::vector<uint64_t>> tdead(ns), tact(ns);
   std::vector<std::vector<int>> simPods(ns);
   parallel_for(ns, 16, [&](int k) {
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
@@ -762,7 +841,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     ptopo.contrib.swap(c.podContrib);
     ptopo.inv.swap(c.podInv);
     parallel_for(ns, 4, [&](int k) {
-      tdel[k] = sim_topology(c, c.sims[(size_t)mine[(size_t)k]], simPods[k], ptopo, tdead[k]);
+      tdel[k] = sim_topology(c, c.sims[(size_t)mine[(size_t)k]], simPods[k], ptopo, tdead[k], tact[k], c.carryStart);
     });
     c.podContrib.swap(ptopo.contrib);
     c.podInv.swap(ptopo.inv);
@@ -823,7 +902,9 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       o.tg_cpos = a.add(4 * (size_t)d.G);
       o.tdel = ai.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
       o.tdead = ai.add(8 * (size_t)d.GMW);
+      o.tact = ai.add(8 * (size_t)d.GMW);
     }
+    if (c.carryStart) o.sstart = ai.add(4 * c.carryStart->size());
   }
   c.L.lnent = (int)entries.size();
   const size_t inBase = a.total;
@@ -1023,6 +1104,12 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       w.ntdel = (int32_t)(tdel[k].size() / 2);
       memcpy(stage.data() + o.tdead, tdead[k].data(), 8 * tdead[k].size());
       w.tdead = (const uint64_t*)(ibase + o.tdead);
+      memcpy(stage.data() + o.tact, tact[k].data(), 8 * tact[k].size());
+      w.tact = (const uint64_t*)(ibase + o.tact);
+    }
+    if (c.carryStart) {
+      memcpy(stage.data() + o.sstart, c.carryStart->data(), 4 * c.carryStart->size());
+      w.sstart = (const int32_t*)(ibase + o.sstart);
     }
     works[k] = w;
   });
@@ -1108,17 +1195,47 @@ struct RecView {
   }
 };
 
-std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool allSims, const RsFn& rsOf,
-                        bool withCandidates = true, const ks_cons_clock* clk = nullptr, bool withSims = true) {
-  const double simS = clk ? clk->sim_seconds : 0.0;
-  const Host& h = c.pb->host;
+// Record invariants (a lost or stale device store becomes a loud error, not a wrong decision): the action
+// agrees with the NodeClaim count (computeConsolidation, consolidation.go:113-194: Delete = none, Replace =
+// exactly one); NewNodeClaims[0]'s options lie in its template's list and number RF_NOPT; filterByPrice's
+// and filterOutSameType's outputs are subsets of their inputs.
+void check_record(const Host& h, const int32_t* r, const std::string& what) {
   const KsDims& d = h.dims;
-  auto rec = [&](int sim) -> const int32_t* { return rv.head(sim); };
+  if (r[RF_ERROR] != KE_OK)
+    throw KsError(r[RF_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
+                  what + " reported kernel error " + std::to_string(r[RF_ERROR]));
+  auto bad = [&](const char* m) { throw KsError(KS_ERR_INTERNAL, what + " record check: " + m); };
+  if (r[RF_ACTION] < CA_NOOP || r[RF_ACTION] > CA_ERROR) bad("action out of range");
+  if (r[RF_NCLAIMS] < 0 || r[RF_HOSTINCR] < r[RF_NCLAIMS]) bad("NodeClaim counts");
+  if (r[RF_ACTION] == CA_DELETE && r[RF_NCLAIMS] != 0) bad("Delete with NodeClaims");
+  if (r[RF_ACTION] == CA_REPLACE && r[RF_NCLAIMS] != 1) bad("Replace without exactly one NodeClaim");
+  if (r[RF_NCLAIMS] == 0) return;
+  if (r[RF_TPL] < 0 || r[RF_TPL] >= d.NTPL) bad("template out of range");
+  const int nIT = (int)h.tpls[(size_t)r[RF_TPL]].its.size();
+  const uint32_t* o = (const uint32_t*)r + RF_HDR;
+  int nopt = 0, nprice = 0, nsame = 0;
+  for (int w = 0; w < d.TW; w++) {
+    const int lo = w * 32;
+    const uint32_t valid = nIT >= lo + 32 ? ~0u : nIT > lo ? (1u << (nIT - lo)) - 1u : 0u;
+    if (o[w] & ~valid) bad("options beyond the template's list");
+    if (o[d.TW + w] & ~o[w]) bad("filterByPrice output not a subset of the options");
+    if (o[2 * d.TW + w] & ~o[d.TW + w]) bad("filterOutSameType output not a subset of filterByPrice's");
+    nopt += __builtin_popcount(o[w]);
+    nprice += __builtin_popcount(o[d.TW + w]);
+    nsame += __builtin_popcount(o[2 * d.TW + w]);
+  }
+  if (nopt != r[RF_NOPT] || nopt == 0) bad("option count");
+  if (nprice != r[RF_NPRICE] || nsame != r[RF_NSAME]) bad("price-filter counts");
+}
+
+// Every gathered record (full records: checked here; headers: k_rec_headers checked them on the device and left
+// its verdict in the two status words).
+void check_records(const ks_cons& c, const RecView& rv) {
   static const char* checkName[] = {"", "action out of range", "NodeClaim counts", "Delete with NodeClaims",
                                     "Replace without exactly one NodeClaim", "template out of range",
                                     "options beyond the template's list", "price filter output not a subset of its input",
                                     "option count", "price-filter counts"};
-  if (!rv.full_) {  // headers: k_rec_headers checked every record on the device
+  if (!rv.full_) {
     const uint64_t* status = (const uint64_t*)(rv.hdr_ + (size_t)RF_HDR * c.sims.size());
     if (status[1] != ~0ull) {
       const int s = (int)(status[1] >> 32), e = (int)(uint32_t)status[1];
@@ -1130,42 +1247,57 @@ std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool all
       throw KsError(KS_ERR_INTERNAL, "simulation " + std::to_string(status[0] >> 32) + " record check (device): " +
                                          (k < 10 ? checkName[k] : "?"));
     }
+    return;
   }
-  for (size_t s = 0; s < c.sims.size() && rv.full_; s++)
-    if (rec((int)s)[RF_ERROR] != KE_OK)
-      throw KsError(rec((int)s)[RF_ERROR] == KE_CLAIM_CAP ? KS_ERR_CAPACITY : KS_ERR_INTERNAL,
-                    "simulation " + std::to_string(s) + " reported kernel error " + std::to_string(rec((int)s)[RF_ERROR]));
-  // Record invariants (a lost or stale device store becomes a loud error, not a wrong decision): the action
-  // agrees with the NodeClaim count (computeConsolidation, consolidation.go:113-194: Delete = none, Replace =
-  // exactly one); NewNodeClaims[0]'s options lie in its template's list and number RF_NOPT; filterByPrice's
-  // and filterOutSameType's outputs are subsets of their inputs.  (Headers only: checked on the device.)
-  for (size_t s = 0; s < c.sims.size() && rv.full_; s++) {
-    const int32_t* r = rec((int)s);
-    auto bad = [&](const char* what) {
-      throw KsError(KS_ERR_INTERNAL, "simulation " + std::to_string(s) + " record check: " + what);
-    };
-    if (r[RF_ACTION] < CA_NOOP || r[RF_ACTION] > CA_ERROR) bad("action out of range");
-    if (r[RF_NCLAIMS] < 0 || r[RF_HOSTINCR] < r[RF_NCLAIMS]) bad("NodeClaim counts");
-    if (r[RF_ACTION] == CA_DELETE && r[RF_NCLAIMS] != 0) bad("Delete with NodeClaims");
-    if (r[RF_ACTION] == CA_REPLACE && r[RF_NCLAIMS] != 1) bad("Replace without exactly one NodeClaim");
-    if (r[RF_NCLAIMS] == 0) continue;
-    if (r[RF_TPL] < 0 || r[RF_TPL] >= d.NTPL) bad("template out of range");
-    const int nIT = (int)h.tpls[(size_t)r[RF_TPL]].its.size();
-    const uint32_t* o = (const uint32_t*)r + RF_HDR;
-    int nopt = 0, nprice = 0, nsame = 0;
-    for (int w = 0; w < d.TW; w++) {
-      const int lo = w * 32;
-      const uint32_t valid = nIT >= lo + 32 ? ~0u : nIT > lo ? (1u << (nIT - lo)) - 1u : 0u;
-      if (o[w] & ~valid) bad("options beyond the template's list");
-      if (o[d.TW + w] & ~o[w]) bad("filterByPrice output not a subset of the options");
-      if (o[2 * d.TW + w] & ~o[d.TW + w]) bad("filterOutSameType output not a subset of filterByPrice's");
-      nopt += __builtin_popcount(o[w]);
-      nprice += __builtin_popcount(o[d.TW + w]);
-      nsame += __builtin_popcount(o[2 * d.TW + w]);
-    }
-    if (nopt != r[RF_NOPT] || nopt == 0) bad("option count");
-    if (nprice != r[RF_NPRICE] || nsame != r[RF_NSAME]) bad("price-filter counts");
+  for (size_t s = 0; s < c.sims.size(); s++) check_record(c.pb->host, rv.head((int)s), "simulation " + std::to_string(s));
+}
+
+// Decode one relaxation-state readback of a simulation (its workspace's pod_map / pod_state, P entries): the
+// states the candidates' pods of prefix [0, mid] were left in become their carried states.
+void carry_states(const ks_cons& c, int mid, const std::vector<int32_t>& podmap, const std::vector<int32_t>& state,
+                  std::vector<int32_t>& cur, std::vector<char>& moved) {
+  const Host& h = c.pb->host;
+  std::vector<char> cand(h.pods.size(), 0);
+  for (int i = 0; i <= mid; i++)
+    for (int p : c.cands[(size_t)i].pods) cand[(size_t)p] = 1;
+  for (size_t i = 0; i < podmap.size(); i++) {
+    const int g = podmap[i];
+    if (g < 0 || (size_t)g >= cand.size() || !cand[(size_t)g]) continue;  // pending / deleting pods: fresh per probe
+    const int s0 = h.tab.pod_state0[(size_t)g];
+    if (state[i] < s0 || state[i] >= s0 + h.tab.pod_nstate[(size_t)g])
+      throw KsError(KS_ERR_INTERNAL, "carried relaxation state outside the pod's chain");
+    cur[(size_t)g] = state[i];
+    moved[(size_t)g] = state[i] != s0;
   }
+}
+
+// One multi-node probe (candidates [0, mid]) in a launch of its own on this GPU, from the relaxation states
+// `start` (null: every pod's first state): its record, NewNodeClaims[0]'s requirements and the states its Solve
+// left the pods in.  The pass's plan and launch come back afterwards (the re-runs keep their own buffers, c.LR).
+void rerun_probe(ks_cons& c, int mid, const std::vector<int32_t>* start, ks_cons::Probe& out,
+                 std::vector<int32_t>& podmap, std::vector<int32_t>& state);
+
+std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool allSims, const RsFn& rsOf,
+                        bool withCandidates = true, const ks_cons_clock* clk = nullptr, bool withSims = true) {
+  const double simS = clk ? clk->sim_seconds : 0.0;
+  const Host& h = c.pb->host;
+  const KsDims& d = h.dims;
+  const ks_cons::Walk& wk = c.walk;
+  // a decision key: a simulation of the pass (>= 0), or -(2 + i) for carry_walk's re-run probe i
+  auto rec = [&](int key) -> const int32_t* { return key >= 0 ? rv.head(key) : wk.probes[(size_t)(-2 - key)].rec.data(); };
+  auto fullOf = [&](int key) -> const int32_t* {
+    return key >= 0 ? rv.full(key) : wk.probes[(size_t)(-2 - key)].rec.data();
+  };
+  auto rsK = [&](int key) -> const uint32_t* { return key >= 0 ? rsOf(key) : wk.probes[(size_t)(-2 - key)].rs.data(); };
+  auto candsOf = [&](int key) {
+    if (key >= 0) return c.sims[(size_t)key].cands;
+    std::vector<int> cs((size_t)wk.probes[(size_t)(-2 - key)].mid + 1);
+    for (size_t i = 0; i < cs.size(); i++) cs[i] = (int)i;
+    return cs;
+  };
+  auto multiOf = [&](int key) { return key < 0 || c.sims[(size_t)key].multi; };
+  check_records(c, rv);
+  if (!wk.valid) throw KsError(KS_ERR_INTERNAL, "decide without the multi-node search (carry_walk)");
   const int n = c.nPass;
   int64_t counter = c.hostnameSeed;
   std::map<int, int64_t> before;  // sim -> hostname counter before it ran
@@ -1184,15 +1316,15 @@ std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool all
   };
   auto simJSON = [&](int sim) {
     const int32_t* r = rec(sim);
-    std::string o = "{\"candidates\":" + candNames(c.sims[(size_t)sim].cands) + ",\"allNonPendingScheduled\":" +
+    std::string o = "{\"candidates\":" + candNames(candsOf(sim)) + ",\"allNonPendingScheduled\":" +
                     ((r[RF_FLAGS] & RB_ALL_SCHEDULED) ? "true" : "false") +
                     ",\"newNodeClaims\":" + std::to_string(r[RF_NCLAIMS]);
     if (r[RF_NCLAIMS] > 0) {
       o += ",\"claim0\":{\"nodePoolName\":";
       ksjson::quote(o, h.tpls[(size_t)r[RF_TPL]].pool);
-      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], rv.full(sim) + RF_HDR));
+      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], fullOf(sim) + RF_HDR));
       o += ",\"requirementsString\":";
-      ksjson::quote(o, h.reqsString(rsOf(sim), before.at(sim) + r[RF_HOST]));
+      ksjson::quote(o, h.reqsString(rsK(sim), before.at(sim) + r[RF_HOST]));
       o += "}";
     }
     // the simulation's own computeConsolidation outcome: action, the replacement's options after
@@ -1200,22 +1332,23 @@ std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool all
     static const char* sact[] = {"no-op", "delete", "replace", "error"};
     o += std::string(",\"action\":\"") + sact[r[RF_ACTION]] + "\"";
     if (r[RF_ACTION] == CA_REPLACE) {
-      o += ",\"priceOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], rv.full(sim) + RF_HDR + d.TW));
-      if (c.sims[(size_t)sim].multi)
-        o += ",\"sameTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], rv.full(sim) + RF_HDR + 2 * d.TW));
+      o += ",\"priceOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], fullOf(sim) + RF_HDR + d.TW));
+      if (multiOf(sim))
+        o += ",\"sameTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], fullOf(sim) + RF_HDR + 2 * d.TW));
     }
     return o + "}";
   };
   // commandJSON: action, candidates, replacement (multi: filterOutSameType's options)
+  constexpr int kNone = -1;
   auto cmdJSON = [&](int sim, bool err) {
-    if (sim < 0) return std::string("{\"action\":\"no-op\",\"candidates\":[]") + (err ? ",\"error\":true}" : "}");
+    if (sim == kNone) return std::string("{\"action\":\"no-op\",\"candidates\":[]") + (err ? ",\"error\":true}" : "}");
     const int32_t* r = rec(sim);
     static const char* act[] = {"no-op", "delete", "replace", "no-op"};
     std::string o = std::string("{\"action\":\"") + act[r[RF_ACTION]] + "\",\"candidates\":" +
-                    (r[RF_ACTION] == CA_NOOP || r[RF_ACTION] == CA_ERROR ? std::string("[]") : candNames(c.sims[(size_t)sim].cands));
+                    (r[RF_ACTION] == CA_NOOP || r[RF_ACTION] == CA_ERROR ? std::string("[]") : candNames(candsOf(sim)));
     if (r[RF_ACTION] == CA_REPLACE) {
-      const bool multi = c.sims[(size_t)sim].multi;
-      const uint32_t* r0 = rsOf(sim);
+      const bool multi = multiOf(sim);
+      const uint32_t* r0 = rsK(sim);
       std::vector<uint32_t> rs(r0, r0 + d.RSW);
       if (r[RF_FLAGS] & RB_NARROWED) {
         std::vector<uint32_t> spot = h.emptyRec();
@@ -1224,7 +1357,7 @@ std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool all
       }
       o += ",\"replacement\":{\"nodePoolName\":";
       ksjson::quote(o, h.tpls[(size_t)r[RF_TPL]].pool);
-      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], rv.full(sim) + RF_HDR + (multi ? 2 : 1) * d.TW));
+      o += ",\"instanceTypeOptions\":" + names_json(h, bits_to_its(h, r[RF_TPL], fullOf(sim) + RF_HDR + (multi ? 2 : 1) * d.TW));
       o += ",\"requirements\":[";
       const uint64_t pr = rs_present(rs.data());
       bool first = true;
@@ -1250,43 +1383,32 @@ std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool all
       snprintf(buf, sizeof buf, ",\"disruptionCost\":%.17g}", c.cands[(size_t)i].cost);
       o += buf;
     }
-  // MultiNodeConsolidation.firstNConsolidationOption: binary search over the prefix length
-  int multiSim = -1;
-  bool multiErr = false;
-  std::set<int> multiRan;
-  if (c.multiHi >= 1) {
-    int lo = 1, hi = c.multiHi;
-    if (allSims)
-      for (int mid = 1; mid <= c.multiHi; mid++) {
-        run(c.sim_of_multi(mid));
-        multiRan.insert(mid);
-      }
-    double now = 0;  // the search's clock; timeout = start + MultiNodeConsolidationTimeoutDuration
-    while (lo <= hi) {
-      if (clk && now > clk->multi_timeout_s) break;  // m.clock.Now().After(timeout): lastSavedCommand
-      now += simS;
-      const int mid = (lo + hi) / 2;
-      const int sim = c.sim_of_multi(mid);
-      run(sim);
-      multiRan.insert(mid);
-      const int32_t* r = rec(sim);
-      if (r[RF_ACTION] == CA_ERROR) {
-        multiErr = true;
-        multiSim = -1;
-        break;
-      }
-      const bool validReplace = r[RF_ACTION] == CA_REPLACE && r[RF_NSAME] > 0;
-      if (validReplace || r[RF_ACTION] == CA_DELETE) {
-        multiSim = sim;
-        lo = mid + 1;
-      } else {
-        hi = mid - 1;
-      }
+  // MultiNodeConsolidation.firstNConsolidationOption: the binary search over the prefix length as carry_walk
+  // resolved it (the pass's simulations, and the probes re-run from carried pod objects)
+  if (allSims)
+    for (int mid = 1; mid <= c.multiHi; mid++) run(c.sim_of_multi(mid));
+  auto keyOf = [&](size_t i) { return wk.probes[i].carried ? -2 - (int)i : wk.probes[i].sim; };
+  for (size_t i = 0; i < wk.probes.size(); i++) run(keyOf(i));
+  const int multiSim = wk.chosen >= 0 ? keyOf((size_t)wk.chosen) : kNone;
+  const bool multiErr = wk.err;
+  std::string multiSims, multiPath;
+  if (withSims) {
+    if (allSims) {  // every prefix's simulation from the pass's (pristine) pods
+      for (int mid = 1; mid <= c.multiHi; mid++) multiSims += (multiSims.empty() ? "" : ",") + simJSON(c.sim_of_multi(mid));
+    } else {  // the probes the reference runs
+      for (size_t i = 0; i < wk.probes.size(); i++) multiSims += (i ? "," : "") + simJSON(keyOf(i));
     }
   }
-  std::string multiSims;
-  if (withSims)
-    for (int mid : multiRan) multiSims += (multiSims.empty() ? "" : ",") + simJSON(c.sim_of_multi(mid));
+  for (size_t i = 0; i < wk.probes.size(); i++) {
+    multiPath += (i ? "," : "") + std::string("{\"mid\":") + std::to_string(wk.probes[i].mid) + ",\"carried\":" +
+                 (wk.probes[i].carried ? "true" : "false");
+    if (withSims) {
+      multiPath += "," + simJSON(keyOf(i)).substr(1);
+    } else {
+      static const char* sact[] = {"no-op", "delete", "replace", "error"};
+      multiPath += std::string(",\"action\":\"") + sact[rec(keyOf(i))[RF_ACTION]] + "\"}";
+    }
+  }
   // SingleNodeConsolidation.ComputeCommand: the first candidate whose simulation yields an action
   int singleSim = -1;
   std::string singleSims;
@@ -1306,7 +1428,8 @@ std::string decide_json(const ks_cons& c, const RecView& rv, int world, bool all
     if (singleSim >= 0 || timedOut || a == CA_ERROR || a == CA_NOOP) continue;
     singleSim = sim;
   }
-  o += "],\"multi\":{\"command\":" + cmdJSON(multiSim, multiErr) + ",\"sims\":[" + multiSims + "]}";
+  o += "],\"multi\":{\"command\":" + cmdJSON(multiSim, multiErr) + ",\"sims\":[" + multiSims + "],\"path\":[" +
+       multiPath + "]}";
   o += ",\"single\":{\"command\":" + cmdJSON(singleSim, false) + ",\"sims\":[" + singleSims + "]}}";
   return o;
 }
@@ -1383,6 +1506,143 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
     if (all > bytes) memset((char*)records + bytes, 0, all - bytes);
   }
   return ms;
+}
+
+void rerun_probe(ks_cons& c, int mid, const std::vector<int32_t>* start, ks_cons::Probe& out,
+                 std::vector<int32_t>& podmap, std::vector<int32_t>& state) {
+  PhaseTimer pt("rerun_probe");
+  std::vector<ks_cons::Sim> one(1);
+  one[0].multi = true;
+  one[0].cands.resize((size_t)mid + 1);
+  for (int i = 0; i <= mid; i++) one[0].cands[(size_t)i] = i;
+  one.swap(c.sims);
+  std::swap(c.L, c.LR);
+  c.L.invalidate();  // a new plan every time (the prefix and the starting states change), the buffers stay
+  c.carryStart = start;
+  auto restore = [&]() {
+    c.carryStart = nullptr;
+    c.L.invalidate();
+    std::swap(c.L, c.LR);
+    c.sims.swap(one);
+  };
+  try {
+    out.rec.assign((size_t)c.recWords, 0);
+    (void)run_sims(c, 0, 1, out.rec.data(), false);
+    check_record(c.pb->host, out.rec.data(), "multi-node probe " + std::to_string(mid) + " (carried)");
+    const KsWork& w = c.L.lhost[0];
+    const int RSW = c.pb->host.dims.RSW;
+    out.rs.clear();
+    if (out.rec[RF_NCLAIMS] > 0) {
+      out.rs.resize((size_t)RSW);
+      HIPCHK(hipMemcpy(out.rs.data(), w.c_rs + (size_t)out.rec[RF_CLAIM] * RSW, 4 * (size_t)RSW, hipMemcpyDeviceToHost));
+    }
+    podmap.resize((size_t)w.P);
+    state.resize((size_t)w.P);
+    if (w.P) {
+      HIPCHK(hipMemcpy(podmap.data(), w.pod_map, 4 * (size_t)w.P, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(state.data(), w.pod_state, 4 * (size_t)w.P, hipMemcpyDeviceToHost));
+    }
+    pt.mark("launch + readback");
+  } catch (...) {
+    restore();
+    throw;
+  }
+  restore();
+}
+
+// firstNConsolidationOption (multinodeconsolidation.go:87-137) over the pass's records, with the reference's pod
+// objects: NewCandidate lists each candidate's pods once per pass (types.go:114-126) and every probe appends
+// those same *v1.Pod pointers to its simulation (helpers.go:102-104); a probe's Solve relaxes them in place
+// (Preferences.Relax, preferences.go:60-147) and nothing deep-copies them, so a pod one probe relaxed starts the
+// next probe in that relaxation state.  (The in-place sort of preferred node-affinity terms, requirements.go:
+// 89-91, and VolumeTopology.Inject's re-appended requirements, volumetopology.go:68-71, leave every requirement
+// set as it was.)  A probe none of whose candidates' pods an earlier probe relaxed is the pass's own simulation
+// of its prefix; one that holds such a pod runs again on this GPU from the carried states (rerun_probe).  A probe
+// whose record says it relaxed a pod (RB_RELAXED) hands its final states on: read back from this handle's
+// workspace when this rank ran it, else from a re-run of it here.  Most passes relax nothing on the search path
+// and launch nothing.
+void carry_walk(ks_cons& c, const RecView& rv, int world, const ks_cons_clock* clk) {
+  ks_cons::Walk& wk = c.walk;
+  if (wk.valid && wk.pass == c.passId && wk.world == world && wk.hasClock == (clk != nullptr) &&
+      (!clk || (wk.clock[0] == clk->multi_timeout_s && wk.clock[1] == clk->single_timeout_s &&
+                wk.clock[2] == clk->sim_seconds)))
+    return;
+  PhaseTimer pt("carry_walk");
+  check_records(c, rv);
+  wk = ks_cons::Walk{};
+  const Host& h = c.pb->host;
+  const int P = (int)h.pods.size();
+  std::vector<int32_t> cur(h.tab.pod_state0.begin(), h.tab.pod_state0.begin() + P);
+  std::vector<char> moved((size_t)P, 0);  // relaxed by an earlier probe
+  std::vector<int32_t> podmap, state;
+  const double simS = clk ? clk->sim_seconds : 0.0;
+  double now = 0;  // the search's clock; timeout = start + MultiNodeConsolidationTimeoutDuration
+  int lo = 1, hi = c.multiHi;
+  while (c.multiHi >= 1 && lo <= hi) {
+    if (clk && now > clk->multi_timeout_s) break;  // m.clock.Now().After(timeout): lastSavedCommand
+    now += simS;
+    ks_cons::Probe pr;
+    pr.mid = (lo + hi) / 2;
+    pr.sim = c.sim_of_multi(pr.mid);
+    for (int i = 0; i <= pr.mid && !pr.carried; i++)
+      for (int p : c.cands[(size_t)i].pods)
+        if (moved[(size_t)p]) {
+          pr.carried = true;
+          break;
+        }
+    const int32_t* r = nullptr;
+    if (pr.carried) {
+      rerun_probe(c, pr.mid, &cur, pr, podmap, state);
+      wk.reruns++;
+      r = pr.rec.data();
+      carry_states(c, pr.mid, podmap, state, cur, moved);
+    } else {
+      r = rv.head(pr.sim);
+      if (r[RF_FLAGS] & RB_RELAXED) {  // the states its Solve left the candidates' pods in
+        int slot = -1;
+        if (c.L.lworld == world && world >= 1 && pr.sim % world == c.L.lrank)
+          for (size_t k = 0; k < c.L.lsims.size() && slot < 0; k++)
+            if (c.L.lsims[k] == pr.sim) slot = (int)k;
+        if (slot >= 0) {
+          const KsWork& w = c.L.lhost[(size_t)slot];
+          podmap.resize((size_t)w.P);
+          state.resize((size_t)w.P);
+          if (w.P) {
+            HIPCHK(hipMemcpy(podmap.data(), w.pod_map, 4 * (size_t)w.P, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(state.data(), w.pod_state, 4 * (size_t)w.P, hipMemcpyDeviceToHost));
+          }
+        } else {  // another rank ran it: the same simulation here
+          ks_cons::Probe tmp;
+          rerun_probe(c, pr.mid, nullptr, tmp, podmap, state);
+          wk.reruns++;
+        }
+        carry_states(c, pr.mid, podmap, state, cur, moved);
+      }
+    }
+    wk.probes.push_back(std::move(pr));
+    if (r[RF_ACTION] == CA_ERROR) {  // getCandidatePrices failed: ComputeCommand returns the error
+      wk.err = true;
+      wk.chosen = -1;
+      break;
+    }
+    const bool validReplace = r[RF_ACTION] == CA_REPLACE && r[RF_NSAME] > 0;
+    if (validReplace || r[RF_ACTION] == CA_DELETE) {  // filterOutSameType left options, or a Delete
+      wk.chosen = (int)wk.probes.size() - 1;
+      lo = wk.probes.back().mid + 1;
+    } else {
+      hi = wk.probes.back().mid - 1;
+    }
+  }
+  wk.valid = true;
+  wk.pass = c.passId;
+  wk.world = world;
+  wk.hasClock = clk != nullptr;
+  if (clk) {
+    wk.clock[0] = clk->multi_timeout_s;
+    wk.clock[1] = clk->single_timeout_s;
+    wk.clock[2] = clk->sim_seconds;
+  }
+  pt.mark("walk");
 }
 
 // Validation.IsValid after its wait (validation.go:68-107) + ValidateCommand (:120-180): the handle
@@ -1466,8 +1726,9 @@ std::string validate_json(ks_cons& c, const Value& cmd) {
 // rows move with StateNode.Available() (allocatable minus pod requests, lhs keys only, resources.go
 // Subtract), a removed node's capacity returns to its pool's limits (provisioner.go:204-296 re-reads them
 // per pass) and the node can take no pod in any simulation.  The candidates and simulations are re-derived
-// (order_candidates).  Refused (KS_ERR_UNSUPPORTED, nothing applied): clusters with topology groups or
-// volume limits (their counts are encoded per pod and node) and pods with host ports.
+// (order_candidates).  Topology clusters move the shared NewTopology counts with the pods (round 5).  Refused
+// (KS_ERR_UNSUPPORTED, nothing applied): clusters with volume limits (their counts are encoded per pod and
+// node), pods with host ports, and a topology update that would leave a group only a relaxation creates.
 void apply_update(ks_cons& c, const Value& delta, bool device) {
   PhaseTimer pt("ks_cons_update");
   ks_problem& pb = *c.pb;
@@ -1582,6 +1843,10 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   }
 
   pt.mark("validate");
+  // From here on the host model is edited in place: any failure (a count that would go below zero, a device
+  // upload) leaves it ahead of HBM or half-applied, so the handle refuses every later call (c.broken) instead of
+  // simulating a mix.
+  try {
   std::set<int> rows;  // node rows to re-derive
   auto move = [&](int n, const PodH& p, int sign) {  // StateNode.Available() after a pod leaves / lands
     Host::Node& hn = h.nodes[(size_t)n];
@@ -1766,7 +2031,6 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   // builds its plan into the previous plan's buffers
   c.invalidate_launch();
   KsDev& D = pb.dev;
-  try {
   if (!rows.empty() || !rm.empty())
     HIPCHK(hipMemcpyAsync((void*)D.n_avail, h.tab.n_avail.data(), 8 * h.tab.n_avail.size(), hipMemcpyHostToDevice,
                           pb.stream));
@@ -1780,11 +2044,11 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     HIPCHK(hipMemcpyAsync((void*)D.pool_rem0, h.tab.pool_rem0.data(), 8 * h.tab.pool_rem0.size(),
                           hipMemcpyHostToDevice, pb.stream));
   HIPCHK(hipStreamSynchronize(pb.stream));
+  pt.mark("upload rows");
   } catch (const std::exception& e) {
     c.broken = e.what();
     throw;
   }
-  pt.mark("upload rows");
 }
 
 // The shared NewTopology state of a topology cluster, keyed by group identity (an FNV-1a digest of the
@@ -1989,7 +2253,8 @@ template <class A> void io(A& a, ks_cons::Sim& x) { io_all(a, x.cands, x.multi);
 template <class A> void io(A& a, ks_cons::CandIn& x) { io_all(a, x.k, x.remaining, x.passOk); }
 }  // namespace ks
 namespace {
-// 03 = round 5 (the embedded problem's format, KSPROB03); 02 = round 4
+// the format version, with the embedded problem's (KSPROBnn): 04 = round 5's final layout (KSPROB04);
+// 03 = round 5's first (KSPROB03); 02 = round 4; 01 = round 3.  Another version is refused (snapshot_check_header).
 constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '4'};
 template <class A> void cons_io(A& a, ks_cons& c) {
   io_all(a, c.cands, c.nPass, c.sims, c.multiHi, c.pending, c.deleting, c.nominated, c.hostnameSeed, c.recWords,
@@ -2141,6 +2406,7 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
     throw KsError(KS_ERR_ARG, "bad argument");
   c->check_usable();
   DeviceGuard guard(c->pb->device, opts);
+  c->passId++;  // (a decision's multi-node search is re-resolved for the new records)
   const double ms = run_sims(*c, rank, world, records, records_on_device != 0);
   if (kernel_ms) *kernel_ms = ms;
   return KS_OK;
@@ -2161,7 +2427,8 @@ int ks_cons_validate(ks_cons* c, const char* command_json, size_t len, const ks_
 
 // The simulations whose NewNodeClaims[0] requirement record the decision output needs, in the order
 // ks_cons_decide consumes them (a dry run of the replay that records every lookup).
-static std::vector<int> needed_sims(const ks_cons& c, const RecView& recs, int world, bool allSims) {
+static std::vector<int> needed_sims(const ks_cons& c, const RecView& recs, int world, bool allSims,
+                                    const ks_cons_clock* clk = nullptr) {
   std::vector<int> need;
   std::set<int> seen;
   std::vector<uint32_t> zero(std::max(c.pb->host.dims.RSW, 1), 0);
@@ -2171,16 +2438,20 @@ static std::vector<int> needed_sims(const ks_cons& c, const RecView& recs, int w
         if (seen.insert(sim).second) need.push_back(sim);
         return zero.data();
       },
-      false);
+      false, clk);
   return need;
 }
 
 int ks_cons_requirement_words(const ks_cons* c) { return c ? c->pb->host.dims.RSW : 0; }
 
-int ks_cons_needed_sims(const ks_cons* c, const void* records, int world, int flags, int32_t* out, int cap) {
+int ks_cons_needed_sims(ks_cons* c, const void* records, int world, int flags, int32_t* out, int cap) {
   API_TRY
   if (!c || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
-  std::vector<int> need = needed_sims(*c, host_records(c, records, world), world, (flags & KS_CONS_ALL_SIMS) != 0);
+  c->check_usable();
+  DeviceGuard guard(c->pb->device, nullptr);
+  const RecView recs = host_records(c, records, world);
+  carry_walk(*c, recs, world, nullptr);
+  std::vector<int> need = needed_sims(*c, recs, world, (flags & KS_CONS_ALL_SIMS) != 0);
   for (int i = 0; i < (int)need.size() && i < cap; i++) out[i] = need[(size_t)i];
   return (int)need.size();
   API_CATCH
@@ -2204,16 +2475,19 @@ int ks_cons_claim_requirements(ks_cons* c, int sim, uint32_t* out) {
   API_CATCH
 }
 
-int ks_cons_decide(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
+int ks_cons_decide(ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
                    char** json_out) {
   return ks_cons_decide_clock(c, records, world, flags, rs_table, nullptr, json_out);
 }
 
-int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
+int ks_cons_decide_clock(ks_cons* c, const void* records, int world, int flags, const uint32_t* rs_table,
                          const ks_cons_clock* clock, char** json_out) {
   API_TRY
   if (!c || !json_out || world < 1) throw KsError(KS_ERR_ARG, "bad argument");
+  c->check_usable();
+  DeviceGuard guard(c->pb->device, nullptr);  // (carried probes run on the handle's GPU)
   const RecView recs = host_records(c, records, world);
+  carry_walk(*c, recs, world, clock);
   const bool all_sims = (flags & KS_CONS_ALL_SIMS) != 0;
   if (!rs_table && world == 1 && c->L.lworld == 1) {
     // One rank ran every simulation: the requirement records the output needs are read from this handle's
@@ -2237,7 +2511,7 @@ int ks_cons_decide_clock(const ks_cons* c, const void* records, int world, int f
                            .c_str());
     return KS_OK;
   }
-  std::vector<int> need = needed_sims(*c, recs, world, all_sims);
+  std::vector<int> need = needed_sims(*c, recs, world, all_sims, clock);
   if (!need.empty() && !rs_table) throw KsError(KS_ERR_ARG, "requirement records of the needed simulations missing");
   std::map<int, const uint32_t*> table;
   for (size_t i = 0; i < need.size(); i++) table[need[i]] = rs_table + i * c->pb->host.dims.RSW;
@@ -2267,6 +2541,8 @@ int ks_cons_sim_counters_n(ks_cons* c, int sim, int64_t* out, int n) {
   throw KsError(KS_ERR_ARG, "simulation not in this rank's launch");
   API_CATCH
 }
+
+int ks_cons_last_reruns(const ks_cons* c) { return c && c->walk.valid ? c->walk.reruns : -1; }
 
 double ks_cons_records_alg_bytes(const ks_cons* c, const void* records, int world) {
   if (!c || world < 1 || (!records && !(world == 1 && c->L.lworld == 1 && (c->L.hdrOnly || c->L.keptFull)))) return 0;

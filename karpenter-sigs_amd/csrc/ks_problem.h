@@ -225,7 +225,9 @@ enum RecField {
   RF_CLAIM,         // claim id of NewNodeClaims[0] in the simulation's workspace (its requirements stay there)
   RF_HDR = 16,      // then: [TW] options, [TW] after filterByPrice, [TW] after filterOutSameType
 };
-enum RecBit { RB_ALL_SCHEDULED = 1, RB_NARROWED = 2, RB_HAS_SPOT = 4, RB_HAS_OD = 8 };
+// RB_RELAXED: Preferences.Relax changed some pod of the simulation (the pod objects a multi-node probe relaxes
+// carry into the next probe, multinodeconsolidation.go:111-114; ks_cons.cpp carry_walk)
+enum RecBit { RB_ALL_SCHEDULED = 1, RB_NARROWED = 2, RB_HAS_SPOT = 4, RB_HAS_OD = 8, RB_RELAXED = 16 };
 KS_HD int rec_words(int TW) { return RF_HDR + 3 * TW; }
 
 // Per-solve workspace (one slice per replica / simulation).
@@ -282,6 +284,11 @@ struct KsWork {
   const int32_t KS_G* tdel;     // [ntdel][2]: tg_cnt offset, (pods removed << 1) | unregister-if-zero
   int32_t ntdel;
   const uint64_t KS_G* tdead;   // [GMW] inverse groups none of whose owners exist in this simulation
+  const uint64_t KS_G* tact;    // [GMW] groups in t.topologies at this simulation's start (those its pods' starting
+                                // states own, and the inverse groups); null: all but tg_late
+  // a multi-node probe re-run from carried pods (ks_cons.cpp carry_walk): per global pod, the relaxation state it
+  // starts in (the state the previous probe left it in); null: every pod starts in pod_state0
+  const int32_t KS_G* sstart;
   // volumes (volA)
   int32_t KS_G* n_vslot;    // SIM: [N] n_vc row of a node whose volume usage changed (valid where s_tvol is set)
   int32_t KS_G* vlog;       // [vLogCap][2] (PVC u, node): PF_VSHARED pods' PVCs a placement mounted on a node

@@ -1157,8 +1157,8 @@ struct Solver {
   // ExistingNode.Add's topology step for node n (one lane each): a node's single domain of each matching group
   // must be the one TopologyGroup.Get returns (existingnode.go:106-114).  0 fails, 1 passes, 2: every labelled
   // group passes, but the node lacks the label of some group's key (its domain then comes from the
-  // requirements it accumulated; node_slow decides).  (A batched form -- all nodes' and groups' loads issued
-  // before any test -- measured slower, DESIGN §3, and is not kept.)
+  // requirements it accumulated; node_slow decides).  The node scan's default, topo_node_stateK, applies these
+  // tests group by group to a lane's KN nodes (their loads issued together); KS_TOPO_SEQ calls this per node.
   __device__ __forceinline__ int topo_node_state1(int n) const {
     int st = 1;
     for (int w = 0; w < d.GMW; w++)
@@ -2407,7 +2407,8 @@ struct Solver {
   // simulateScheduling's post-check (helpers.go:115-124) + computeConsolidation (consolidation.go:
   // 113-194) + filterOutSameType (multinodeconsolidation.go:155-188), into the record W.rec
   // anyPushed: some pod failed an attempt (its status array exists, sim_queue_init); otherwise every pod was placed.
-  __device__ __forceinline__ void sim_record(int P, int nclaims, int hostCtr, bool allSched, int err, bool anyPushed) {
+  __device__ __forceinline__ void sim_record(int P, int nclaims, int hostCtr, bool allSched, int err, bool anyPushed,
+                                             bool anyRelaxed) {
     if (anyPushed) {
       hbm_release();  // pod statuses written by lane 0
       bool bad = false;
@@ -2421,7 +2422,8 @@ struct Solver {
     int32_t KS_G* o_price = o_opt + TW;
     int32_t KS_G* o_same = o_price + TW;
     for (int i = lane(); i < 3 * TW; i += kWave) o_opt[i] = 0;
-    int flags = allSched ? RB_ALL_SCHEDULED : 0, tpl = -1, host = -1, nopt = 0, nprice = 0, nsame = 0;
+    int flags = (allSched ? RB_ALL_SCHEDULED : 0) | (anyRelaxed ? RB_RELAXED : 0), tpl = -1, host = -1, nopt = 0,
+        nprice = 0, nsame = 0;
     int action = CA_NOOP;
     if (nclaims > 0 && err == KE_OK) {
       const int c = uni(s_order[0]);
@@ -2496,7 +2498,7 @@ struct Solver {
   __device__ __forceinline__ void sim_queue_init(int P) {
     for (int i = lane(); i < P; i += kWave) {
       W.queue[i] = i;
-      W.pod_state[i] = D.pod_state0[W.pod_map[i]];
+      W.pod_state[i] = W.sstart ? W.sstart[W.pod_map[i]] : D.pod_state0[W.pod_map[i]];
       W.pod_status[i] = ST_PENDING;
       W.pod_fstate[i] = -1;
       W.last_len[i] = 0;
@@ -2832,7 +2834,21 @@ hipError_t launch_solve_plain(const KsDev& D, const KsWork* w, int n, const Plan
 // One-Solve launches use the whole 160 KiB of a CU; batched simulations pass a smaller budget.
 // wideKO: a Solve that created more NodeClaims than the default plan holds is re-planned with the
 // instance-type tables in HBM and almost all LDS given to claim positions.
+static Plan make_plan_live(const KsDims& d, size_t budget, bool sim, bool wideKO, bool live);
 Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
+  // The live node list serves the non-LEAN Solve instantiations with a register window (RT 3 or 4, launch_family):
+  // a lean problem runs LEAN whenever its instance-type tables fit in LDS (talloc), so its plan reserves the list
+  // only when they do not.
+  const bool rt = d.R == 3 || d.R == 4;
+  if (sim || !rt) return make_plan_live(d, budget, sim, wideKO, false);
+  if (d.lean) {
+    const Plan lean = make_plan_live(d, budget, sim, wideKO, false);
+    if (lean.talloc) return lean;
+  }
+  return make_plan_live(d, budget, sim, wideKO, true);
+}
+
+static Plan make_plan_live(const KsDims& d, size_t budget, bool sim, bool wideKO, bool live) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   Plan pl{};
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
@@ -2863,7 +2879,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   avail = avail > tdlB ? avail - tdlB : 0;
   // a Solve's live node list: the existing nodes past the register window passing Fits for the current
   // request vector (ks_solve_body.inc)
-  pl.livl = !sim && d.N > 0 && !d.negReq && !d.tgUnlab && 4 * (size_t)d.N <= avail / 4 ? d.N : 0;
+  pl.livl = live && d.N > 0 && !d.negReq && !d.tgUnlab && 4 * (size_t)d.N <= avail / 4 ? d.N : 0;
   const size_t livB = r16(4 * (size_t)pl.livl);
   avail = avail > livB ? avail - livB : 0;
   // The threshold filter needs the sorted lists only without negative requests.

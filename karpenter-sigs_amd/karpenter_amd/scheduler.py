@@ -377,6 +377,8 @@ def _cons_lib():
         l.ks_cons_sim_counters_n.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
         l.ks_cons_records_alg_bytes.argtypes = [vp, vp, ctypes.c_int]
         l.ks_cons_records_alg_bytes.restype = ctypes.c_double
+        l.ks_cons_last_reruns.argtypes = [vp]
+        l.ks_cons_last_reruns.restype = ctypes.c_int
         l._cons_ready = True
     return l
 
@@ -539,6 +541,12 @@ class Consolidator:
         if n < 0:
             _check(n)
         return list(out)[:n]
+
+    @property
+    def last_reruns(self):
+        """Multi-node probes the last decide() / needed_sims() re-simulated on this GPU from the pod objects
+        earlier probes relaxed (ks_cons_last_reruns; -1: no decision yet)."""
+        return _cons_lib().ks_cons_last_reruns(self._h)
 
     def alg_bytes(self, records, world=1):
         if records is None:

@@ -1113,6 +1113,7 @@ class Scheduler {
     head_ = 0;
     errors_.assign(pb_.pods.size(), Result{});
     attempted_.assign(pb_.pods.size(), false);
+    relaxCount_.assign(pb_.pods.size(), 0);
     for (;;) {
       int p;
       if (!Pop(p)) break;
@@ -1120,6 +1121,7 @@ class Scheduler {
       errors_[p] = add(p);
       if (errors_[p].ok) continue;
       bool relaxed = Relax(pb_.pods[p]);
+      if (relaxed) relaxCount_[p]++;
       Push(p, relaxed);
       if (relaxed && !pb_.emptyTopology) topo_.Update(pb_.pods[p]);
     }
@@ -1134,6 +1136,9 @@ class Scheduler {
   const vector<ExistingNode>& existingNodes() const { return existing_; }
   bool podError(int p) const { return attempted_[p] && !errors_[p].ok; }
   int64_t nodeIDCounter() const { return nodeID_; }
+  // Relax calls that changed pod p's spec in this Solve (Preferences.Relax mutates the *v1.Pod in place,
+  // preferences.go:38-147; the consolidation restatement carries such pods into the next probe)
+  int relaxCount(int p) const { return relaxCount_[p]; }
 
   long long attempts = 0;  // statistics: NodeClaim.Add calls
   int64_t algBytes() const { return algBytes_; }
@@ -1176,6 +1181,7 @@ class Scheduler {
   map<string, int> lastLen_;
   vector<Result> errors_;
   vector<bool> attempted_;
+  vector<int> relaxCount_;
   vector<ResourceList> reqsCache_;
 
   ResourceList CeilingRequestsFor(int p) { return RequestsForPods({&pb_.pods[p]}); }

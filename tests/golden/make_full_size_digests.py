@@ -28,6 +28,11 @@ deletes, C4 places every pod on an existing node):
 Per config: one digest of the whole canonical Results document (json.dumps with sorted keys and no
 whitespace) and one digest per NewNodeClaim / existing node / simulation, so a mismatch names the
 first differing element.  Re-run: python tests/golden/make_full_size_digests.py [names...]
+
+Round 6 regenerated every config on the current oracle: the consolidation documents gained the multi-node search
+path ("path": each probe with "carried", the pod objects earlier probes relaxed, multinodeconsolidation.go:111-114),
+so their "all" digests changed; the simulations' and commands' digests did not (no probe of C5 / C5R / C5T's
+search holds a pod an earlier probe relaxed: summary.pathCarried 0).
 """
 import hashlib
 import json
@@ -64,11 +69,13 @@ def solve_digest(results):
 def cons_digest(doc):
     """Digests of a consolidation pass with every simulation reported (all_sims)."""
     return {"all": sha(doc), "candidates": sha(doc["candidates"]),
-            "multi": {"command": sha(doc["multi"]["command"]), "sims": [sha(s) for s in doc["multi"]["sims"]]},
+            "multi": {"command": sha(doc["multi"]["command"]), "sims": [sha(s) for s in doc["multi"]["sims"]],
+                      "path": [sha(p) for p in doc["multi"]["path"]]},
             "single": {"command": sha(doc["single"]["command"]), "sims": [sha(s) for s in doc["single"]["sims"]]},
             "summary": {"multi": doc["multi"]["command"]["action"], "single": doc["single"]["command"]["action"],
                         "candidates": len(doc["candidates"]),
-                        "singleActions": _actions(doc["single"]["sims"]), "multiActions": _actions(doc["multi"]["sims"])}}
+                        "singleActions": _actions(doc["single"]["sims"]), "multiActions": _actions(doc["multi"]["sims"]),
+                        "pathCarried": sum(1 for p in doc["multi"]["path"] if p["carried"])}}
 
 
 def _actions(sims):

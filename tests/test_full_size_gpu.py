@@ -94,4 +94,5 @@ def test_c5_every_consolidation_simulation(name):
         for i, (a, b) in enumerate(zip(got[kind]["sims"], want[kind]["sims"])):
             assert a == b, "%s simulation %d (%s) differs from the oracle" % (kind, i, doc[kind]["sims"][i]["candidates"][:3])
         assert got[kind]["command"] == want[kind]["command"], "%s command differs" % kind
+    assert got["multi"]["path"] == want["multi"]["path"], "multi-node search path differs"
     assert got["all"] == want["all"]
