@@ -167,44 +167,22 @@ def consolidation_bench(args, rank, world, local, dist, barrier_sync, topology=0
     import torch
 
     from karpenter_amd import Consolidator, synth
+    from karpenter_amd.sharded import ShardBuffers, sharded_pass
 
     snap = json.dumps(synth.config5(args.cons_nodes) if not topology else
                       synth.cluster_snapshot(args.cons_nodes, 20, 400, seed=4205, topology=topology))
     c, create_ms = _create(Consolidator, snap)
     save_ms, create_bin_ms, snap_bytes = _create_binary(c, Consolidator)
-    per, rb = c.records_per_rank(world), c.record_bytes
     dev = "cuda:%d" % local
-    out = gathered = None
-    if world > 1:
-        out = torch.empty(per * rb, dtype=torch.uint8, device=dev)
-        gathered = torch.empty(world * per * rb, dtype=torch.uint8, device=dev)
+    bufs = ShardBuffers(c, world, dev) if world > 1 else None
 
     def one_pass():
         if world == 1:  # the records stay in the handle's pinned buffer (decide reads them there)
             recs, ms = c.run(0, 1, device=local, keep=True)
-        else:
-            _, ms = c.run(rank, world, device=local, out_ptr=out.data_ptr())
-            dist.all_gather_into_tensor(gathered, out)
-            recs = gathered.cpu().numpy().tobytes()
-        if world == 1:
-            doc = c.decide(recs, 1, candidates=False, sims=False)
-        else:
-            # every rank holds the gathered records, so every rank knows which simulations' NodeClaim
-            # requirements the decision needs; each is broadcast by the rank that ran it
-            need = c.needed_sims(recs, world)
-            rsw = c.requirement_words
-            table = {}
-            if need:  # one collective: each owner fills its rows, zeros elsewhere, summed over the ranks
-                t = torch.zeros(len(need) * rsw, dtype=torch.int32, device=dev)
-                for i, s in enumerate(need):
-                    if s % world == rank:
-                        t[i * rsw:(i + 1) * rsw].copy_(torch.frombuffer(bytearray(c.claim_requirements(s)),
-                                                                        dtype=torch.int32))
-                dist.all_reduce(t)
-                host = t.cpu().numpy()
-                table = {s: host[i * rsw:(i + 1) * rsw].tobytes() for i, s in enumerate(need)}
-            doc = c.decide(recs, world, fetch=table.__getitem__, candidates=False, sims=False) if rank == 0 else None
-        return ms, recs, doc
+            return ms, recs, c.decide(recs, 1, candidates=False, sims=False)
+        # records on the device, all-gathered over RCCL; the needed requirement records in one all_reduce; rank 0
+        # decides (karpenter_amd.sharded: the same function the multi-process GPU tests run)
+        return sharded_pass(c, rank, world, local, bufs)
 
     t0 = time.perf_counter()
     one_pass()  # first pass: includes the launch plan's build and upload (prepare_launch)

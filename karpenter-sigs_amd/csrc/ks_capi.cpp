@@ -936,10 +936,11 @@ int ks_problem_create(const char* json, size_t len, ks_problem** out) {
 // --- binary snapshot (ks_archive.h, ks_snapshot.cpp) ----------------------------------------------------
 extern "C++" {
 namespace {
-// the format version: 04 = round 5's final layout (taint and host-port classes, live resource names, sparse
+// the format version: 05 = round 6 (per relaxation state, the minDomains its spread groups would be created
+// with, PodState::gmd); 04 = round 5's final layout (taint and host-port classes, live resource names, sparse
 // volume tables, injectFailed); 03 = round 5's first (sparse volume tables, injectFailed); 02 = round 4 (group
 // sets); 01 = round 3.  A blob of another version is refused with a version error (snapshot_check_header).
-constexpr char kProblemMagic[8] = {'K', 'S', 'P', 'R', 'O', 'B', '0', '4'};
+constexpr char kProblemMagic[8] = {'K', 'S', 'P', 'R', 'O', 'B', '0', '5'};
 }  // namespace
 
 void snapshot_header(ArOut& a, const char magic[8]) {

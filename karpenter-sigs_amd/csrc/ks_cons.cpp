@@ -20,6 +20,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <exception>
 #include <ctime>
 #include <functional>
 #include <limits>
@@ -688,9 +689,15 @@ PodTopo pod_topo(const Host& h) {
 // pod's first state creates it); a hostname group this simulation creates in the other form gets per-node
 // entries that register (or unregister) those hostnames -- only for groups some relaxation in the simulation can
 // still create, the others are never read.
+// `md` gets this simulation's minDomains overrides (group, value): a spread group takes the minDomains of the
+// pod whose Update creates it (its Hash leaves minDomains out, topologygroup.go:142-158), the first simulation
+// pod, in NewTopology's Update order (the pods list: pending, the candidates', the deleting nodes'), whose
+// starting state owns it; a group only a relaxation creates takes its relaxing pod's (refused when those differ).
+// `altGroups`: the groups some state gives another minDomains (PodState::gmd; empty: nothing to do).
 std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, const std::vector<int>& simPods,
                                   const PodTopo& pt, std::vector<uint64_t>& dead, std::vector<uint64_t>& act,
-                                  const std::vector<int32_t>* start) {
+                                  const std::vector<int32_t>* start, const std::vector<int>& altGroups,
+                                  std::vector<int32_t>& md) {
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
   const int GMW = d.GMW;
@@ -707,6 +714,43 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
   }
   for (int g = d.G1; g < 64 * GMW; g++) act[(size_t)(g >> 6)] |= 1ull << (g & 63);  // inverse groups (and unused bits)
   auto simLate = [&](int g) { return g < d.G1 && !((act[(size_t)(g >> 6)] >> (g & 63)) & 1ull); };
+  md.clear();
+  for (int g : altGroups) {
+    auto owns = [&](int s) { return ((h.tab.st_gown[(size_t)s * GMW + (size_t)(g >> 6)] >> (g & 63)) & 1ull) != 0; };
+    auto mdOf = [&](int p, int s) {  // the minDomains state s of pod p creates group g with
+      for (auto& e : h.states[(size_t)p][(size_t)(s - h.tab.pod_state0[(size_t)p])].gmd)
+        if (e.first == g) return e.second;
+      return h.groups[(size_t)g].minDomains;
+    };
+    int32_t v = INT32_MIN;
+    bool found = false;
+    for (int p : simPods) {  // the creator at NewTopology time
+      const int s = start ? (*start)[(size_t)p] : h.tab.pod_state0[(size_t)p];
+      if (owns(s)) {
+        v = mdOf(p, s);
+        found = true;
+        break;
+      }
+    }
+    if (!found) {  // created by a relaxation, if at all: every possible creator must agree
+      for (int p : simPods) {
+        const int s0 = h.tab.pod_state0[(size_t)p], sEnd = s0 + h.tab.pod_nstate[(size_t)p];
+        for (int k = (start ? (*start)[(size_t)p] : s0) + 1; k < sEnd; k++) {
+          if (!owns(k)) continue;
+          const int32_t x = mdOf(p, k);
+          if (found && x != v)
+            throw KsError(KS_ERR_UNSUPPORTED, "a simulation's topology group is created by relaxations whose spread "
+                                              "constraints differ in minDomains");
+          v = x;
+          found = true;
+        }
+      }
+    }
+    if (found && v != h.groups[(size_t)g].minDomains) {
+      md.push_back(g);
+      md.push_back(v);
+    }
+  }
   std::vector<std::pair<int, int>> touched;  // (group, value) per removed pod's contribution (sorted below)
   std::vector<int> ownersGone((size_t)d.G, 0);
   std::set<int> goneHosts;  // hostname value ids of the removed candidates
@@ -729,13 +773,14 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
     dec.push_back({touched[i], (int)(j - i)});
     i = j;
   }
-  // hostname groups this simulation can create in the other late / initial form than the shared table's
+  // hostname groups this simulation holds in the other late / initial form than the shared table's: created at
+  // its start but late in the table, or late here but not in the table and creatable by one of its relaxations
   std::vector<int> flip;
   if (hostKey >= 0)
-    for (int g = 0; g < d.G1; g++)
-      if (h.groups[(size_t)g].keyId == hostKey && simLate(g) != h.groups[(size_t)g].late &&
-          ((later[(size_t)(g >> 6)] >> (g & 63)) & 1ull))
-        flip.push_back(g);
+    for (int g = 0; g < d.G1; g++) {
+      if (h.groups[(size_t)g].keyId != hostKey || simLate(g) == h.groups[(size_t)g].late) continue;
+      if (!simLate(g) || ((later[(size_t)(g >> 6)] >> (g & 63)) & 1ull)) flip.push_back(g);
+    }
   if (!goneHosts.empty() || !flip.empty()) {  // the removed candidates' hostname domains, touched or not (0 pods removed)
     std::vector<std::pair<std::pair<int, int>, int>> hostOnly;
     auto has = [&](int g, int v) {
@@ -816,13 +861,14 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   struct Off {
     size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, n_slot, queue, pod_state,
         last_len, log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, counters, rm, pool0, st_price, n_hp,
-        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, tdead, tact, sstart, n_vslot, n_vc, vlog, vspec;
+        c_hp, tg_cnt, tg_ccnt, tg_cpos, tdel, tdead, tact, tmd, sstart, n_vslot, n_vc, vlog, vspec;
   };
   std::vector<Off> offs(ns);
   std::vector<int> simP(ns), entBeg(ns + 1, 0);
   std::vector<int32_t> entries, entrySim;
   std::vector<std::vector<int32_t>> tdel(ns);
   std::vector<std::vector<uint64_t>> tdead(ns), tact(ns);
+  std::vector<std::vector<int32_t>> tmd(ns);
   std::vector<std::vector<int>> simPods(ns);
   parallel_for(ns, 16, [&](int k) {
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
@@ -840,9 +886,30 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     PodTopo ptopo;
     ptopo.contrib.swap(c.podContrib);
     ptopo.inv.swap(c.podInv);
+    std::vector<int> altGroups;  // groups some relaxation state creates with another minDomains
+    {
+      std::vector<char> alt((size_t)d.G, 0);
+      for (auto& chain : h.states)
+        for (auto& st : chain)
+          for (auto& e : st.gmd) alt[(size_t)e.first] = 1;
+      for (int g = 0; g < d.G; g++)
+        if (alt[(size_t)g]) altGroups.push_back(g);
+    }
+    std::vector<std::exception_ptr> err((size_t)ns);
     parallel_for(ns, 4, [&](int k) {
-      tdel[k] = sim_topology(c, c.sims[(size_t)mine[(size_t)k]], simPods[k], ptopo, tdead[k], tact[k], c.carryStart);
+      try {
+        tdel[k] = sim_topology(c, c.sims[(size_t)mine[(size_t)k]], simPods[k], ptopo, tdead[k], tact[k], c.carryStart,
+                               altGroups, tmd[k]);
+      } catch (...) {
+        err[(size_t)k] = std::current_exception();
+      }
     });
+    for (auto& e : err)
+      if (e) {
+        c.podContrib.swap(ptopo.contrib);
+        c.podInv.swap(ptopo.inv);
+        std::rethrow_exception(e);
+      }
     c.podContrib.swap(ptopo.contrib);
     c.podInv.swap(ptopo.inv);
   }
@@ -903,6 +970,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       o.tdel = ai.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
       o.tdead = ai.add(8 * (size_t)d.GMW);
       o.tact = ai.add(8 * (size_t)d.GMW);
+      o.tmd = ai.add(4 * std::max<size_t>(tmd[k].size(), 1));
     }
     if (c.carryStart) o.sstart = ai.add(4 * c.carryStart->size());
   }
@@ -995,6 +1063,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     }
   }
   std::vector<KsWork> works(ns);
+  const bool noTact = std::getenv("KS_NO_TACT") != nullptr;
   parallel_for(ns, 64, [&](int k) {  // independent per simulation (each writes its own stage slices and work)
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
     const Off& o = offs[k];
@@ -1105,7 +1174,11 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       memcpy(stage.data() + o.tdead, tdead[k].data(), 8 * tdead[k].size());
       w.tdead = (const uint64_t*)(ibase + o.tdead);
       memcpy(stage.data() + o.tact, tact[k].data(), 8 * tact[k].size());
-      w.tact = (const uint64_t*)(ibase + o.tact);
+      // (KS_NO_TACT: every group but the problem's late ones active at the start, round 5's form; diagnostics)
+      w.tact = noTact ? nullptr : (const uint64_t*)(ibase + o.tact);
+      if (!tmd[k].empty()) memcpy(stage.data() + o.tmd, tmd[k].data(), 4 * tmd[k].size());
+      w.tmd = (const int32_t*)(ibase + o.tmd);
+      w.ntmd = (int32_t)(tmd[k].size() / 2);
     }
     if (c.carryStart) {
       memcpy(stage.data() + o.sstart, c.carryStart->data(), 4 * c.carryStart->size());
@@ -1728,7 +1801,7 @@ std::string validate_json(ks_cons& c, const Value& cmd) {
 // per pass) and the node can take no pod in any simulation.  The candidates and simulations are re-derived
 // (order_candidates).  Topology clusters move the shared NewTopology counts with the pods (round 5).  Refused
 // (KS_ERR_UNSUPPORTED, nothing applied): clusters with volume limits (their counts are encoded per pod and
-// node), pods with host ports, and a topology update that would leave a group only a relaxation creates.
+// node) and pods with host ports.
 void apply_update(ks_cons& c, const Value& delta, bool device) {
   PhaseTimer pt("ks_cons_update");
   ks_problem& pb = *c.pb;
@@ -1798,6 +1871,7 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   std::vector<std::vector<std::pair<int, int>>> bindContrib(bind.size());
   std::vector<std::vector<int32_t>> bindInv(bind.size());
   std::map<int32_t, int> topoLeave, topoLeaveLate;  // owner counts to take away once the update applies
+  std::vector<int> toLate;                          // groups only relaxations create from now on
   if (d.G) {
     for (size_t i = 0; i < bind.size(); i++) {
       PodH cp = h.pods[(size_t)bind[i]];
@@ -1808,8 +1882,10 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
                                               " counts in a topology domain or inverse group the handle does not hold");
     }
     // A group that a leaving pod's first state creates and that remaining pods own only in later relaxation
-    // states would be a late group (created mid-Solve, ks_topo.cpp) in a fresh build: refused.  Per-group
-    // owner counts over the remaining pods (built once) make the test proportional to the leaving pods.
+    // states is a late group (created mid-Solve, ks_topo.cpp) in a fresh build: it becomes one here (toLate,
+    // applied below).  (The simulations do not depend on it: each starts with the groups its own pods' starting
+    // states create, sim_topology.)  Per-group owner counts over the remaining pods (built once) make the test
+    // proportional to the leaving pods.
     auto lateOnly = [&](int p, std::vector<int32_t>& out) { late_only_groups(h, p, out); };
     if (!c.topoIndexed) topo_index(c);
     std::set<int> rmSet(rm.begin(), rm.end());
@@ -1834,9 +1910,7 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     for (auto& e : d0) {
       const int g = e.first;
       const int own0 = c.gOwn0[(size_t)g] - e.second, late = c.gOwnLate[(size_t)g] - (dl.count(g) ? dl[g] : 0);
-      if (own0 <= 0 && late > 0)
-        throw KsError(KS_ERR_UNSUPPORTED, "update: topology group " + std::to_string(g) +
-                                              " would only be created by a relaxation (rebuild the handle)");
+      if (own0 <= 0 && late > 0 && !h.groups[(size_t)g].late) toLate.push_back(g);
     }
     topoLeave.swap(d0);
     topoLeaveLate.swap(dl);
@@ -2010,6 +2084,18 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
         if (h.groups[(size_t)g].keyId == hostKey && cnt(g, hv->second) == 0 && !keep(g, hv->second))
           cnt(g, hv->second) = -1;
     }
+    // a group now late: as a fresh build makes it, its domains are the universe's and the counted ones (no
+    // NewExistingNode hostname registration, existingnode.go:60, ran after it)
+    for (int g : toLate) {
+      h.groups[(size_t)g].late = true;
+      gset(h.tab.tg_late, 0, d.GMW, g);
+      if (h.groups[(size_t)g].keyId != hostKey) continue;
+      for (const Host::Node& hn : h.nodes) {
+        auto hv = h.valueId[(size_t)hostKey].find(hn.hostName);
+        if (hv != h.valueId[(size_t)hostKey].end() && cnt(g, hv->second) == 0 && !keep(g, hv->second))
+          cnt(g, hv->second) = -1;
+      }
+    }
   }
   for (int n : rows) {
     int64_t* row = &h.tab.n_avail[(size_t)n * R];
@@ -2039,6 +2125,9 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
                           hipMemcpyHostToDevice, pb.stream));
   if (d.G && (!del.empty() || !bind.empty() || !rm.empty()))
     HIPCHK(hipMemcpyAsync((void*)D.tg_cnt0, h.tab.tg_cnt0.data(), 4 * h.tab.tg_cnt0.size(), hipMemcpyHostToDevice,
+                          pb.stream));
+  if (!toLate.empty())
+    HIPCHK(hipMemcpyAsync((void*)D.tg_late, h.tab.tg_late.data(), 8 * h.tab.tg_late.size(), hipMemcpyHostToDevice,
                           pb.stream));
   if (pools)
     HIPCHK(hipMemcpyAsync((void*)D.pool_rem0, h.tab.pool_rem0.data(), 8 * h.tab.pool_rem0.size(),
@@ -2253,9 +2342,10 @@ template <class A> void io(A& a, ks_cons::Sim& x) { io_all(a, x.cands, x.multi);
 template <class A> void io(A& a, ks_cons::CandIn& x) { io_all(a, x.k, x.remaining, x.passOk); }
 }  // namespace ks
 namespace {
-// the format version, with the embedded problem's (KSPROBnn): 04 = round 5's final layout (KSPROB04);
+// the format version, with the embedded problem's (KSPROBnn): 05 = round 6 (KSPROB05); 04 = round 5's final
+// layout (KSPROB04);
 // 03 = round 5's first (KSPROB03); 02 = round 4; 01 = round 3.  Another version is refused (snapshot_check_header).
-constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '4'};
+constexpr char kConsMagic[8] = {'K', 'S', 'C', 'O', 'N', 'S', '0', '5'};
 template <class A> void cons_io(A& a, ks_cons& c) {
   io_all(a, c.cands, c.nPass, c.sims, c.multiHi, c.pending, c.deleting, c.nominated, c.hostnameSeed, c.recWords,
          c.candIn, c.nodePods, c.podNode, c.podBlock, c.podCost, c.nodeGone, c.updates);

@@ -81,6 +81,10 @@ struct PodState {  // one point of the relaxation chain
   bool hasPreferred = false;
   std::vector<TolH> tols;
   std::vector<int32_t> gown;  // topology groups the pod owns in this state (Topology.Update, topology.go:91-122)
+  // (group, minDomains) of this state's spread constraints whose minDomains differs from the group's: a group's
+  // Hash leaves minDomains out (topologygroup.go:142-158), so a group takes the minDomains of the pod whose
+  // Update creates it (topology.go:108-118), which depends on which pods a Solve / simulation holds
+  std::vector<std::pair<int32_t, int32_t>> gmd;
   std::shared_ptr<PodH> spec;  // the (relaxed) pod spec of this state, kept for topology pods only
 };
 

@@ -289,6 +289,10 @@ struct KsWork {
   // a multi-node probe re-run from carried pods (ks_cons.cpp carry_walk): per global pod, the relaxation state it
   // starts in (the state the previous probe left it in); null: every pod starts in pod_state0
   const int32_t KS_G* sstart;
+  // (group, minDomains) pairs: this simulation's spread groups whose creating pod (its first pod, in NewTopology's
+  // Update order, whose starting state owns the group) gives another minDomains than the shared meta row's
+  const int32_t KS_G* tmd;
+  int32_t ntmd;
   // volumes (volA)
   int32_t KS_G* n_vslot;    // SIM: [N] n_vc row of a node whose volume usage changed (valid where s_tvol is set)
   int32_t KS_G* vlog;       // [vLogCap][2] (PVC u, node): PF_VSHARED pods' PVCs a placement mounted on a node

@@ -27,7 +27,7 @@ template <class A> void io(A& a, PodH& x) {
          x.notReady, x.priority);
 }
 // (rsAll / rsStrict are the rows tab.st_rs / tab.st_rss already hold: restored from them after a load)
-template <class A> void io(A& a, PodState& x) { io_all(a, x.hasPreferred, x.tols, x.gown, x.spec); }
+template <class A> void io(A& a, PodState& x) { io_all(a, x.hasPreferred, x.tols, x.gown, x.gmd, x.spec); }
 template <class A> void io(A& a, TopoGroup& x) {
   io_all(a, x.type, x.key, x.hash, x.keyId, x.maxSkew, x.minDomains, x.namespaces, x.sel, x.filterNil, x.filter, x.domains,
          x.late);
@@ -322,7 +322,7 @@ static_assert(sizeof(Host::Node) == 456, "Host::Node changed: update io(Host::No
 static_assert(sizeof(Host::Tpl) == 280, "Host::Tpl changed: update io(Host::Tpl)");
 static_assert(sizeof(Host::IT) == 224, "Host::IT changed: update io(Host::IT)");
 static_assert(sizeof(TopoGroup) == 256, "TopoGroup changed: update io(TopoGroup)");
-static_assert(sizeof(PodState) == 120, "PodState changed: update io(PodState)");
+static_assert(sizeof(PodState) == 144, "PodState changed: update io(PodState)");
 static_assert(sizeof(Host) == 3000, "Host changed: update host_io");
 static_assert(sizeof(HostPortH) == 88 && sizeof(AffTerm) == 128 && sizeof(SpreadC) == 104 && sizeof(LabelSel) == 32,
               "a pod-spec type changed: update its io()");

@@ -276,6 +276,12 @@ void Host::buildTopology() {
     }
   };
   auto antiGroups = [&](const PodH& p) { return anti_groups(*this, p); };
+  // a state's first constraint of each group sets the minDomains its Update would create the group with; those
+  // differing from the group's (the whole problem's first creator's) are kept per state (PodState::gmd)
+  auto noteMd = [&](const std::vector<int32_t>& seen, std::vector<std::pair<int32_t, int32_t>>& gmd, int idx, int32_t md) {
+    if (std::find(seen.begin(), seen.end(), idx) != seen.end()) return;
+    if (md != own[(size_t)idx].minDomains) gmd.push_back({idx, md});
+  };
   auto inverseAnti = [&](const PodH& p, std::vector<TopoGroup> gs, const std::map<std::string, std::string>* labels,
                          bool cluster) {
     std::vector<int32_t> owned;  // updateInverseAntiAffinity (topology.go:207-232): inverse group indices
@@ -344,6 +350,7 @@ void Host::buildTopology() {
     if (!sp || injFailed(p)) continue;
     if (podHasAnti[(size_t)p]) invOwned[(size_t)p] = inverseAnti(*sp, std::move(podAnti[(size_t)p]), nullptr, false);
     std::vector<int32_t> gown;
+    std::vector<std::pair<int32_t, int32_t>> gmd;
     for (auto& g : podOwn[(size_t)p]) {
       auto it = ownByHash.find(g.hash);
       int idx;
@@ -356,11 +363,13 @@ void Host::buildTopology() {
       } else {
         idx = it->second;
       }
+      noteMd(gown, gmd, idx, g.minDomains);
       gown.push_back(idx);
     }
     std::sort(gown.begin(), gown.end());
     gown.erase(std::unique(gown.begin(), gown.end()), gown.end());
     states[(size_t)p][0].gown = std::move(gown);
+    states[(size_t)p][0].gmd = std::move(gmd);
   }
   pt.mark("pods' groups + countDomains");
   std::vector<int32_t> late;
@@ -369,6 +378,7 @@ void Host::buildTopology() {
       PodState& st = states[(size_t)p][k];
       if (!st.spec) continue;
       std::vector<int32_t> gown;
+      std::vector<std::pair<int32_t, int32_t>> gmd;
       for (auto& g : ownedSpecGroups(*st.spec)) {
         auto it = ownByHash.find(g.hash);
         int idx;
@@ -383,12 +393,20 @@ void Host::buildTopology() {
         } else {
           idx = it->second;
         }
+        noteMd(gown, gmd, idx, g.minDomains);
         gown.push_back(idx);
       }
       std::sort(gown.begin(), gown.end());
       gown.erase(std::unique(gown.begin(), gown.end()), gown.end());
       st.gown = std::move(gown);
+      st.gmd = std::move(gmd);
     }
+  for (int p = 0; p < P; p++)
+    for (size_t k = 1; k < states[(size_t)p].size(); k++)
+      for (auto& gm : states[(size_t)p][k].gmd)
+        if (own[(size_t)gm.first].late)
+          throw KsError(-2, "topology group created by relaxations whose spread constraints differ in minDomains "
+                            "(the group's minDomains would depend on which relaxation runs first)");
   pt.mark("relaxation states' groups");
   // Group sets are GMW-word bitsets on the device (no 64-group limit); the group index rides in bits 16..31
   // of a topology failure code (FC_TOPO), and the group table must fit the LDS plan (make_plan refuses it

@@ -212,15 +212,16 @@ def test_update_then_validate_gpu(seed):
         assert got == want, cmd
 
 
-def test_topology_update_refuses_a_group_only_a_relaxation_would_create():
+def _late_snap():
     """Pod A's first state owns a zonal spread group whose node filter is term T2; pod B's first state has
     required node-affinity terms [T1, T2] (another group), and its relaxation (removeRequiredNodeAffinityTerm,
-    preferences.go) leaves [T2]: A's group.  Deleting A leaves that group owned only by B's relaxed state, a
-    group a fresh build would create mid-Solve (late): the update is refused whole; deleting B is fine."""
+    preferences.go:75-89) leaves [T2]: A's group."""
     snap = synth.cluster_snapshot(n_nodes=6, pods_per_node=3, n_its=40, seed=5, n_pending=2)
     t1 = {"matchExpressions": [{"key": "kubernetes.io/arch", "operator": "In", "values": ["arm64"]}]}
     t2 = {"matchExpressions": [{"key": "kubernetes.io/os", "operator": "In", "values": ["linux"]}]}
     spread = [{"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "DoNotSchedule",
+               "labelSelector": {"matchLabels": {"app": "x"}}},
+              {"maxSkew": 1, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "DoNotSchedule",
                "labelSelector": {"matchLabels": {"app": "x"}}}]
     a, b = snap["stateNodes"][0]["pods"][0], snap["stateNodes"][1]["pods"][0]
     for p, terms in ((a, [t2]), (b, [t1, t2])):
@@ -229,12 +230,32 @@ def test_topology_update_refuses_a_group_only_a_relaxation_would_create():
         p["spec"]["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
             "nodeSelectorTerms": terms}}}
     snap["clusterPods"] = [p for n in snap["stateNodes"] for p in n["pods"]]
+    return snap, a, b
+
+
+def test_topology_update_turns_a_group_late():
+    """Deleting A leaves A's groups owned only by B's relaxed state: a fresh build of the edited cluster creates
+    them mid-Solve (late: no node hostname registered).  The update turns them late the same way (round 5
+    refused it); deleting B instead changes no group's form."""
+    snap, a, b = _late_snap()
     base = inspect_consolidation_update(json.dumps(snap))
-    assert base["groups"] >= 2
-    with pytest.raises(KsError) as e:
-        inspect_consolidation_update(json.dumps(snap), {"deletePods": [a["metadata"]["uid"]]})
-    assert "KS_ERR_UNSUPPORTED" in str(e.value) and "relaxation" in str(e.value)
-    d = {"deletePods": [b["metadata"]["uid"]]}
-    got = inspect_consolidation_update(json.dumps(snap), d)
-    want = inspect_consolidation_update(json.dumps(apply_delta(snap, d)))
-    assert _owned_topology(got) == _owned_topology(want)
+    assert base["groups"] >= 4
+    for p in (a, b):
+        d = {"deletePods": [p["metadata"]["uid"]]}
+        got = inspect_consolidation_update(json.dumps(snap), d)
+        want = inspect_consolidation_update(json.dumps(apply_delta(snap, d)))
+        assert _owned_topology(got) == _owned_topology(want)
+        if p is a:
+            assert any(late for late, _ in _owned_topology(want).values())
+
+
+@pytest.mark.gpu
+def test_topology_update_turns_a_group_late_gpu():
+    snap, a, _ = _late_snap()
+    d = {"deletePods": [a["metadata"]["uid"]]}
+    c = Consolidator(json.dumps(snap))
+    c.update(d)
+    want, _ = bridge.consolidate(json.dumps(apply_delta(snap, d)), all_sims=True)
+    got = c.consolidate(all_sims=True)
+    got.pop("kernel_ms")
+    assert got == want

@@ -169,11 +169,11 @@ def test_create_binary_rejects_flipped_dims():
 
 
 def test_binary_snapshot_version_mismatch_is_named():
-    """a blob of an older format version (KSPROB01 / 02 / 03) is refused as a version mismatch,
+    """a blob of an older format version (KSPROB01 / 02 / 03 / 04) is refused as a version mismatch,
     not as an inconsistent table."""
     blob = encode_binary(json.dumps(problems.random_problem(3)))
-    assert blob[:8] == b"KSPROB04"
-    for old in (b"KSPROB01", b"KSPROB02", b"KSPROB03"):
+    assert blob[:8] == b"KSPROB05"
+    for old in (b"KSPROB01", b"KSPROB02", b"KSPROB03", b"KSPROB04"):
         with pytest.raises(KsError) as e:
             check_binary(old + blob[8:])
         assert e.value.code == KS_ERR_PARSE and "format version" in str(e.value), str(e.value)
