@@ -1249,7 +1249,8 @@ int ks_results_json(const ks_results* r, char** json_out) {
                                 "sorts", "sortsWithDescent", "claimFull", "claimQuickFail", "windows",
                                 "cycPop", "cycNodes", "cycSort", "cycQuick", "cycFull", "cycCommit", "cycTemplates",
                                 "cycTotal", "cycNodeCommit", "cycFullRs", "cycFullThr", "cycFullMasks", "cycFullApply",
-                                "runs", "runPods", "sortsExact"};
+                                "runs", "runPods", "sortsExact", "fineTopoPop", "fineState", "fineRefill",
+                                "fineWindowTests", "fineWindowBlocks", "fineRecord", "fineNodeCommit", "fineWindowTopo"};
   for (int i = 0; i < CT_NCOUNTERS; i++) o += std::string(i ? "," : "") + "\"" + names[i] + "\":" + std::to_string(r->counters[i]);
   o += "}}";
   *json_out = strdup(o.c_str());

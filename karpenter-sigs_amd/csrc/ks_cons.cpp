@@ -523,10 +523,9 @@ void build_cons(ks_cons& c, const Value& rootIn) {
   const std::vector<PodH>& podH = h.pods;
   pt.mark("Host::build");
   if (h.dims.dupUids) throw KsError(KS_ERR_UNSUPPORTED, "consolidation snapshot has duplicate pod UIDs");
-  // a pod whose VolumeTopology.Inject fails stays out of every simulation's NewTopology pod list
-  // (provisioner.go:432-442), which the per-simulation count offsets do not model
-  if (h.dims.G && std::find(h.injectFailed.begin(), h.injectFailed.end(), 1) != h.injectFailed.end())
-    throw KsError(KS_ERR_UNSUPPORTED, "consolidation with topology groups: a pod's volume topology injection failed");
+  // (a pod whose VolumeTopology.Inject fails stays out of every simulation's NewTopology pod list,
+  // provisioner.go:432-442: it is not excluded from the counts, ks_topo.cpp, and sim_topology leaves its
+  // contributions in place when its node is a candidate)
   c.hostnameSeed = h.hostnameSeed;
   std::map<std::string, int> hostNode;  // node name -> host.nodes index (sorted order)
   for (size_t i = 0; i < h.nodes.size(); i++) hostNode[h.nodes[i].name] = (int)i;
@@ -754,9 +753,13 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
   std::vector<std::pair<int, int>> touched;  // (group, value) per removed pod's contribution (sorted below)
   std::vector<int> ownersGone((size_t)d.G, 0);
   std::set<int> goneHosts;  // hostname value ids of the removed candidates
+  const bool anyInjFailed = std::find(h.injectFailed.begin(), h.injectFailed.end(), 1) != h.injectFailed.end();
   for (int ci : sm.cands) {
     const ks_cons::Cand& k = c.cands[(size_t)ci];
     for (int p : k.pods) {
+      // NewTopology excludes the pods it receives: not one whose volume injection failed (provisioner.go:432-442),
+      // which stays counted where it is bound
+      if (anyInjFailed && (size_t)p < h.injectFailed.size() && h.injectFailed[(size_t)p]) continue;
       if (const auto* ct = pt.contrib[(size_t)p]) touched.insert(touched.end(), ct->begin(), ct->end());
       if (const auto* io = pt.inv[(size_t)p])
         for (int32_t g : *io) ownersGone[(size_t)g]++;
@@ -1645,8 +1648,16 @@ void carry_walk(ks_cons& c, const RecView& rv, int world, const ks_cons_clock* c
   wk = ks_cons::Walk{};
   const Host& h = c.pb->host;
   const int P = (int)h.pods.size();
-  std::vector<int32_t> cur(h.tab.pod_state0.begin(), h.tab.pod_state0.begin() + P);
-  std::vector<char> moved((size_t)P, 0);  // relaxed by an earlier probe
+  // the carried relaxation state per pod and whether an earlier probe relaxed it; built at the first relaxation
+  // on the path (most passes have none: no per-pass work proportional to the pods)
+  std::vector<int32_t> cur;
+  std::vector<char> moved;
+  auto carrying = [&]() {
+    if (cur.empty()) {
+      cur.assign(h.tab.pod_state0.begin(), h.tab.pod_state0.begin() + P);
+      moved.assign((size_t)P, 0);
+    }
+  };
   std::vector<int32_t> podmap, state;
   const double simS = clk ? clk->sim_seconds : 0.0;
   double now = 0;  // the search's clock; timeout = start + MultiNodeConsolidationTimeoutDuration
@@ -1657,7 +1668,7 @@ void carry_walk(ks_cons& c, const RecView& rv, int world, const ks_cons_clock* c
     ks_cons::Probe pr;
     pr.mid = (lo + hi) / 2;
     pr.sim = c.sim_of_multi(pr.mid);
-    for (int i = 0; i <= pr.mid && !pr.carried; i++)
+    for (int i = 0; i <= pr.mid && !pr.carried && !moved.empty(); i++)
       for (int p : c.cands[(size_t)i].pods)
         if (moved[(size_t)p]) {
           pr.carried = true;
@@ -1689,6 +1700,7 @@ void carry_walk(ks_cons& c, const RecView& rv, int world, const ks_cons_clock* c
           rerun_probe(c, pr.mid, nullptr, tmp, podmap, state);
           wk.reruns++;
         }
+        carrying();
         carry_states(c, pr.mid, podmap, state, cur, moved);
       }
     }

@@ -310,7 +310,9 @@ enum Counter {
   CT_RUNS = 24,    // runs of identical pods placed in one step (simulation fast path; Solve NodeClaim runs)
   CT_RUN_PODS,     // pods those runs placed
   CT_SORT_EXACT,   // claim re-sorts that ran the lane-0 pdqsort (not the wave-parallel partialInsertionSort)
-  CT_NCOUNTERS = 27
+  CT_FINE,         // [8] diagnostic build: topo_pop, state record, window refill, window-block tests, window blocks
+                   // tested (count), Topology.Record, simulation node commit, window-block tests' topology share
+  CT_NCOUNTERS = 35
 };
 // KE_LEAN_EXIT: a LEAN Solve of pods sharing a UID met its first push-back (the host re-runs it non-LEAN)
 enum KernelError { KE_OK = 0, KE_CLAIM_CAP = 1, KE_ITER_CAP = 2, KE_STACK = 3, KE_LEAN_EXIT = 4 };

@@ -186,11 +186,13 @@ __device__ __forceinline__ void lds_copy(T KS_L* dst, const T KS_G* src, int n) 
 #define PH_END(v, slot) cyc[slot] += __builtin_amdgcn_s_memtime() - v
 #define PHS_END(v, slot) scyc[slot] += __builtin_amdgcn_s_memtime() - v  // sub-phases (Solver member)
 #define SPHS_END(o, v, slot) o.scyc[slot] += __builtin_amdgcn_s_memtime() - v  // (from k_solve)
+#define FPH_END(v, slot) fcyc[slot] += __builtin_amdgcn_s_memtime() - v  // fine phases (k_solve, CT_FINE)
 #else
 #define PH_BEGIN(v)
 #define PH_END(v, slot)
 #define PHS_END(v, slot)
 #define SPHS_END(o, v, slot)
+#define FPH_END(v, slot)
 #endif
 
 // ------------------------------------------------------------------------------------------------

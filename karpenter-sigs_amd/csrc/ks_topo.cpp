@@ -211,11 +211,18 @@ void Host::buildTopology() {
 
   pt.mark("universe");
   // --- groups
+  // NewTopology's excludedPods: the UIDs of the pods it receives, which leaves out those whose injection failed
+  // (provisioner.go:432-442).  The consolidation view excludes only the pods every simulation schedules (pending,
+  // deleting nodes'); each simulation then takes its candidates' counted pods out (ks_cons.cpp sim_topology).
   std::set<std::string> excluded;
-  if (topoExcluded) excluded = *topoExcluded;
-  else
+  if (topoExcluded) {
+    excluded = *topoExcluded;
+    for (int p = 0; p < P; p++)
+      if (injFailed(p)) excluded.erase(pods[(size_t)p].uid);
+  } else {
     for (int p = 0; p < P; p++)
       if (!injFailed(p)) excluded.insert(pods[(size_t)p].uid);
+  }
   topoContrib.clear();
   topoInvOwner.clear();
   // (group index, domain) per counted cluster pod, resolved to value ids once the groups are final

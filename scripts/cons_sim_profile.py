@@ -14,7 +14,8 @@ from karpenter_amd import Consolidator, synth  # noqa: E402
 
 NAMES = ["nclaims", "ncommits", "hostCtr", "error", "pops", "algBytes", "sorts", "sortSlow", "claimFull",
          "quickFail", "windows", "cycPop", "cycNodes", "cycSort", "cycQuick", "cycFull", "cycCommit", "cycTpl",
-         "cycTotal", "cycNodeCommit", "cycFullRs", "cycFullThr", "cycFullMasks", "cycFullApply", "runs", "runPods"]
+         "cycTotal", "cycNodeCommit", "cycFullRs", "cycFullThr", "cycFullMasks", "cycFullApply", "runs", "runPods",
+         "sortsExact", "fTopoPop", "fState", "fRefill", "fWinTests", "fWinBlocks", "fRecord", "fNodeCommit", "fWinTopo"]
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
 topo = int(sys.argv[2]) if len(sys.argv) > 2 else 0
@@ -36,6 +37,19 @@ print("simulations %d; cycTotal max %d, p50 %d, p90 %d, p99 %d, mean %.0f" % (
     len(tot), mx, tot[len(tot) // 2], tot[len(tot) // 10], tot[len(tot) // 100], sum(tot) / len(tot)))
 print("sum of all simulations' cycles / max = %.1f (the pass cannot be shorter than its longest simulation)"
       % (sum(tot) / mx))
+# the node phase split (scyc slots, shared with claim_full's sub-phases, which these simulations barely run):
+# [0] the node phase up to the scan past the register window, [2] scan steps past the window, [3] their cycles
+for cyc, s, d in rows[:4]:
+    pops = max(d["pops"], 1)
+    print("sim %5d node phase per pop: window part %.0f cyc, past-window steps %.2f, past-window cyc %.0f, commit %.0f" % (
+        s, d["cycFullRs"] / pops, d["cycFullMasks"] / pops, d["cycFullApply"] / pops, d["cycNodeCommit"] / pops))
+for cyc, s, d in rows[:4]:
+    pops = max(d["pops"], 1)
+    if "fTopoPop" in d:
+        print("sim %5d fine per pop: topo_pop %.0f, state %.0f, refill %.0f, window tests %.0f (blocks %.2f, topology %.0f),"
+              " record %.0f, node commit %.0f" % (s, d["fTopoPop"] / pops, d["fState"] / pops, d["fRefill"] / pops,
+                                                  d["fWinTests"] / pops, d["fWinBlocks"] / pops, d["fWinTopo"] / pops,
+                                                  d["fRecord"] / pops, d["fNodeCommit"] / pops))
 for cyc, s, d in rows[:12]:
     pops = max(d["pops"], 1)
     print("sim %5d: cyc %9d (%.2f of max) pops %5d runs %4d (%5d pods, %.0f cyc) windows %3d (%.0f cyc) | pop %.0f nodes %.0f (commit %.0f) claims %.0f tpl %.0f per pod" % (
