@@ -80,13 +80,34 @@ def _oracle_full(name, snap_json, units, unit):
             "where": "build container, when the full-size digests were made (tests/golden/full_size_digests.json)"}
 
 
+_LIB_SHA = None
+
+
+def _lib_sha():
+    """sha256 of the libkarpenter_amd build this process loaded."""
+    global _LIB_SHA
+    if _LIB_SHA is None:
+        from karpenter_amd.scheduler import library_path
+
+        with open(library_path(), "rb") as f:
+            _LIB_SHA = hashlib.sha256(f.read()).hexdigest()
+    return _LIB_SHA
+
+
 def _traffic(tag):
+    """(HBM bytes per launch, source, build match) of the committed PMC profile for `tag`.  build match: the
+    profile was taken on the library this process loaded (False: a different build -- the figure is stale;
+    None: the profile predates the build record)."""
     tpath = os.path.join(ROOT, "profiles", "traffic_%s.json" % tag)
     if os.path.exists(tpath):
         with open(tpath) as f:
             t = json.load(f)
-        return t.get("hbm_bytes_per_launch"), "profiles/traffic_%s.json (rocprofv3 PMC, profile tag %s)" % (tag, t.get("tag"))
-    return None, None
+        match = None if not t.get("lib_sha256") else t["lib_sha256"] == _lib_sha()
+        src = "profiles/traffic_%s.json (rocprofv3 PMC, profile tag %s%s)" % (
+            tag, t.get("tag"), "" if match else ", STALE: profiled on another build" if match is False
+            else ", build unrecorded")
+        return t.get("hbm_bytes_per_launch"), src, match
+    return None, None, None
 
 
 def _roofline(kernel, k_ms, kernel_bytes, ref_bytes, traffic_tag, per_gpu_div=1, extra=None):
@@ -102,14 +123,14 @@ def _roofline(kernel, k_ms, kernel_bytes, ref_bytes, traffic_tag, per_gpu_div=1,
     hbm_achieved / hbm_frac: the PMC rate on every line that has a committed profile.
     kernel_scan_bytes / kernel_scan_frac: the kernel's own scan count (each pod of an identical-pod run
     credited with the first pod's scan), a bookkeeping figure."""
-    traffic, src = _traffic(traffic_tag)
+    traffic, src, match = _traffic(traffic_tag)
     sec = k_ms / 1000.0
     alg, asrc = (ref_bytes, "SURVEY 8d reference scan, oracle count (tests/golden/full_size_digests.json)") if ref_bytes \
         else (kernel_bytes, "kernel-counted scan (no oracle count for this workload)")
     ref_achieved = alg / sec / 1e9 / per_gpu_div
     r = {"bound": "hbm", "kernel": kernel, "achieved": round(ref_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": ref_achieved / HBM_PEAK_GBS, "frac_basis": "algorithmic bytes (%s)" % asrc, "traffic": traffic,
-         "traffic_source": src, "algorithmic_bytes_per_launch": alg, "algorithmic_bytes_source": asrc,
+         "traffic_source": src, "traffic_build_match": match, "algorithmic_bytes_per_launch": alg, "algorithmic_bytes_source": asrc,
          "kernel_ms": round(k_ms, 3), "reference_scan_achieved": round(ref_achieved, 3),
          "reference_scan_frac": ref_achieved / HBM_PEAK_GBS, "hbm_achieved": None, "hbm_frac": None,
          "kernel_scan_bytes": kernel_bytes,

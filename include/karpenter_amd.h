@@ -175,7 +175,8 @@ int ks_cons_run(ks_cons* c, int rank, int world, const ks_solve_opts* opts, void
  * until its next run, and ks_cons_decide / ks_cons_needed_sims / ks_cons_records_alg_bytes take records NULL
  * to read them there (no copy of the pass's records). */
 /* Replay the reference's sequential choice over the gathered records ([rank][slot] layout):
- * JSON {"candidates":[{name, disruptionCost}], "multi":{"command", "sims"}, "single":{"command", "sims"}}.
+ * JSON {"candidates":[{name, disruptionCost}], "multi":{"command", "sims", "path"}, "single":{"command", "sims"}}
+ * ("path": the binary search's probes {mid, carried, action}: carried = re-run from pod objects an earlier probe relaxed).
  * flags: KS_CONS_ALL_SIMS reports every simulation (otherwise only those the reference would have
  * run); KS_CONS_CANDIDATES includes the candidate list (otherwise "candidates" is empty).
  * Requirement records (NewNodeClaims[0].Requirements) stay on the GPU that ran a simulation:

@@ -238,6 +238,10 @@ struct ks_cons {
   // per pod: its topoContrib / topoInvOwner entry (resolved once, kept current by ks_cons_update)
   std::vector<const std::vector<std::pair<int, int>>*> podContrib;
   std::vector<const std::vector<int32_t>*> podInv;
+  // the groups some relaxation state creates with another minDomains (PodState::gmd), built on first use: the
+  // states are fixed at create (an update only removes or binds pods, so the list stays a superset)
+  std::vector<int> altGroups;
+  bool altBuilt = false;
   int64_t updates = 0;
   // per host node, for the per-simulation limits (prepare_launch): the NodePools it counts against and its
   // capacity in device units (static for the handle; built on first use)
@@ -692,11 +696,12 @@ PodTopo pod_topo(const Host& h) {
 // pod whose Update creates it (its Hash leaves minDomains out, topologygroup.go:142-158), the first simulation
 // pod, in NewTopology's Update order (the pods list: pending, the candidates', the deleting nodes'), whose
 // starting state owns it; a group only a relaxation creates takes its relaxing pod's (refused when those differ).
-// `altGroups`: the groups some state gives another minDomains (PodState::gmd; empty: nothing to do).
+// `altGroups`: the groups some state gives another minDomains (PodState::gmd; empty: nothing to do);
+// `anyInjFailed`: some pod's volume injection failed (Host::injectFailed) -- both once per launch plan.
 std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, const std::vector<int>& simPods,
                                   const PodTopo& pt, std::vector<uint64_t>& dead, std::vector<uint64_t>& act,
                                   const std::vector<int32_t>* start, const std::vector<int>& altGroups,
-                                  std::vector<int32_t>& md) {
+                                  bool anyInjFailed, std::vector<int32_t>& md) {
   const Host& h = c.pb->host;
   const KsDims& d = h.dims;
   const int GMW = d.GMW;
@@ -753,7 +758,6 @@ std::vector<int32_t> sim_topology(const ks_cons& c, const ks_cons::Sim& sm, cons
   std::vector<std::pair<int, int>> touched;  // (group, value) per removed pod's contribution (sorted below)
   std::vector<int> ownersGone((size_t)d.G, 0);
   std::set<int> goneHosts;  // hostname value ids of the removed candidates
-  const bool anyInjFailed = std::find(h.injectFailed.begin(), h.injectFailed.end(), 1) != h.injectFailed.end();
   for (int ci : sm.cands) {
     const ks_cons::Cand& k = c.cands[(size_t)ci];
     for (int p : k.pods) {
@@ -889,20 +893,24 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     PodTopo ptopo;
     ptopo.contrib.swap(c.podContrib);
     ptopo.inv.swap(c.podInv);
-    std::vector<int> altGroups;  // groups some relaxation state creates with another minDomains
-    {
+    if (!c.altBuilt) {
       std::vector<char> alt((size_t)d.G, 0);
       for (auto& chain : h.states)
         for (auto& st : chain)
           for (auto& e : st.gmd) alt[(size_t)e.first] = 1;
+      c.altGroups.clear();
       for (int g = 0; g < d.G; g++)
-        if (alt[(size_t)g]) altGroups.push_back(g);
+        if (alt[(size_t)g]) c.altGroups.push_back(g);
+      c.altBuilt = true;
     }
+    const std::vector<int>& altGroups = c.altGroups;
+    const bool anyInjFailed = std::find(h.injectFailed.begin(), h.injectFailed.end(), 1) != h.injectFailed.end();
+    pt.mark("minDomains groups");
     std::vector<std::exception_ptr> err((size_t)ns);
     parallel_for(ns, 4, [&](int k) {
       try {
         tdel[k] = sim_topology(c, c.sims[(size_t)mine[(size_t)k]], simPods[k], ptopo, tdead[k], tact[k], c.carryStart,
-                               altGroups, tmd[k]);
+                               altGroups, anyInjFailed, tmd[k]);
       } catch (...) {
         err[(size_t)k] = std::current_exception();
       }

@@ -519,6 +519,10 @@ __global__ __launch_bounds__(256) void k_feasibility_nodes(KsDev D, int nbx) {
 }
 #endif
 
+// A topology simulation keeps its register window's node domains in LDS (Solver::s_tdw): the first kTdw nodes,
+// the first kTdwKeys key slots (make_plan counts the bytes).
+constexpr int kTdw = 256, kTdwKeys = 4;
+
 template <int RT, bool TL, bool SIM, bool TOPO, bool LEAN>
 struct Solver {
   static constexpr int RM = RT > 0 ? RT : kMaxR;
@@ -570,6 +574,7 @@ struct Solver {
   LU32 s_trs0;          // [RSW] AddRequirements' nodeRequirements snapshot
   LU32 s_trs1;          // [RSW] one group's domains as a single-key record
   LI32 s_tdom;          // [pl.tdl] the node domain table (a Solve whose table fits)
+  LI32 s_tdw;           // SIM + TOPO: the register window's node domains, [key slot < kTdwKeys][kTdw]
   LI32 s_live;          // [pl.livl] a Solve's live node list (ks_solve_body.inc)
   LI32 s_tcs;           // [pl.tcl] the count table's LDS-resident prefix: the small-key groups (a Solve: the
                         // whole table when it fits, make_plan)
@@ -1023,8 +1028,11 @@ struct Solver {
     return ld_sc1(W.tg_cnt + off);
   }
   __device__ __forceinline__ int tcnt(int g, int v) const { return tcnt_at(tg(g, TGM_CNT) + v); }
-  // node n's domain of group g's key (-1: the node lacks the label): LDS in a Solve whose table fits
+  // node n's domain of group g's key (-1: the node lacks the label): LDS in a Solve whose table fits, and for
+  // a topology simulation's register-window nodes (the first kTdw nodes: every scan starts there)
   __device__ __forceinline__ int tdom(int g, int n) const {
+    if constexpr (SIM && TOPO)
+      if (n < kTdw && tg(g, TGM_KSLOT) < kTdwKeys) return s_tdw[tg(g, TGM_KSLOT) * kTdw + n];
     const int off = tg(g, TGM_KSLOT) * d.N + n;
     return off < pl.tdl ? s_tdom[off] : D.n_tdom[off];
   }
@@ -2859,7 +2867,7 @@ static Plan make_plan_live(const KsDims& d, size_t budget, bool sim, bool wideKO
                        (sim ? 4 * r16(4 * (size_t)((d.N + 31) / 32)) : d.fnOn ? r16(4 * (size_t)((d.N + 31) / 32)) : 0) +
                        (d.G ? r16(4 * (size_t)d.G * TGM_WORDS) + r16(4 * (size_t)d.G) + 2 * r16(4 * (size_t)d.RSW) +
                                   (d.GMW > 1 ? r16(8 * (size_t)GS_N * d.GMW) : 0) +
-                                  (sim ? r16(4 * (size_t)((d.tgCntWords - d.tgSmall + 31) / 32)) : 0)
+                                  (sim ? r16(4 * (size_t)((d.tgCntWords - d.tgSmall + 31) / 32)) + 4 * kTdwKeys * kTdw : 0)
                               : 0);
   const size_t posB = 16 + 8 * R;                        // order, okey, ptpl, phead (+ rounding)
   const size_t clmB = 16 + 16 * R + 4 * TW + 4 * R;      // tpl, cnt, req, max, rem, thr (+ rounding)

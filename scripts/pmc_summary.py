@@ -10,6 +10,7 @@ FETCH_SIZE reports half the bytes of a coalesced read, so it is doubled.
 """
 import collections
 import csv
+import hashlib
 import json
 import os
 import shutil
@@ -46,9 +47,13 @@ def main():
         rd = 2 * vals["FETCH_SIZE"] * 1024
         wr = vals["WRITE_SIZE"] * 1024
         lines.append("HBM bytes per launch: read %.0f (FETCH_SIZE x2 KiB) + write %.0f = %.0f" % (rd, wr, rd + wr))
+        # the build profiled (bench.py flags the figure stale when the library it loads differs)
+        so = os.path.join(ROOT, "karpenter-sigs_amd", "karpenter_amd", "libkarpenter_amd.so")
+        lib_sha = hashlib.sha256(open(so, "rb").read()).hexdigest() if os.path.exists(so) else None
         with open(os.path.join(prof, "traffic_%s.json" % tname), "w") as f:
             json.dump({"tag": tag, "kernel": kname, "hbm_read_bytes_per_launch": rd,
-                       "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr}, f, indent=1)
+                       "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
+                       "lib_sha256": lib_sha}, f, indent=1)
     if "SQ_WAVE_CYCLES" in vals and "SQ_BUSY_CYCLES" in vals:
         lines.append("SQ_WAIT_ANY / SQ_WAVE_CYCLES = %.3f ; SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES = %.3f" % (
             vals.get("SQ_WAIT_ANY", 0) / vals["SQ_WAVE_CYCLES"], vals.get("SQ_ACTIVE_INST_ANY", 0) / vals["SQ_WAVE_CYCLES"]))
