@@ -1812,6 +1812,60 @@ std::string validate_json(ks_cons& c, const Value& cmd) {
   return out(true, "", sim);
 }
 
+// A node's initial HostPortUsage mask (KsDev::n_hp0) over the host-port element classes of the build
+// (ks_host.cpp): the classes are re-derived from the persisted pods' ports and universe exactly as the build formed
+// them (same signatures, same numbering; checked against the pods' masks), then node n's remaining entries are
+// OR-ed in.  ks_cons_update after deleting a pod that holds host ports on n (HostPortUsage.DeletePod,
+// hostportusage.go:87-90).
+uint64_t node_host_port_mask(const Host& h, int n) {
+  const size_t NUH = h.hostPortUniverse.size();
+  if (NUH == 0) return 0;
+  std::set<std::string> podKeys, ownerKeys;
+  for (const PodH& p : h.pods) podKeys.insert(p.ns + "/" + p.name);
+  for (const std::string& o : h.hostPortOwner)
+    if (!o.empty()) ownerKeys.insert(o);
+  std::vector<std::vector<int32_t>> sig(NUH);
+  for (size_t i = 0; i < h.pods.size(); i++) {
+    const PodH& p = h.pods[i];
+    const std::string key = p.ns + "/" + p.name;
+    if (p.ports.empty() && !ownerKeys.count(key)) continue;
+    for (size_t u = 0; u < NUH; u++) {
+      const HostPortH& e = h.hostPortUniverse[u];
+      bool hpc = false, hpu = false;
+      for (const HostPortH& x : p.ports) {
+        hpu = hpu || (e.ip == x.ip && e.port == x.port && e.proto == x.proto && h.hostPortOwner[u].empty());
+        hpc = hpc || (x.matches(e) && h.hostPortOwner[u] != key);
+      }
+      const int code = (hpc ? 1 : 0) | (hpu ? 2 : 0) | (h.hostPortOwner[u] == key ? 4 : 0);
+      if (code) sig[u].push_back((int32_t)i * 8 + code);
+    }
+  }
+  std::map<std::vector<int32_t>, int> cls;
+  std::vector<int> cl(NUH);
+  for (size_t u = 0; u < NUH; u++) cl[u] = cls.emplace(sig[u], (int)cls.size()).first->second;
+  std::vector<uint64_t> hpc(h.pods.size(), 0), hpu(h.pods.size(), 0), hpo(h.pods.size(), 0);
+  for (size_t u = 0; u < NUH; u++)
+    for (int32_t e : sig[u]) {
+      if (e & 1) hpc[(size_t)(e >> 3)] |= 1ull << cl[u];
+      if (e & 2) hpu[(size_t)(e >> 3)] |= 1ull << cl[u];
+      if (e & 4) hpo[(size_t)(e >> 3)] |= 1ull << cl[u];
+    }
+  for (size_t i = 0; i < h.pods.size(); i++)
+    if (hpc[i] != h.tab.pod_hpc[i] || hpu[i] != h.tab.pod_hpu[i] || hpo[i] != h.tab.pod_hpo[i])
+      throw KsError(KS_ERR_INTERNAL, "update: host-port classes differ from the build's");
+  uint64_t m = 0;
+  for (const auto& e : h.nodes[(size_t)n].hostPorts) {
+    const std::string owner = podKeys.count(e.first) ? e.first : "";
+    size_t u = 0;
+    while (u < NUH && !(h.hostPortUniverse[u].ip == e.second.ip && h.hostPortUniverse[u].port == e.second.port &&
+                        h.hostPortUniverse[u].proto == e.second.proto && h.hostPortOwner[u] == owner))
+      u++;
+    if (u == NUH) throw KsError(KS_ERR_INTERNAL, "update: a node's host-port entry is outside the universe");
+    m |= 1ull << cl[u];
+  }
+  return m;
+}
+
 // ks_cons_update: the cluster-state events between two passes (state/cluster.go:220-512 UpdatePod /
 // DeletePod / DeleteNode) applied to the resident handle, so the next pass needs no re-parse, no
 // re-encode and no re-upload of the problem.  Applied in order: deletePods, bindPods (a pending pod now
@@ -1820,8 +1874,10 @@ std::string validate_json(ks_cons& c, const Value& cmd) {
 // Subtract), a removed node's capacity returns to its pool's limits (provisioner.go:204-296 re-reads them
 // per pass) and the node can take no pod in any simulation.  The candidates and simulations are re-derived
 // (order_candidates).  Topology clusters move the shared NewTopology counts with the pods (round 5).  Refused
-// (KS_ERR_UNSUPPORTED, nothing applied): clusters with volume limits (their counts are encoded per pod and
-// node) and pods with host ports.
+// (KS_ERR_UNSUPPORTED, nothing applied): clusters with volume limits (a snapshot reports a node's VolumeUsage as
+// one union, so a pod's share of it is not known) and binding a pod with host ports (its entries would need
+// universe elements and classes of their own).  Deleting a pod with host ports drops its node's entries
+// (HostPortUsage.DeletePod, node_host_port_mask).
 void apply_update(ks_cons& c, const Value& delta, bool device) {
   PhaseTimer pt("ks_cons_update");
   ks_problem& pb = *c.pb;
@@ -1865,7 +1921,6 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     const int p = podOf(v);
     if (c.podNode[(size_t)p] == ks_cons::PN_GONE || !seenPod.insert(p).second)
       throw KsError(KS_ERR_ARG, "update: pod " + v.str() + " is already deleted");
-    if (h.pods[(size_t)p].hostPorts) throw KsError(KS_ERR_UNSUPPORTED, "update: pod " + v.str() + " has host ports");
     del.push_back(p);
   }
   for (const Value& v : (bv ? *bv : kNone).arr()) {
@@ -1955,11 +2010,17 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     auto it = std::find(v.begin(), v.end(), x);
     if (it != v.end()) v.erase(it);
   };
+  std::set<int> hpNodes;  // nodes whose HostPortUsage lost a pod's entries
   for (int p : del) {
     const int32_t where = c.podNode[(size_t)p];
     if (where >= 0) {
       erase(c.nodePods[(size_t)where], p);
       move(where, h.pods[(size_t)p], +1);
+      auto& hp = h.nodes[(size_t)where].hostPorts;  // StateNode.hostPortUsage.DeletePod (statenode.go:314-339)
+      const std::string key = h.pods[(size_t)p].ns + "/" + h.pods[(size_t)p].name;
+      const size_t before = hp.size();
+      hp.erase(std::remove_if(hp.begin(), hp.end(), [&](const auto& e) { return e.first == key; }), hp.end());
+      if (hp.size() != before) hpNodes.insert(where);
     } else if (where == ks_cons::PN_PENDING) {
       erase(c.pending, p);
     } else if (where == ks_cons::PN_DELETING) {
@@ -2117,6 +2178,7 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
       }
     }
   }
+  for (int n : hpNodes) h.tab.n_hp0[(size_t)n] = node_host_port_mask(h, n);
   for (int n : rows) {
     int64_t* row = &h.tab.n_avail[(size_t)n * R];
     for (int r = 0; r < R; r++) row[r] = 0;
@@ -2139,6 +2201,9 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   KsDev& D = pb.dev;
   if (!rows.empty() || !rm.empty())
     HIPCHK(hipMemcpyAsync((void*)D.n_avail, h.tab.n_avail.data(), 8 * h.tab.n_avail.size(), hipMemcpyHostToDevice,
+                          pb.stream));
+  if (!hpNodes.empty())
+    HIPCHK(hipMemcpyAsync((void*)D.n_hp0, h.tab.n_hp0.data(), 8 * h.tab.n_hp0.size(), hipMemcpyHostToDevice,
                           pb.stream));
   if (!bind.empty())
     HIPCHK(hipMemcpyAsync((void*)D.pod_flags, h.tab.pod_flags.data(), 4 * h.tab.pod_flags.size(),

@@ -58,6 +58,16 @@ def _move(node, pod, sign):
             av[k] = fmt_q(parse_q(av[k]) + sign * v)
 
 
+def _key(pod):
+    return "%s/%s" % (pod["metadata"].get("namespace", "default"), pod["metadata"]["name"])
+
+
+def _host_ports(pod):
+    """GetHostPorts (hostportusage.go:92-114) as StateNode.HostPortUsage() reports them."""
+    return [{"ip": e.get("hostIP", "0.0.0.0"), "port": e["hostPort"], "protocol": e.get("protocol", "TCP")}
+            for c in pod["spec"].get("containers", []) for e in c.get("ports", []) if e.get("hostPort")]
+
+
 def apply_delta(snap, delta):
     """The snapshot after ks_cons_update's delta (deletePods, then bindPods, then removeNodes)."""
     s = copy.deepcopy(snap)
@@ -79,6 +89,7 @@ def apply_delta(snap, delta):
             if hit:
                 n["pods"].remove(hit[0])
                 _move(n, hit[0], +1)
+                n.get("hostPortUsage", {}).pop(_key(hit[0]), None)  # HostPortUsage.DeletePod
                 break
         else:
             raise KeyError(uid)
@@ -90,6 +101,8 @@ def apply_delta(snap, delta):
         node = nodes[b["node"]]
         node.setdefault("pods", []).append(pod)
         _move(node, pod, -1)
+        if _host_ports(pod):  # HostPortUsage.Add
+            node.setdefault("hostPortUsage", {})[_key(pod)] = _host_ports(pod)
         unlist(lambda p: p["metadata"]["uid"] == b["uid"])
         if listed:
             s["clusterPods"].append(pod)

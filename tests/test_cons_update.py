@@ -12,6 +12,7 @@ JSON independently of the C++ update):
        the edited snapshot (every simulation's outcome and both commands), also through save/from_binary.
 """
 import json
+import random
 
 import pytest
 
@@ -210,6 +211,67 @@ def test_update_then_validate_gpu(seed):
         want = bridge.validate(cur, cmd)
         got = c.validate(cmd)
         assert got == want, cmd
+
+
+def _ports_snap(seed):
+    """Bound pods holding host ports (their nodes' HostPortUsage lists them under the pod's key) and pending pods
+    asking for the same ports: a deleted holder frees its port on that node."""
+    rng = random.Random(seed)
+    snap = _snap(seed, n_nodes=24, pods_per_node=4, n_pending=6, pdbs=False)
+    ports = [8080, 9090]
+    holders = []
+    for n in snap["stateNodes"]:
+        for p in n.get("pods", []):
+            if rng.random() < 0.5:
+                port = rng.choice(ports)
+                p["spec"]["containers"][0]["ports"] = [{"containerPort": port, "hostPort": port, "protocol": "TCP"}]
+                n.setdefault("hostPortUsage", {})["default/" + p["metadata"]["name"]] = [
+                    {"ip": "0.0.0.0", "port": port, "protocol": "TCP"}]
+                holders.append(p["metadata"]["uid"])
+    for p in snap["pendingPods"][:4]:
+        port = rng.choice(ports)
+        p["spec"]["containers"][0]["ports"] = [{"containerPort": port, "hostPort": port, "protocol": "TCP"}]
+    return snap, holders
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_host_port_pod_deletion_host_state(seed):
+    """Deleting pods that hold host ports (round 6: HostPortUsage.DeletePod on the node's mask); binding one is
+    still refused (its entries would need host-port classes of their own)."""
+    snap, holders = _ports_snap(seed)
+    d = {"deletePods": holders[:5], "removeNodes": [snap["stateNodes"][-1]["name"]]}
+    got = inspect_consolidation_update(json.dumps(snap), d)
+    want = inspect_consolidation_update(json.dumps(apply_delta(snap, d)))
+    for k in ("candidates", "pendingPods", "nodeRows", "poolRemaining", "sims"):
+        assert got[k] == want[k], k
+    with pytest.raises(KsError) as e:
+        inspect_consolidation_update(json.dumps(snap), {"bindPods": [
+            {"uid": snap["pendingPods"][0]["metadata"]["uid"], "node": snap["stateNodes"][0]["name"]}]})
+    assert "KS_ERR_UNSUPPORTED" in str(e.value)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [41, 42, 43])
+def test_host_port_pod_deletion_gpu_parity(seed):
+    """After deleting host-port holders (and binding port-less pods), a pass on the updated handle equals the
+    oracle's consolidation of the edited snapshot, where the deleted pods' entries left their nodes."""
+    snap, holders = _ports_snap(seed)
+    c = Consolidator(json.dumps(snap))
+    plain = [p["metadata"]["uid"] for p in snap["pendingPods"][4:]]
+    cur = snap
+    for d in ({"deletePods": holders[:4]},
+              {"deletePods": holders[4:8], "bindPods": [{"uid": plain[0], "node": snap["stateNodes"][1]["name"]}]},
+              {"deletePods": holders[8:10], "removeNodes": [snap["stateNodes"][2]["name"]]}):
+        c.update(d)
+        cur = apply_delta(cur, d)
+        want, _ = bridge.consolidate(json.dumps(cur), all_sims=True)
+        got = c.consolidate(all_sims=True)
+        got.pop("kernel_ms")
+        assert got == want, d
+    c2 = Consolidator.from_binary(c.save())
+    got = c2.consolidate(all_sims=True)
+    got.pop("kernel_ms")
+    assert got == want
 
 
 def _late_snap():
