@@ -21,10 +21,14 @@ cmd_for() {
     c5t) echo "$P --only-consolidation --no-c5" ;;
   esac
 }
+if [ -z "$NO_TRACE" ]; then  # NO_TRACE=1: only the per-workload passes (a second call for the remaining workloads)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_${tag}_trace -o run -- \
   python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $out/prof_${tag}_trace.log 2>&1 || exit $?
+fi
 for w in $W; do
   C=$(cmd_for $w)
+  # the workload's own kernel trace: per-workload averages (C1 and C2 launch the same instantiation)
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_${tag}_${w}_trace -o run -- $C > $out/prof_${tag}_${w}_trace.log 2>&1 || exit $?
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/prof_${tag}_${w}_fetch -o run -- $C > $out/prof_${tag}_${w}_fetch.log 2>&1 || exit $?
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/prof_${tag}_${w}_write -o run -- $C > $out/prof_${tag}_${w}_write.log 2>&1 || exit $?
   timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VMEM --output-format csv -d $out/prof_${tag}_${w}_sq -o run -- $C > $out/prof_${tag}_${w}_sq.log 2>&1 || exit $?
