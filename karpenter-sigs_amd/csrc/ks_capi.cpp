@@ -27,7 +27,7 @@ namespace {
 struct WorkLayout {
   size_t c_tpl, c_cnt, c_thr, c_host, c_req, c_max, c_rs, c_rem, order, n_req, n_rs, queue, qorder, pod_state, last_len,
       log_pod, log_tgt, pod_status, pod_fstate, fail_code, fail_host, pool_rem, counters, n_hp, c_hp, n_vc, vlog, vspec, tg_cnt,
-      tg_ccnt, tg_cpos, fail_rs, log_hg, tg_act, total;
+      tg_ccnt, tg_cpos, fail_rs, log_hg, tg_act, run_len, run_words, total;
   int32_t ccs;  // tg_ccnt row stride
 };
 
@@ -70,6 +70,8 @@ WorkLayout work_layout(const KsDims& d) {
   w.fail_rs = a.add(d.G ? 4 * (size_t)P * std::max(d.NTPL, 1) * d.FSW : 4);
   w.log_hg = a.add(d.G ? 8 * P * (size_t)d.GMW : 8);
   w.tg_act = a.add(4 * (size_t)std::max(d.G, 1));
+  w.run_len = a.add(4 * P);
+  w.run_words = a.add(8 * ((P + 63) / 64));
   w.total = a.total;
   return w;
 }
@@ -111,6 +113,7 @@ KsWork work_ptrs(char* base, const WorkLayout& w) {
   k.fail_rs = (uint32_t*)(base + w.fail_rs);
   k.log_hg = (uint64_t*)(base + w.log_hg);
   k.tg_act = (int32_t*)(base + w.tg_act);
+  k.run_len = (const int32_t*)(base + w.run_len);
   k.ccs = w.ccs;
   return k;
 }
@@ -1140,6 +1143,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
     HIPCHK(hipMalloc(&pb->works_dev, sizeof(KsWork) * reps));
     std::vector<KsWork> ws;
     for (int r = 0; r < reps; r++) ws.push_back(work_ptrs((char*)pb->wbuf + wl.total * r, wl));
+    for (auto& x : ws) x.run_len = ws[0].run_len;  // one queue order (k_init copies it to every replica)
     HIPCHK(hipMemcpy(pb->works_dev, ws.data(), sizeof(KsWork) * reps, hipMemcpyHostToDevice));
     pb->wbytes = need;
     pb->wreps = reps;
@@ -1158,7 +1162,8 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
     attempts++;
     HIPCHK(hipEventRecord(e0, pb->stream));
     HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp,
-                        pb->stempBytes, pb->stream, em, pb->hqorder, ef));
+                        pb->stempBytes, pb->stream, em, pb->hqorder, ef, (int32_t*)w0.run_len,
+                        (uint64_t*)((char*)pb->wbuf + wl.run_words)));
     HIPCHK(hipEventRecord(e1, pb->stream));
     HIPCHK(hipEventSynchronize(e1));
     float a = 0, b = 0, f = 0;

@@ -107,15 +107,21 @@ hipError_t sim_queue_sort(const int32_t* rank, const int32_t* entries, const int
 // step while no pod has been pushed back, ks_solve.hip): entry i of the sorted CSR starts a run when it is its
 // simulation's first entry or its pod differs from the previous entry's in requests, tolerations (the pod's first
 // relaxation state) or the provisionable flag.  One bit per entry, 64 per word (one ballot per wave).
+// A Solve's queue (entry_sim null, strict): one segment, and the pods' template-toleration sets and state flags
+// (pod_s0 words 2, 3) must match too -- the LEAN Solve's claim runs (ks_solve_body.inc).
 __global__ __launch_bounds__(256) void k_sim_run_breaks(const int32_t* podmap, const int32_t* entry_sim,
                                                         const int64_t* pod_req, const uint64_t* pod_s0,
-                                                        const int32_t* pod_flags, int R, int n, uint64_t* words) {
+                                                        const int32_t* pod_flags, int R, int n, uint64_t* words,
+                                                        int strict) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   bool brk = true;
-  if (i < n && i > 0 && entry_sim[i] == entry_sim[i - 1]) {
+  if (i < n && i > 0 && (!entry_sim || entry_sim[i] == entry_sim[i - 1])) {
     const int p = podmap[i], q = podmap[i - 1];
     bool same = pod_s0[4 * (int64_t)p] == pod_s0[4 * (int64_t)q] && pod_s0[4 * (int64_t)p + 1] == pod_s0[4 * (int64_t)q + 1] &&
                 ((pod_flags[p] ^ pod_flags[q]) & PF_PROVISIONABLE) == 0;
+    if (strict)
+      same = same && pod_s0[4 * (int64_t)p + 2] == pod_s0[4 * (int64_t)q + 2] &&
+             pod_s0[4 * (int64_t)p + 3] == pod_s0[4 * (int64_t)q + 3];
     for (int r = 0; r < R; r++) same = same && pod_req[(int64_t)p * R + r] == pod_req[(int64_t)q * R + r];
     brk = !same;
   }
@@ -136,11 +142,12 @@ __global__ __launch_bounds__(256) void k_sim_run_len(const uint64_t* words, int 
 }
 
 hipError_t sim_run_lengths(const int32_t* podmap, const int32_t* entry_sim, const int64_t* pod_req, const uint64_t* pod_s0,
-                           const int32_t* pod_flags, int R, int n, uint64_t* words, int32_t* run_len, hipStream_t st) {
+                           const int32_t* pod_flags, int R, int n, uint64_t* words, int32_t* run_len, hipStream_t st,
+                           bool strict) {
   if (n == 0) return hipSuccess;
   const int blocks = (n + 255) / 256;
   hipLaunchKernelGGL(k_sim_run_breaks, dim3(blocks), dim3(256), 0, st, podmap, entry_sim, pod_req, pod_s0, pod_flags, R,
-                     n, words);
+                     n, words, strict ? 1 : 0);
   hipLaunchKernelGGL(k_sim_run_len, dim3(blocks), dim3(256), 0, st, words, n, run_len);
   return hipGetLastError();
 }

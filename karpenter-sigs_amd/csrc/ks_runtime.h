@@ -13,7 +13,8 @@
 namespace ks {
 hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
-                        hipEvent_t mid, const int32_t* fixed_order = nullptr, hipEvent_t* feas = nullptr);
+                        hipEvent_t mid, const int32_t* fixed_order = nullptr, hipEvent_t* feas = nullptr,
+                        int32_t* run_len = nullptr, uint64_t* run_words = nullptr);
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st);
 // The first nmw simulations (the long multi-node prefixes) on 4-wave workgroups when the problem allows it
 // (sims_mw_supported: resource-only pods, no topology), concurrently with the rest.
@@ -28,8 +29,10 @@ hipError_t rank_from_order(const int32_t* order, int32_t* rank, int n, hipStream
 // consolidation record headers + device-side record invariants (ks_queue.hip k_rec_headers)
 hipError_t rec_headers(const int32_t* recs, int ns, int recWords, int TW, const int32_t* tplBeg, int ntpl, int32_t* hdr,
                        unsigned long long* status, unsigned* counter, unsigned long long* statusOut, hipStream_t st);
+// entry_sim null: one run segment (a Solve's queue); strict: also the pods' template-toleration sets and flags
 hipError_t sim_run_lengths(const int32_t* podmap, const int32_t* entry_sim, const int64_t* pod_req, const uint64_t* pod_s0,
-                           const int32_t* pod_flags, int R, int n, uint64_t* words, int32_t* run_len, hipStream_t st);
+                           const int32_t* pod_flags, int R, int n, uint64_t* words, int32_t* run_len, hipStream_t st,
+                           bool strict = false);
 hipError_t sim_queue_sort(const int32_t* rank, const int32_t* entries, const int32_t* entry_sim, int n, int rbits,
                           int sbits, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
                           hipStream_t st);

@@ -241,7 +241,7 @@ template <> struct ClaimView<false> { GI32 tpl; GI64 req; GI64 max; GU32 rem; GI
 template <int RT>
 struct Window {
   int p, g, uid, s, flags, pf, st;
-  int rl;  // SIM, nothing pushed back yet: identical pods from this queue position to the end of their run
+  int rl;  // LEAN, nothing pushed back yet: identical pods from this queue position to the end of their run
   uint64_t ll, tol0, tol1, toltpl, hpc, hpu, hpo;
   uint64_t tsel, tinv, town, trss;  // TOPO: word 0 of the pod's selecting / inverse / owned group sets, st_rss keys
   int64_t req[RT > 0 ? RT : kMaxR];
@@ -2550,7 +2550,7 @@ struct Solver {
         w.tol1 = D.st_tol[2 * w.s + 1];
       }
       w.pf = SIM || (!LEAN && d.volAny) ? D.pod_flags[w.g] : 0;
-      w.rl = SIM && LEAN && ident ? W.run_len[pos] : 1;
+      w.rl = LEAN && ident ? W.run_len[pos] : 1;
       w.hpc = D.pod_hpc[w.g];
       w.hpu = D.pod_hpu[w.g];
       w.hpo = D.pod_hpo[w.g];
@@ -2933,17 +2933,28 @@ void launch_feasibility_nodes(const KsDev& D, hipStream_t st) {
 
 hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
                       hipStream_t st);
+hipError_t sim_run_lengths(const int32_t* podmap, const int32_t* entry_sim, const int64_t* pod_req, const uint64_t* pod_s0,
+                           const int32_t* pod_flags, int R, int n, uint64_t* words, int32_t* run_len, hipStream_t st,
+                           bool strict);
 
 // One ks_solve: queue sort -> workspace init -> [mid event] -> k_solve (all on one stream).
 // Topology problems get their own instantiation: the group state would otherwise occupy SGPRs (and
 // their spills) across the whole commit loop of every topology-free Solve.
 // fixed_order: NewQueue's order computed on the host (pods tying on the whole sort key), no radix sort.
+// run_len / run_words (LEAN problems): the identical pods left in each queue position's run, which the LEAN
+// Solve's claim runs read while nothing has been pushed back (they may then reach past the queue window).
 hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const Plan& pl, int32_t* qorder,
                         uint64_t* skeys, int32_t* svals, void* stemp, size_t stempBytes, hipStream_t st,
-                        hipEvent_t mid, const int32_t* fixed_order, hipEvent_t* feas) {
+                        hipEvent_t mid, const int32_t* fixed_order, hipEvent_t* feas, int32_t* run_len,
+                        uint64_t* run_words) {
   if (pl.lds > 160 * 1024) return hipErrorInvalidValue;
   if (!fixed_order) {
     hipError_t e = queue_sort(D, skeys, svals, stemp, stempBytes, qorder, st);
+    if (e != hipSuccess) return e;
+  }
+  if (D.d.lean && run_len && run_words) {
+    hipError_t e = sim_run_lengths(fixed_order ? fixed_order : qorder, nullptr, D.pod_req, D.pod_s0, D.pod_flags, D.d.R,
+                                   D.d.P, run_words, run_len, st, true);
     if (e != hipSuccess) return e;
   }
   if (D.d.fmOn) {
