@@ -217,6 +217,30 @@ def test_lean_shared_uids_with_push_backs(seed):
         assert want["podErrors"], "the case must push pods back"
 
 
+@pytest.mark.parametrize("seed", [460, 461, 462, 463, 464])
+def test_lean_runs_past_the_queue_window(seed):
+    """Resource-only pods with distinct UIDs (the LEAN Solve keeps running after a push-back): long runs of
+    identical pods whose NodeClaim runs reach past the 64-pod queue window while nothing has been pushed back
+    (run lengths over NewQueue's order, round 6); a pod too large for every instance type (461, 463) or a
+    NodePool limit (462, 463) pushes pods back, after which runs stay inside the window; 464 mixes the pods'
+    tolerations (same requests, different toleration sets never share a run)."""
+    snap = synth.benchmark_snapshot(3000, 60, seed, diverse=False)
+    if seed in (461, 463):
+        for k in range(3):
+            snap["pods"].insert(700 * (k + 1), synth.pod(900000 + k, cpu="1000", mem="1Gi"))
+    if seed in (462, 463):
+        snap["nodePools"] = [synth.node_pool("default-pool", limits={"cpu": "1500"})]
+    if seed == 464:
+        for i, p in enumerate(snap["pods"]):
+            if i % 3 == 0:
+                p["spec"]["tolerations"] = [{"key": "batch", "operator": "Exists"}]
+    want, got = _solve_both(snap)
+    d = _diff(want, got)
+    assert d is None, d
+    if seed in (461, 462, 463):
+        assert want["podErrors"], "the case must push pods back"
+
+
 @pytest.mark.parametrize("seed", list(range(400, 412)))
 def test_queue_ties_parity(seed):
     """Random problems whose pods share UIDs and timestamps in groups, so NewQueue's order of equal
