@@ -1158,7 +1158,7 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
   // caller pays both launches, so the reported times are their sums (the re-plan is remembered).
   float ms = 0, setup = 0, fms = 0, fnms = 0;
   int feasLaunches = 0, attempts = 0;
-  for (int attempt = 0; attempt < 3; attempt++) {
+  for (int attempt = 0; attempt < 4; attempt++) {
     attempts++;
     HIPCHK(hipEventRecord(e0, pb->stream));
     HIPCHK(launch_solve(pb->dev, pb->works_dev, reps, pl, w0.qorder, pb->skeys, pb->svals, pb->stemp,
@@ -1188,11 +1188,14 @@ int ks_solve(ks_problem* pb, const ks_solve_opts* opts, ks_results** out) {
       pb->dev.d.lean = 0;
       continue;
     }
-    if (err != KE_CLAIM_CAP || pb->wideKO) break;
-    // more NodeClaims than the default plan holds: re-plan with claim positions filling the LDS
-    // (remembered for later Solves of this problem) and solve again
-    pb->wideKO = true;
-    pl = make_plan(d, budget, false, true);
+    if (err != KE_CLAIM_CAP || pb->wideKO >= 2) break;
+    // more NodeClaims than the plan holds: re-plan with claim positions filling the LDS (level 1 keeps the
+    // instance-type tables in LDS, level 2 moves them to HBM; remembered for later Solves of this problem)
+    // and solve again
+    const int prevKO = pl.KO;
+    pb->wideKO++;
+    pl = make_plan(d, budget, false, pb->wideKO);
+    if (pb->wideKO == 1 && pl.KO <= prevKO) pl = make_plan(d, budget, false, pb->wideKO = 2);
     if (pl.lds > 160 * 1024 || pl.KO < 1) break;
     pb->lastKO = pl.KO;
   }

@@ -21,7 +21,7 @@ hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const
 bool sims_mw_supported(const KsDev& D, const Plan& pl);
 hipError_t launch_sims_split(const KsDev& D, const KsWork* works_dev, int nsims, int nmw, const Plan& pl, hipStream_t st,
                              hipStream_t st2, hipEvent_t fork, hipEvent_t join);
-Plan make_plan(const KsDims& d, size_t budget, bool sim = false, bool wideKO = false);
+Plan make_plan(const KsDims& d, size_t budget, bool sim = false, int wideKO = 0);
 size_t queue_sort_temp_bytes(int n);
 hipError_t queue_sort(const KsDev& D, uint64_t* keys, int32_t* vals, void* temp, size_t tempBytes, int32_t* out,
                       hipStream_t st);
@@ -73,7 +73,7 @@ struct ks_problem {
   hipStream_t stream = nullptr;
   int device = -1;
   int lastKO = 0;  // claim capacity of the last launch plan
-  bool wideKO = false;  // a Solve of this problem outgrew the default plan's NodeClaim capacity
+  int wideKO = 0;  // a Solve of this problem outgrew the default plan's NodeClaim capacity (make_plan's level)
   // NewQueue radix-sort workspace
   uint64_t* skeys = nullptr;
   int32_t* svals = nullptr;

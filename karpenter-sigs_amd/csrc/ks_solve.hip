@@ -2842,10 +2842,11 @@ hipError_t launch_solve_plain(const KsDev& D, const KsWork* w, int n, const Plan
 // per Solve (KO); claims [0, KL) also keep their template/requests/max/options/thresholds in LDS,
 // the rest in HBM.  The instance-type tables go to LDS first when they leave room for 64 claims.
 // One-Solve launches use the whole 160 KiB of a CU; batched simulations pass a smaller budget.
-// wideKO: a Solve that created more NodeClaims than the default plan holds is re-planned with the
-// instance-type tables in HBM and almost all LDS given to claim positions.
-static Plan make_plan_live(const KsDims& d, size_t budget, bool sim, bool wideKO, bool live);
-Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
+// wideKO: a Solve that created more NodeClaims than the default plan holds is re-planned with 64 LDS-resident
+// claims and the rest of the LDS given to claim positions: level 1 keeps the instance-type tables in LDS, level 2
+// (when 1 still holds too few) moves them to HBM.  C3 (844 NodeClaims): 56.0k -> 59.1k pods/s at level 1.
+static Plan make_plan_live(const KsDims& d, size_t budget, bool sim, int wideKO, bool live);
+Plan make_plan(const KsDims& d, size_t budget, bool sim, int wideKO) {
   // The live node list serves the non-LEAN Solve instantiations with a register window (RT 3 or 4, launch_family):
   // a lean problem runs LEAN whenever its instance-type tables fit in LDS (talloc), so its plan reserves the list
   // only when they do not.
@@ -2858,7 +2859,7 @@ Plan make_plan(const KsDims& d, size_t budget, bool sim, bool wideKO) {
   return make_plan_live(d, budget, sim, wideKO, true);
 }
 
-static Plan make_plan_live(const KsDims& d, size_t budget, bool sim, bool wideKO, bool live) {
+static Plan make_plan_live(const KsDims& d, size_t budget, bool sim, int wideKO, bool live) {
   auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   Plan pl{};
   const size_t R = d.R, TW = d.TW, tot = d.totalTplIts;
@@ -2894,14 +2895,14 @@ static Plan make_plan_live(const KsDims& d, size_t budget, bool sim, bool wideKO
   avail = avail > livB ? avail - livB : 0;
   // The threshold filter needs the sorted lists only without negative requests.
   const size_t tablesB = tallocB + (d.negReq ? 0 : tsortB);
-  pl.talloc = (!wideKO && tablesB + 64 * (posB + clmB) <= avail) ? 1 : 0;
+  pl.talloc = (wideKO < 2 && tablesB + 64 * (posB + clmB) <= avail) ? 1 : 0;
   pl.tsort = pl.talloc && !d.negReq;
   if (pl.talloc) avail -= tablesB;
   const size_t kAll = avail / (posB + clmB);
   size_t ko, kl;
   if (kAll >= (size_t)d.Kcap) {
     ko = kl = d.Kcap;
-  } else if (wideKO) {  // 64 LDS-resident claims, the rest to positions
+  } else if (wideKO) {  // 64 LDS-resident claims, the rest to positions (C3: 8-96 claims measured within 1.5 %)
     kl = std::min<size_t>(64, kAll);
     ko = std::min((size_t)d.Kcap, (avail - kl * clmB) / posB);
   } else {  // half the LDS to positions, half to claim state
