@@ -336,7 +336,7 @@ def solve_line(args, local, name, snap, metric, reps, cpu_sample=None, extra=Non
     t = time.perf_counter()
     r = sch.solve(device=local)
     full_ms = (time.perf_counter() - t) * 1000.0
-    for _ in range(max(args.warmup - 1, 0)):
+    for _ in range(max(args.warmup - 1, reps // 20)):  # (sub-ms Solves: a warm-up proportional to the reps)
         sch.solve(device=local, timing_only=True)
     t0 = time.perf_counter()
     ks, algb, fms, fbytes = [], [], [], 0.0
@@ -431,7 +431,7 @@ def main():
         return
     if args.only_solve in ("c1", "c2", "c3", "c4"):
         if args.only_solve == "c1":
-            line = solve_line(args, local, "C1", synth.config1(literal=True), "C1 profile", 10, traffic_tag="c1")
+            line = solve_line(args, local, "C1", synth.config1(literal=True), "C1 profile", 200, traffic_tag="c1")
         elif args.only_solve == "c2":
             line = solve_line(args, local, "C2", synth.config2(args.pods), "C2 profile", args.steps, traffic_tag="c2")
         elif args.only_solve == "c3":
@@ -506,7 +506,7 @@ def main():
             c1 = synth.config1(literal=True)
             lines["solve_c1"] = solve_line(
                 args, local, "C1", c1, "pods/sec in Scheduler.Solve (C1: BenchmarkScheduling2000, the benchmark's "
-                "literal pods: empty UIDs, zero timestamps; 400 fake instance types, empty topology)", 10,
+                "literal pods: empty UIDs, zero timestamps; 400 fake instance types, empty topology)", 200,
                 cpu_sample=(c1, 2000, "20 Solves of C1", 20), traffic_tag="c1")
         if not args.no_c3:
             sp = min(args.c3_cpu_pods, args.c3_pods)
