@@ -1874,9 +1874,10 @@ uint64_t node_host_port_mask(const Host& h, int n) {
 // Subtract), a removed node's capacity returns to its pool's limits (provisioner.go:204-296 re-reads them
 // per pass) and the node can take no pod in any simulation.  The candidates and simulations are re-derived
 // (order_candidates).  Topology clusters move the shared NewTopology counts with the pods (round 5).  Refused
-// (KS_ERR_UNSUPPORTED, nothing applied): clusters with volume limits (a snapshot reports a node's VolumeUsage as
-// one union, so a pod's share of it is not known) and binding a pod with host ports (its entries would need
-// universe elements and classes of their own).  Deleting a pod with host ports drops its node's entries
+// (KS_ERR_UNSUPPORTED, nothing applied): in clusters with volume limits, deleting or binding a pod that mounts
+// volumes (a snapshot reports a node's VolumeUsage as one union, so a pod's share of it is not known; pods without
+// volumes and node removals leave every node's usage as it is), and binding a pod with host ports (its entries
+// would need universe elements and classes of their own).  Deleting a pod with host ports drops its node's entries
 // (HostPortUsage.DeletePod, node_host_port_mask).
 void apply_update(ks_cons& c, const Value& delta, bool device) {
   PhaseTimer pt("ks_cons_update");
@@ -1888,7 +1889,6 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
   for (const auto& kv : delta.obj())
     if (kv.first != "deletePods" && kv.first != "bindPods" && kv.first != "removeNodes")
       throw KsError(KS_ERR_PARSE, "update: unknown field " + kv.first);
-  if (d.volAny) throw KsError(KS_ERR_UNSUPPORTED, "update: the cluster has volume limits");
   if (c.uidIndex.empty()) {
     c.uidIndex.reserve(h.pods.size());
     for (size_t i = 0; i < h.pods.size(); i++) c.uidIndex.emplace(h.pods[i].uid, (int)i);
@@ -1921,6 +1921,8 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     const int p = podOf(v);
     if (c.podNode[(size_t)p] == ks_cons::PN_GONE || !seenPod.insert(p).second)
       throw KsError(KS_ERR_ARG, "update: pod " + v.str() + " is already deleted");
+    if (d.volAny && h.pods[(size_t)p].volumes)
+      throw KsError(KS_ERR_UNSUPPORTED, "update: pod " + v.str() + " mounts volumes in a cluster with volume limits");
     del.push_back(p);
   }
   for (const Value& v : (bv ? *bv : kNone).arr()) {
@@ -1929,6 +1931,8 @@ void apply_update(ks_cons& c, const Value& delta, bool device) {
     if (c.podNode[(size_t)p] != ks_cons::PN_PENDING || !seenPod.insert(p).second)
       throw KsError(KS_ERR_ARG, "update: pod " + v.get("uid")->str() + " is not pending");
     if (h.pods[(size_t)p].hostPorts) throw KsError(KS_ERR_UNSUPPORTED, "update: pod has host ports");
+    if (d.volAny && h.pods[(size_t)p].volumes)
+      throw KsError(KS_ERR_UNSUPPORTED, "update: pod mounts volumes in a cluster with volume limits");
     bind.push_back(p);
     bindNode.push_back(n);
   }

@@ -274,6 +274,66 @@ def test_host_port_pod_deletion_gpu_parity(seed):
     assert got == want
 
 
+def _mounts(pod):
+    return any(v.get("persistentVolumeClaim") or v.get("ephemeral") for v in pod["spec"].get("volumes", []))
+
+
+def _volume_delta(snap, seed):
+    """Events that leave every node's VolumeUsage as it is: volume-free pods deleted and bound, a node removed
+    (with its pods, volumes or not)."""
+    rng = random.Random(seed)
+    nodes = snap["stateNodes"]
+    free = [p["metadata"]["uid"] for n in nodes[:-1] for p in n.get("pods", []) if not _mounts(p)]
+    pend = [p["metadata"]["uid"] for p in snap.get("pendingPods", []) if not _mounts(p)]
+    d = {"deletePods": rng.sample(free, min(4, len(free))), "removeNodes": [nodes[-1]["name"]]}
+    if pend:
+        d["bindPods"] = [{"uid": pend[0], "node": nodes[1]["name"]}]
+    return d
+
+
+@pytest.mark.parametrize("seed", [71, 72])
+def test_volume_cluster_update_host_state(seed):
+    """Clusters with volume limits take updates whose pods mount no volumes (round 6); a pod that mounts one is
+    refused (a snapshot reports a node's VolumeUsage as one union per driver, so its share is not known)."""
+    from test_volume_topology import _volume_cluster
+
+    snap = _volume_cluster(seed, n_nodes=24, ppn=10)
+    d = _volume_delta(snap, seed)
+    assert d["deletePods"], "the cluster must hold volume-free pods"
+    got = inspect_consolidation_update(json.dumps(snap), d)
+    want = inspect_consolidation_update(json.dumps(apply_delta(snap, d)))
+    for k in ("candidates", "pendingPods", "nodeRows", "poolRemaining", "sims"):
+        assert got[k] == want[k], k
+    vol = [p["metadata"]["uid"] for n in snap["stateNodes"] for p in n.get("pods", []) if _mounts(p)]
+    with pytest.raises(KsError) as e:
+        inspect_consolidation_update(json.dumps(snap), {"deletePods": vol[:1]})
+    assert "KS_ERR_UNSUPPORTED" in str(e.value)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [71, 72, 73])
+def test_volume_cluster_update_gpu_parity(seed):
+    """A pass on the updated handle of a volume-limit cluster equals the oracle's consolidation of the edited
+    snapshot, over two successive updates and through save/from_binary."""
+    from test_volume_topology import _volume_cluster
+
+    snap = _volume_cluster(seed, n_nodes=24, ppn=10)
+    c = Consolidator(json.dumps(snap))
+    cur = snap
+    for i in range(2):
+        d = _volume_delta(cur, seed + i)
+        c.update(d)
+        cur = apply_delta(cur, d)
+        want, _ = bridge.consolidate(json.dumps(cur), all_sims=True)
+        got = c.consolidate(all_sims=True)
+        got.pop("kernel_ms")
+        assert got == want, (seed, i)
+    c2 = Consolidator.from_binary(c.save())
+    got = c2.consolidate(all_sims=True)
+    got.pop("kernel_ms")
+    assert got == want
+
+
 def _late_snap():
     """Pod A's first state owns a zonal spread group whose node filter is term T2; pod B's first state has
     required node-affinity terms [T1, T2] (another group), and its relaxation (removeRequiredNodeAffinityTerm,
