@@ -281,14 +281,26 @@ struct ks_cons {
     bool lsorted = false;  // lpodmap holds every simulation's NewQueue order (a plan's pods never change)
     Plan lplan{};
     std::vector<KsWork> lhost;  // host copy of the launch's workspace views (diagnostics)
+    // A topology plan is built in two phases: the multi-node prefixes (the long simulations, first in the plan)
+    // get their NewTopology deltas in prepare_launch and are launched at once; the single-node simulations'
+    // deltas are built while those run (pipeB: still to do, finish_topology) and launched behind them.
+    bool pipeB = false;
+    int nA = 0;                              // simulations [0, nA) launched first
+    std::vector<std::vector<int>> podsB;     // pod lists of simulations [nA, ns)
+    void* ltopoB = nullptr;                  // device: their topology inputs
+    char* htopoB = nullptr;                  // pinned staging of those
+    KsWork* hworksB = nullptr;               // pinned staging of their workspace views
+    size_t capTopoB = 0, capHtopoB = 0, capHworksB = 0;
     // allocation capacities: a new plan (another rank / world, an update) reuses the buffers that fit
     size_t capBuf = 0, capWorks = 0, capRec = 0, capHrec = 0, capEnt = 0, capRunw = 0, capTemp = 0, capHdr = 0, capHhdr = 0;
     void release() {
       for (void* p : {(void*)lbuf, (void*)lworks, (void*)lrec, (void*)lentries, (void*)lentrySim, (void*)lpodmap,
-                      (void*)lrunlen, (void*)lrunw, (void*)lkeys, (void*)lvals, ltemp, (void*)lhdr, (void*)lst})
+                      (void*)lrunlen, (void*)lrunw, (void*)lkeys, (void*)lvals, ltemp, (void*)lhdr, (void*)lst, ltopoB})
         if (p) (void)hipFree(p);
       if (hrec) (void)hipHostFree(hrec);
       if (hhdr) (void)hipHostFree(hhdr);
+      if (htopoB) (void)hipHostFree(htopoB);
+      if (hworksB) (void)hipHostFree(hworksB);
       *this = Launch{};  // stale lookups (claim requirements, counters) now fail cleanly
     }
     // drop the plan, keep the allocations
@@ -300,6 +312,9 @@ struct ks_cons {
       lsorted = false;
       hdrOnly = keptFull = false;
       lplan = Plan{};
+      pipeB = false;
+      nA = 0;
+      podsB.clear();
     }
   };
   Launch L;
@@ -877,6 +892,12 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   std::vector<std::vector<uint64_t>> tdead(ns), tact(ns);
   std::vector<std::vector<int32_t>> tmd(ns);
   std::vector<std::vector<int>> simPods(ns);
+  // the leading multi-node prefixes (the long simulations): a topology plan builds the others' deltas while these
+  // run (Launch::pipeB; KS_NO_PIPE=1: all before the launch)
+  int nA = 0;
+  while (nA < ns && c.sims[(size_t)mine[(size_t)nA]].multi) nA++;
+  const bool pipe = d.G && nA > 0 && nA < ns && !std::getenv("KS_NO_PIPE");
+  const int nTopo = pipe ? nA : ns;
   parallel_for(ns, 16, [&](int k) {
     const ks_cons::Sim& sm = c.sims[(size_t)mine[(size_t)k]];
     std::vector<int>& pods = simPods[k];
@@ -907,7 +928,7 @@ void prepare_launch(ks_cons& c, int rank, int world) {
     const bool anyInjFailed = std::find(h.injectFailed.begin(), h.injectFailed.end(), 1) != h.injectFailed.end();
     pt.mark("minDomains groups");
     std::vector<std::exception_ptr> err((size_t)ns);
-    parallel_for(ns, 4, [&](int k) {
+    parallel_for(nTopo, 4, [&](int k) {
       try {
         tdel[k] = sim_topology(c, c.sims[(size_t)mine[(size_t)k]], simPods[k], ptopo, tdead[k], tact[k], c.carryStart,
                                altGroups, anyInjFailed, tmd[k]);
@@ -978,10 +999,12 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       o.tg_cnt = a.add(4 * (size_t)d.tgCntWords);
       o.tg_ccnt = a.add(4 * (size_t)d.G * (P + 1));
       o.tg_cpos = a.add(4 * (size_t)d.G);
-      o.tdel = ai.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
-      o.tdead = ai.add(8 * (size_t)d.GMW);
-      o.tact = ai.add(8 * (size_t)d.GMW);
-      o.tmd = ai.add(4 * std::max<size_t>(tmd[k].size(), 1));
+      if (k < nTopo) {
+        o.tdel = ai.add(8 * std::max<size_t>(tdel[k].size() / 2, 1));
+        o.tdead = ai.add(8 * (size_t)d.GMW);
+        o.tact = ai.add(8 * (size_t)d.GMW);
+        o.tmd = ai.add(4 * std::max<size_t>(tmd[k].size(), 1));
+      }
     }
     if (c.carryStart) o.sstart = ai.add(4 * c.carryStart->size());
   }
@@ -1179,6 +1202,8 @@ void prepare_launch(ks_cons& c, int rank, int world) {
       w.tg_cnt = (int32_t*)(base + o.tg_cnt);
       w.tg_ccnt = (int32_t*)(base + o.tg_ccnt);
       w.tg_cpos = (int32_t*)(base + o.tg_cpos);
+    }
+    if (d.G && k < nTopo) {  // (the others' topology inputs: finish_topology)
       memcpy(stage.data() + o.tdel, tdel[k].data(), 4 * tdel[k].size());
       w.tdel = (const int32_t*)(ibase + o.tdel);
       w.ntdel = (int32_t)(tdel[k].size() / 2);
@@ -1226,9 +1251,97 @@ void prepare_launch(ks_cons& c, int rank, int world) {
   c.L.lnmw = 0;
   if (mwWanted && sims_mw_supported(pb.dev, c.L.lplan))
     while (c.L.lnmw < ns && simP[(size_t)c.L.lnmw] >= mwMin) c.L.lnmw++;
+  c.L.pipeB = pipe;
+  c.L.nA = pipe ? nA : 0;
+  if (pipe) c.L.podsB.assign(std::make_move_iterator(simPods.begin() + nA), std::make_move_iterator(simPods.end()));
   c.L.lrank = rank;
   c.L.lworld = world;
   pt.mark("zero + upload + LDS plan");
+}
+
+// The second phase of a topology plan (Launch::pipeB): the NewTopology deltas of simulations [nA, ns), built on
+// the host while [0, nA) run, then their inputs and workspace views copied on stream `st` once `ready` (the plan's
+// queue sort and feasibility rows) has passed -- pinned staging, so nothing waits for the running launch.
+void finish_topology(ks_cons& c, hipStream_t st, hipEvent_t ready) {
+  PhaseTimer pt("finish_topology");
+  ks_problem& pb = *c.pb;
+  Host& h = pb.host;
+  const KsDims& d = h.dims;
+  const int nA = c.L.nA, ns = (int)c.L.lsims.size(), nB = ns - nA;
+  std::vector<std::vector<int32_t>> tdel((size_t)nB), tmd((size_t)nB);
+  std::vector<std::vector<uint64_t>> tdead((size_t)nB), tact((size_t)nB);
+  PodTopo ptopo;
+  ptopo.contrib.swap(c.podContrib);
+  ptopo.inv.swap(c.podInv);
+  const bool anyInjFailed = std::find(h.injectFailed.begin(), h.injectFailed.end(), 1) != h.injectFailed.end();
+  std::vector<std::exception_ptr> err((size_t)nB);
+  parallel_for(nB, 4, [&](int k) {
+    try {
+      tdel[(size_t)k] = sim_topology(c, c.sims[(size_t)c.L.lsims[(size_t)(nA + k)]], c.L.podsB[(size_t)k], ptopo,
+                                     tdead[(size_t)k], tact[(size_t)k], c.carryStart, c.altGroups, anyInjFailed,
+                                     tmd[(size_t)k]);
+    } catch (...) {
+      err[(size_t)k] = std::current_exception();
+    }
+  });
+  c.podContrib.swap(ptopo.contrib);
+  c.podInv.swap(ptopo.inv);
+  for (auto& e : err)
+    if (e) {
+      c.invalidate_launch();  // (the first phase's launch is in flight; the next call builds a new plan)
+      std::rethrow_exception(e);
+    }
+  pt.mark("topology deltas");
+  Arena at;
+  std::vector<size_t> o((size_t)nB * 4);
+  for (int k = 0; k < nB; k++) {
+    o[(size_t)k * 4 + 0] = at.add(8 * std::max<size_t>(tdel[(size_t)k].size() / 2, 1));
+    o[(size_t)k * 4 + 1] = at.add(8 * (size_t)d.GMW);
+    o[(size_t)k * 4 + 2] = at.add(8 * (size_t)d.GMW);
+    o[(size_t)k * 4 + 3] = at.add(4 * std::max<size_t>(tmd[(size_t)k].size(), 1));
+  }
+  const size_t bytes = std::max<size_t>(at.total, 256), wbytes = sizeof(KsWork) * (size_t)std::max(nB, 1);
+  if (!c.L.ltopoB || bytes > c.L.capTopoB) {
+    if (c.L.ltopoB) HIPCHK(hipFree(c.L.ltopoB));
+    c.L.ltopoB = nullptr;
+    HIPCHK(hipMalloc(&c.L.ltopoB, bytes));
+    c.L.capTopoB = bytes;
+  }
+  if (!c.L.htopoB || bytes > c.L.capHtopoB) {
+    if (c.L.htopoB) HIPCHK(hipHostFree(c.L.htopoB));
+    c.L.htopoB = nullptr;
+    HIPCHK(hipHostMalloc((void**)&c.L.htopoB, bytes, hipHostMallocDefault));
+    c.L.capHtopoB = bytes;
+  }
+  if (!c.L.hworksB || wbytes > c.L.capHworksB) {
+    if (c.L.hworksB) HIPCHK(hipHostFree(c.L.hworksB));
+    c.L.hworksB = nullptr;
+    HIPCHK(hipHostMalloc((void**)&c.L.hworksB, wbytes, hipHostMallocDefault));
+    c.L.capHworksB = wbytes;
+  }
+  char* stage = c.L.htopoB;
+  const char* dev = (const char*)c.L.ltopoB;
+  parallel_for(nB, 64, [&](int k) {
+    const size_t* ok = &o[(size_t)k * 4];
+    KsWork& w = c.L.lhost[(size_t)(nA + k)];
+    memcpy(stage + ok[0], tdel[(size_t)k].data(), 4 * tdel[(size_t)k].size());
+    w.tdel = (const int32_t*)(dev + ok[0]);
+    w.ntdel = (int32_t)(tdel[(size_t)k].size() / 2);
+    memcpy(stage + ok[1], tdead[(size_t)k].data(), 8 * tdead[(size_t)k].size());
+    w.tdead = (const uint64_t*)(dev + ok[1]);
+    memcpy(stage + ok[2], tact[(size_t)k].data(), 8 * tact[(size_t)k].size());
+    w.tact = std::getenv("KS_NO_TACT") ? nullptr : (const uint64_t*)(dev + ok[2]);
+    if (!tmd[(size_t)k].empty()) memcpy(stage + ok[3], tmd[(size_t)k].data(), 4 * tmd[(size_t)k].size());
+    w.tmd = (const int32_t*)(dev + ok[3]);
+    w.ntmd = (int32_t)(tmd[(size_t)k].size() / 2);
+    c.L.hworksB[k] = w;
+  });
+  HIPCHK(hipStreamWaitEvent(st, ready, 0));  // the plan's queue sort and feasibility rows
+  HIPCHK(hipMemcpyAsync(c.L.ltopoB, c.L.htopoB, at.total ? at.total : 8, hipMemcpyHostToDevice, st));
+  if (nB) HIPCHK(hipMemcpyAsync(c.L.lworks + nA, c.L.hworksB, sizeof(KsWork) * (size_t)nB, hipMemcpyHostToDevice, st));
+  c.L.pipeB = false;
+  c.L.podsB.clear();
+  pt.mark("inputs staged");
 }
 
 std::string names_json(const Host& h, const std::vector<int>& its) {
@@ -1542,6 +1655,7 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
     HIPCHK(sim_run_lengths(c.L.lpodmap, c.L.lentrySim, pb.dev.pod_req, pb.dev.pod_s0, pb.dev.pod_flags, pb.host.dims.R,
                            c.L.lnent, c.L.lrunw, c.L.lrunlen, pb.stream));
     c.L.lsorted = true;
+    pt.mark("queue sort + run lengths enqueued");
   }
   if (c.L.lnmw > 0 && !c.st2) {
     // the long simulations' stream at the highest priority: their workgroups must be dispatched before the
@@ -1552,7 +1666,28 @@ double run_sims(ks_cons& c, int rank, int world, void* records, bool onDevice) {
     HIPCHK(hipEventCreateWithFlags(&c.evFork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c.evJoin, hipEventDisableTiming));
   }
-  HIPCHK(launch_sims_split(pb.dev, c.L.lworks, ns, c.L.lnmw, c.L.lplan, pb.stream, c.st2, c.evFork, c.evJoin));
+  if (c.L.pipeB) {
+    // a new topology plan: the multi-node prefixes start at once, the single-node simulations' inputs are built
+    // while they run and launched on the second stream (they fill the CUs the long prefixes leave idle)
+    if (!c.st2) {
+      int least = 0, greatest = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIPCHK(hipStreamCreateWithPriority(&c.st2, hipStreamNonBlocking, greatest));
+      HIPCHK(hipEventCreateWithFlags(&c.evFork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&c.evJoin, hipEventDisableTiming));
+    }
+    if (pb.dev.d.fmOn) launch_feasibility(pb.dev, pb.stream);
+    if (pb.dev.d.fnOn) launch_feasibility_nodes(pb.dev, pb.stream);
+    HIPCHK(hipEventRecord(c.evFork, pb.stream));
+    HIPCHK(launch_sims_topo(pb.dev, c.L.lworks, c.L.nA, c.L.lplan, pb.stream));
+    pt.mark("first phase launched");
+    finish_topology(c, c.st2, c.evFork);
+    HIPCHK(launch_sims_topo(pb.dev, c.L.lworks + c.L.nA, ns - c.L.nA, c.L.lplan, c.st2));
+    HIPCHK(hipEventRecord(c.evJoin, c.st2));
+    HIPCHK(hipStreamWaitEvent(pb.stream, c.evJoin, 0));
+  } else {
+    HIPCHK(launch_sims_split(pb.dev, c.L.lworks, ns, c.L.lnmw, c.L.lplan, pb.stream, c.st2, c.evFork, c.evJoin));
+  }
   HIPCHK(hipEventRecord(c.ev[1], pb.stream));
   pt.mark("launches enqueued");
   // the records follow on the same stream; one synchronisation covers both

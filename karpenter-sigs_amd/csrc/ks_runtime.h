@@ -16,6 +16,11 @@ hipError_t launch_solve(const KsDev& D, const KsWork* works_dev, int nrep, const
                         hipEvent_t mid, const int32_t* fixed_order = nullptr, hipEvent_t* feas = nullptr,
                         int32_t* run_len = nullptr, uint64_t* run_words = nullptr);
 hipError_t launch_sims(const KsDev& D, const KsWork* works_dev, int nsims, const Plan& pl, hipStream_t st);
+// The topology simulations' kernel alone, and the feasibility launches launch_sims makes before it (a two-phase
+// consolidation plan, ks_cons.cpp run_sims).
+hipError_t launch_sims_topo(const KsDev& D, const KsWork* w, int n, const Plan& pl, hipStream_t st);
+void launch_feasibility(const KsDev& D, hipStream_t st);
+void launch_feasibility_nodes(const KsDev& D, hipStream_t st);
 // The first nmw simulations (the long multi-node prefixes) on 4-wave workgroups when the problem allows it
 // (sims_mw_supported: resource-only pods, no topology), concurrently with the rest.
 bool sims_mw_supported(const KsDev& D, const Plan& pl);
