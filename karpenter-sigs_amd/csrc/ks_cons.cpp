@@ -1288,7 +1288,9 @@ void finish_topology(ks_cons& c, hipStream_t st, hipEvent_t ready) {
   c.podInv.swap(ptopo.inv);
   for (auto& e : err)
     if (e) {
-      c.invalidate_launch();  // (the first phase's launch is in flight; the next call builds a new plan)
+      // the first phase's launch is in flight: let it finish before the next call's plan re-zeroes its buffers
+      (void)hipStreamSynchronize(pb.stream);
+      c.invalidate_launch();
       std::rethrow_exception(e);
     }
   pt.mark("topology deltas");
